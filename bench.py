@@ -1,0 +1,186 @@
+#!/usr/bin/env python3
+"""Benchmark: particle-steps/s of the MPH explicit hot path on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], SURVEY 8d "D1M"): 3-D dam break, 1,397,200 particles
+(970,000 fluid + 427,200 wall), dx = 1 mm, Dt = 1e-4 s, generated in memory with the reference
+generator's algorithm and the reference's results/Dam/dam.data parameters.  One "step" = one
+iteration of the reference's time loop (main.cpp:597-686): wall motion, periodic wrap, cell sort,
+neighbour search, density/pressure sums, pressure/surface/viscous forces, gravity, kick, drift
+(+ elastic substeps when structure particles exist).  Inputs are resident in HBM before timing.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--case d1m] [--no-cpu-baseline]
+
+For N > 1 (torchrun, one rank per GPU) every rank runs the slab decomposition of a dam whose
+z-extent is N times D1M's, so the per-GPU work stays fixed (weak scaling).
+
+Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel's algorithmic HBM bytes per
+launch (SURVEY 8d per-particle figures) over its HIP-event-timed average
+launch duration; `cpu_baseline` times the reference solver itself (oracle/_ref, built from
+/root/reference) on a bounded sample of the same workload on this host's cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector spec
+# algorithmic bytes per particle per launch
+ALG_BYTES = {"pass_a": 92.0, "pass_b": 140.0, "sort": 140.0}
+B_ALG_STEP = 372.0          # grid build 140 + pass 1 92 + pass 2 140
+
+
+def dist_env():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return rank, world, local
+
+
+def cpu_baseline(case_name: str, seconds_target: float = 15.0):
+    """Time the reference (oracle/_ref) -- or, if absent, the CPU oracle port -- on the same
+    workload, in a child process, on this host's cores (OMP_NUM_THREADS)."""
+    script = r"""
+import sys, os, time, json, ctypes, numpy as np, tempfile
+sys.path.insert(0, %(root)r); sys.path.insert(0, %(root)r + '/tests')
+from particlemethod_fsi_amd import cases, solver
+from oracle_bindings import RefSolver, OracleSolver, ref_available
+c = cases.get(%(case)r)
+cfg, p = c.build()
+threads = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
+if ref_available(c.dim, c.module):
+    d = tempfile.mkdtemp(prefix='mphcpu_')
+    dp, gp = os.path.join(d, 'c.data'), os.path.join(d, 'c.grid')
+    open(dp, 'w').write(cases.data_text(c.data()))
+    L = solver.load_library()
+    L.mph_write_prof_arrays(gp.encode(), ctypes.byref(cfg), 0.0, p.n, p.property.ctypes.data,
+                            p.position.ctypes.data, p.initial_position.ctypes.data, p.velocity.ctypes.data)
+    s = RefSolver(c.dim, c.module, dp, gp); kind = 'reference'
+else:
+    s = OracleSolver(cfg, p); kind = 'port'
+s.init()
+t0 = time.time(); s.step(1); t1 = time.time()
+per = t1 - t0
+k = max(1, min(20, int(%(target)f / max(per, 1e-6))))
+t2 = time.time(); s.step(k); t3 = time.time()
+print(json.dumps({'value': p.n * k / (t3 - t2), 'unit': 'particle-steps/s', 'cores': threads,
+                  'kind': kind, 'sample': '%%s: %%d particles, %%d timed steps after 1 warm-up step (%%.1f s)'
+                  %% (%(case)r, p.n, k, t3 - t2)}))
+""" % {"root": ROOT, "case": case_name, "target": seconds_target}
+    try:
+        r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=900)
+        for line in r.stdout.splitlines()[::-1]:
+            if line.startswith("{"):
+                return json.loads(line)
+        return {"error": (r.stderr or r.stdout)[-500:]}
+    except Exception as e:  # pragma: no cover
+        return {"error": repr(e)}
+
+
+def load_pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if present."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--case", default="d1m")
+    ap.add_argument("--profile-steps", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank, world, local = dist_env()
+    import numpy as np
+    from particlemethod_fsi_amd import MphSolver, cases
+
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = tdist
+
+    case = cases.get(args.case)
+    cfg, parts = case.build()
+    solver = MphSolver(cfg, parts, device=local)
+    n_total = parts.n
+
+    def barrier():
+        solver.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    solver.step(args.warmup)
+    barrier()
+    t0 = time.perf_counter()
+    solver.step(args.steps)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = n_total * world * args.steps / elapsed   # replicas: every rank advances its own set
+
+    mean_nb, max_nb = solver.neighbor_stats()
+    prof = solver.profile(args.profile_steps)
+    dom = max((k for k in prof if k in ALG_BYTES), key=lambda k: prof[k]["avg_ms"])
+    step_ms = sum(v["avg_ms"] * v["launches"] for v in prof.values()) / args.profile_steps
+    alg_bytes = ALG_BYTES[dom] * parts.n
+    achieved = alg_bytes / (prof[dom]["avg_ms"] * 1e-3) / 1e9
+    traffic = load_pmc_traffic(dom)
+    out = {
+        "metric": "particle-steps/sec + achieved HBM GB/s, dam-break, 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "particle-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (reference generator algorithm + results/Dam/dam.data parameters)",
+        "config": {"workload": "%s: 3-D dam break (SURVEY 8d D1M), %d particles per GPU" % (args.case, parts.n),
+                   "particles": n_total * world, "dim": case.dim, "module": case.module,
+                   "dt": cfg.dt, "parallelism": "replicas" if world > 1 else "single"},
+        "achieved_hbm_gbps_alg": B_ALG_STEP * value / 1e9,
+        "neighbors": {"mean": mean_nb, "max": max_nb},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
+                     "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
+                     "avg_launch_ms": prof[dom]["avg_ms"]},
+        "kernels_ms": {k: round(v["avg_ms"], 5) for k, v in prof.items()},
+        "profiled_step_ms": step_ms,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.case)
+    solver.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,204 @@
+/*
+ * mph_gpu.h -- C ABI of the MI355X-native MPH explicit hot path (libmph_gpu.so).
+ *
+ * Drop-in boundary for the reference solver Ryo1011gd/ParticleMethod_FSI (src/main.cpp).
+ * The reference has no plugin/FFI layer: its hot path is a set of `static void calculateX(void)`
+ * functions over file-scope globals (main.cpp:200-241) called in a fixed order by main()
+ * (main.cpp:581-688).  This header replaces that whole layer with a context object:
+ *
+ *   reference                                              | this ABI
+ *   -------------------------------------------------------+--------------------------------------
+ *   readDataFile          main.cpp:729-786                 | mph_read_data_file
+ *   readGridFile          main.cpp:788-955                 | mph_read_grid_header/_particles
+ *   initializeWeight/Fluid/Wall/Domain main.cpp:534-537,    | mph_create  (derives every constant,
+ *     1191-1469; acc update device main.cpp:549-560;       |   uploads, builds the structure
+ *     calculateInitialNeighbor/Neighbor/DensityA/          |   Lagrangian lists and normalizer,
+ *     GravityCenter/DensityP/Lamesconstant/Normalizer      |   runs the init sums)
+ *     main.cpp:564-570                                     |
+ *   one iteration of the time loop main.cpp:597-686       | mph_step(ctx, 1)
+ *   acc update host main.cpp:987-989 + array reads         | mph_get
+ *   writeProfFile main.cpp:957-982                         | mph_write_prof
+ *   writeVtkFile  main.cpp:984-1189                        | mph_write_vtk
+ *   err_malloc/err_fopen exit(1) errorfunc.cpp:8-31        | negative MphStatus + mph_last_error
+ *
+ * Data at the boundary is the reference's own layout (vec3T.hpp:31-34 / main.cpp:105-197):
+ * AoS double[n][3] for vectors, row-major double[n][3][3] for tensors, int[n] for ints, always in
+ * the ORIGINAL particle order of the .grid file.  Internally the device keeps a cell-sorted
+ * struct-of-arrays copy and a permutation; nothing of that leaks through this header.
+ *
+ * Threading: one host thread per context; several contexts may coexist (no global state).
+ * mph_step is stream-ordered; mph_get/mph_write_* synchronise.
+ */
+#ifndef MPH_GPU_H_INCLUDED
+#define MPH_GPU_H_INCLUDED
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPH_TYPE_COUNT 6            /* main.cpp:68 */
+#define MPH_MAX_NEIGHBOR_COUNT 512  /* main.cpp:100 (semantic limit; overflow is an error here) */
+#define MPH_ABI_VERSION 1
+
+/* Compile-time case modules of the reference (main.cpp:54-59) as a runtime switch.  The module
+ * selects the clamp rule of updateElasticPosition (main.cpp:1918-2044).                        */
+typedef enum MphModule {
+    MPH_MODULE_BAR = 0,          /* Bar_Module: x0.x < 0.001 clamped, force zeroed   (1918-1943) */
+    MPH_MODULE_DAM = 1,          /* DAM_Module: x0.y < 0.002 clamped, force zeroed   (1967-1992) */
+    MPH_MODULE_TUREK_HRON = 2,   /* Turek_Hron: x0.x < 0.205 clamped                 (1944-1966) */
+    MPH_MODULE_ROLLING1 = 3,     /* Rolling1:   x0.y < 0.003 clamped, force zeroed   (1993-2018) */
+    MPH_MODULE_HYDROELASTIC = 4, /* Hydroelastic: x0.x<0.01||>1.99, force zeroed     (2019-2044) */
+    MPH_MODULE_NONE = 5          /* no clamp (only the unconditional drift of 2070-2079)          */
+} MphModule;
+
+typedef enum MphStatus {
+    MPH_OK = 0,
+    MPH_ERR_ARG = -1,
+    MPH_ERR_IO = -2,
+    MPH_ERR_NEIGHBOR_OVERFLOW = -3,  /* a particle found >= 512 neighbours (main.cpp:1766-1768) */
+    MPH_ERR_DEVICE_OOM = -4,
+    MPH_ERR_HIP = -5,
+    MPH_ERR_RCCL = -6,
+    MPH_ERR_DOMAIN = -7,             /* domain too small for the cell stencil        */
+    MPH_ERR_UNSUPPORTED = -8,
+    MPH_ERR_NONFINITE = -9
+} MphStatus;
+
+/* Everything the reference reads from its .data file (main.cpp:743-767) and .grid header
+ * (main.cpp:797-804), plus the two compile-time switches.  All derived constants (radii, kernel
+ * normalisations, N0a/N0p, CofA, cell grid, wall rotations ...) are computed inside mph_create
+ * exactly as initializeWeight/Fluid/Wall/Domain do.                                             */
+typedef struct MphConfig {
+    int    dim;                       /* 2 or 3: TWO_DIMENSIONAL main.cpp:50 */
+    int    module;                    /* MphModule */
+    double dt;                        /* Dt */
+    double elastic_dt;                /* ElasticDt */
+    double output_interval;           /* OutputInterval */
+    double vtk_output_interval;       /* VtkOutputInterval */
+    double end_time;                  /* EndTime */
+    double radius_ratio_a;            /* RadiusRatioA (RadiusRatioG = RadiusRatioA, main.cpp:1193) */
+    double radius_ratio_p;            /* RadiusRatioP */
+    double radius_ratio_v;            /* RadiusRatioV */
+    double density[MPH_TYPE_COUNT];
+    double bulk_modulus[MPH_TYPE_COUNT];
+    double bulk_viscosity[MPH_TYPE_COUNT];
+    double shear_viscosity[MPH_TYPE_COUNT];
+    double surface_tension[MPH_TYPE_COUNT];   /* .data gives types 0,1,4,5 (main.cpp:756) */
+    double young_modulus[MPH_TYPE_COUNT];     /* .data gives types 2..5     (main.cpp:757) */
+    double poisson_ratio[MPH_TYPE_COUNT];     /* .data gives types 2..5     (main.cpp:758) */
+    double interaction_ratio[MPH_TYPE_COUNT][MPH_TYPE_COUNT];
+    double gravity[3];
+    double wall_center[MPH_TYPE_COUNT][3];    /* only Wall6/Wall7 -> types 4/5 are parsed (766-767) */
+    double wall_velocity[MPH_TYPE_COUNT][3];
+    double wall_omega[MPH_TYPE_COUNT][3];
+    double time;                      /* .grid line 1 (restart time) */
+    double particle_spacing;          /* .grid line 2 */
+    double domain_min[3];
+    double domain_max[3];
+} MphConfig;
+
+/* Per-particle arrays readable with mph_get (original particle order). */
+typedef enum MphField {
+    MPH_FIELD_POSITION = 0,           /* double[n][3] */
+    MPH_FIELD_INITIAL_POSITION = 1,   /* double[n][3] */
+    MPH_FIELD_VELOCITY = 2,           /* double[n][3] */
+    MPH_FIELD_FORCE = 3,              /* double[n][3] */
+    MPH_FIELD_ACCELERATION = 4,       /* double[n][3] */
+    MPH_FIELD_GRAVITY_CENTER = 5,     /* double[n][3] */
+    MPH_FIELD_PRESSURE_P = 6,         /* double[n] */
+    MPH_FIELD_PRESSURE_A = 7,         /* double[n] */
+    MPH_FIELD_DENSITY_A = 8,          /* double[n] */
+    MPH_FIELD_VOL_STRAIN_P = 9,       /* double[n] */
+    MPH_FIELD_DIVERGENCE_P = 10,      /* double[n] */
+    MPH_FIELD_MASS = 11,              /* double[n] */
+    MPH_FIELD_KAPPA = 12,             /* double[n] */
+    MPH_FIELD_LAMBDA = 13,            /* double[n] */
+    MPH_FIELD_MU = 14,                /* double[n] */
+    MPH_FIELD_NEIGHBOR_COUNT = 15,    /* int[n] */
+    MPH_FIELD_INITIAL_STRUCTURE_NEIGHBOR_COUNT = 16, /* int[n] */
+    MPH_FIELD_PROPERTY = 17,          /* int[n] */
+    MPH_FIELD_DEFORM_GRADIENT = 18,   /* double[n][3][3] */
+    MPH_FIELD_STRAIN = 19,            /* double[n][3][3] */
+    MPH_FIELD_STRESS = 20,            /* double[n][3][3] */
+    MPH_FIELD_NORMALIZER = 21,        /* double[n][3][3] */
+    MPH_FIELD_LAMBDA_LAMES = 22,      /* double[n] */
+    MPH_FIELD_MU_LAMES = 23,          /* double[n] */
+    MPH_FIELD_COUNT = 24
+} MphField;
+
+typedef struct MphCtx MphCtx;
+
+/* ---- host-side file formats (no device needed) ------------------------------------------- */
+
+/* Fill cfg with the reference's static defaults (zeros, Dt=ElasticDt=1e100) for dim/module. */
+int mph_config_default(MphConfig* cfg, int dim, int module);
+/* .data keyword file, main.cpp:729-786.  Unknown lines are ignored like the reference.      */
+int mph_read_data_file(const char* path, MphConfig* cfg);
+/* .grid / .prof header (Time; N dx xmin xmax ymin ymax zmin zmax), main.cpp:796-804.        */
+int mph_read_grid_header(const char* path, MphConfig* cfg, int* n);
+/* .grid / .prof body: n lines "type x y z x0 y0 z0 vx vy vz", main.cpp:896-904.             */
+int mph_read_grid_particles(const char* path, int n, int* property, double* pos, double* pos0,
+                            double* vel);
+/* .prof writer with the reference's exact format, main.cpp:957-982.                          */
+int mph_write_prof_arrays(const char* path, const MphConfig* cfg, double time, int n,
+                          const int* property, const double* pos, const double* pos0,
+                          const double* vel);
+/* legacy-ASCII .vtk writer with the reference's exact format, main.cpp:984-1189.            */
+int mph_write_vtk_arrays(const char* path, int n, const int* property, const double* pos,
+                         const double* pos0, const double* vel, const double* accel,
+                         const double* force, const double* stress, const double* strain,
+                         const int* initial_structure_neighbor_count, const int* neighbor_count);
+
+/* Every constant the reference derives before its time loop (initializeWeight/Fluid/Wall/Domain,
+ * main.cpp:1191-1469), without a device: 36 doubles in the slot order of mph_get_scalars.      */
+int mph_derive_scalars(const MphConfig* cfg, double* out36);
+
+/* ---- device context ------------------------------------------------------------------------ */
+
+/* Create a context on HIP device `device`, upload the particles, derive all constants and run
+ * the reference's initialisation sums (main.cpp:534-570).                                    */
+int mph_create(MphCtx** ctx, const MphConfig* cfg, int n, const int* property,
+               const double* pos, const double* pos0, const double* vel, int device);
+/* Advance nsteps time steps (main.cpp:597-686 each).  Steps are replayed from a captured
+ * hipGraph; returns MPH_ERR_NEIGHBOR_OVERFLOW if any particle reached 512 neighbours.        */
+int mph_step(MphCtx* ctx, int nsteps);
+int mph_synchronize(MphCtx* ctx);
+/* Copy a field to host, AoS, original particle order.                                      */
+int mph_get(MphCtx* ctx, int field, void* host_out);
+/* Overwrite Position or Velocity (original order) -- the reference's `acc update device`.    */
+int mph_set(MphCtx* ctx, int field, const void* host_in);
+int mph_particle_count(const MphCtx* ctx);
+double mph_time(const MphCtx* ctx);
+/* Derived scalar constants, same slots as oracle/ref_harness.inc ref_scalars (36 doubles).  */
+int mph_get_scalars(const MphCtx* ctx, double* out36);
+int mph_write_prof(MphCtx* ctx, const char* path);
+int mph_write_vtk(MphCtx* ctx, const char* path);
+const char* mph_last_error(const MphCtx* ctx);
+void mph_destroy(MphCtx* ctx);
+
+/* ---- measurement ---------------------------------------------------------------------------- */
+
+/* Run nsteps with a HIP event pair around every kernel launch (direct launches on the
+ * context's stream, no graph) and report per-kernel-kind average duration in milliseconds.
+ * names: MPH_PROFILE_MAX slots of 32 chars; returns the number of kernel kinds.              */
+#define MPH_PROFILE_MAX 24
+int mph_profile_steps(MphCtx* ctx, int nsteps, double* avg_ms, int* launches, char* names32);
+/* Mean/max neighbour count of the last step (for algorithmic byte/flop accounting).         */
+int mph_neighbor_stats(MphCtx* ctx, double* mean, int* max);
+
+/* ---- multi-GPU slab decomposition (one process per GPU, RCCL over xGMI) ------------------ */
+
+/* 128-byte RCCL unique id generated on rank 0 and shared out of band by the caller.          */
+int mph_dist_unique_id(char* out128);
+/* Same as mph_create, but this rank owns only the particles whose slab (along `axis`) is
+ * `rank` of `nranks`; all ranks pass the full particle set (any rank may pass it).           */
+int mph_create_dist(MphCtx** ctx, const MphConfig* cfg, int n, const int* property,
+                    const double* pos, const double* pos0, const double* vel, int device,
+                    int rank, int nranks, const char* unique_id128, int axis);
+/* Particles currently owned by this rank (after migration).                                  */
+int mph_owned_count(const MphCtx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPH_GPU_H_INCLUDED */

@@ -1,0 +1,182 @@
+"""Benchmark and parity configurations, generated in memory.
+
+All particle sets come from the reference generator's Cuboid algorithm (mphio.generate, byte-
+identical to generator/generator.cpp on results/Dam/dam.boid) and all physical parameters from
+the reference example ``results/Dam/dam.data`` (values below), with the documented changes.
+There is no RNG anywhere in the reference, so the cases are fully deterministic.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+from . import mphio
+from .mphio import Cuboid
+
+# results/Dam/dam.data (the reference's only example parameter file), as key -> values.
+DAM_DATA = {
+    "Dt": [1.0e-4],
+    "ElasticDt": [1.0e-4],
+    "OutputInterval": [1.0],
+    "VtkOutputInterval": [1.0e-2],
+    "EndTime": [1.0],
+    "RadiusRatioA": [2.5],
+    "RadiusRatioP": [2.5],
+    "RadiusRatioV": [2.5],
+    "Density": [1.0e+3, 1.0e+3, 1.1e+3, 1.0e+3, 1.0e+3, 6.0e+3],
+    "BulkModulus": [1.0e+4, 1.0e+4, 1.0e+4, 1.0e+6, 1.0e+4, 1.0e+5],
+    "BulkViscosity": [1.0e+1, 1.0e-1, 1.0e-1, 1.0e+3, 1.0e-1, 1.0e+2],
+    "ShearViscosity": [1.0e-2, 1.0e-3, 1.0e-2, 1.0e-1, 1.0e+3, 1.0e-1],
+    "SurfaceTension": [0.0, 0.0, 0.0, 0.0],
+    "YoungModulus": [1e5, 1e+5, 1e+8, 1e+4],
+    "PoissonRatio": [0.2, 0.4, 0.3, 0.3],
+    "Gravity": [0.0, -1.0, 0.0],
+}
+for _t in range(6):
+    DAM_DATA["InteractionRatio(Type%d)" % _t] = [1.0] * 6
+
+
+def data_text(values: dict) -> str:
+    """A .data file in the reference's keyword format (main.cpp:743-767)."""
+    lines = ["#######"]
+    for k, v in values.items():
+        lines.append("%s\t%s" % (k, "\t".join(repr(float(x)) for x in v)))
+    return "\n".join(lines) + "\n"
+
+
+@dataclass
+class Case:
+    name: str
+    dim: int
+    module: str
+    spacing: float
+    lower: tuple
+    upper: tuple
+    cuboids: list
+    data_changes: dict = field(default_factory=dict)
+    note: str = ""
+
+    def data(self) -> dict:
+        d = dict(DAM_DATA)
+        d.update(self.data_changes)
+        return d
+
+    def build(self):
+        """-> (MphConfig, Particles), exactly what the reference reads from data + grid files."""
+        cfg = mphio.config_default(self.dim, self.module)
+        _apply_data(cfg, self.data())
+        parts = mphio.generate(self.cuboids)
+        cfg.time = 0.0
+        cfg.particle_spacing = mphio._e(self.spacing)
+        for d in range(3):
+            cfg.domain_min[d] = mphio._e(self.lower[d])
+            cfg.domain_max[d] = mphio._e(self.upper[d])
+        return cfg, parts
+
+    def grid_text(self) -> str:
+        return mphio.format_grid(mphio.generate(self.cuboids), self.spacing, self.lower, self.upper)
+
+
+def _apply_data(cfg, values):
+    import tempfile, os
+    with tempfile.NamedTemporaryFile("w", suffix=".data", delete=False) as fh:
+        fh.write(data_text(values))
+        path = fh.name
+    try:
+        mphio.read_data_file(path, cfg)
+    finally:
+        os.unlink(path)
+
+
+CASES: dict[str, Case] = {}
+
+
+def _reg(c: Case):
+    CASES[c.name] = c
+    return c
+
+
+# results/Dam (as-shipped 2-D Bar_Module binary; no structure particles) -- 6,650 particles
+_reg(Case("dam2d", 2, "bar", 0.001, (-0.01, 0.0, 0.0), (0.21, 0.40, 0.001), [
+    Cuboid(1, (0.0, 0.003, 0.0), (0.05, 0.10, 0.001), 0.001),
+    Cuboid(4, (0.0, 0.0, 0.0), (0.2, 0.003, 0.001), 0.001),
+    Cuboid(4, (0.2, 0.0, 0.0), (0.203, 0.20, 0.001), 0.001),
+    Cuboid(4, (-0.003, 0.0, 0.0), (0.0, 0.20, 0.001), 0.001),
+], note="results/Dam/dam.boid"))
+
+# 3-D dam break, 1,397,200 particles (970,000 fluid / 427,200 wall)
+_reg(Case("d1m", 3, "dam", 0.001, (-0.01, 0.0, -0.01), (0.21, 0.40, 0.11), [
+    Cuboid(1, (0.0, 0.003, 0.0), (0.1, 0.1, 0.1), 0.001),
+    Cuboid(4, (0.0, 0.0, 0.0), (0.2, 0.003, 0.1), 0.001),
+    Cuboid(4, (0.2, 0.0, 0.0), (0.203, 0.2, 0.1), 0.001),
+    Cuboid(4, (-0.003, 0.0, 0.0), (0.0, 0.2, 0.1), 0.001),
+    Cuboid(4, (-0.003, 0.0, -0.003), (0.203, 0.2, 0.0), 0.001),
+    Cuboid(4, (-0.003, 0.0, 0.1), (0.203, 0.2, 0.103), 0.001),
+]))
+
+# 3-D dam break, dx 4e-4, 16,205,500 particles, Dt = ElasticDt = 4e-5
+_reg(Case("d16m", 3, "dam", 0.0004, (-0.004, 0.0, -0.004), (0.208, 0.40, 0.108), [
+    Cuboid(1, (0.0, 0.0012, 0.0), (0.1, 0.088, 0.1), 0.0004),
+    Cuboid(4, (0.0, 0.0, 0.0), (0.2, 0.0012, 0.1), 0.0004),
+    Cuboid(4, (0.2, 0.0, 0.0), (0.2012, 0.2, 0.1), 0.0004),
+    Cuboid(4, (-0.0012, 0.0, 0.0), (0.0, 0.2, 0.1), 0.0004),
+    Cuboid(4, (-0.0012, 0.0, -0.0012), (0.2012, 0.2, 0.0), 0.0004),
+    Cuboid(4, (-0.0012, 0.0, 0.1), (0.2012, 0.2, 0.1012), 0.0004),
+], data_changes={"Dt": [4e-5], "ElasticDt": [4e-5]}))
+
+# SURVEY 8d FSI: 3-D dam break onto an elastic gate, DAM_Module, 2,259,700 particles
+_reg(Case("fsi3d", 3, "dam", 0.001, (-0.01, 0.0, -0.01), (0.31, 0.40, 0.11), [
+    Cuboid(1, (0.0, 0.003, 0.0), (0.12, 0.14, 0.1), 0.001),
+    Cuboid(2, (0.2, 0.0, 0.0), (0.205, 0.08, 0.1), 0.001),
+    Cuboid(4, (0.0, 0.0, 0.0), (0.2, 0.003, 0.1), 0.001),
+    Cuboid(4, (0.205, 0.0, 0.0), (0.3, 0.003, 0.1), 0.001),
+    Cuboid(4, (0.3, 0.0, 0.0), (0.303, 0.2, 0.1), 0.001),
+    Cuboid(4, (-0.003, 0.0, 0.0), (0.0, 0.2, 0.1), 0.001),
+    Cuboid(4, (-0.003, 0.0, -0.003), (0.303, 0.2, 0.0), 0.001),
+    Cuboid(4, (-0.003, 0.0, 0.1), (0.303, 0.2, 0.103), 0.001),
+]))
+
+# SURVEY 8d Bar (parity size): 2-D cantilever, Bar_Module, 4,000 structure particles
+_reg(Case("bar2d", 2, "bar", 0.001, (-0.01, -0.1, 0.0), (0.25, 0.1, 0.001), [
+    Cuboid(2, (0.0, -0.01, 0.0), (0.2, 0.01, 0.001), 0.001),
+]))
+
+# SURVEY 8d Bar (perf size): dx 1e-4, 400,000 structure particles, Dt = ElasticDt = 1e-5
+_reg(Case("bar2d_400k", 2, "bar", 0.0001, (-0.001, -0.05, 0.0), (0.25, 0.05, 0.0001), [
+    Cuboid(2, (0.0, -0.01, 0.0), (0.2, 0.01, 0.0001), 0.0001),
+], data_changes={"Dt": [1e-5], "ElasticDt": [1e-5]}))
+
+# 2-D dam break onto an elastic gate (DAM_Module), 7,035 particles = 4,850 + 400 + 1,785
+_reg(Case("gate2d", 2, "dam", 0.001, (-0.01, 0.0, 0.0), (0.21, 0.40, 0.001), [
+    Cuboid(1, (0.0, 0.003, 0.0), (0.05, 0.10, 0.001), 0.001),
+    Cuboid(2, (0.1, 0.0, 0.0), (0.105, 0.08, 0.001), 0.001),
+    Cuboid(4, (0.0, 0.0, 0.0), (0.1, 0.003, 0.001), 0.001),
+    Cuboid(4, (0.105, 0.0, 0.0), (0.2, 0.003, 0.001), 0.001),
+    Cuboid(4, (0.2, 0.0, 0.0), (0.203, 0.20, 0.001), 0.001),
+    Cuboid(4, (-0.003, 0.0, 0.0), (0.0, 0.20, 0.001), 0.001),
+]))
+
+# small 3-D dam break in a closed tank (parity size for the 3-D code path)
+_reg(Case("box3d", 3, "dam", 0.001, (-0.01, 0.0, -0.01), (0.04, 0.05, 0.025), [
+    Cuboid(1, (0.0, 0.003, 0.0), (0.012, 0.02, 0.012), 0.001),
+    Cuboid(4, (0.0, 0.0, 0.0), (0.025, 0.003, 0.012), 0.001),
+    Cuboid(4, (0.025, 0.0, 0.0), (0.028, 0.025, 0.012), 0.001),
+    Cuboid(4, (-0.003, 0.0, 0.0), (0.0, 0.025, 0.012), 0.001),
+    Cuboid(4, (-0.003, 0.0, -0.003), (0.028, 0.025, 0.0), 0.001),
+    Cuboid(4, (-0.003, 0.0, 0.012), (0.028, 0.025, 0.015), 0.001),
+]))
+
+# small 3-D dam break onto an elastic gate (DAM_Module): 3-D structure + FSI coupling path
+_reg(Case("gate3d", 3, "dam", 0.001, (-0.01, 0.0, -0.01), (0.05, 0.05, 0.018), [
+    Cuboid(1, (0.0, 0.003, 0.0), (0.012, 0.02, 0.008), 0.001),
+    Cuboid(2, (0.022, 0.0, 0.0), (0.025, 0.015, 0.008), 0.001),
+    Cuboid(4, (0.0, 0.0, 0.0), (0.022, 0.003, 0.008), 0.001),
+    Cuboid(4, (0.025, 0.0, 0.0), (0.035, 0.003, 0.008), 0.001),
+    Cuboid(4, (0.035, 0.0, 0.0), (0.038, 0.025, 0.008), 0.001),
+    Cuboid(4, (-0.003, 0.0, 0.0), (0.0, 0.025, 0.008), 0.001),
+    Cuboid(4, (-0.003, 0.0, -0.003), (0.038, 0.025, 0.0), 0.001),
+    Cuboid(4, (-0.003, 0.0, 0.008), (0.038, 0.025, 0.011), 0.001),
+]))
+
+
+def get(name: str) -> Case:
+    return CASES[name]

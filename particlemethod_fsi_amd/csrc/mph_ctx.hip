@@ -1,0 +1,570 @@
+// mph_ctx.hip -- the C ABI of include/mph_gpu.h: device context, uploads, graph-replayed steps,
+// field download in the reference's AoS layout and original particle order.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "mph_internal.h"
+#include "mph_kernels.h"
+
+using namespace mph;
+
+struct MphCtx {
+    int device = 0;
+    int n = 0;
+    MphConfig cfg{};
+    HostDerived h{};
+    DevParams P{};
+    DevTables T{};
+    std::string err;
+    double time = 0.0;           // host mirror of Time (same additions as the device)
+    bool stepped = false;
+    hipStream_t stream = nullptr;
+    hipGraphExec_t graph1 = nullptr, graph8 = nullptr;
+    // host copies (original order)
+    std::vector<int> prop;
+    std::vector<double> pos0;
+    StructureInit S;
+    // device
+    DevTables* dT = nullptr;
+    DevState* dst = nullptr;
+    double4 *xa = nullptr, *va = nullptr, *xb = nullptr, *vb = nullptr;
+    int *ida = nullptr, *idb = nullptr, *rank_of = nullptr;
+    int *key = nullptr, *slot = nullptr, *tmp = nullptr, *cnt = nullptr, *start = nullptr, *bsum = nullptr;
+    int *nbr = nullptr, *ncount = nullptr;
+    double4 *pv = nullptr, *gca = nullptr, *force = nullptr, *acc = nullptr;
+    double *dens_a = nullptr, *vstrain = nullptr, *divp = nullptr;
+    StructDev Sd;
+    std::vector<void*> allocs;
+    Launch L;
+};
+
+namespace {
+
+int fail(MphCtx* c, int code, const std::string& msg)
+{
+    if (c) c->err = msg;
+    return code;
+}
+
+#define HIP_OK(ctx, expr)                                                                       \
+    do {                                                                                        \
+        hipError_t _e = (expr);                                                                 \
+        if (_e != hipSuccess)                                                                   \
+            return fail(ctx, _e == hipErrorOutOfMemory ? MPH_ERR_DEVICE_OOM : MPH_ERR_HIP,      \
+                        std::string(#expr) + ": " + hipGetErrorString(_e));                     \
+    } while (0)
+
+template <typename T>
+int dalloc(MphCtx* c, T** p, size_t count)
+{
+    *p = nullptr;
+    if (count == 0) count = 1;
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, count * sizeof(T));
+    if (e != hipSuccess)
+        return fail(c, e == hipErrorOutOfMemory ? MPH_ERR_DEVICE_OOM : MPH_ERR_HIP,
+                    "hipMalloc(" + std::to_string(count * sizeof(T)) + " B): " + hipGetErrorString(e));
+    c->allocs.push_back(q);
+    *p = (T*)q;
+    return MPH_OK;
+}
+
+#define CK(expr)                       \
+    do {                               \
+        int _r = (expr);               \
+        if (_r != MPH_OK) return _r;   \
+    } while (0)
+
+void fill_launch(MphCtx* c)
+{
+    Launch& L = c->L;
+    L.P = &c->P;
+    L.T = c->dT;
+    L.st = c->dst;
+    L.stream = c->stream;
+    L.prof = nullptr;
+    L.xa = c->xa; L.va = c->va; L.xb = c->xb; L.vb = c->vb;
+    L.ida = c->ida; L.idb = c->idb; L.rank_of = c->rank_of;
+    L.key = c->key; L.slot = c->slot; L.tmp = c->tmp; L.cnt = c->cnt; L.start = c->start; L.bsum = c->bsum;
+    L.nbr = c->nbr; L.ncount = c->ncount;
+    L.pv = c->pv; L.gca = c->gca; L.force = c->force; L.acc = c->acc;
+    L.dens_a = c->dens_a; L.vstrain = c->vstrain; L.divp = c->divp;
+    L.S = &c->Sd;
+}
+
+void enqueue_step(const Launch& L)
+{
+    launch_sort(L, 1);
+    launch_neighbors(L);
+    launch_pass_a(L);
+    launch_pass_b(L);
+    launch_structure(L);
+}
+
+int capture(MphCtx* c, int steps, hipGraphExec_t* out)
+{
+    hipGraph_t g = nullptr;
+    HIP_OK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    for (int k = 0; k < steps; ++k) enqueue_step(c->L);
+    HIP_OK(c, hipStreamEndCapture(c->stream, &g));
+    HIP_OK(c, hipGraphInstantiate(out, g, nullptr, nullptr, 0));
+    HIP_OK(c, hipGraphDestroy(g));
+    return MPH_OK;
+}
+
+// Device sorted arrays -> host original order via the id arrays.
+int download_vec(MphCtx* c, const double4* d, const int* ids, double* out, int width)
+{
+    const int n = c->n;
+    std::vector<double4> h(n);
+    std::vector<int> id(n);
+    HIP_OK(c, hipMemcpyAsync(h.data(), d, sizeof(double4) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipMemcpyAsync(id.data(), ids, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < n; ++i) {
+        double* o = out + (size_t)width * id[i];
+        o[0] = h[i].x;
+        if (width > 1) { o[1] = h[i].y; o[2] = h[i].z; }
+    }
+    return MPH_OK;
+}
+
+template <typename T>
+int download_scalar(MphCtx* c, const T* d, const int* ids, T* out)
+{
+    const int n = c->n;
+    std::vector<T> h(n);
+    std::vector<int> id(n);
+    HIP_OK(c, hipMemcpyAsync(h.data(), d, sizeof(T) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipMemcpyAsync(id.data(), ids, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < n; ++i) out[id[i]] = h[i];
+    return MPH_OK;
+}
+
+int download_w(MphCtx* c, const double4* d, const int* ids, double* out)
+{
+    const int n = c->n;
+    std::vector<double4> h(n);
+    std::vector<int> id(n);
+    HIP_OK(c, hipMemcpyAsync(h.data(), d, sizeof(double4) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipMemcpyAsync(id.data(), ids, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < n; ++i) out[id[i]] = h[i].w;
+    return MPH_OK;
+}
+
+int download_struct_m33(MphCtx* c, const double* d, double* out)
+{
+    const int ns = (int)c->S.orig.size();
+    std::memset(out, 0, sizeof(double) * 9 * (size_t)c->n);
+    if (ns == 0) return MPH_OK;
+    std::vector<double> h((size_t)ns * 9);
+    HIP_OK(c, hipMemcpyAsync(h.data(), d, sizeof(double) * 9 * ns, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    for (int s = 0; s < ns; ++s) std::memcpy(out + (size_t)9 * c->S.orig[s], &h[(size_t)9 * s], sizeof(double) * 9);
+    return MPH_OK;
+}
+
+struct EventProfiler final : Profiler {
+    struct Rec { std::string name; hipEvent_t a, b; };
+    std::vector<Rec> recs;
+    int begin(const char* name, hipStream_t s) override
+    {
+        Rec r{name, nullptr, nullptr};
+        (void)hipEventCreate(&r.a);
+        (void)hipEventCreate(&r.b);
+        (void)hipEventRecord(r.a, s);
+        recs.push_back(r);
+        return (int)recs.size() - 1;
+    }
+    void end(int slot, hipStream_t s) override { (void)hipEventRecord(recs[slot].b, s); }
+    ~EventProfiler() override
+    {
+        for (auto& r : recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int mph_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, const double* pos,
+               const double* pos0, const double* vel, int device)
+{
+    if (!out || !cfg || n < 0 || (n > 0 && (!property || !pos || !pos0 || !vel))) return MPH_ERR_ARG;
+    *out = nullptr;
+    std::unique_ptr<MphCtx> up(new MphCtx());
+    MphCtx* c = up.get();
+    if (cfg->dim != 2 && cfg->dim != 3) return MPH_ERR_ARG;
+    if (cfg->module < 0 || cfg->module > MPH_MODULE_NONE) return MPH_ERR_ARG;
+    if (!(cfg->particle_spacing > 0.0) || !(cfg->dt > 0.0) || !(cfg->elastic_dt > 0.0)) return MPH_ERR_ARG;
+    for (int i = 0; i < n; ++i)
+        if (property[i] < 0 || property[i] >= kTypes) return MPH_ERR_ARG;
+    c->cfg = *cfg;
+    c->n = n;
+    c->device = device;
+    c->time = cfg->time;
+    HIP_OK(nullptr, hipSetDevice(device));
+    HIP_OK(nullptr, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    derive_constants(c->cfg, c->h);
+    c->prop.assign(property, property + n);
+    c->pos0.assign(pos0, pos0 + 3 * (size_t)n);
+    std::string err;
+    CK(fail(c, build_structure(c->cfg, c->h, n, property, pos0, c->S, err), err));
+    const int ns = (int)c->S.orig.size();
+    make_dev_params(c->cfg, c->h, n, ns, c->P);
+    const double rc = std::sqrt(c->P.rc2);
+    {
+        int r = choose_grid(c->h, cfg->dim, rc, c->P.gc, c->P.ginv, err);
+        if (r != MPH_OK) return fail(c, r, err);
+    }
+    c->P.ncell = c->P.gc[0] * c->P.gc[1] * c->P.gc[2];
+    // tables
+    for (int t = 0; t < kTypes; ++t) {
+        for (int u = 0; u < kTypes; ++u) {
+            c->T.ratio[t * kTypes + u] = c->P.ratio[t][u];
+            c->T.mu_ij[t * kTypes + u] = c->P.mu_ij[t][u];
+        }
+        c->T.cofa[t] = c->P.cofa[t];
+        c->T.mass[t] = c->P.mass[t];
+        c->T.inv_mass[t] = c->P.inv_mass[t];
+        c->T.bulk[t] = c->P.bulk[t];
+        c->T.bulk_visc[t] = c->P.bulk_visc[t];
+    }
+    // device allocations
+    const size_t ntile = ((size_t)n + kTile - 1) / kTile;
+    CK(dalloc(c, &c->dT, 1));
+    CK(dalloc(c, &c->dst, 1));
+    CK(dalloc(c, &c->xa, n)); CK(dalloc(c, &c->va, n)); CK(dalloc(c, &c->xb, n)); CK(dalloc(c, &c->vb, n));
+    CK(dalloc(c, &c->ida, n)); CK(dalloc(c, &c->idb, n)); CK(dalloc(c, &c->rank_of, n));
+    CK(dalloc(c, &c->key, n)); CK(dalloc(c, &c->slot, n)); CK(dalloc(c, &c->tmp, n));
+    CK(dalloc(c, &c->cnt, c->P.ncell)); CK(dalloc(c, &c->start, (size_t)c->P.ncell + 1));
+    CK(dalloc(c, &c->bsum, (size_t)c->P.ncell / 4096 + 2));
+    CK(dalloc(c, &c->nbr, ntile * kTile * kMaxNeighbor)); CK(dalloc(c, &c->ncount, n));
+    CK(dalloc(c, &c->pv, n)); CK(dalloc(c, &c->gca, n)); CK(dalloc(c, &c->force, n)); CK(dalloc(c, &c->acc, n));
+    CK(dalloc(c, &c->dens_a, n)); CK(dalloc(c, &c->vstrain, n)); CK(dalloc(c, &c->divp, n));
+    HIP_OK(c, hipMemsetAsync(c->cnt, 0, sizeof(int) * c->P.ncell, c->stream));
+    HIP_OK(c, hipMemsetAsync(c->force, 0, sizeof(double4) * std::max(n, 1), c->stream));
+    HIP_OK(c, hipMemsetAsync(c->acc, 0, sizeof(double4) * std::max(n, 1), c->stream));
+    HIP_OK(c, hipMemcpyAsync(c->dT, &c->T, sizeof(DevTables), hipMemcpyHostToDevice, c->stream));
+    DevState st{};
+    st.time = cfg->time;
+    for (int t = 0; t < kTypes; ++t)
+        for (int d = 0; d < 3; ++d) {
+            st.wall_c[t][d] = cfg->wall_center[t][d];
+            st.wall_vel[t][d] = cfg->wall_velocity[t][d];
+            st.wall_omega[t][d] = cfg->wall_omega[t][d];
+            for (int e = 0; e < 3; ++e) st.wall_rot[t][d][e] = c->h.wall_rot[t][d][e];
+        }
+    HIP_OK(c, hipMemcpyAsync(c->dst, &st, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
+    {
+        std::vector<double4> hx(n), hv(n);
+        std::vector<int> id(n);
+        for (int i = 0; i < n; ++i) {
+            hx[i] = make_double4(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2], (double)property[i]);
+            hv[i] = make_double4(vel[3 * i], vel[3 * i + 1], vel[3 * i + 2], 0.0);
+            id[i] = i;
+        }
+        HIP_OK(c, hipMemcpyAsync(c->xb, hx.data(), sizeof(double4) * n, hipMemcpyHostToDevice, c->stream));
+        HIP_OK(c, hipMemcpyAsync(c->vb, hv.data(), sizeof(double4) * n, hipMemcpyHostToDevice, c->stream));
+        HIP_OK(c, hipMemcpyAsync(c->idb, id.data(), sizeof(int) * n, hipMemcpyHostToDevice, c->stream));
+        HIP_OK(c, hipStreamSynchronize(c->stream));
+    }
+    // elastic solid
+    if (ns > 0) {
+        StructDev& D = c->Sd;
+        const StructureInit& S = c->S;
+        const size_t np = S.nbr.size(), npi = S.in_nbr.size();
+        CK(dalloc(c, &D.orig, ns)); CK(dalloc(c, &D.off, ns + 1)); CK(dalloc(c, &D.nb, np));
+        CK(dalloc(c, &D.in_off, ns + 1)); CK(dalloc(c, &D.in_nb, npi));
+        CK(dalloc(c, &D.pair_out, np)); CK(dalloc(c, &D.pair_in, npi));
+        CK(dalloc(c, &D.L, (size_t)ns * 9)); CK(dalloc(c, &D.lame, ns)); CK(dalloc(c, &D.inv_rho, ns));
+        CK(dalloc(c, &D.clamp, ns)); CK(dalloc(c, &D.x0, ns)); CK(dalloc(c, &D.x, ns)); CK(dalloc(c, &D.v, ns));
+        CK(dalloc(c, &D.P, (size_t)ns * 9)); CK(dalloc(c, &D.F, (size_t)ns * 9));
+        CK(dalloc(c, &D.E, (size_t)ns * 9)); CK(dalloc(c, &D.S, (size_t)ns * 9));
+        std::vector<double2> lame(ns);
+        std::vector<double> irho(ns);
+        std::vector<int> clamp(ns);
+        std::vector<double4> x0(ns);
+        for (int s = 0; s < ns; ++s) {
+            const int i = S.orig[s];
+            const int t = property[i];
+            lame[s] = make_double2(S.lame_l[s], S.lame_m[s]);
+            irho[s] = 1.0 / cfg->density[t];
+            const double* p0 = pos0 + 3 * i;
+            int cl = 0;   // updateElasticPosition module clamps (main.cpp:1918-2044)
+            switch (cfg->module) {
+            case MPH_MODULE_BAR: cl = p0[0] < 0.001 ? 1 : 0; break;
+            case MPH_MODULE_DAM: cl = p0[1] < 0.002 ? 1 : 0; break;
+            case MPH_MODULE_TUREK_HRON: cl = p0[0] < 0.205 ? 2 : 0; break;
+            case MPH_MODULE_ROLLING1: cl = p0[1] < 0.003 ? 1 : 0; break;
+            case MPH_MODULE_HYDROELASTIC: cl = (p0[0] < 0.01 || p0[0] > 1.99) ? 1 : 0; break;
+            default: cl = 0;
+            }
+            clamp[s] = cl;
+            x0[s] = make_double4(p0[0], p0[1], p0[2], (double)t);
+        }
+        auto up4 = [&](double4* d, const std::vector<double>& v) {
+            return hipMemcpyAsync(d, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice, c->stream);
+        };
+        HIP_OK(c, hipMemcpyAsync(D.orig, S.orig.data(), sizeof(int) * ns, hipMemcpyHostToDevice, c->stream));
+        HIP_OK(c, hipMemcpyAsync(D.off, S.offset.data(), sizeof(int) * (ns + 1), hipMemcpyHostToDevice, c->stream));
+        HIP_OK(c, hipMemcpyAsync(D.in_off, S.in_offset.data(), sizeof(int) * (ns + 1), hipMemcpyHostToDevice, c->stream));
+        if (np) {
+            HIP_OK(c, hipMemcpyAsync(D.nb, S.nbr.data(), sizeof(int) * np, hipMemcpyHostToDevice, c->stream));
+            HIP_OK(c, up4(D.pair_out, S.pair_out));
+        }
+        if (npi) {
+            HIP_OK(c, hipMemcpyAsync(D.in_nb, S.in_nbr.data(), sizeof(int) * npi, hipMemcpyHostToDevice, c->stream));
+            HIP_OK(c, up4(D.pair_in, S.pair_in));
+        }
+        HIP_OK(c, hipMemcpyAsync(D.L, S.normalizer.data(), sizeof(double) * 9 * ns, hipMemcpyHostToDevice, c->stream));
+        HIP_OK(c, hipMemcpyAsync(D.lame, lame.data(), sizeof(double2) * ns, hipMemcpyHostToDevice, c->stream));
+        HIP_OK(c, hipMemcpyAsync(D.inv_rho, irho.data(), sizeof(double) * ns, hipMemcpyHostToDevice, c->stream));
+        HIP_OK(c, hipMemcpyAsync(D.clamp, clamp.data(), sizeof(int) * ns, hipMemcpyHostToDevice, c->stream));
+        HIP_OK(c, hipMemcpyAsync(D.x0, x0.data(), sizeof(double4) * ns, hipMemcpyHostToDevice, c->stream));
+        for (double* m : {D.P, D.F, D.E, D.S})
+            HIP_OK(c, hipMemsetAsync(m, 0, sizeof(double) * 9 * ns, c->stream));
+        HIP_OK(c, hipStreamSynchronize(c->stream));
+    }
+    fill_launch(c);
+    // initialisation sums, main.cpp:565-568 (calculateNeighbor, DensityA, GravityCenter, DensityP)
+    launch_sort(c->L, 0);
+    launch_neighbors(c->L);
+    launch_pass_a(c->L);
+    HIP_OK(c, hipGetLastError());
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    {
+        DevState hs;
+        HIP_OK(c, hipMemcpy(&hs, c->dst, sizeof(DevState), hipMemcpyDeviceToHost));
+        if (hs.overflow) return fail(c, MPH_ERR_NEIGHBOR_OVERFLOW, "a particle has more than 512 neighbours");
+    }
+    *out = up.release();
+    return MPH_OK;
+}
+
+int mph_step(MphCtx* c, int nsteps)
+{
+    if (!c || nsteps < 0) return MPH_ERR_ARG;
+    HIP_OK(c, hipSetDevice(c->device));
+    if (nsteps == 0 || c->n == 0) {
+        for (int k = 0; k < nsteps; ++k) c->time += c->cfg.dt;
+        return MPH_OK;
+    }
+    if (!c->graph1) CK(capture(c, 1, &c->graph1));
+    if (!c->graph8 && nsteps >= 8) CK(capture(c, 8, &c->graph8));
+    int left = nsteps;
+    while (left >= 8) { HIP_OK(c, hipGraphLaunch(c->graph8, c->stream)); left -= 8; }
+    while (left > 0) { HIP_OK(c, hipGraphLaunch(c->graph1, c->stream)); left -= 1; }
+    for (int k = 0; k < nsteps; ++k) c->time += c->cfg.dt;
+    c->stepped = true;
+    DevState hs;
+    HIP_OK(c, hipMemcpyAsync(&hs, c->dst, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    if (hs.overflow) return fail(c, MPH_ERR_NEIGHBOR_OVERFLOW, "a particle has more than 512 neighbours");
+    return MPH_OK;
+}
+
+int mph_synchronize(MphCtx* c)
+{
+    if (!c) return MPH_ERR_ARG;
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    return MPH_OK;
+}
+
+int mph_particle_count(const MphCtx* c) { return c ? c->n : -1; }
+double mph_time(const MphCtx* c) { return c ? c->time : 0.0; }
+const char* mph_last_error(const MphCtx* c) { return c ? c->err.c_str() : "null context"; }
+
+int mph_get_scalars(const MphCtx* c, double* out)
+{
+    if (!c || !out) return MPH_ERR_ARG;
+    fill_scalars(c->h, c->cfg, out);
+    return MPH_OK;
+}
+
+int mph_get(MphCtx* c, int field, void* out)
+{
+    if (!c || !out) return MPH_ERR_ARG;
+    HIP_OK(c, hipSetDevice(c->device));
+    const int n = c->n;
+    double* o = (double*)out;
+    int* oi = (int*)out;
+    const int ns = (int)c->S.orig.size();
+    switch (field) {
+    case MPH_FIELD_POSITION: return download_vec(c, c->xb, c->idb, o, 3);
+    case MPH_FIELD_VELOCITY: return download_vec(c, c->vb, c->idb, o, 3);
+    case MPH_FIELD_INITIAL_POSITION: std::memcpy(o, c->pos0.data(), sizeof(double) * 3 * n); return MPH_OK;
+    case MPH_FIELD_FORCE: return download_vec(c, c->force, c->ida, o, 3);
+    case MPH_FIELD_ACCELERATION: return download_vec(c, c->acc, c->ida, o, 3);
+    case MPH_FIELD_GRAVITY_CENTER: return download_vec(c, c->gca, c->ida, o, 3);
+    case MPH_FIELD_PRESSURE_P: return download_w(c, c->pv, c->ida, o);
+    case MPH_FIELD_PRESSURE_A: return download_w(c, c->gca, c->ida, o);
+    case MPH_FIELD_DENSITY_A: return download_scalar(c, c->dens_a, c->ida, o);
+    case MPH_FIELD_VOL_STRAIN_P: return download_scalar(c, c->vstrain, c->ida, o);
+    case MPH_FIELD_DIVERGENCE_P: return download_scalar(c, c->divp, c->ida, o);
+    case MPH_FIELD_NEIGHBOR_COUNT: return download_scalar(c, c->ncount, c->ida, oi);
+    case MPH_FIELD_MASS:
+        for (int i = 0; i < n; ++i) o[i] = c->cfg.density[c->prop[i]] * c->h.vol;
+        return MPH_OK;
+    case MPH_FIELD_KAPPA: {
+        // initializeFluid (1317-1319) before the first step, calculatePhysicalCoefficients after
+        std::vector<double> vs(n);
+        if (c->stepped) CK(download_scalar(c, c->vstrain, c->ida, vs.data()));
+        for (int i = 0; i < n; ++i)
+            o[i] = (c->stepped && vs[i] < 0.0) ? 0.0 : c->cfg.bulk_modulus[c->prop[i]];
+        return MPH_OK;
+    }
+    case MPH_FIELD_LAMBDA:
+        for (int i = 0; i < n; ++i) o[i] = c->cfg.bulk_viscosity[c->prop[i]];
+        return MPH_OK;
+    case MPH_FIELD_MU:
+        for (int i = 0; i < n; ++i) o[i] = c->cfg.shear_viscosity[c->prop[i]];
+        return MPH_OK;
+    case MPH_FIELD_PROPERTY: std::memcpy(oi, c->prop.data(), sizeof(int) * n); return MPH_OK;
+    case MPH_FIELD_INITIAL_STRUCTURE_NEIGHBOR_COUNT:
+        std::memset(oi, 0, sizeof(int) * n);
+        for (int s = 0; s < ns; ++s) oi[c->S.orig[s]] = c->S.count[s];
+        return MPH_OK;
+    case MPH_FIELD_DEFORM_GRADIENT: return download_struct_m33(c, c->Sd.F, o);
+    case MPH_FIELD_STRAIN: return download_struct_m33(c, c->Sd.E, o);
+    case MPH_FIELD_STRESS: return download_struct_m33(c, c->Sd.S, o);
+    case MPH_FIELD_NORMALIZER:
+        std::memset(o, 0, sizeof(double) * 9 * (size_t)n);
+        for (int s = 0; s < ns; ++s)
+            std::memcpy(o + (size_t)9 * c->S.orig[s], &c->S.normalizer[(size_t)9 * s], sizeof(double) * 9);
+        return MPH_OK;
+    case MPH_FIELD_LAMBDA_LAMES:
+    case MPH_FIELD_MU_LAMES:
+        std::memset(o, 0, sizeof(double) * n);
+        for (int s = 0; s < ns; ++s)
+            o[c->S.orig[s]] = field == MPH_FIELD_LAMBDA_LAMES ? c->S.lame_l[s] : c->S.lame_m[s];
+        return MPH_OK;
+    default: return fail(c, MPH_ERR_ARG, "unknown field " + std::to_string(field));
+    }
+}
+
+int mph_set(MphCtx* c, int field, const void* in)
+{
+    if (!c || !in) return MPH_ERR_ARG;
+    if (field != MPH_FIELD_POSITION && field != MPH_FIELD_VELOCITY)
+        return fail(c, MPH_ERR_ARG, "mph_set supports Position and Velocity");
+    HIP_OK(c, hipSetDevice(c->device));
+    const int n = c->n;
+    const double* v = (const double*)in;
+    // current state lives in the B set in the order of idb: rewrite it in that order
+    std::vector<double4> h(n);
+    std::vector<int> id(n);
+    double4* dst = field == MPH_FIELD_POSITION ? c->xb : c->vb;
+    HIP_OK(c, hipMemcpyAsync(h.data(), dst, sizeof(double4) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipMemcpyAsync(id.data(), c->idb, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < n; ++i) {
+        const double* s = v + 3 * (size_t)id[i];
+        h[i].x = s[0]; h[i].y = s[1]; h[i].z = s[2];
+    }
+    HIP_OK(c, hipMemcpyAsync(dst, h.data(), sizeof(double4) * n, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    return MPH_OK;
+}
+
+int mph_write_prof(MphCtx* c, const char* path)
+{
+    if (!c || !path) return MPH_ERR_ARG;
+    const int n = c->n;
+    std::vector<double> pos(3 * (size_t)n), vel(3 * (size_t)n);
+    CK(mph_get(c, MPH_FIELD_POSITION, pos.data()));
+    CK(mph_get(c, MPH_FIELD_VELOCITY, vel.data()));
+    return mph_write_prof_arrays(path, &c->cfg, c->time, n, c->prop.data(), pos.data(), c->pos0.data(),
+                                 vel.data());
+}
+
+int mph_write_vtk(MphCtx* c, const char* path)
+{
+    if (!c || !path) return MPH_ERR_ARG;
+    const size_t n = (size_t)c->n;
+    std::vector<double> pos(3 * n), vel(3 * n), acc(3 * n), force(3 * n), stress(9 * n), strain(9 * n);
+    std::vector<int> isnc(n), nc(n);
+    CK(mph_get(c, MPH_FIELD_POSITION, pos.data()));
+    CK(mph_get(c, MPH_FIELD_VELOCITY, vel.data()));
+    CK(mph_get(c, MPH_FIELD_ACCELERATION, acc.data()));
+    CK(mph_get(c, MPH_FIELD_FORCE, force.data()));
+    CK(mph_get(c, MPH_FIELD_STRESS, stress.data()));
+    CK(mph_get(c, MPH_FIELD_STRAIN, strain.data()));
+    CK(mph_get(c, MPH_FIELD_INITIAL_STRUCTURE_NEIGHBOR_COUNT, isnc.data()));
+    CK(mph_get(c, MPH_FIELD_NEIGHBOR_COUNT, nc.data()));
+    return mph_write_vtk_arrays(path, c->n, c->prop.data(), pos.data(), c->pos0.data(), vel.data(),
+                                acc.data(), force.data(), stress.data(), strain.data(), isnc.data(), nc.data());
+}
+
+int mph_profile_steps(MphCtx* c, int nsteps, double* avg_ms, int* launches, char* names32)
+{
+    if (!c || nsteps <= 0 || !avg_ms || !launches || !names32) return MPH_ERR_ARG;
+    HIP_OK(c, hipSetDevice(c->device));
+    EventProfiler prof;
+    Launch L = c->L;
+    L.prof = &prof;
+    for (int k = 0; k < nsteps; ++k) enqueue_step(L);
+    HIP_OK(c, hipGetLastError());
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    for (int k = 0; k < nsteps; ++k) c->time += c->cfg.dt;
+    c->stepped = true;
+    std::vector<std::string> order;
+    std::map<std::string, std::pair<double, int>> acc;
+    for (auto& r : prof.recs) {
+        float ms = 0.0f;
+        HIP_OK(c, hipEventElapsedTime(&ms, r.a, r.b));
+        if (!acc.count(r.name)) order.push_back(r.name);
+        acc[r.name].first += ms;
+        acc[r.name].second += 1;
+    }
+    int k = 0;
+    for (auto& name : order) {
+        if (k >= MPH_PROFILE_MAX) break;
+        avg_ms[k] = acc[name].first / acc[name].second;
+        launches[k] = acc[name].second;
+        std::snprintf(names32 + 32 * k, 32, "%s", name.c_str());
+        ++k;
+    }
+    DevState hs;
+    HIP_OK(c, hipMemcpy(&hs, c->dst, sizeof(DevState), hipMemcpyDeviceToHost));
+    if (hs.overflow) return fail(c, MPH_ERR_NEIGHBOR_OVERFLOW, "a particle has more than 512 neighbours");
+    return k;
+}
+
+int mph_neighbor_stats(MphCtx* c, double* mean, int* mx)
+{
+    if (!c || !mean || !mx) return MPH_ERR_ARG;
+    HIP_OK(c, hipSetDevice(c->device));
+    DevState hs;
+    HIP_OK(c, hipMemcpy(&hs, c->dst, sizeof(DevState), hipMemcpyDeviceToHost));
+    *mean = c->n ? (double)hs.sum_count / c->n : 0.0;
+    *mx = hs.max_count;
+    return MPH_OK;
+}
+
+void mph_destroy(MphCtx* c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->graph1) (void)hipGraphExecDestroy(c->graph1);
+    if (c->graph8) (void)hipGraphExecDestroy(c->graph8);
+    for (void* p : c->allocs) (void)hipFree(p);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+}  // extern "C"
+
+// ---- multi-GPU slab decomposition: see mph_dist.hip ------------------------------------------

@@ -1,0 +1,62 @@
+// mph_kernels.h -- launch interface of the HIP kernels (mph_kernels.hip) used by mph_ctx.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "mph_params.h"
+
+namespace mph {
+
+// Device arrays of the elastic solid, in structure-slot order (see StructureInit).
+struct StructDev {
+    int* orig = nullptr;          // slot -> original particle index
+    int* off = nullptr;           // CSR offsets of the fixed neighbour list
+    int* nb = nullptr;
+    int* in_off = nullptr;        // transpose
+    int* in_nb = nullptr;
+    double4* pair_out = nullptr;  // {x0_ij, w_ij}
+    double4* pair_in = nullptr;   // {x0_is, w_is} of the sender i
+    double* L = nullptr;          // Normalizer [ns][9]
+    double2* lame = nullptr;      // (LambdaLames, MuLames)
+    double* inv_rho = nullptr;    // 1/Density[type]
+    int* clamp = nullptr;         // 0 free, 1 clamped + force zeroed, 2 clamped
+    double4* x0 = nullptr;        // InitialPosition
+    double4* x = nullptr;         // current position (valid during the substeps)
+    double4* v = nullptr;
+    double* P = nullptr;          // first Piola-Kirchhoff F S L [ns][9]
+    double* F = nullptr;          // DeformGradient [ns][9]
+    double* E = nullptr;          // Strain
+    double* S = nullptr;          // Stress
+};
+
+// Per-kernel HIP event timing (mph_profile_steps); nullptr in normal runs.
+struct Profiler {
+    virtual int begin(const char* name, hipStream_t s) = 0;
+    virtual void end(int slot, hipStream_t s) = 0;
+    virtual ~Profiler() = default;
+};
+
+// Everything one launch sequence needs.
+struct Launch {
+    const DevParams* P = nullptr;
+    const DevTables* T = nullptr;
+    DevState* st = nullptr;
+    hipStream_t stream = nullptr;
+    Profiler* prof = nullptr;
+    // B set: integrated state in the previous order; A set: cell-sorted current order
+    double4 *xb = nullptr, *vb = nullptr, *xa = nullptr, *va = nullptr;
+    int *idb = nullptr, *ida = nullptr, *rank_of = nullptr;
+    int *key = nullptr, *slot = nullptr, *tmp = nullptr, *cnt = nullptr, *start = nullptr, *bsum = nullptr;
+    int *nbr = nullptr, *ncount = nullptr;
+    double4 *pv = nullptr, *gca = nullptr, *force = nullptr, *acc = nullptr;
+    double *dens_a = nullptr, *vstrain = nullptr, *divp = nullptr;
+    const StructDev* S = nullptr;
+};
+
+void launch_sort(const Launch& L, int mode);   // mode 0 init, 1 step
+void launch_neighbors(const Launch& L);
+void launch_pass_a(const Launch& L);
+void launch_pass_b(const Launch& L);
+void launch_structure(const Launch& L);
+
+}  // namespace mph

@@ -1,0 +1,860 @@
+// mph_kernels.hip -- hand-written HIP/CDNA4 (gfx950) kernels of the MPH explicit hot path.
+//
+// One time step of the reference (main.cpp:597-686) is mapped onto these launches:
+//
+//   k_prep           calculateWall (3031-3071) + calculatePeriodicBoundary (3322-3333) + cell key
+//                    + cell histogram (first half of the counting sort that replaces the
+//                    reference's bitonic sort, 1683-1708)
+//   k_scan_*         exclusive scan of the cell histogram -> cell start offsets (1711-1728)
+//   k_place          scatter particle ids into their cells (unordered) + Time/WallCenter advance
+//   k_rank_scatter   deterministic in-cell rank (by previous sorted index) and particle reorder
+//   k_neighbors      linked-cell search (1743-1810): 5x5(x5) stencil of cells >= rc/2, the
+//                    reference's exact FP64 acceptance test, ELL neighbour list per wavefront
+//   k_pass_a         DensityA (2141), GravityCenter (2174), DensityP (2314), DivergenceP (2343),
+//                    PhysicalCoefficients (2099), pressure values PressureP (2384) / PressureA (2218)
+//   k_pass_b         PressureP force (2394), PressureA force (2225), DiffuseInterface (2261),
+//                    ViscosityV (2478), InterfaceForce (2427), Gravity (2917), Acceleration (2938),
+//                    Convection (1892)
+//   k_struct_*       elastic substeps: DeformationVector (2673) + Stress (2756) -> PK1 stress;
+//                    StressForce (2812) in gather form + updateElasticPosition (1910)
+//
+// All arithmetic is FP64.  Neighbour membership and every per-kernel radius test reproduce the
+// reference's FP64 expressions bit for bit (no contraction, IEEE division), so NeighborCount is
+// exact; the weighted sums are reassociated (own order, FMA) and agree within the tolerances
+// written in tests/.
+#include <hip/hip_runtime.h>
+
+#include "mph_kernels.h"
+#include "mph_params.h"
+
+namespace mph {
+
+// ------------------------------------------------------------------------------ helpers ------
+
+// Mod(x,w) of main.cpp:98, exact (IEEE division, floor, no contraction).
+__device__ __forceinline__ double mod_exact(double x, double w)
+{
+#pragma clang fp contract(off)
+    return x - w * floor(x / w);
+}
+
+// Periodic minimum image Mod(d + w/2, w) - w/2 of every pair loop (e.g. main.cpp:1762), bit-
+// identical to the reference.  Fast path: for 0 <= s < 0.75 w, floor(s/w) == 0 exactly and
+// Mod(s,w) == s - w*0 == s, so the division is skipped.
+__device__ __forceinline__ double image_exact(double d, double w, double hw, double w075)
+{
+#pragma clang fp contract(off)
+    const double s = d + hw;
+    double m;
+    if (__builtin_expect(s >= 0.0 && s < w075, 1)) {
+        m = s;
+    } else {
+        m = s - w * floor(s / w);
+    }
+    return m - hw;
+}
+
+__device__ __forceinline__ double r2_exact(double q0, double q1, double q2)
+{
+#pragma clang fp contract(off)
+    return q0 * q0 + q1 * q1 + q2 * q2;
+}
+
+__device__ __forceinline__ int wrap_cell(int c, int g)
+{
+    c = c < 0 ? c + g : c;
+    return c >= g ? c - g : c;
+}
+
+__device__ __forceinline__ int cell_axis(double x, double dmin, double ginv, int g)
+{
+    int c = (int)floor((x - dmin) * ginv);
+    c = c < 0 ? c + g : c;
+    c = c >= g ? c - g : c;
+    c = c < 0 ? 0 : c;
+    return c >= g ? g - 1 : c;
+}
+
+__device__ __forceinline__ int cell_id(const DevParams& P, double x, double y, double z)
+{
+    const int cx = cell_axis(x, P.dmin[0], P.ginv[0], P.gc[0]);
+    const int cy = cell_axis(y, P.dmin[1], P.ginv[1], P.gc[1]);
+    const int cz = P.dim == 3 ? cell_axis(z, P.dmin[2], P.ginv[2], P.gc[2]) : 0;
+    return (cx * P.gc[1] + cy) * P.gc[2] + cz;
+}
+
+__device__ __forceinline__ bool dev_is_struct(int t) { return t == 2 || t == 3; }
+__device__ __forceinline__ bool dev_is_fluid(int t) { return t == 0 || t == 1; }
+__device__ __forceinline__ bool dev_is_wall(int t) { return t == 4 || t == 5; }
+
+// XCD-aware block order: hardware deals consecutive blocks round-robin over the 8 XCDs; remap so
+// that each XCD sweeps one contiguous 1/8 of the (cell-sorted) particles and neighbour gathers
+// hit its own L2 (cdna_hip_programming.md T1, bijective form).
+__device__ __forceinline__ int xcd_block(int b, int nb)
+{
+    const int xcd = b & 7;
+    const int q = nb >> 3, r = nb & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+__device__ __forceinline__ const int* ell_row(const int* nbr, int i)
+{
+    return nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
+}
+
+// ------------------------------------------------------------------------- sort phase -------
+
+// calculateWall (main.cpp:3031-3060) + calculatePeriodicBoundary (3322-3333) + cell histogram.
+// mode 0: initialisation (no motion), 1: time step.
+__global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __restrict__ st,
+                                              double4* __restrict__ xb, double4* __restrict__ vb,
+                                              int* __restrict__ key, int* __restrict__ slot,
+                                              int* __restrict__ cnt, int mode)
+{
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P.n) return;
+    double4 x = xb[p];
+    if (mode) {
+#pragma clang fp contract(off)
+        const int t = (int)x.w;
+        if (dev_is_wall(t) && st->time < 0.2) {
+            const double* C = st->wall_c[t];
+            const double* V = st->wall_vel[t];
+            const double* w = st->wall_omega[t];
+            const double (*R)[3] = st->wall_rot[t];
+            const double r0 = x.x - C[0], r1 = x.y - C[1], r2 = x.z - C[2];
+            const double a0 = R[0][0] * r0 + R[0][1] * r1 + R[0][2] * r2;
+            const double a1 = R[1][0] * r0 + R[1][1] * r1 + R[1][2] * r2;
+            const double a2 = R[2][0] * r0 + R[2][1] * r1 + R[2][2] * r2;
+            double4 v = vb[p];
+            v.x = w[1] * a2 - w[2] * a1 + V[0];
+            v.y = w[2] * a0 - w[0] * a2 + V[1];
+            v.z = w[0] * a1 - w[1] * a0 + V[2];
+            vb[p] = v;
+            x.x = a0 + C[0] + V[0] * P.dt;
+            x.y = a1 + C[1] + V[1] * P.dt;
+            x.z = a2 + C[2] + V[2] * P.dt;
+        }
+        x.x = mod_exact(x.x - P.dmin[0], P.dw[0]) + P.dmin[0];
+        x.y = mod_exact(x.y - P.dmin[1], P.dw[1]) + P.dmin[1];
+        x.z = mod_exact(x.z - P.dmin[2], P.dw[2]) + P.dmin[2];
+        xb[p] = x;
+    }
+    const int k = cell_id(P, x.x, x.y, x.z);
+    key[p] = k;
+    slot[p] = atomicAdd(&cnt[k], 1);
+}
+
+// Exclusive scan of the cell histogram: 3 launches (block reduce, top-level scan, down-sweep).
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 16;
+constexpr int kScanBlock = kScanThreads * kScanItems;   // 4096 cells per block
+
+__device__ __forceinline__ int block_exclusive_scan(int v, int* lds, int& total)
+{
+    // wave-level inclusive scan (64 lanes) + cross-wave via LDS
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds[wid] = x;
+    __syncthreads();
+    int wsum = 0;
+    const int nw = blockDim.x >> 6;
+    total = 0;
+    for (int w = 0; w < nw; ++w) {
+        const int s = lds[w];
+        if (w < wid) wsum += s;
+        total += s;
+    }
+    __syncthreads();
+    return wsum + x - v;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const int* __restrict__ cnt, int ncell,
+                                                              int* __restrict__ bsum)
+{
+    __shared__ int lds[kScanThreads / 64];
+    const int base = blockIdx.x * kScanBlock + threadIdx.x * kScanItems;
+    int s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) s += (base + k < ncell) ? cnt[base + k] : 0;
+    int total;
+    block_exclusive_scan(s, lds, total);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_top(int* __restrict__ bsum, int nb)
+{
+    __shared__ int lds[16];
+    __shared__ int carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int base = 0; base < nb; base += blockDim.x) {
+        const int i = base + threadIdx.x;
+        const int v = i < nb ? bsum[i] : 0;
+        int total;
+        const int ex = block_exclusive_scan(v, lds, total);
+        const int c = carry;
+        if (i < nb) bsum[i] = ex + c;
+        __syncthreads();
+        if (threadIdx.x == 0) carry = c + total;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_down(int* __restrict__ cnt, int ncell,
+                                                            const int* __restrict__ bsum,
+                                                            int* __restrict__ start, int n)
+{
+    __shared__ int lds[kScanThreads / 64];
+    const int base = blockIdx.x * kScanBlock + threadIdx.x * kScanItems;
+    int v[kScanItems];
+    int s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        v[k] = (base + k < ncell) ? cnt[base + k] : 0;
+        s += v[k];
+    }
+    int total;
+    int run = block_exclusive_scan(s, lds, total) + bsum[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        if (base + k < ncell) {
+            start[base + k] = run;
+            cnt[base + k] = 0;   // histogram ready for the next step
+        }
+        run += v[k];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) start[ncell] = n;
+}
+
+// Unordered placement; block 0 also advances Time and WallCenter (main.cpp:685, 3066-3070)
+// after k_prep consumed them, and clears the neighbour statistics of the coming search.
+__global__ __launch_bounds__(256) void k_place(DevParams P, DevState* __restrict__ st,
+                                               const int* __restrict__ key, const int* __restrict__ slot,
+                                               const int* __restrict__ start, int* __restrict__ tmp,
+                                               int mode)
+{
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (mode) {
+#pragma clang fp contract(off)
+            for (int t = 4; t < 6; ++t)
+                for (int d = 0; d < 3; ++d) st->wall_c[t][d] += st->wall_vel[t][d] * P.dt;
+            st->time += P.dt;
+        }
+        st->max_count = 0;
+        st->sum_count = 0;
+    }
+    if (p >= P.n) return;
+    tmp[start[key[p]] + slot[p]] = p;
+}
+
+// Deterministic stable order inside a cell: rank = number of cell-mates with a smaller previous
+// sorted index.  Reorders the persistent particle state (x, v, id) into the new cell order.
+__global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __restrict__ key,
+                                                      const int* __restrict__ start,
+                                                      const int* __restrict__ tmp,
+                                                      const double4* __restrict__ xb,
+                                                      const double4* __restrict__ vb,
+                                                      const int* __restrict__ idb,
+                                                      double4* __restrict__ xa, double4* __restrict__ va,
+                                                      int* __restrict__ ida, int* __restrict__ rank_of)
+{
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P.n) return;
+    const int k = key[p];
+    const int s = start[k], e = start[k + 1];
+    int r = 0;
+    for (int q = s; q < e; ++q) r += tmp[q] < p;
+    const int dst = s + r;
+    xa[dst] = xb[p];
+    va[dst] = vb[p];
+    const int id = idb[p];
+    ida[dst] = id;
+    rank_of[id] = dst;
+}
+
+// ---------------------------------------------------------------------- neighbour search ----
+
+// calculateNeighbor (main.cpp:1743-1810).  The reference scans (2*3+1)^d cells of width dx; here
+// cells are >= rc/2 wide, so a +-2 stencil covers the acceptance sphere: 25 columns (3-D) or 5
+// (2-D) along which the cells of the last axis are contiguous in memory.  Acceptance is the
+// reference's own test  q0^2+q1^2+q2^2 <= (MaxRadius+MARGIN)^2  with the Mod-based minimum image.
+template <int DIM>
+__global__ __launch_bounds__(256) void k_neighbors(DevParams P, const double4* __restrict__ x,
+                                                   const int* __restrict__ start,
+                                                   int* __restrict__ nbr, int* __restrict__ ncount,
+                                                   DevState* __restrict__ st)
+{
+    const int i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    const bool live = i < P.n;
+    int cnt = 0;
+    if (live) {
+        const double4 xi = x[i];
+        const int cx = cell_axis(xi.x, P.dmin[0], P.ginv[0], P.gc[0]);
+        const int cy = cell_axis(xi.y, P.dmin[1], P.ginv[1], P.gc[1]);
+        const int cz = DIM == 3 ? cell_axis(xi.z, P.dmin[2], P.ginv[2], P.gc[2]) : 0;
+        int* out = nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
+        constexpr int NCOL = DIM == 3 ? 25 : 5;
+        const int gca = DIM == 3 ? P.gc[2] : P.gc[1];   // contiguous axis
+        const int cca = DIM == 3 ? cz : cy;
+        for (int col = 0; col < NCOL; ++col) {
+            int base;
+            if (DIM == 3) {
+                const int jx = wrap_cell(cx + col / 5 - 2, P.gc[0]);
+                const int jy = wrap_cell(cy + col % 5 - 2, P.gc[1]);
+                base = (jx * P.gc[1] + jy) * P.gc[2];
+            } else {
+                base = wrap_cell(cx + col - 2, P.gc[0]) * P.gc[1];
+            }
+            const int lo = cca - 2, hi = cca + 2;
+            int seg_a[2], seg_b[2], nseg;
+            if (lo < 0) { seg_a[0] = lo + gca; seg_b[0] = gca - 1; seg_a[1] = 0; seg_b[1] = hi; nseg = 2; }
+            else if (hi >= gca) { seg_a[0] = lo; seg_b[0] = gca - 1; seg_a[1] = 0; seg_b[1] = hi - gca; nseg = 2; }
+            else { seg_a[0] = lo; seg_b[0] = hi; seg_a[1] = 0; seg_b[1] = -1; nseg = 1; }
+            for (int sg = 0; sg < nseg; ++sg) {
+                const int jb = start[base + seg_a[sg]];
+                const int je = start[base + seg_b[sg] + 1];
+                for (int j = jb; j < je; ++j) {
+                    const double4 xj = x[j];
+                    const double q0 = image_exact(xj.x - xi.x, P.dw[0], P.hw[0], P.w075[0]);
+                    const double q1 = image_exact(xj.y - xi.y, P.dw[1], P.hw[1], P.w075[1]);
+                    const double q2 = image_exact(xj.z - xi.z, P.dw[2], P.hw[2], P.w075[2]);
+                    const double r2 = r2_exact(q0, q1, q2);
+                    if (r2 <= P.rc2 && j != i) {
+                        if (cnt < kMaxNeighbor) out[cnt * kTile] = j;
+                        ++cnt;
+                    }
+                }
+            }
+        }
+        ncount[i] = cnt;
+    }
+    // wave reduction of the statistics (mean/max neighbours, overflow flag)
+    int mx = cnt;
+    unsigned long long sm = (unsigned long long)cnt;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int m2 = __shfl_xor(mx, o, 64);
+        mx = m2 > mx ? m2 : mx;
+        sm += __shfl_xor(sm, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(&st->max_count, mx);
+        atomicAdd(&st->sum_count, sm);
+        if (mx > kMaxNeighbor) atomicOr(&st->overflow, 1);
+    }
+}
+
+// ---------------------------------------------------------------------------- pass A -------
+
+// DensityA (2141-2171), GravityCenter (2174-2210), DensityP (2314-2341), DivergenceP
+// (2343-2379); epilogue: PhysicalCoefficients (2099-2137) and the pressure values of
+// calculatePressureP (2384-2392) and calculatePressureA (2218-2223).
+template <bool SURF>
+__global__ __launch_bounds__(256) void k_pass_a(DevParams P, const DevTables* __restrict__ T,
+                                                const double4* __restrict__ x,
+                                                const double4* __restrict__ v,
+                                                const int* __restrict__ nbr,
+                                                const int* __restrict__ ncount,
+                                                double4* __restrict__ pv, double4* __restrict__ gca,
+                                                double* __restrict__ dens_a,
+                                                double* __restrict__ vstrain,
+                                                double* __restrict__ divp)
+{
+    __shared__ double s_ratio[kTypes * kTypes];
+    if (threadIdx.x < kTypes * kTypes) s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
+    __syncthreads();
+    const int i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    const double4 xi = x[i];
+    const double4 vi = v[i];
+    const int ti = (int)xi.w;
+    const bool solid = dev_is_struct(ti);
+    const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
+    const int* row = ell_row(nbr, i);
+    double da = 0.0, g0 = 0.0, g1 = 0.0, g2 = 0.0, vs = 0.0, dv = 0.0;
+    const double gscale = P.rg / P.r2g;
+    for (int k = 0; k < cnt; ++k) {
+        const int j = row[k * kTile];
+        const double4 xj = x[j];
+        const double q0 = image_exact(xj.x - xi.x, P.dw[0], P.hw[0], P.w075[0]);
+        const double q1 = image_exact(xj.y - xi.y, P.dw[1], P.hw[1], P.w075[1]);
+        const double q2 = image_exact(xj.z - xi.z, P.dw[2], P.hw[2], P.w075[2]);
+        const double r2 = r2_exact(q0, q1, q2);
+        const double r = sqrt(r2);
+        const double ir = 1.0 / r;
+        if (r2 <= P.rp2) {
+            const double4 vj = v[j];
+            const double omt = 1.0 - r * P.inv_rp;
+            vs += P.cp * omt * omt;
+            const double dot = (vj.x - vi.x) * q0 + (vj.y - vi.y) * q1 + (vj.z - vi.z) * q2;
+            dv -= dot * ir * (P.cdp * omt);
+        }
+        if (!solid) {
+            const double ratio = s_ratio[ti * kTypes + (int)xj.w];
+            if (r2 <= P.ra2) {
+                const double t = r * P.inv_ra;
+                const double omt = 1.0 - t;
+                da += ratio * (P.ca * t * omt * omt);
+            }
+            if (r2 <= P.rg2) {
+                const double omt = 1.0 - r * P.inv_rg;
+                const double w = ratio * (P.cg * omt * omt) * gscale;
+                g0 += q0 * w;
+                g1 += q1 * w;
+                g2 += q2 * w;
+            }
+        }
+    }
+    const double vstr = vs - P.n0p;
+    const double kappa = vstr < 0.0 ? 0.0 : T->bulk[ti];
+    double pres = -T->bulk_visc[ti] * dv;
+    if (vstr > 0.0) pres += kappa * vstr;
+    double pa = T->cofa[ti] * (da - P.n0a) / P.dx;
+    if (P.n0a <= da) pa = 0.0;
+    pv[i] = make_double4(vi.x, vi.y, vi.z, pres);
+    gca[i] = make_double4(g0, g1, g2, pa);
+    dens_a[i] = da;
+    vstrain[i] = vstr;
+    divp[i] = dv;
+}
+
+// ---------------------------------------------------------------------------- pass B -------
+
+// Pair forces of PressureP (2394-2424), PressureA (2225-2258), DiffuseInterface (2261-2312),
+// ViscosityV (2478-2522) for non-structure i; InterfaceForce (2439-2472) for structure i; then
+// Gravity (2917-2936), Acceleration/kick (2938-2956) and Convection/drift (1892-1907).
+template <bool SURF>
+__global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __restrict__ T,
+                                                const double4* __restrict__ x,
+                                                const double4* __restrict__ pv,
+                                                const double4* __restrict__ gca,
+                                                const int* __restrict__ nbr,
+                                                const int* __restrict__ ncount,
+                                                const int* __restrict__ ida,
+                                                double4* __restrict__ force,
+                                                double4* __restrict__ acc,
+                                                double4* __restrict__ xb, double4* __restrict__ vb,
+                                                int* __restrict__ idb)
+{
+    __shared__ double s_ratio[kTypes * kTypes];
+    __shared__ double s_mu[kTypes * kTypes];
+    if (threadIdx.x < kTypes * kTypes) {
+        s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
+        s_mu[threadIdx.x] = T->mu_ij[threadIdx.x];
+    }
+    __syncthreads();
+    const int i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    const double4 xi = x[i];
+    const double4 pvi = pv[i];
+    const int ti = (int)xi.w;
+    const bool solid = dev_is_struct(ti);
+    const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
+    const int* row = ell_row(nbr, i);
+    double f0 = 0.0, f1 = 0.0, f2 = 0.0;
+    double4 gi = make_double4(0.0, 0.0, 0.0, 0.0);
+    double ai = 0.0;
+    if (SURF) {
+        gi = gca[i];
+        ai = T->cofa[ti] * P.cofk * P.cofk;
+    }
+    const double dscale = P.rg / P.r2g * (P.vol / P.dx);
+    for (int k = 0; k < cnt; ++k) {
+        const int j = row[k * kTile];
+        const double4 xj = x[j];
+        const int tj = (int)xj.w;
+        if (solid && dev_is_struct(tj)) continue;
+        const double q0 = image_exact(xj.x - xi.x, P.dw[0], P.hw[0], P.w075[0]);
+        const double q1 = image_exact(xj.y - xi.y, P.dw[1], P.hw[1], P.w075[1]);
+        const double q2 = image_exact(xj.z - xi.z, P.dw[2], P.hw[2], P.w075[2]);
+        const double r2 = r2_exact(q0, q1, q2);
+        const double4 pvj = pv[j];
+        const double r = sqrt(r2);
+        const double ir = 1.0 / r;
+        double c = 0.0;
+        if (r2 < P.rp2) {
+            const double dw = P.cdp * (1.0 - r * P.inv_rp);
+            c += (pvi.w + pvj.w) * dw * ir * P.vol;
+        }
+        if (!solid) {
+            if (SURF) {
+                const double4 gj = gca[j];
+                const double rij = s_ratio[ti * kTypes + tj];
+                const double rji = s_ratio[tj * kTypes + ti];
+                if (r2 < P.ra2) {
+                    const double t = r * P.inv_ra;
+                    const double dwa = P.cda * (1.0 - t) * (1.0 - 3.0 * t);
+                    c += (gi.w * rij + gj.w * rji) * dwa * ir * P.vol;
+                }
+                if (r2 < P.rg2) {
+                    const double omt = 1.0 - r * P.inv_rg;
+                    const double wg = P.cg * omt * omt;
+                    const double dwg = P.cdg * omt;
+                    const double wij = rij * wg, wji = rji * wg;
+                    f0 -= (ai * gj.x * wji - ai * gi.x * wij) * dscale;
+                    f1 -= (ai * gj.y * wji - ai * gi.y * wij) * dscale;
+                    f2 -= (ai * gj.z * wji - ai * gi.z * wij) * dscale;
+                    const double dwij = rij * dwg, dwji = rji * dwg;
+                    const double gr = (ai * gj.x * dwji - ai * gi.x * dwij) * q0 +
+                                      (ai * gj.y * dwji - ai * gi.y * dwij) * q1 +
+                                      (ai * gj.z * dwji - ai * gi.z * dwij) * q2;
+                    c -= gr * ir * dscale;
+                }
+            }
+            if (r2 < P.rv2) {
+                const double dwij = -P.cdv * (1.0 - r * P.inv_rv);
+                const double dot = (pvj.x - pvi.x) * q0 + (pvj.y - pvi.y) * q1 + (pvj.z - pvi.z) * q2;
+                c += P.cvis * s_mu[ti * kTypes + tj] * dot * dwij * (ir * ir * ir) * P.vol;
+            }
+        }
+        f0 += c * q0;
+        f1 += c * q1;
+        f2 += c * q2;
+    }
+    double4 vo = make_double4(pvi.x, pvi.y, pvi.z, 0.0);
+    double4 xo = xi;
+    double4 ao = make_double4(0.0, 0.0, 0.0, 0.0);
+    if (dev_is_fluid(ti) || solid) {
+        const double m = T->mass[ti], im = T->inv_mass[ti];
+        f0 += m * P.gravity[0];
+        f1 += m * P.gravity[1];
+        f2 += m * P.gravity[2];
+        vo.x += f0 * im * P.dt;
+        vo.y += f1 * im * P.dt;
+        vo.z += f2 * im * P.dt;
+        if (!solid) {
+            ao = make_double4(f0 * im, f1 * im, f2 * im, 0.0);
+            xo.x += vo.x * P.dt;
+            xo.y += vo.y * P.dt;
+            xo.z += vo.z * P.dt;
+        }
+    }
+    force[i] = make_double4(f0, f1, f2, 0.0);
+    acc[i] = ao;
+    xb[i] = xo;
+    vb[i] = vo;
+    idb[i] = ida[i];
+}
+
+// ------------------------------------------------------------------------ elastic solid ----
+
+__global__ __launch_bounds__(256) void k_struct_gather(int ns, const int* __restrict__ sorig,
+                                                       const int* __restrict__ rank_of,
+                                                       const double4* __restrict__ xb,
+                                                       const double4* __restrict__ vb,
+                                                       double4* __restrict__ sx, double4* __restrict__ sv)
+{
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ns) return;
+    const int r = rank_of[sorig[s]];
+    sx[s] = xb[r];
+    sv[s] = vb[r];
+}
+
+// calculateElasticDeformationVector (2673-2754) + calculateStress (2756-2809) + the first
+// Piola-Kirchhoff tensor P = F S L of calculateStressForce (2837-2852).
+template <int DIM>
+__global__ __launch_bounds__(256) void k_struct_stress(DevParams P, int ns,
+                                                       const double4* __restrict__ sx,
+                                                       const double4* __restrict__ sx0,
+                                                       const int* __restrict__ off,
+                                                       const int* __restrict__ nb,
+                                                       const double4* __restrict__ pair,
+                                                       const double* __restrict__ L,
+                                                       const double2* __restrict__ lame,
+                                                       double* __restrict__ sP, double* __restrict__ sF,
+                                                       double* __restrict__ sE, double* __restrict__ sS)
+{
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ns) return;
+    const double4 xi = sx[s], x0i = sx0[s];
+    double ui[3];
+    ui[0] = image_exact(xi.x - x0i.x, P.dw[0], P.hw[0], P.w075[0]);
+    ui[1] = image_exact(xi.y - x0i.y, P.dw[1], P.hw[1], P.w075[1]);
+    ui[2] = image_exact(xi.z - x0i.z, P.dw[2], P.hw[2], P.w075[2]);
+    double Fr[DIM][DIM];
+#pragma unroll
+    for (int a = 0; a < DIM; ++a)
+#pragma unroll
+        for (int b = 0; b < DIM; ++b) Fr[a][b] = 0.0;
+    for (int k = off[s]; k < off[s + 1]; ++k) {
+        const int t = nb[k];
+        const double4 pr = pair[k];
+        const double4 xj = sx[t], x0j = sx0[t];
+        const double x0ij[3] = {pr.x, pr.y, pr.z};
+        const double uj[3] = {image_exact(xj.x - x0j.x, P.dw[0], P.hw[0], P.w075[0]),
+                              image_exact(xj.y - x0j.y, P.dw[1], P.hw[1], P.w075[1]),
+                              image_exact(xj.z - x0j.z, P.dw[2], P.hw[2], P.w075[2])};
+#pragma unroll
+        for (int a = 0; a < DIM; ++a) {
+            const double xa = x0ij[a] + (uj[a] - ui[a]);
+#pragma unroll
+            for (int b = 0; b < DIM; ++b) Fr[a][b] += pr.w * xa * x0ij[b];
+        }
+    }
+    double Lm[DIM][DIM], F[DIM][DIM], E[DIM][DIM], S[DIM][DIM], PK[DIM][DIM];
+#pragma unroll
+    for (int a = 0; a < DIM; ++a)
+#pragma unroll
+        for (int b = 0; b < DIM; ++b) Lm[a][b] = L[(size_t)s * 9 + 3 * a + b];
+#pragma unroll
+    for (int a = 0; a < DIM; ++a)
+#pragma unroll
+        for (int b = 0; b < DIM; ++b) {
+            double acc = 0.0;
+#pragma unroll
+            for (int k = 0; k < DIM; ++k) acc += Fr[a][k] * Lm[k][b];
+            F[a][b] = acc;
+        }
+    double tr = 0.0;
+#pragma unroll
+    for (int a = 0; a < DIM; ++a)
+#pragma unroll
+        for (int b = 0; b < DIM; ++b) {
+            double acc = 0.0;
+#pragma unroll
+            for (int k = 0; k < DIM; ++k) acc += F[k][a] * F[k][b];
+            E[a][b] = 0.5 * (acc - (a == b ? 1.0 : 0.0));
+            if (a == b) tr += E[a][b];
+        }
+    const double2 lm = lame[s];   // (lambda, mu)
+#pragma unroll
+    for (int a = 0; a < DIM; ++a)
+#pragma unroll
+        for (int b = 0; b < DIM; ++b) S[a][b] = 2.0 * lm.y * E[a][b] + (a == b ? lm.x * tr : 0.0);
+    // P = F S L
+#pragma unroll
+    for (int a = 0; a < DIM; ++a)
+#pragma unroll
+        for (int b = 0; b < DIM; ++b) {
+            double acc = 0.0;
+#pragma unroll
+            for (int k = 0; k < DIM; ++k)
+#pragma unroll
+                for (int l = 0; l < DIM; ++l) acc += F[a][k] * S[k][l] * Lm[l][b];
+            PK[a][b] = acc;
+        }
+    double* oP = sP + (size_t)s * 9;
+    double* oF = sF + (size_t)s * 9;
+    double* oE = sE + (size_t)s * 9;
+    double* oS = sS + (size_t)s * 9;
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            const bool in = a < DIM && b < DIM;
+            oP[3 * a + b] = in ? PK[a < DIM ? a : 0][b < DIM ? b : 0] : 0.0;
+            oF[3 * a + b] = in ? F[a < DIM ? a : 0][b < DIM ? b : 0] : 0.0;
+            oE[3 * a + b] = in ? E[a < DIM ? a : 0][b < DIM ? b : 0] : 0.0;
+            oS[3 * a + b] = in ? S[a < DIM ? a : 0][b < DIM ? b : 0] : 0.0;
+        }
+}
+
+// calculateStressForce (2854-2887) in gather form: v_s += dt_e/rho_s * [sum_j w_sj P_s x0_sj -
+// sum_{i lists s} w_is P_i x0_is] (exactly the reference's scatter, regrouped by receiver),
+// followed by updateElasticPosition (1910-2082): module clamp, then the always-compiled second
+// drift of 2070-2079 (free particles drift twice per substep; structure acceleration is zero).
+template <int DIM>
+__global__ __launch_bounds__(256) void k_struct_velocity(DevParams P, int ns,
+                                                         const int* __restrict__ off,
+                                                         const double4* __restrict__ pair_out,
+                                                         const int* __restrict__ in_off,
+                                                         const int* __restrict__ in_nb,
+                                                         const double4* __restrict__ pair_in,
+                                                         const double* __restrict__ sP,
+                                                         const double* __restrict__ inv_rho,
+                                                         const int* __restrict__ clamp,
+                                                         const double4* __restrict__ sx0,
+                                                         double4* __restrict__ sx, double4* __restrict__ sv)
+{
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ns) return;
+    double Ps[DIM][DIM];
+#pragma unroll
+    for (int a = 0; a < DIM; ++a)
+#pragma unroll
+        for (int b = 0; b < DIM; ++b) Ps[a][b] = sP[(size_t)s * 9 + 3 * a + b];
+    double dv[DIM];
+#pragma unroll
+    for (int a = 0; a < DIM; ++a) dv[a] = 0.0;
+    for (int k = off[s]; k < off[s + 1]; ++k) {
+        const double4 pr = pair_out[k];
+        const double x0[3] = {pr.x, pr.y, pr.z};
+#pragma unroll
+        for (int a = 0; a < DIM; ++a) {
+            double f = 0.0;
+#pragma unroll
+            for (int b = 0; b < DIM; ++b) f += Ps[a][b] * x0[b];
+            dv[a] += f * pr.w;
+        }
+    }
+    for (int k = in_off[s]; k < in_off[s + 1]; ++k) {
+        const int i = in_nb[k];
+        const double4 pr = pair_in[k];
+        const double x0[3] = {pr.x, pr.y, pr.z};
+        const double* Pi = sP + (size_t)i * 9;
+#pragma unroll
+        for (int a = 0; a < DIM; ++a) {
+            double f = 0.0;
+#pragma unroll
+            for (int b = 0; b < DIM; ++b) f += Pi[3 * a + b] * x0[b];
+            dv[a] -= f * pr.w;
+        }
+    }
+    double4 v = sv[s];
+    double4 xo = sx[s];
+    const double ir = inv_rho[s];
+    double vv[3] = {v.x, v.y, v.z};
+#pragma unroll
+    for (int a = 0; a < DIM; ++a) vv[a] += ir * dv[a] * P.edt;
+    double xx[3] = {xo.x, xo.y, xo.z};
+    const int cl = clamp[s];
+    if (cl) {
+        const double4 x0 = sx0[s];
+        xx[0] = x0.x; xx[1] = x0.y; xx[2] = x0.z;
+        vv[0] = vv[1] = vv[2] = 0.0;
+    } else if (P.module != MPH_MODULE_NONE) {
+        for (int d = 0; d < 3; ++d) xx[d] += vv[d] * P.edt;
+    }
+    for (int d = 0; d < 3; ++d) xx[d] += vv[d] * P.edt;
+    sv[s] = make_double4(vv[0], vv[1], vv[2], 0.0);
+    sx[s] = make_double4(xx[0], xx[1], xx[2], xo.w);
+}
+
+__global__ __launch_bounds__(256) void k_struct_scatter(int ns, const int* __restrict__ sorig,
+                                                        const int* __restrict__ rank_of,
+                                                        const int* __restrict__ clamp,
+                                                        const double4* __restrict__ sx,
+                                                        const double4* __restrict__ sv,
+                                                        double4* __restrict__ xb, double4* __restrict__ vb,
+                                                        double4* __restrict__ force)
+{
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ns) return;
+    const int r = rank_of[sorig[s]];
+    xb[r] = sx[s];
+    vb[r] = sv[s];
+    if (clamp[s] == 1) force[r] = make_double4(0.0, 0.0, 0.0, 0.0);
+}
+
+// ---------------------------------------------------------------------------- launchers -----
+
+static inline int blocks(int n, int t) { return (n + t - 1) / t; }
+
+#define MPH_LAUNCH(name, grid, block, stream, ...)                                  \
+    do {                                                                            \
+        ProfScope _ps(prof, name, stream);                                          \
+        hipLaunchKernelGGL(__VA_ARGS__);                                            \
+    } while (0)
+
+struct ProfScope {
+    Profiler* p;
+    int slot;
+    hipStream_t s;
+    ProfScope(Profiler* prof, const char* name, hipStream_t st) : p(prof), slot(-1), s(st)
+    {
+        if (p) slot = p->begin(name, st);
+    }
+    ~ProfScope()
+    {
+        if (p) p->end(slot, s);
+    }
+};
+
+void launch_sort(const Launch& L, int mode)
+{
+    Profiler* prof = L.prof;
+    const DevParams& P = *L.P;
+    const int n = P.n;
+    if (n == 0) return;
+    MPH_LAUNCH("prep", 0, 0, L.stream, k_prep, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st,
+               L.xb, L.vb, L.key, L.slot, L.cnt, mode);
+    const int nb = blocks(P.ncell, kScanBlock);
+    MPH_LAUNCH("scan_reduce", 0, 0, L.stream, k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, L.stream,
+               L.cnt, P.ncell, L.bsum);
+    MPH_LAUNCH("scan_top", 0, 0, L.stream, k_scan_top, dim3(1), dim3(1024), 0, L.stream, L.bsum, nb);
+    MPH_LAUNCH("scan_down", 0, 0, L.stream, k_scan_down, dim3(nb), dim3(kScanThreads), 0, L.stream,
+               L.cnt, P.ncell, L.bsum, L.start, n);
+    MPH_LAUNCH("place", 0, 0, L.stream, k_place, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st,
+               L.key, L.slot, L.start, L.tmp, mode);
+    MPH_LAUNCH("rank_scatter", 0, 0, L.stream, k_rank_scatter, dim3(blocks(n, 256)), dim3(256), 0,
+               L.stream, P, L.key, L.start, L.tmp, L.xb, L.vb, L.idb, L.xa, L.va, L.ida, L.rank_of);
+}
+
+void launch_neighbors(const Launch& L)
+{
+    Profiler* prof = L.prof;
+    const DevParams& P = *L.P;
+    if (P.n == 0) return;
+    if (P.dim == 3)
+        MPH_LAUNCH("neighbors", 0, 0, L.stream, k_neighbors<3>, dim3(blocks(P.n, 256)), dim3(256), 0,
+                   L.stream, P, L.xa, L.start, L.nbr, L.ncount, L.st);
+    else
+        MPH_LAUNCH("neighbors", 0, 0, L.stream, k_neighbors<2>, dim3(blocks(P.n, 256)), dim3(256), 0,
+                   L.stream, P, L.xa, L.start, L.nbr, L.ncount, L.st);
+}
+
+void launch_pass_a(const Launch& L)
+{
+    Profiler* prof = L.prof;
+    const DevParams& P = *L.P;
+    if (P.n == 0) return;
+    if (P.surface)
+        MPH_LAUNCH("pass_a", 0, 0, L.stream, k_pass_a<true>, dim3(blocks(P.n, 256)), dim3(256), 0,
+                   L.stream, P, L.T, L.xa, L.va, L.nbr, L.ncount, L.pv, L.gca, L.dens_a, L.vstrain, L.divp);
+    else
+        MPH_LAUNCH("pass_a", 0, 0, L.stream, k_pass_a<false>, dim3(blocks(P.n, 256)), dim3(256), 0,
+                   L.stream, P, L.T, L.xa, L.va, L.nbr, L.ncount, L.pv, L.gca, L.dens_a, L.vstrain, L.divp);
+}
+
+void launch_pass_b(const Launch& L)
+{
+    Profiler* prof = L.prof;
+    const DevParams& P = *L.P;
+    if (P.n == 0) return;
+    if (P.surface)
+        MPH_LAUNCH("pass_b", 0, 0, L.stream, k_pass_b<true>, dim3(blocks(P.n, 256)), dim3(256), 0,
+                   L.stream, P, L.T, L.xa, L.pv, L.gca, L.nbr, L.ncount, L.ida, L.force, L.acc, L.xb,
+                   L.vb, L.idb);
+    else
+        MPH_LAUNCH("pass_b", 0, 0, L.stream, k_pass_b<false>, dim3(blocks(P.n, 256)), dim3(256), 0,
+                   L.stream, P, L.T, L.xa, L.pv, L.gca, L.nbr, L.ncount, L.ida, L.force, L.acc, L.xb,
+                   L.vb, L.idb);
+}
+
+void launch_structure(const Launch& L)
+{
+    Profiler* prof = L.prof;
+    const DevParams& P = *L.P;
+    const int ns = P.n_struct;
+    if (ns == 0) return;
+    const StructDev& S = *L.S;
+    MPH_LAUNCH("struct_gather", 0, 0, L.stream, k_struct_gather, dim3(blocks(ns, 256)), dim3(256), 0,
+               L.stream, ns, S.orig, L.rank_of, L.xb, L.vb, S.x, S.v);
+    for (int sub = 0; sub < P.substeps; ++sub) {
+        if (P.dim == 3) {
+            MPH_LAUNCH("struct_stress", 0, 0, L.stream, k_struct_stress<3>, dim3(blocks(ns, 256)), dim3(256),
+                       0, L.stream, P, ns, S.x, S.x0, S.off, S.nb, S.pair_out, S.L, S.lame, S.P, S.F, S.E, S.S);
+            MPH_LAUNCH("struct_velocity", 0, 0, L.stream, k_struct_velocity<3>, dim3(blocks(ns, 256)),
+                       dim3(256), 0, L.stream, P, ns, S.off, S.pair_out, S.in_off, S.in_nb, S.pair_in, S.P,
+                       S.inv_rho, S.clamp, S.x0, S.x, S.v);
+        } else {
+            MPH_LAUNCH("struct_stress", 0, 0, L.stream, k_struct_stress<2>, dim3(blocks(ns, 256)), dim3(256),
+                       0, L.stream, P, ns, S.x, S.x0, S.off, S.nb, S.pair_out, S.L, S.lame, S.P, S.F, S.E, S.S);
+            MPH_LAUNCH("struct_velocity", 0, 0, L.stream, k_struct_velocity<2>, dim3(blocks(ns, 256)),
+                       dim3(256), 0, L.stream, P, ns, S.off, S.pair_out, S.in_off, S.in_nb, S.pair_in, S.P,
+                       S.inv_rho, S.clamp, S.x0, S.x, S.v);
+        }
+    }
+    MPH_LAUNCH("struct_scatter", 0, 0, L.stream, k_struct_scatter, dim3(blocks(ns, 256)), dim3(256), 0,
+               L.stream, ns, S.orig, L.rank_of, S.clamp, S.x, S.v, L.xb, L.vb, L.force);
+}
+
+}  // namespace mph

@@ -1,0 +1,83 @@
+// mph_params.h -- plain-old-data structures shared by the host layer (mph_host.cpp) and the
+// HIP kernels (mph_kernels.hip).  No HIP types here, so the host files build with g++/hipcc alike.
+#pragma once
+
+#include <cstdint>
+
+#include "../../include/mph_gpu.h"
+
+namespace mph {
+
+constexpr int kTypes = MPH_TYPE_COUNT;
+constexpr int kMaxNeighbor = MPH_MAX_NEIGHBOR_COUNT;
+constexpr int kTile = 64;  // ELL neighbour-list tile = one wavefront of i-particles
+
+inline bool is_fluid(int t) { return t >= 0 && t < 2; }   // main.cpp:69-70
+inline bool is_struct(int t) { return t >= 2 && t < 4; }  // main.cpp:71-72
+inline bool is_wall(int t) { return t >= 4 && t < 6; }    // main.cpp:73-74
+
+// Every constant the reference derives in initializeWeight/Fluid/Wall/Domain
+// (main.cpp:1191-1469), in the reference's own arithmetic, plus what the GPU path precomputes.
+// Passed by value as a kernel argument (kernarg segment -> scalar loads).
+struct DevParams {
+    int n;             // particles held by this context
+    int dim;           // 2 or 3
+    int module;        // MphModule
+    int surface;       // any CofA != 0 -> surface-tension terms live (K12/K13)
+    int n_struct;      // structure particles (types 2,3)
+    int gc[3];         // GPU linked-cell grid (gc[2] == 1 in 2-D)
+    int ncell;         // gc[0]*gc[1]*gc[2]
+    int substeps;      // (int)(Dt/Elastic_Dt + 0.5), main.cpp:653
+    double dmin[3], dw[3], hw[3], w075[3];   // domain min / width / half width / 0.75 width
+    double ginv[3];    // 1 / GPU cell width per axis
+    double rc2;        // (MaxRadius + MARGIN)^2, main.cpp:1765
+    double ra, rg, rp, rv;                   // radii (main.cpp:1195-1198)
+    double ra2, rg2, rp2, rv2;               // radius*radius as the reference compares them
+    double inv_ra, inv_rg, inv_rp, inv_rv;
+    // kernel prefactors: wa = ca*t*(1-t)^2, dwa = cda*(1-t)*(1-3t), w_x = c_x*(1-t)^2,
+    // dw_x = cd_x*(1-t)  with t = r/h (main.cpp:298-368)
+    double ca, cda, cg, cdg, cp, cdp, cv, cdv;
+    double cw;          // weight(): (1/Swp)/rp^dim (main.cpp:268-295)
+    double n0a, n0p, r2g, cofk, dx, vol, dt, edt, cvis;
+    double gravity[3];
+    double ratio[kTypes][kTypes];   // InteractionRatio
+    double mu_ij[kTypes][kTypes];   // 2 mu_i mu_j / (mu_i + mu_j) from ShearViscosity
+    double cofa[kTypes];            // CofA (main.cpp:1339-1341)
+    double mass[kTypes], inv_mass[kTypes], density[kTypes], inv_density[kTypes];
+    double bulk[kTypes], bulk_visc[kTypes];
+    double wall_rot[kTypes][3][3];  // initializeWall (main.cpp:1371-1410)
+    double wall_omega[kTypes][3];
+    double wall_vel[kTypes][3];
+};
+
+// Mutable per-step device scalars (so a captured hipGraph can replay many steps).
+struct DevState {
+    double time;                 // Time
+    double wall_c[kTypes][3];    // WallCenter (advanced by V*Dt every step, main.cpp:3066-3070)
+    double wall_vel[kTypes][3];  // WallVelocity
+    double wall_omega[kTypes][3];// WallOmega
+    double wall_rot[kTypes][3][3];  // WallRotation (initializeWall)
+    int overflow;                // some particle reached MAX_NEIGHBOR_COUNT
+    int max_count;               // max neighbour count of the last search
+    unsigned long long sum_count;
+};
+
+// Per-type tables read with per-lane type indices (device memory; staged through LDS where hot).
+struct DevTables {
+    double ratio[kTypes * kTypes];   // InteractionRatio[ti][tj]
+    double mu_ij[kTypes * kTypes];   // 2 mu_i mu_j / (mu_i + mu_j)
+    double cofa[kTypes], mass[kTypes], inv_mass[kTypes], bulk[kTypes], bulk_visc[kTypes];
+};
+
+// Host-side derived constants (reference arithmetic, bit-identical to the reference's globals).
+struct HostDerived {
+    double ra, rg, rp, rv, max_radius;
+    double swa, swg, swp, swv, n0a, n0p, r2g, cofk, cofa[kTypes];
+    double vol, dx;
+    double dmin[3], dmax[3], dw[3];
+    double cell_w;
+    int cell_n[3];
+    double wall_rot[kTypes][3][3];
+};
+
+}  // namespace mph

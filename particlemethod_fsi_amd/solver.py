@@ -1,0 +1,248 @@
+"""Python mirror of the reference driver over the C ABI of ``include/mph_gpu.h``.
+
+``MphSolver`` plays the role of the reference's ``main()`` (src/main.cpp:490-727) for tests,
+benchmarks and scripting: construct it from a ``.data``/``.grid`` pair (or an in-memory case),
+advance with ``step(k)`` (each step = main.cpp:597-686) and read any per-particle array with
+``get(<reference array name>)`` in the reference's layout and original particle order.
+
+All compute runs in libmph_gpu.so (HIP kernels for gfx950).  There is no CPU fallback: if the
+library is missing or no HIP device is present the constructor raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from . import mphio
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libmph_gpu.so")
+CSRC_DIR = os.path.join(PKG_DIR, "csrc")
+
+# MphField (include/mph_gpu.h) keyed by the reference's array names (main.cpp:102-197)
+FIELDS = {
+    "Position": (0, 3, np.float64), "InitialPosition": (1, 3, np.float64),
+    "Velocity": (2, 3, np.float64), "Force": (3, 3, np.float64),
+    "Acceleration": (4, 3, np.float64), "GravityCenter": (5, 3, np.float64),
+    "PressureP": (6, 1, np.float64), "PressureA": (7, 1, np.float64),
+    "DensityA": (8, 1, np.float64), "VolStrainP": (9, 1, np.float64),
+    "DivergenceP": (10, 1, np.float64), "Mass": (11, 1, np.float64), "Kappa": (12, 1, np.float64),
+    "Lambda": (13, 1, np.float64), "Mu": (14, 1, np.float64),
+    "NeighborCount": (15, 1, np.int32), "InitialStructureNeighborCount": (16, 1, np.int32),
+    "Property": (17, 1, np.int32), "DeformGradient": (18, 9, np.float64),
+    "Strain": (19, 9, np.float64), "Stress": (20, 9, np.float64),
+    "Normalizer": (21, 9, np.float64), "LambdaLames": (22, 1, np.float64),
+    "MuLames": (23, 1, np.float64),
+}
+
+STATUS = {0: "MPH_OK", -1: "MPH_ERR_ARG", -2: "MPH_ERR_IO", -3: "MPH_ERR_NEIGHBOR_OVERFLOW",
+          -4: "MPH_ERR_DEVICE_OOM", -5: "MPH_ERR_HIP", -6: "MPH_ERR_RCCL", -7: "MPH_ERR_DOMAIN",
+          -8: "MPH_ERR_UNSUPPORTED", -9: "MPH_ERR_NONFINITE"}
+
+EXPORTED_SYMBOLS = [
+    "mph_config_default", "mph_read_data_file", "mph_read_grid_header", "mph_read_grid_particles",
+    "mph_write_prof_arrays", "mph_write_vtk_arrays", "mph_create", "mph_step", "mph_synchronize",
+    "mph_get", "mph_set", "mph_particle_count", "mph_time", "mph_get_scalars", "mph_write_prof",
+    "mph_write_vtk", "mph_last_error", "mph_destroy", "mph_profile_steps", "mph_neighbor_stats",
+    "mph_dist_unique_id", "mph_create_dist", "mph_owned_count", "mph_derive_scalars",
+]
+
+
+class MphError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__("%s (%d): %s" % (STATUS.get(code, "?"), code, msg))
+        self.code = code
+
+
+def build(verbose: bool = False) -> str:
+    """Compile libmph_gpu.so and mph_explicit for gfx950 (hipcc, in-tree)."""
+    r = subprocess.run(["make", "-C", CSRC_DIR, "-j8"], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("building libmph_gpu.so failed:\n" + r.stdout + r.stderr)
+    if verbose:
+        print(r.stdout)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def load_library() -> ctypes.CDLL:
+    """Load libmph_gpu.so (fails loudly when it is missing -- there is no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libmph_gpu.so not built (run particlemethod_fsi_amd.solver.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, ip, dp = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+    cfgp = ctypes.POINTER(mphio.MphConfig)
+    sig = {
+        "mph_config_default": (ip, [cfgp, ip, ip]),
+        "mph_read_data_file": (ip, [ctypes.c_char_p, cfgp]),
+        "mph_read_grid_header": (ip, [ctypes.c_char_p, cfgp, ctypes.POINTER(ctypes.c_int)]),
+        "mph_read_grid_particles": (ip, [ctypes.c_char_p, ip, vp, vp, vp, vp]),
+        "mph_write_prof_arrays": (ip, [ctypes.c_char_p, cfgp, dp, ip, vp, vp, vp, vp]),
+        "mph_write_vtk_arrays": (ip, [ctypes.c_char_p, ip] + [vp] * 10),
+        "mph_create": (ip, [ctypes.POINTER(vp), cfgp, ip, vp, vp, vp, vp, ip]),
+        "mph_step": (ip, [vp, ip]),
+        "mph_synchronize": (ip, [vp]),
+        "mph_get": (ip, [vp, ip, vp]),
+        "mph_set": (ip, [vp, ip, vp]),
+        "mph_particle_count": (ip, [vp]),
+        "mph_time": (dp, [vp]),
+        "mph_get_scalars": (ip, [vp, vp]),
+        "mph_write_prof": (ip, [vp, ctypes.c_char_p]),
+        "mph_write_vtk": (ip, [vp, ctypes.c_char_p]),
+        "mph_last_error": (ctypes.c_char_p, [vp]),
+        "mph_destroy": (None, [vp]),
+        "mph_profile_steps": (ip, [vp, ip, vp, vp, vp]),
+        "mph_neighbor_stats": (ip, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
+        "mph_dist_unique_id": (ip, [vp]),
+        "mph_create_dist": (ip, [ctypes.POINTER(vp), cfgp, ip, vp, vp, vp, vp, ip, ip, ip, vp, ip]),
+        "mph_owned_count": (ip, [vp]),
+        "mph_derive_scalars": (ip, [cfgp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def read_case_files(data_path: str, grid_path: str, dim: int, module: str | int = "bar"):
+    """readDataFile + readGridFile through the C++ host layer -> (MphConfig, Particles)."""
+    L = load_library()
+    cfg = mphio.MphConfig()
+    mod = mphio.MODULES[module] if isinstance(module, str) else int(module)
+    _check(L.mph_config_default(ctypes.byref(cfg), int(dim), mod))
+    _check(L.mph_read_data_file(data_path.encode(), ctypes.byref(cfg)))
+    n = ctypes.c_int(0)
+    _check(L.mph_read_grid_header(grid_path.encode(), ctypes.byref(cfg), ctypes.byref(n)))
+    N = n.value
+    prop = np.zeros(N, np.int32)
+    pos, pos0, vel = (np.zeros((N, 3)) for _ in range(3))
+    _check(L.mph_read_grid_particles(grid_path.encode(), N, prop.ctypes.data, pos.ctypes.data,
+                                     pos0.ctypes.data, vel.ctypes.data))
+    return cfg, mphio.Particles(prop, pos, pos0, vel)
+
+
+def derive_scalars(cfg: mphio.MphConfig) -> np.ndarray:
+    """Derived constants of initializeWeight/Fluid/Wall/Domain, host only (no device needed)."""
+    out = np.zeros(36)
+    _check(load_library().mph_derive_scalars(ctypes.byref(cfg), out.ctypes.data))
+    return out
+
+
+def _check(rc, ctx=None):
+    if rc < 0:
+        msg = ""
+        if ctx is not None:
+            msg = (load_library().mph_last_error(ctx) or b"").decode()
+        raise MphError(rc, msg)
+    return rc
+
+
+class MphSolver:
+    """One MI355X context running the reference hot path (see module docstring)."""
+
+    def __init__(self, cfg: mphio.MphConfig, parts: mphio.Particles, device: int = 0):
+        L = load_library()
+        self._L = L
+        self.cfg = cfg.copy()
+        self.n = parts.n
+        self._arrays = [np.ascontiguousarray(parts.property, np.int32),
+                        np.ascontiguousarray(parts.position, np.float64),
+                        np.ascontiguousarray(parts.initial_position, np.float64),
+                        np.ascontiguousarray(parts.velocity, np.float64)]
+        h = ctypes.c_void_p()
+        rc = L.mph_create(ctypes.byref(h), ctypes.byref(self.cfg), self.n,
+                          *[a.ctypes.data for a in self._arrays], int(device))
+        if rc < 0:
+            msg = (L.mph_last_error(h) or b"").decode() if h.value else ""
+            raise MphError(rc, msg or "mph_create failed")
+        self._h = h
+
+    @classmethod
+    def from_files(cls, data_path: str, grid_path: str, dim: int, module="bar", device: int = 0):
+        cfg, parts = read_case_files(data_path, grid_path, dim, module)
+        return cls(cfg, parts, device)
+
+    # -- lifecycle -------------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._L.mph_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- stepping ----------------------------------------------------------------------------
+    def step(self, k: int = 1):
+        _check(self._L.mph_step(self._h, int(k)), self._h)
+
+    def synchronize(self):
+        _check(self._L.mph_synchronize(self._h), self._h)
+
+    @property
+    def time(self) -> float:
+        return self._L.mph_time(self._h)
+
+    # -- data ----------------------------------------------------------------------------------
+    def get(self, name: str) -> np.ndarray:
+        fid, w, dt = FIELDS[name]
+        shape = (self.n,) if w == 1 else ((self.n, 3) if w == 3 else (self.n, 3, 3))
+        out = np.zeros(shape, dt)
+        _check(self._L.mph_get(self._h, fid, out.ctypes.data), self._h)
+        return out
+
+    def set(self, name: str, values: np.ndarray):
+        fid, _, _ = FIELDS[name]
+        arr = np.ascontiguousarray(values, np.float64)
+        _check(self._L.mph_set(self._h, fid, arr.ctypes.data), self._h)
+
+    def scalars(self) -> np.ndarray:
+        out = np.zeros(36)
+        _check(self._L.mph_get_scalars(self._h, out.ctypes.data), self._h)
+        return out
+
+    def write_vtk(self, path: str):
+        _check(self._L.mph_write_vtk(self._h, path.encode()), self._h)
+
+    def write_prof(self, path: str):
+        _check(self._L.mph_write_prof(self._h, path.encode()), self._h)
+
+    # -- measurement ----------------------------------------------------------------------------
+    def profile(self, nsteps: int) -> dict:
+        """Per-kernel average duration (ms) over nsteps, HIP events around every launch."""
+        avg = np.zeros(24)
+        cnt = np.zeros(24, np.int32)
+        names = ctypes.create_string_buffer(24 * 32)
+        k = _check(self._L.mph_profile_steps(self._h, int(nsteps), avg.ctypes.data, cnt.ctypes.data,
+                                             ctypes.addressof(names)), self._h)
+        raw = names.raw
+        out = {}
+        for i in range(k):
+            nm = raw[32 * i:32 * (i + 1)].split(b"\0", 1)[0].decode()
+            out[nm] = {"avg_ms": float(avg[i]), "launches": int(cnt[i])}
+        return out
+
+    def neighbor_stats(self):
+        m = ctypes.c_double()
+        x = ctypes.c_int()
+        _check(self._L.mph_neighbor_stats(self._h, ctypes.byref(m), ctypes.byref(x)), self._h)
+        return m.value, x.value

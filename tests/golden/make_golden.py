@@ -1,0 +1,115 @@
+"""Generate the golden vectors of tests/golden/ from the REFERENCE solver itself.
+
+Runs oracle/_ref/libmphref_<dim>_<module>.so (the reference's src/main.cpp compiled from
+/root/reference by oracle/Makefile, driven by oracle/ref_harness.inc) on the cases of
+particlemethod_fsi_amd/cases.py and stores snapshots as compressed .npz fixtures:
+
+  <case>.npz   s0/*  after the reference's initialisation (main.cpp:564-570)
+               s<k>/* after k time steps (main.cpp:597-686 each)
+               scalars (the 36 derived constants), meta (json)
+  dam2d_output.vtk.gz / dam2d_000.prof.gz   the reference writers' output at step 0
+
+Entries the reference leaves uninitialised (malloc'd and never written -- DensityA and
+GravityCenter of structure particles, DivergenceP/PressureA before the first step) are stored
+as NaN and skipped by the tests.  Each case runs in its own process because the reference
+keeps its state in file-scope globals.
+
+Usage:  python tests/golden/make_golden.py [case ...]
+"""
+from __future__ import annotations
+
+import gzip
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+FULL = ["Position", "Velocity", "Force", "Acceleration", "GravityCenter", "PressureP", "PressureA",
+        "DensityA", "VolStrainP", "DivergenceP", "NeighborCount"]
+SHORT = ["Position", "Velocity", "PressureP", "NeighborCount"]
+SOLID = ["DeformGradient", "Strain", "Stress"]
+INIT = ["NeighborCount", "DensityA", "VolStrainP", "GravityCenter", "InitialStructureNeighborCount",
+        "Normalizer", "LambdaLames", "MuLames"]
+
+PLAN = {  # case -> steps (cumulative) to snapshot; the first is the full-field snapshot
+    "dam2d": [1, 10, 100, 1000],
+    "gate2d": [1, 10, 100],
+    "bar2d": [1, 10, 100],
+    "box3d": [1, 10],
+    "gate3d": [1, 10],
+}
+
+
+def run_case(name: str):
+    from oracle_bindings import RefSolver, write_case_files
+    from particlemethod_fsi_amd import cases
+    c = cases.get(name)
+    tmp = tempfile.mkdtemp(prefix="golden_")
+    dp, gp = write_case_files(cases.data_text(c.data()), c.grid_text(), tmp)
+    ref = RefSolver(c.dim, c.module, dp, gp)
+    ref.init()
+    prop = ref.get("Property")
+    solid = (prop >= 2) & (prop < 4)
+    out = {"scalars": ref.scalars(), "Property": prop}
+
+    def snap(tag, names, stepped):
+        for f in names:
+            a = ref.get(f)
+            if f in ("DensityA", "GravityCenter"):
+                a = a.astype(np.float64)
+                a[solid] = np.nan
+            if not stepped and f in ("DivergenceP", "PressureA"):
+                a = np.full_like(a, np.nan)
+            if f in SOLID or f in ("Normalizer", "LambdaLames", "MuLames"):
+                a = a[solid]
+            out["%s/%s" % (tag, f)] = a
+
+    snap("s0", INIT, False)
+    if name == "dam2d":
+        ref.write_vtk(os.path.join(tmp, "output.vtk"))
+        ref.write_prof(os.path.join(tmp, "dam000.prof"))
+        for src, dst in (("output.vtk", "dam2d_output.vtk.gz"), ("dam000.prof", "dam2d_000.prof.gz")):
+            raw = open(os.path.join(tmp, src), "rb").read()
+            with gzip.GzipFile(os.path.join(HERE, dst), "wb", mtime=0) as fh:
+                fh.write(raw)
+            out["sha256/" + src] = np.frombuffer(hashlib.sha256(raw).digest(), np.uint8)
+    done = 0
+    for k, s in enumerate(PLAN[name]):
+        ref.step(s - done)
+        done = s
+        names = FULL if k == 0 else SHORT
+        if solid.any():
+            names = names + SOLID
+        snap("s%d" % s, names, True)
+        if k == 0 and name == "dam2d":
+            rows = [np.sort(ref.neighbors(i)) for i in range(ref.n)]
+            out["s%d/nbr_offsets" % s] = np.cumsum([0] + [len(r) for r in rows]).astype(np.int32)
+            out["s%d/nbr_ids" % s] = np.concatenate(rows).astype(np.int32)
+    meta = {"case": name, "n": int(ref.n), "dim": c.dim, "module": c.module, "steps": PLAN[name],
+            "time": ref.time, "generator": "tests/golden/make_golden.py",
+            "reference": "oracle/_ref/libmphref_%dd_%s.so" % (c.dim, c.module)}
+    out["meta"] = np.frombuffer(json.dumps(meta).encode(), np.uint8)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print(name, "n=%d" % ref.n, "->", os.path.getsize(os.path.join(HERE, name + ".npz")), "bytes")
+
+
+def main(argv):
+    names = argv or list(PLAN)
+    if len(names) == 1:
+        run_case(names[0])
+        return
+    for nm in names:   # one process per case (the reference uses globals)
+        subprocess.run([sys.executable, __file__, nm], check=True, stderr=subprocess.DEVNULL)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -1,0 +1,141 @@
+"""GPU parity: the HIP path (libmph_gpu.so through the C ABI) against the reference's golden
+vectors and against the CPU oracle on the same inputs.
+
+Tolerances (FP64; the GPU sums neighbours in its own order with FMA, so results differ from the
+reference by reassociation only; SURVEY 8c measured the chaotic growth of such differences):
+  * NeighborCount / InitialStructureNeighborCount:  bit-exact (integer).
+  * positions:   |dx|_inf <= 1e-12 m up to 100 steps, <= 1e-10 m at 1000 steps (dx = 1e-3 m).
+  * velocities:  |dv|_inf <= 1e-9 m/s up to 100 steps, <= 1e-7 m/s at 1000 steps.
+  * pressures / other per-step sums (one step): |d|_inf <= 1e-9 * max|ref| + 1e-12;
+    PressureP at 10/100 steps <= 1e-8 * max|P| + 1e-9, at 1000 steps <= 1e-6 * max|P|.
+  * elastic tensors (DeformGradient, Strain, Stress): <= 1e-9 * max|ref| + 1e-12.
+"""
+import numpy as np
+import pytest
+
+from golden_utils import CASES, Golden, restrict
+from particlemethod_fsi_amd import MphSolver, cases
+
+pytestmark = pytest.mark.gpu
+
+
+def tol(field: str, step: int, ref: np.ndarray) -> float:
+    scale = float(np.nanmax(np.abs(ref))) if ref.size and ref.dtype.kind == "f" else 0.0
+    long = step >= 1000
+    if field == "Position":
+        return 1e-10 if long else 1e-12
+    if field == "Velocity":
+        return 1e-7 if long else 1e-9
+    if field == "PressureP" and step > 1:
+        return (1e-6 * scale) if long else (1e-8 * scale + 1e-9)
+    return 1e-9 * scale + 1e-12
+
+
+def compare(g: Golden, solver: MphSolver, step: int):
+    report = {}
+    for f in g.fields(step):
+        ref = g.get(step, f)
+        mine = restrict(g, f, solver.get(f))
+        if ref.dtype.kind != "f":
+            assert np.array_equal(mine, ref), "%s step %d %s: %d mismatches" % (
+                g.case, step, f, int((mine != ref).sum()))
+            continue
+        m = ~np.isnan(ref)
+        err = float(np.max(np.abs(mine[m] - ref[m]))) if m.any() else 0.0
+        report[f] = err
+        t = tol(f, step, ref[m])
+        assert err <= t, "%s step %d %s: max|diff| %.3e > tol %.3e" % (g.case, step, f, err, t)
+    return report
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_gpu_matches_reference_golden(case):
+    g = Golden(case)
+    cfg, parts = cases.get(case).build()
+    with MphSolver(cfg, parts) as s:
+        assert np.array_equal(s.scalars(), g.z["scalars"])
+        compare(g, s, 0)
+        done = 0
+        for step in g.steps:
+            s.step(step - done)
+            done = step
+            compare(g, s, step)
+        assert abs(s.time - g.meta["time"]) == 0.0
+
+
+@pytest.mark.parametrize("case", ["dam2d", "gate3d"])
+def test_gpu_matches_oracle_every_step(case):
+    """Step-by-step against the oracle for 20 steps: all fields, including the ones the golden
+    files do not store at every step (Force, DensityA, GravityCenter, VolStrainP, ...)."""
+    from oracle_bindings import OracleSolver
+    cfg, parts = cases.get(case).build()
+    o = OracleSolver(cfg, parts)
+    o.init()
+    solid = (parts.property >= 2) & (parts.property < 4)
+    with MphSolver(cfg, parts) as s:
+        for k in range(20):
+            s.step(1)
+            o.step(1)
+            assert np.array_equal(s.get("NeighborCount"), o.get("NeighborCount")), k
+            for f in ["Position", "Velocity", "Force", "PressureP", "VolStrainP", "DivergenceP",
+                      "DensityA", "GravityCenter", "Acceleration", "Kappa"]:
+                a, b = s.get(f), o.get(f)
+                if f in ("DensityA", "GravityCenter"):
+                    a, b = a[~solid], b[~solid]
+                scale = float(np.max(np.abs(b))) if b.size else 0.0
+                t = {"Position": 1e-12, "Velocity": 1e-9}.get(f, 1e-8 * scale + 1e-11)
+                assert float(np.max(np.abs(a - b))) <= t, (k, f, float(np.max(np.abs(a - b))), t)
+            if solid.any():
+                for f in ["DeformGradient", "Stress", "Strain"]:
+                    a, b = s.get(f)[solid], o.get(f)[solid]
+                    t = 1e-9 * float(np.max(np.abs(b))) + 1e-12
+                    assert float(np.max(np.abs(a - b))) <= t, (k, f)
+
+
+def test_gpu_neighbor_sets_exact_dam():
+    """NeighborCount is exact by construction; check the acceptance itself on the golden lists:
+    every reference neighbour is within the cutoff the GPU uses and counts agree per particle."""
+    g = Golden("dam2d")
+    cfg, parts = cases.get("dam2d").build()
+    with MphSolver(cfg, parts) as s:
+        s.step(1)
+        nc = s.get("NeighborCount")
+        off = g.get(1, "nbr_offsets")
+        assert np.array_equal(nc, np.diff(off))
+
+
+def test_gpu_deterministic_rerun():
+    cfg, parts = cases.get("gate2d").build()
+    outs = []
+    for _ in range(2):
+        with MphSolver(cfg, parts) as s:
+            s.step(25)
+            outs.append((s.get("Position"), s.get("Velocity"), s.get("PressureP")))
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+
+
+def test_gpu_vtk_byte_identical_at_step0(tmp_path):
+    import gzip
+    import hashlib
+    import os
+    g = Golden("dam2d")
+    cfg, parts = cases.get("dam2d").build()
+    with MphSolver(cfg, parts) as s:
+        p = str(tmp_path / "output.vtk")
+        s.write_vtk(p)
+        assert hashlib.sha256(open(p, "rb").read()).digest() == bytes(g.z["sha256/output.vtk"])
+        q = str(tmp_path / "dam000.prof")
+        s.write_prof(q)
+        assert hashlib.sha256(open(q, "rb").read()).digest() == bytes(g.z["sha256/dam000.prof"])
+
+
+def test_gpu_graph_chunking_equivalence():
+    """mph_step(8) (one 8-step graph) == 8 x mph_step(1) bitwise."""
+    cfg, parts = cases.get("box3d").build()
+    with MphSolver(cfg, parts) as a, MphSolver(cfg, parts) as b:
+        a.step(8)
+        for _ in range(8):
+            b.step(1)
+        assert np.array_equal(a.get("Position"), b.get("Position"))
+        assert np.array_equal(a.get("Velocity"), b.get("Velocity"))
