@@ -152,6 +152,13 @@ int mph_write_vtk_arrays(const char* path, int n, const int* property, const dou
 /* Every constant the reference derives before its time loop (initializeWeight/Fluid/Wall/Domain,
  * main.cpp:1191-1469), without a device: 36 doubles in the slot order of mph_get_scalars.      */
 int mph_derive_scalars(const MphConfig* cfg, double* out36);
+/* Host-side initialisation of the elastic solid that mph_create performs: the fixed Lagrangian
+ * neighbour lists (calculateInitialNeighbor, main.cpp:1497-1658), calculateLamesconstant
+ * (2526-2540) and calculateNormalizer (2544-2653).  Outputs are per particle, original order,
+ * zero for non-structure particles: isnc int[n], normalizer double[n][3][3], lame_l/lame_m
+ * double[n].  Any output pointer may be NULL.                                                   */
+int mph_structure_init(const MphConfig* cfg, int n, const int* property, const double* pos0,
+                       int* isnc, double* normalizer, double* lame_l, double* lame_m);
 
 /* ---- device context ------------------------------------------------------------------------ */
 

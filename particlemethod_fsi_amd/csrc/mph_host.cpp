@@ -232,6 +232,30 @@ extern "C" int mph_derive_scalars(const MphConfig* cfg, double* out36)
     return MPH_OK;
 }
 
+extern "C" int mph_structure_init(const MphConfig* cfg, int n, const int* prop, const double* pos0,
+                                  int* isnc, double* normalizer, double* lame_l, double* lame_m)
+{
+    if (!cfg || n < 0 || (n > 0 && (!prop || !pos0))) return MPH_ERR_ARG;
+    mph::HostDerived h;
+    mph::derive_constants(*cfg, h);
+    mph::StructureInit S;
+    std::string err;
+    const int rc = mph::build_structure(*cfg, h, n, prop, pos0, S, err);
+    if (rc != MPH_OK) return rc;
+    if (isnc) std::memset(isnc, 0, sizeof(int) * (size_t)n);
+    if (normalizer) std::memset(normalizer, 0, sizeof(double) * 9 * (size_t)n);
+    if (lame_l) std::memset(lame_l, 0, sizeof(double) * (size_t)n);
+    if (lame_m) std::memset(lame_m, 0, sizeof(double) * (size_t)n);
+    for (size_t s = 0; s < S.orig.size(); ++s) {
+        const int i = S.orig[s];
+        if (isnc) isnc[i] = S.count[s];
+        if (normalizer) std::memcpy(normalizer + (size_t)9 * i, &S.normalizer[9 * s], sizeof(double) * 9);
+        if (lame_l) lame_l[i] = S.lame_l[s];
+        if (lame_m) lame_m[i] = S.lame_m[s];
+    }
+    return MPH_OK;
+}
+
 namespace mph {
 
 // ---- derived constants: initializeWeight/Fluid/Wall/Domain (main.cpp:1191-1469) ------------
@@ -459,8 +483,6 @@ int build_structure(const MphConfig& c, const HostDerived& h, int n, const int* 
         next[s] = head[k];
         head[k] = s;
     }
-    std::vector<int> local(ns, -1);   // orig index -> structure slot
-    for (int s = 0; s < ns; ++s) local[S.orig[s]] = s;
     std::vector<std::vector<int>> rows(ns);
     for (int s = 0; s < ns; ++s) {
         const int i = S.orig[s];

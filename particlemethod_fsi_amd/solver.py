@@ -49,6 +49,7 @@ EXPORTED_SYMBOLS = [
     "mph_get", "mph_set", "mph_particle_count", "mph_time", "mph_get_scalars", "mph_write_prof",
     "mph_write_vtk", "mph_last_error", "mph_destroy", "mph_profile_steps", "mph_neighbor_stats",
     "mph_dist_unique_id", "mph_create_dist", "mph_owned_count", "mph_derive_scalars",
+    "mph_structure_init",
 ]
 
 
@@ -106,6 +107,7 @@ def load_library() -> ctypes.CDLL:
         "mph_create_dist": (ip, [ctypes.POINTER(vp), cfgp, ip, vp, vp, vp, vp, ip, ip, ip, vp, ip]),
         "mph_owned_count": (ip, [vp]),
         "mph_derive_scalars": (ip, [cfgp, vp]),
+        "mph_structure_init": (ip, [cfgp, ip, vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -126,3 +126,24 @@ def test_data_reader_keeps_partial_lists_and_ignores_unknown_lines():
         assert bytes(cfg) == bytes(cfg2)
         assert cfg.dt == 2e-4 and list(cfg.density)[:3] == [1.0, 2.0, 3.0]
         assert list(cfg.wall_omega[4]) == [7.0, 8.0, 9.0] and cfg.gravity[1] == -9.8
+
+
+@pytest.mark.parametrize("case", ["bar2d", "gate2d", "gate3d"])
+def test_structure_init_matches_reference(case):
+    """calculateInitialNeighbor / Lamesconstant / Normalizer as done by mph_create (host)."""
+    g = Golden(case)
+    cfg, p = cases.get(case).build()
+    n = p.n
+    L = solver.load_library()
+    isnc = np.zeros(n, np.int32)
+    N = np.zeros((n, 3, 3))
+    ll, lm = np.zeros(n), np.zeros(n)
+    assert L.mph_structure_init(ctypes.byref(cfg), n, p.property.ctypes.data,
+                                p.initial_position.ctypes.data, isnc.ctypes.data, N.ctypes.data,
+                                ll.ctypes.data, lm.ctypes.data) == 0
+    assert np.array_equal(isnc, g.get(0, "InitialStructureNeighborCount"))
+    assert np.array_equal(ll[g.solid], g.get(0, "LambdaLames"))
+    assert np.array_equal(lm[g.solid], g.get(0, "MuLames"))
+    ref = g.get(0, "Normalizer")
+    # neighbour sums in slot order instead of the reference's cell-scan order: reassociation only
+    assert np.max(np.abs(N[g.solid] - ref)) <= 1e-12 * np.max(np.abs(ref))
