@@ -1,0 +1,15 @@
+#!/bin/bash
+# Diagnostic PMC passes (one rocprofv3 --pmc run per counter group) on a short bench.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/pmc
+mkdir -p $OUT
+CASE=${CASE:-d1m}
+timeout -k 10 120 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
+i=0
+for grp in "$@"; do
+  i=$((i+1))
+  timeout -k 10 600 rocprofv3 --pmc $grp --output-format csv -d $OUT/g$i -o g$i -- \
+      python3 bench.py --case $CASE --steps 3 --warmup 1 --no-cpu-baseline --profile-steps 1 > $OUT/g$i.log 2>&1 || exit 30
+done
