@@ -178,5 +178,25 @@ _reg(Case("gate3d", 3, "dam", 0.001, (-0.01, 0.0, -0.01), (0.05, 0.05, 0.018), [
 ]))
 
 
+# surface-tension variants (the reference example has SurfaceTension = 0): exercise PressureA
+# (main.cpp:2212-2259) and DiffuseInterface (2261-2312) with asymmetric InteractionRatio tables
+_ST = {"SurfaceTension": [0.072, 0.05, 0.03, 0.01],
+       "InteractionRatio(Type1)": [1.0, 1.0, 1.0, 1.0, 0.5, 0.7],
+       "InteractionRatio(Type4)": [1.0, 0.8, 1.0, 1.0, 1.0, 1.0]}
+_reg(Case("dam2d_st", 2, "bar", 0.001, CASES["dam2d"].lower, CASES["dam2d"].upper,
+          CASES["dam2d"].cuboids, data_changes=_ST, note="dam2d with surface tension"))
+_reg(Case("box3d_st", 3, "dam", 0.001, CASES["box3d"].lower, CASES["box3d"].upper,
+          CASES["box3d"].cuboids, data_changes=_ST, note="box3d with surface tension"))
+
+
+# elastic sub-stepping (main.cpp:653-663): ElasticDt = Dt/5 -> 5 substeps per step.  With the
+# example's ElasticDt = Dt the 3-D gate runs at dt*c/dx ~ 1 and (with the doubled drift of
+# updateElasticPosition) goes unstable after ~20 steps; sub-stepping keeps it stable.
+_reg(Case("gate2d_sub", 2, "dam", 0.001, CASES["gate2d"].lower, CASES["gate2d"].upper,
+          CASES["gate2d"].cuboids, data_changes={"ElasticDt": [2e-5]}, note="gate2d, 5 substeps"))
+_reg(Case("gate3d_sub", 3, "dam", 0.001, CASES["gate3d"].lower, CASES["gate3d"].upper,
+          CASES["gate3d"].cuboids, data_changes={"ElasticDt": [2.5e-5]}, note="gate3d, 4 substeps"))
+
+
 def get(name: str) -> Case:
     return CASES[name]

@@ -36,11 +36,12 @@ struct MphCtx {
     // device
     DevTables* dT = nullptr;
     DevState* dst = nullptr;
-    double4 *xa = nullptr, *va = nullptr, *xb = nullptr, *vb = nullptr;
-    int *ida = nullptr, *idb = nullptr, *rank_of = nullptr;
+    Soa A, B;                    // sorted current state / integrated state (see mph_kernels.h)
+    int* rank_of = nullptr;
     int *key = nullptr, *slot = nullptr, *tmp = nullptr, *cnt = nullptr, *start = nullptr, *bsum = nullptr;
     int *nbr = nullptr, *ncount = nullptr;
-    double4 *pv = nullptr, *gca = nullptr, *force = nullptr, *acc = nullptr;
+    double *pres = nullptr, *gx = nullptr, *gy = nullptr, *gz = nullptr, *pa = nullptr;
+    double4 *force = nullptr, *acc = nullptr;
     double *dens_a = nullptr, *vstrain = nullptr, *divp = nullptr;
     StructDev Sd;
     std::vector<void*> allocs;
@@ -92,11 +93,11 @@ void fill_launch(MphCtx* c)
     L.st = c->dst;
     L.stream = c->stream;
     L.prof = nullptr;
-    L.xa = c->xa; L.va = c->va; L.xb = c->xb; L.vb = c->vb;
-    L.ida = c->ida; L.idb = c->idb; L.rank_of = c->rank_of;
+    L.A = c->A; L.B = c->B; L.rank_of = c->rank_of;
     L.key = c->key; L.slot = c->slot; L.tmp = c->tmp; L.cnt = c->cnt; L.start = c->start; L.bsum = c->bsum;
     L.nbr = c->nbr; L.ncount = c->ncount;
-    L.pv = c->pv; L.gca = c->gca; L.force = c->force; L.acc = c->acc;
+    L.pres = c->pres; L.gx = c->gx; L.gy = c->gy; L.gz = c->gz; L.pa = c->pa;
+    L.force = c->force; L.acc = c->acc;
     L.dens_a = c->dens_a; L.vstrain = c->vstrain; L.divp = c->divp;
     L.S = &c->Sd;
 }
@@ -148,6 +149,24 @@ int download_scalar(MphCtx* c, const T* d, const int* ids, T* out)
     HIP_OK(c, hipMemcpyAsync(id.data(), ids, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipStreamSynchronize(c->stream));
     for (int i = 0; i < n; ++i) out[id[i]] = h[i];
+    return MPH_OK;
+}
+
+// three SoA component arrays -> AoS double[n][3] in original order
+int download_soa3(MphCtx* c, const double* dx, const double* dy, const double* dz, const int* ids,
+                  double* out)
+{
+    const int n = c->n;
+    std::vector<double> h(3 * (size_t)n);
+    std::vector<int> id(n);
+    const double* src[3] = {dx, dy, dz};
+    for (int k = 0; k < 3; ++k)
+        HIP_OK(c, hipMemcpyAsync(h.data() + (size_t)k * n, src[k], sizeof(double) * n, hipMemcpyDeviceToHost,
+                                 c->stream));
+    HIP_OK(c, hipMemcpyAsync(id.data(), ids, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k) out[3 * (size_t)id[i] + k] = h[(size_t)k * n + i];
     return MPH_OK;
 }
 
@@ -229,6 +248,16 @@ int mph_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, c
         if (r != MPH_OK) return fail(c, r, err);
     }
     c->P.ncell = c->P.gc[0] * c->P.gc[1] * c->P.gc[2];
+    // interior box for the wave-uniform fast minimum image (k_neighbors / passes): >= 3 cells
+    // (+1e-9 relative margin) from every periodic face; needs > 12 cells on every active axis
+    c->P.fast_ok = 1;
+    for (int d = 0; d < 3; ++d) {
+        if (d == 2 && cfg->dim == 2) { c->P.inner_lo[d] = -1e300; c->P.inner_hi[d] = 1e300; continue; }
+        if (c->P.gc[d] <= 12) c->P.fast_ok = 0;
+        const double cw = c->h.dw[d] / c->P.gc[d];
+        c->P.inner_lo[d] = c->h.dmin[d] + 3.0 * cw * (1.0 + 1e-9);
+        c->P.inner_hi[d] = c->h.dmax[d] - 3.0 * cw * (1.0 + 1e-9);
+    }
     // tables
     for (int t = 0; t < kTypes; ++t) {
         for (int u = 0; u < kTypes; ++u) {
@@ -245,13 +274,18 @@ int mph_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, c
     const size_t ntile = ((size_t)n + kTile - 1) / kTile;
     CK(dalloc(c, &c->dT, 1));
     CK(dalloc(c, &c->dst, 1));
-    CK(dalloc(c, &c->xa, n)); CK(dalloc(c, &c->va, n)); CK(dalloc(c, &c->xb, n)); CK(dalloc(c, &c->vb, n));
-    CK(dalloc(c, &c->ida, n)); CK(dalloc(c, &c->idb, n)); CK(dalloc(c, &c->rank_of, n));
+    for (Soa* s : {&c->A, &c->B}) {
+        CK(dalloc(c, &s->x, n)); CK(dalloc(c, &s->y, n)); CK(dalloc(c, &s->z, n));
+        CK(dalloc(c, &s->vx, n)); CK(dalloc(c, &s->vy, n)); CK(dalloc(c, &s->vz, n));
+        CK(dalloc(c, &s->type, n)); CK(dalloc(c, &s->id, n));
+    }
+    CK(dalloc(c, &c->rank_of, n));
     CK(dalloc(c, &c->key, n)); CK(dalloc(c, &c->slot, n)); CK(dalloc(c, &c->tmp, n));
     CK(dalloc(c, &c->cnt, c->P.ncell)); CK(dalloc(c, &c->start, (size_t)c->P.ncell + 1));
     CK(dalloc(c, &c->bsum, (size_t)c->P.ncell / 4096 + 2));
     CK(dalloc(c, &c->nbr, ntile * kTile * kMaxNeighbor)); CK(dalloc(c, &c->ncount, n));
-    CK(dalloc(c, &c->pv, n)); CK(dalloc(c, &c->gca, n)); CK(dalloc(c, &c->force, n)); CK(dalloc(c, &c->acc, n));
+    CK(dalloc(c, &c->pres, n)); CK(dalloc(c, &c->gx, n)); CK(dalloc(c, &c->gy, n)); CK(dalloc(c, &c->gz, n));
+    CK(dalloc(c, &c->pa, n)); CK(dalloc(c, &c->force, n)); CK(dalloc(c, &c->acc, n));
     CK(dalloc(c, &c->dens_a, n)); CK(dalloc(c, &c->vstrain, n)); CK(dalloc(c, &c->divp, n));
     HIP_OK(c, hipMemsetAsync(c->cnt, 0, sizeof(int) * c->P.ncell, c->stream));
     HIP_OK(c, hipMemsetAsync(c->force, 0, sizeof(double4) * std::max(n, 1), c->stream));
@@ -268,17 +302,18 @@ int mph_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, c
         }
     HIP_OK(c, hipMemcpyAsync(c->dst, &st, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
     {
-        std::vector<double4> hx(n), hv(n);
-        std::vector<int> id(n);
-        for (int i = 0; i < n; ++i) {
-            hx[i] = make_double4(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2], (double)property[i]);
-            hv[i] = make_double4(vel[3 * i], vel[3 * i + 1], vel[3 * i + 2], 0.0);
-            id[i] = i;
+        // upload into the B set (original order, id = file index); the init sort reorders it
+        std::vector<double> comp(n);
+        std::vector<int> ids(n);
+        double* dstc[6] = {c->B.x, c->B.y, c->B.z, c->B.vx, c->B.vy, c->B.vz};
+        for (int k = 0; k < 6; ++k) {
+            const double* src = k < 3 ? pos : vel;
+            for (int i = 0; i < n; ++i) comp[i] = src[3 * i + (k % 3)];
+            HIP_OK(c, hipMemcpy(dstc[k], comp.data(), sizeof(double) * n, hipMemcpyHostToDevice));
         }
-        HIP_OK(c, hipMemcpyAsync(c->xb, hx.data(), sizeof(double4) * n, hipMemcpyHostToDevice, c->stream));
-        HIP_OK(c, hipMemcpyAsync(c->vb, hv.data(), sizeof(double4) * n, hipMemcpyHostToDevice, c->stream));
-        HIP_OK(c, hipMemcpyAsync(c->idb, id.data(), sizeof(int) * n, hipMemcpyHostToDevice, c->stream));
-        HIP_OK(c, hipStreamSynchronize(c->stream));
+        for (int i = 0; i < n; ++i) ids[i] = i;
+        HIP_OK(c, hipMemcpy(c->B.type, property, sizeof(int) * n, hipMemcpyHostToDevice));
+        HIP_OK(c, hipMemcpy(c->B.id, ids.data(), sizeof(int) * n, hipMemcpyHostToDevice));
     }
     // elastic solid
     if (ns > 0) {
@@ -402,25 +437,25 @@ int mph_get(MphCtx* c, int field, void* out)
     int* oi = (int*)out;
     const int ns = (int)c->S.orig.size();
     switch (field) {
-    case MPH_FIELD_POSITION: return download_vec(c, c->xb, c->idb, o, 3);
-    case MPH_FIELD_VELOCITY: return download_vec(c, c->vb, c->idb, o, 3);
+    case MPH_FIELD_POSITION: return download_soa3(c, c->B.x, c->B.y, c->B.z, c->B.id, o);
+    case MPH_FIELD_VELOCITY: return download_soa3(c, c->B.vx, c->B.vy, c->B.vz, c->B.id, o);
     case MPH_FIELD_INITIAL_POSITION: std::memcpy(o, c->pos0.data(), sizeof(double) * 3 * n); return MPH_OK;
-    case MPH_FIELD_FORCE: return download_vec(c, c->force, c->ida, o, 3);
-    case MPH_FIELD_ACCELERATION: return download_vec(c, c->acc, c->ida, o, 3);
-    case MPH_FIELD_GRAVITY_CENTER: return download_vec(c, c->gca, c->ida, o, 3);
-    case MPH_FIELD_PRESSURE_P: return download_w(c, c->pv, c->ida, o);
-    case MPH_FIELD_PRESSURE_A: return download_w(c, c->gca, c->ida, o);
-    case MPH_FIELD_DENSITY_A: return download_scalar(c, c->dens_a, c->ida, o);
-    case MPH_FIELD_VOL_STRAIN_P: return download_scalar(c, c->vstrain, c->ida, o);
-    case MPH_FIELD_DIVERGENCE_P: return download_scalar(c, c->divp, c->ida, o);
-    case MPH_FIELD_NEIGHBOR_COUNT: return download_scalar(c, c->ncount, c->ida, oi);
+    case MPH_FIELD_FORCE: return download_vec(c, c->force, c->A.id, o, 3);
+    case MPH_FIELD_ACCELERATION: return download_vec(c, c->acc, c->A.id, o, 3);
+    case MPH_FIELD_GRAVITY_CENTER: return download_soa3(c, c->gx, c->gy, c->gz, c->A.id, o);
+    case MPH_FIELD_PRESSURE_P: return download_scalar(c, c->pres, c->A.id, o);
+    case MPH_FIELD_PRESSURE_A: return download_scalar(c, c->pa, c->A.id, o);
+    case MPH_FIELD_DENSITY_A: return download_scalar(c, c->dens_a, c->A.id, o);
+    case MPH_FIELD_VOL_STRAIN_P: return download_scalar(c, c->vstrain, c->A.id, o);
+    case MPH_FIELD_DIVERGENCE_P: return download_scalar(c, c->divp, c->A.id, o);
+    case MPH_FIELD_NEIGHBOR_COUNT: return download_scalar(c, c->ncount, c->A.id, oi);
     case MPH_FIELD_MASS:
         for (int i = 0; i < n; ++i) o[i] = c->cfg.density[c->prop[i]] * c->h.vol;
         return MPH_OK;
     case MPH_FIELD_KAPPA: {
         // initializeFluid (1317-1319) before the first step, calculatePhysicalCoefficients after
         std::vector<double> vs(n);
-        if (c->stepped) CK(download_scalar(c, c->vstrain, c->ida, vs.data()));
+        if (c->stepped) CK(download_scalar(c, c->vstrain, c->A.id, vs.data()));
         for (int i = 0; i < n; ++i)
             o[i] = (c->stepped && vs[i] < 0.0) ? 0.0 : c->cfg.bulk_modulus[c->prop[i]];
         return MPH_OK;
@@ -462,19 +497,16 @@ int mph_set(MphCtx* c, int field, const void* in)
     HIP_OK(c, hipSetDevice(c->device));
     const int n = c->n;
     const double* v = (const double*)in;
-    // current state lives in the B set in the order of idb: rewrite it in that order
-    std::vector<double4> h(n);
+    // current state lives in the B set in the order of B.id: rewrite it in that order
+    std::vector<double> h(n);
     std::vector<int> id(n);
-    double4* dst = field == MPH_FIELD_POSITION ? c->xb : c->vb;
-    HIP_OK(c, hipMemcpyAsync(h.data(), dst, sizeof(double4) * n, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(c, hipMemcpyAsync(id.data(), c->idb, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(c, hipStreamSynchronize(c->stream));
-    for (int i = 0; i < n; ++i) {
-        const double* s = v + 3 * (size_t)id[i];
-        h[i].x = s[0]; h[i].y = s[1]; h[i].z = s[2];
+    HIP_OK(c, hipMemcpy(id.data(), c->B.id, sizeof(int) * n, hipMemcpyDeviceToHost));
+    double* dst[3] = {c->B.x, c->B.y, c->B.z};
+    if (field == MPH_FIELD_VELOCITY) { dst[0] = c->B.vx; dst[1] = c->B.vy; dst[2] = c->B.vz; }
+    for (int k = 0; k < 3; ++k) {
+        for (int i = 0; i < n; ++i) h[i] = v[3 * (size_t)id[i] + k];
+        HIP_OK(c, hipMemcpy(dst[k], h.data(), sizeof(double) * n, hipMemcpyHostToDevice));
     }
-    HIP_OK(c, hipMemcpyAsync(dst, h.data(), sizeof(double4) * n, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(c, hipStreamSynchronize(c->stream));
     return MPH_OK;
 }
 

@@ -36,6 +36,15 @@ struct Profiler {
     virtual ~Profiler() = default;
 };
 
+// Persistent particle state, one FP64 array per component (structure of arrays): in the
+// neighbour loops consecutive lanes gather consecutive elements, so one 8-byte load per lane
+// touches ~8-10 cache lines per wavefront instead of ~40 for 32-byte records.
+struct Soa {
+    double *x = nullptr, *y = nullptr, *z = nullptr;
+    double *vx = nullptr, *vy = nullptr, *vz = nullptr;
+    int *type = nullptr, *id = nullptr;
+};
+
 // Everything one launch sequence needs.
 struct Launch {
     const DevParams* P = nullptr;
@@ -44,12 +53,14 @@ struct Launch {
     hipStream_t stream = nullptr;
     Profiler* prof = nullptr;
     // B set: integrated state in the previous order; A set: cell-sorted current order
-    double4 *xb = nullptr, *vb = nullptr, *xa = nullptr, *va = nullptr;
-    int *idb = nullptr, *ida = nullptr, *rank_of = nullptr;
+    Soa A, B;
+    int* rank_of = nullptr;
     int *key = nullptr, *slot = nullptr, *tmp = nullptr, *cnt = nullptr, *start = nullptr, *bsum = nullptr;
     int *nbr = nullptr, *ncount = nullptr;
-    double4 *pv = nullptr, *gca = nullptr, *force = nullptr, *acc = nullptr;
+    // pass A products (A order): pressure values, gravity centre (GC, PressureA), sums
+    double *pres = nullptr, *gx = nullptr, *gy = nullptr, *gz = nullptr, *pa = nullptr;
     double *dens_a = nullptr, *vstrain = nullptr, *divp = nullptr;
+    double4 *force = nullptr, *acc = nullptr;   // outputs (A order)
     const StructDev* S = nullptr;
 };
 

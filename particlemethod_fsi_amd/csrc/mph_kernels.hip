@@ -22,6 +22,10 @@
 // reference's FP64 expressions bit for bit (no contraction, IEEE division), so NeighborCount is
 // exact; the weighted sums are reassociated (own order, FMA) and agree within the tolerances
 // written in tests/.
+//
+// Memory layout: particle state is structure-of-arrays FP64 in cell-sorted order (Soa).  The
+// neighbour loops are bound by the per-CU texture-address path (profiles/r01: TA ~75% busy with
+// 32-byte records); SoA makes consecutive lanes gather consecutive doubles.
 #include <hip/hip_runtime.h>
 
 #include "mph_kernels.h"
@@ -39,14 +43,15 @@ __device__ __forceinline__ double mod_exact(double x, double w)
 }
 
 // Periodic minimum image Mod(d + w/2, w) - w/2 of every pair loop (e.g. main.cpp:1762), bit-
-// identical to the reference.  Fast path: for 0 <= s < 0.75 w, floor(s/w) == 0 exactly and
-// Mod(s,w) == s - w*0 == s, so the division is skipped.
+// identical to the reference.  For 0 <= s < 0.75 w, floor(s/w) == 0 exactly and
+// Mod(s,w) == s - w*0 == s; FAST (wave-uniform, interior particles only) relies on that always.
+template <bool FAST>
 __device__ __forceinline__ double image_exact(double d, double w, double hw, double w075)
 {
 #pragma clang fp contract(off)
     const double s = d + hw;
     double m;
-    if (__builtin_expect(s >= 0.0 && s < w075, 1)) {
+    if (FAST || __builtin_expect(s >= 0.0 && s < w075, 1)) {
         m = s;
     } else {
         m = s - w * floor(s / w);
@@ -58,6 +63,16 @@ __device__ __forceinline__ double r2_exact(double q0, double q1, double q2)
 {
 #pragma clang fp contract(off)
     return q0 * q0 + q1 * q1 + q2 * q2;
+}
+
+// r = sqrt(r2) and 1/r from v_rsq_f64 plus one Newton step (relative error ~1e-16).
+__device__ __forceinline__ void rsqrt_pair(double r2, double& r, double& ir)
+{
+    double y = __builtin_amdgcn_rsq(r2);
+    const double e = fma(-(r2 * y), y, 1.0);
+    y = fma(0.5 * y, e, y);
+    ir = y;
+    r = r2 * y;
 }
 
 __device__ __forceinline__ int wrap_cell(int c, int g)
@@ -87,6 +102,15 @@ __device__ __forceinline__ bool dev_is_struct(int t) { return t == 2 || t == 3; 
 __device__ __forceinline__ bool dev_is_fluid(int t) { return t == 0 || t == 1; }
 __device__ __forceinline__ bool dev_is_wall(int t) { return t == 4 || t == 5; }
 
+// wave-uniform: every live lane's particle is >= 3 GPU cells away from every periodic face,
+// so no stencil cell wraps and every candidate's minimum image takes the fast path.
+__device__ __forceinline__ bool wave_interior(const DevParams& P, bool live, double x, double y, double z)
+{
+    bool in = !live || (x >= P.inner_lo[0] && x <= P.inner_hi[0] && y >= P.inner_lo[1] &&
+                        y <= P.inner_hi[1] && (P.dim == 2 || (z >= P.inner_lo[2] && z <= P.inner_hi[2])));
+    return P.fast_ok && __all(in);
+}
+
 // XCD-aware block order: hardware deals consecutive blocks round-robin over the 8 XCDs; remap so
 // that each XCD sweeps one contiguous 1/8 of the (cell-sorted) particles and neighbour gathers
 // hit its own L2 (cdna_hip_programming.md T1, bijective form).
@@ -106,41 +130,40 @@ __device__ __forceinline__ const int* ell_row(const int* nbr, int i)
 
 // calculateWall (main.cpp:3031-3060) + calculatePeriodicBoundary (3322-3333) + cell histogram.
 // mode 0: initialisation (no motion), 1: time step.
-__global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __restrict__ st,
-                                              double4* __restrict__ xb, double4* __restrict__ vb,
+__global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __restrict__ st, Soa B,
                                               int* __restrict__ key, int* __restrict__ slot,
                                               int* __restrict__ cnt, int mode)
 {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P.n) return;
-    double4 x = xb[p];
+    double x = B.x[p], y = B.y[p], z = B.z[p];
     if (mode) {
 #pragma clang fp contract(off)
-        const int t = (int)x.w;
+        const int t = B.type[p];
         if (dev_is_wall(t) && st->time < 0.2) {
             const double* C = st->wall_c[t];
             const double* V = st->wall_vel[t];
             const double* w = st->wall_omega[t];
             const double (*R)[3] = st->wall_rot[t];
-            const double r0 = x.x - C[0], r1 = x.y - C[1], r2 = x.z - C[2];
+            const double r0 = x - C[0], r1 = y - C[1], r2 = z - C[2];
             const double a0 = R[0][0] * r0 + R[0][1] * r1 + R[0][2] * r2;
             const double a1 = R[1][0] * r0 + R[1][1] * r1 + R[1][2] * r2;
             const double a2 = R[2][0] * r0 + R[2][1] * r1 + R[2][2] * r2;
-            double4 v = vb[p];
-            v.x = w[1] * a2 - w[2] * a1 + V[0];
-            v.y = w[2] * a0 - w[0] * a2 + V[1];
-            v.z = w[0] * a1 - w[1] * a0 + V[2];
-            vb[p] = v;
-            x.x = a0 + C[0] + V[0] * P.dt;
-            x.y = a1 + C[1] + V[1] * P.dt;
-            x.z = a2 + C[2] + V[2] * P.dt;
+            B.vx[p] = w[1] * a2 - w[2] * a1 + V[0];
+            B.vy[p] = w[2] * a0 - w[0] * a2 + V[1];
+            B.vz[p] = w[0] * a1 - w[1] * a0 + V[2];
+            x = a0 + C[0] + V[0] * P.dt;
+            y = a1 + C[1] + V[1] * P.dt;
+            z = a2 + C[2] + V[2] * P.dt;
         }
-        x.x = mod_exact(x.x - P.dmin[0], P.dw[0]) + P.dmin[0];
-        x.y = mod_exact(x.y - P.dmin[1], P.dw[1]) + P.dmin[1];
-        x.z = mod_exact(x.z - P.dmin[2], P.dw[2]) + P.dmin[2];
-        xb[p] = x;
+        x = mod_exact(x - P.dmin[0], P.dw[0]) + P.dmin[0];
+        y = mod_exact(y - P.dmin[1], P.dw[1]) + P.dmin[1];
+        z = mod_exact(z - P.dmin[2], P.dw[2]) + P.dmin[2];
+        B.x[p] = x;
+        B.y[p] = y;
+        B.z[p] = z;
     }
-    const int k = cell_id(P, x.x, x.y, x.z);
+    const int k = cell_id(P, x, y, z);
     key[p] = k;
     slot[p] = atomicAdd(&cnt[k], 1);
 }
@@ -255,15 +278,11 @@ __global__ __launch_bounds__(256) void k_place(DevParams P, DevState* __restrict
 }
 
 // Deterministic stable order inside a cell: rank = number of cell-mates with a smaller previous
-// sorted index.  Reorders the persistent particle state (x, v, id) into the new cell order.
+// sorted index.  Reorders the persistent particle state into the new cell order.
 __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __restrict__ key,
                                                       const int* __restrict__ start,
-                                                      const int* __restrict__ tmp,
-                                                      const double4* __restrict__ xb,
-                                                      const double4* __restrict__ vb,
-                                                      const int* __restrict__ idb,
-                                                      double4* __restrict__ xa, double4* __restrict__ va,
-                                                      int* __restrict__ ida, int* __restrict__ rank_of)
+                                                      const int* __restrict__ tmp, Soa B, Soa A,
+                                                      int* __restrict__ rank_of)
 {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P.n) return;
@@ -272,10 +291,15 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
     int r = 0;
     for (int q = s; q < e; ++q) r += tmp[q] < p;
     const int dst = s + r;
-    xa[dst] = xb[p];
-    va[dst] = vb[p];
-    const int id = idb[p];
-    ida[dst] = id;
+    A.x[dst] = B.x[p];
+    A.y[dst] = B.y[p];
+    A.z[dst] = B.z[p];
+    A.vx[dst] = B.vx[p];
+    A.vy[dst] = B.vy[p];
+    A.vz[dst] = B.vz[p];
+    A.type[dst] = B.type[p];
+    const int id = B.id[p];
+    A.id[dst] = id;
     rank_of[id] = dst;
 }
 
@@ -285,54 +309,80 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
 // cells are >= rc/2 wide, so a +-2 stencil covers the acceptance sphere: 25 columns (3-D) or 5
 // (2-D) along which the cells of the last axis are contiguous in memory.  Acceptance is the
 // reference's own test  q0^2+q1^2+q2^2 <= (MaxRadius+MARGIN)^2  with the Mod-based minimum image.
-template <int DIM>
-__global__ __launch_bounds__(256) void k_neighbors(DevParams P, const double4* __restrict__ x,
-                                                   const int* __restrict__ start,
-                                                   int* __restrict__ nbr, int* __restrict__ ncount,
-                                                   DevState* __restrict__ st)
+template <int DIM, bool FAST>
+__device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A, const int* start,
+                                               int i, double xi, double yi, double zi, int cx,
+                                               int cy, int cz, int* out)
 {
-    const int i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    const bool live = i < P.n;
     int cnt = 0;
-    if (live) {
-        const double4 xi = x[i];
-        const int cx = cell_axis(xi.x, P.dmin[0], P.ginv[0], P.gc[0]);
-        const int cy = cell_axis(xi.y, P.dmin[1], P.ginv[1], P.gc[1]);
-        const int cz = DIM == 3 ? cell_axis(xi.z, P.dmin[2], P.ginv[2], P.gc[2]) : 0;
-        int* out = nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
-        constexpr int NCOL = DIM == 3 ? 25 : 5;
-        const int gca = DIM == 3 ? P.gc[2] : P.gc[1];   // contiguous axis
-        const int cca = DIM == 3 ? cz : cy;
-        for (int col = 0; col < NCOL; ++col) {
-            int base;
-            if (DIM == 3) {
-                const int jx = wrap_cell(cx + col / 5 - 2, P.gc[0]);
-                const int jy = wrap_cell(cy + col % 5 - 2, P.gc[1]);
-                base = (jx * P.gc[1] + jy) * P.gc[2];
-            } else {
-                base = wrap_cell(cx + col - 2, P.gc[0]) * P.gc[1];
-            }
-            const int lo = cca - 2, hi = cca + 2;
-            int seg_a[2], seg_b[2], nseg;
-            if (lo < 0) { seg_a[0] = lo + gca; seg_b[0] = gca - 1; seg_a[1] = 0; seg_b[1] = hi; nseg = 2; }
-            else if (hi >= gca) { seg_a[0] = lo; seg_b[0] = gca - 1; seg_a[1] = 0; seg_b[1] = hi - gca; nseg = 2; }
-            else { seg_a[0] = lo; seg_b[0] = hi; seg_a[1] = 0; seg_b[1] = -1; nseg = 1; }
-            for (int sg = 0; sg < nseg; ++sg) {
-                const int jb = start[base + seg_a[sg]];
-                const int je = start[base + seg_b[sg] + 1];
-                for (int j = jb; j < je; ++j) {
-                    const double4 xj = x[j];
-                    const double q0 = image_exact(xj.x - xi.x, P.dw[0], P.hw[0], P.w075[0]);
-                    const double q1 = image_exact(xj.y - xi.y, P.dw[1], P.hw[1], P.w075[1]);
-                    const double q2 = image_exact(xj.z - xi.z, P.dw[2], P.hw[2], P.w075[2]);
+    constexpr int NCOL = DIM == 3 ? 25 : 5;
+    const int gca = DIM == 3 ? P.gc[2] : P.gc[1];   // contiguous axis
+    const int cca = DIM == 3 ? cz : cy;
+    for (int col = 0; col < NCOL; ++col) {
+        int base;
+        if (DIM == 3) {
+            const int jx = FAST ? cx + col / 5 - 2 : wrap_cell(cx + col / 5 - 2, P.gc[0]);
+            const int jy = FAST ? cy + col % 5 - 2 : wrap_cell(cy + col % 5 - 2, P.gc[1]);
+            base = (jx * P.gc[1] + jy) * P.gc[2];
+        } else {
+            base = (FAST ? cx + col - 2 : wrap_cell(cx + col - 2, P.gc[0])) * P.gc[1];
+        }
+        const int lo = cca - 2, hi = cca + 2;
+        int seg_a[2], seg_b[2], nseg;
+        if (FAST) { seg_a[0] = lo; seg_b[0] = hi; seg_a[1] = 0; seg_b[1] = -1; nseg = 1; }
+        else if (lo < 0) { seg_a[0] = lo + gca; seg_b[0] = gca - 1; seg_a[1] = 0; seg_b[1] = hi; nseg = 2; }
+        else if (hi >= gca) { seg_a[0] = lo; seg_b[0] = gca - 1; seg_a[1] = 0; seg_b[1] = hi - gca; nseg = 2; }
+        else { seg_a[0] = lo; seg_b[0] = hi; seg_a[1] = 0; seg_b[1] = -1; nseg = 1; }
+        for (int sg = 0; sg < nseg; ++sg) {
+            const int jb = start[base + seg_a[sg]];
+            const int je = start[base + seg_b[sg] + 1];
+            // batches of 4 candidates: all 12 loads issued before the first test (memory-level
+            // parallelism; the loop is latency-bound, not ALU-bound)
+            for (int j0 = jb; j0 < je; j0 += 4) {
+                double xs[4], ys[4], zs[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int j = j0 + u < je ? j0 + u : je - 1;
+                    xs[u] = A.x[j];
+                    ys[u] = A.y[j];
+                    zs[u] = A.z[j];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int j = j0 + u;
+                    const double q0 = image_exact<FAST>(xs[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
+                    const double q1 = image_exact<FAST>(ys[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
+                    const double q2 = image_exact<FAST || DIM == 2>(zs[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
                     const double r2 = r2_exact(q0, q1, q2);
-                    if (r2 <= P.rc2 && j != i) {
+                    if (j < je && r2 <= P.rc2 && j != i) {
                         if (cnt < kMaxNeighbor) out[cnt * kTile] = j;
                         ++cnt;
                     }
                 }
             }
         }
+    }
+    return cnt;
+}
+
+template <int DIM>
+__global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int* __restrict__ start,
+                                                   int* __restrict__ nbr, int* __restrict__ ncount,
+                                                   DevState* __restrict__ st)
+{
+    const int i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    const bool live = i < P.n;
+    const int ii = live ? i : P.n - 1;
+    const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
+    const bool fast = wave_interior(P, live, xi, yi, zi);
+    int cnt = 0;
+    if (live) {
+        const int cx = cell_axis(xi, P.dmin[0], P.ginv[0], P.gc[0]);
+        const int cy = cell_axis(yi, P.dmin[1], P.ginv[1], P.gc[1]);
+        const int cz = DIM == 3 ? cell_axis(zi, P.dmin[2], P.ginv[2], P.gc[2]) : 0;
+        int* out = nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
+        cnt = fast ? scan_candidates<DIM, true>(P, A, start, i, xi, yi, zi, cx, cy, cz, out)
+                   : scan_candidates<DIM, false>(P, A, start, i, xi, yi, zi, cx, cy, cz, out);
         ncount[i] = cnt;
     }
     // wave reduction of the statistics (mean/max neighbours, overflow flag)
@@ -353,16 +403,59 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, const double4* _
 
 // ---------------------------------------------------------------------------- pass A -------
 
+struct PassA {
+    double da = 0.0, g0 = 0.0, g1 = 0.0, g2 = 0.0, vs = 0.0, dv = 0.0;
+};
+
+template <bool FAST, int DIM>
+__device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_ratio, const Soa& A,
+                                            const int* row, int cnt, int ti, bool solid, double xi,
+                                            double yi, double zi, double vxi, double vyi, double vzi,
+                                            PassA& o)
+{
+    const double gscale = P.rg / P.r2g;
+    for (int k = 0; k < cnt; ++k) {
+        const int j = row[k * kTile];
+        const double q0 = image_exact<FAST>(A.x[j] - xi, P.dw[0], P.hw[0], P.w075[0]);
+        const double q1 = image_exact<FAST>(A.y[j] - yi, P.dw[1], P.hw[1], P.w075[1]);
+        const double q2 = image_exact<FAST || DIM == 2>(A.z[j] - zi, P.dw[2], P.hw[2], P.w075[2]);
+        const double r2 = r2_exact(q0, q1, q2);
+        double r, ir;
+        rsqrt_pair(r2, r, ir);
+        if (r2 <= P.rp2) {
+            const double omt = 1.0 - r * P.inv_rp;
+            o.vs += P.cp * omt * omt;
+            const double dot = (A.vx[j] - vxi) * q0 + (A.vy[j] - vyi) * q1 + (A.vz[j] - vzi) * q2;
+            o.dv -= dot * ir * (P.cdp * omt);
+        }
+        if (!solid) {
+            const double ratio = s_ratio[ti * kTypes + A.type[j]];
+            if (r2 <= P.ra2) {
+                const double t = r * P.inv_ra;
+                const double omt = 1.0 - t;
+                o.da += ratio * (P.ca * t * omt * omt);
+            }
+            if (r2 <= P.rg2) {
+                const double omt = 1.0 - r * P.inv_rg;
+                const double w = ratio * (P.cg * omt * omt) * gscale;
+                o.g0 += q0 * w;
+                o.g1 += q1 * w;
+                o.g2 += q2 * w;
+            }
+        }
+    }
+}
+
 // DensityA (2141-2171), GravityCenter (2174-2210), DensityP (2314-2341), DivergenceP
 // (2343-2379); epilogue: PhysicalCoefficients (2099-2137) and the pressure values of
 // calculatePressureP (2384-2392) and calculatePressureA (2218-2223).
-template <bool SURF>
-__global__ __launch_bounds__(256) void k_pass_a(DevParams P, const DevTables* __restrict__ T,
-                                                const double4* __restrict__ x,
-                                                const double4* __restrict__ v,
+template <int DIM>
+__global__ __launch_bounds__(256) void k_pass_a(DevParams P, const DevTables* __restrict__ T, Soa A,
                                                 const int* __restrict__ nbr,
                                                 const int* __restrict__ ncount,
-                                                double4* __restrict__ pv, double4* __restrict__ gca,
+                                                double* __restrict__ pres, double* __restrict__ gx,
+                                                double* __restrict__ gy, double* __restrict__ gz,
+                                                double* __restrict__ pa_out,
                                                 double* __restrict__ dens_a,
                                                 double* __restrict__ vstrain,
                                                 double* __restrict__ divp)
@@ -371,77 +464,114 @@ __global__ __launch_bounds__(256) void k_pass_a(DevParams P, const DevTables* __
     if (threadIdx.x < kTypes * kTypes) s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
     __syncthreads();
     const int i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    if (i >= P.n) return;
-    const double4 xi = x[i];
-    const double4 vi = v[i];
-    const int ti = (int)xi.w;
+    const bool live = i < P.n;
+    const int ii = live ? i : P.n - 1;
+    const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
+    const bool fast = wave_interior(P, live, xi, yi, zi);
+    if (!live) return;
+    const double vxi = A.vx[i], vyi = A.vy[i], vzi = A.vz[i];
+    const int ti = A.type[i];
     const bool solid = dev_is_struct(ti);
     const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
     const int* row = ell_row(nbr, i);
-    double da = 0.0, g0 = 0.0, g1 = 0.0, g2 = 0.0, vs = 0.0, dv = 0.0;
-    const double gscale = P.rg / P.r2g;
-    for (int k = 0; k < cnt; ++k) {
-        const int j = row[k * kTile];
-        const double4 xj = x[j];
-        const double q0 = image_exact(xj.x - xi.x, P.dw[0], P.hw[0], P.w075[0]);
-        const double q1 = image_exact(xj.y - xi.y, P.dw[1], P.hw[1], P.w075[1]);
-        const double q2 = image_exact(xj.z - xi.z, P.dw[2], P.hw[2], P.w075[2]);
-        const double r2 = r2_exact(q0, q1, q2);
-        const double r = sqrt(r2);
-        const double ir = 1.0 / r;
-        if (r2 <= P.rp2) {
-            const double4 vj = v[j];
-            const double omt = 1.0 - r * P.inv_rp;
-            vs += P.cp * omt * omt;
-            const double dot = (vj.x - vi.x) * q0 + (vj.y - vi.y) * q1 + (vj.z - vi.z) * q2;
-            dv -= dot * ir * (P.cdp * omt);
-        }
-        if (!solid) {
-            const double ratio = s_ratio[ti * kTypes + (int)xj.w];
-            if (r2 <= P.ra2) {
-                const double t = r * P.inv_ra;
-                const double omt = 1.0 - t;
-                da += ratio * (P.ca * t * omt * omt);
-            }
-            if (r2 <= P.rg2) {
-                const double omt = 1.0 - r * P.inv_rg;
-                const double w = ratio * (P.cg * omt * omt) * gscale;
-                g0 += q0 * w;
-                g1 += q1 * w;
-                g2 += q2 * w;
-            }
-        }
-    }
-    const double vstr = vs - P.n0p;
+    PassA o;
+    if (fast) pass_a_loop<true, DIM>(P, s_ratio, A, row, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+    else pass_a_loop<false, DIM>(P, s_ratio, A, row, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+    const double vstr = o.vs - P.n0p;
     const double kappa = vstr < 0.0 ? 0.0 : T->bulk[ti];
-    double pres = -T->bulk_visc[ti] * dv;
-    if (vstr > 0.0) pres += kappa * vstr;
-    double pa = T->cofa[ti] * (da - P.n0a) / P.dx;
-    if (P.n0a <= da) pa = 0.0;
-    pv[i] = make_double4(vi.x, vi.y, vi.z, pres);
-    gca[i] = make_double4(g0, g1, g2, pa);
-    dens_a[i] = da;
+    double p = -T->bulk_visc[ti] * o.dv;
+    if (vstr > 0.0) p += kappa * vstr;
+    double pa = T->cofa[ti] * (o.da - P.n0a) / P.dx;
+    if (P.n0a <= o.da) pa = 0.0;
+    pres[i] = p;
+    gx[i] = o.g0;
+    gy[i] = o.g1;
+    gz[i] = o.g2;
+    pa_out[i] = pa;
+    dens_a[i] = o.da;
     vstrain[i] = vstr;
-    divp[i] = dv;
+    divp[i] = o.dv;
 }
 
 // ---------------------------------------------------------------------------- pass B -------
 
+template <bool FAST, bool SURF, int DIM>
+__device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_ratio, const double* s_mu,
+                                            const Soa& A, const double* pres, const double* gx,
+                                            const double* gy, const double* gz, const double* pa,
+                                            const int* row, int cnt, int ti, bool solid, double xi,
+                                            double yi, double zi, double vxi, double vyi, double vzi,
+                                            double pi, double gxi, double gyi, double gzi, double pai,
+                                            double ai, double& f0, double& f1, double& f2)
+{
+    const double dscale = P.rg / P.r2g * (P.vol / P.dx);
+    for (int k = 0; k < cnt; ++k) {
+        const int j = row[k * kTile];
+        const int tj = A.type[j];
+        if (solid && dev_is_struct(tj)) continue;
+        const double q0 = image_exact<FAST>(A.x[j] - xi, P.dw[0], P.hw[0], P.w075[0]);
+        const double q1 = image_exact<FAST>(A.y[j] - yi, P.dw[1], P.hw[1], P.w075[1]);
+        const double q2 = image_exact<FAST || DIM == 2>(A.z[j] - zi, P.dw[2], P.hw[2], P.w075[2]);
+        const double r2 = r2_exact(q0, q1, q2);
+        const double pj = pres[j];
+        double r, ir;
+        rsqrt_pair(r2, r, ir);
+        double c = 0.0;
+        if (r2 < P.rp2) {
+            const double dw = P.cdp * (1.0 - r * P.inv_rp);
+            c += (pi + pj) * dw * ir * P.vol;
+        }
+        if (!solid) {
+            if (SURF) {
+                const double rij = s_ratio[ti * kTypes + tj];
+                const double rji = s_ratio[tj * kTypes + ti];
+                const double gxj = gx[j], gyj = gy[j], gzj = gz[j], paj = pa[j];
+                if (r2 < P.ra2) {
+                    const double t = r * P.inv_ra;
+                    const double dwa = P.cda * (1.0 - t) * (1.0 - 3.0 * t);
+                    c += (pai * rij + paj * rji) * dwa * ir * P.vol;
+                }
+                if (r2 < P.rg2) {
+                    const double omt = 1.0 - r * P.inv_rg;
+                    const double wg = P.cg * omt * omt;
+                    const double dwg = P.cdg * omt;
+                    const double wij = rij * wg, wji = rji * wg;
+                    f0 -= (ai * gxj * wji - ai * gxi * wij) * dscale;
+                    f1 -= (ai * gyj * wji - ai * gyi * wij) * dscale;
+                    f2 -= (ai * gzj * wji - ai * gzi * wij) * dscale;
+                    const double dwij = rij * dwg, dwji = rji * dwg;
+                    const double gr = (ai * gxj * dwji - ai * gxi * dwij) * q0 +
+                                      (ai * gyj * dwji - ai * gyi * dwij) * q1 +
+                                      (ai * gzj * dwji - ai * gzi * dwij) * q2;
+                    c -= gr * ir * dscale;
+                }
+            }
+            if (r2 < P.rv2) {
+                const double dwij = -P.cdv * (1.0 - r * P.inv_rv);
+                const double dot = (A.vx[j] - vxi) * q0 + (A.vy[j] - vyi) * q1 + (A.vz[j] - vzi) * q2;
+                c += P.cvis * s_mu[ti * kTypes + tj] * dot * dwij * (ir * ir * ir) * P.vol;
+            }
+        }
+        f0 += c * q0;
+        f1 += c * q1;
+        f2 += c * q2;
+    }
+}
+
 // Pair forces of PressureP (2394-2424), PressureA (2225-2258), DiffuseInterface (2261-2312),
 // ViscosityV (2478-2522) for non-structure i; InterfaceForce (2439-2472) for structure i; then
 // Gravity (2917-2936), Acceleration/kick (2938-2956) and Convection/drift (1892-1907).
-template <bool SURF>
-__global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __restrict__ T,
-                                                const double4* __restrict__ x,
-                                                const double4* __restrict__ pv,
-                                                const double4* __restrict__ gca,
+template <bool SURF, int DIM>
+__global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __restrict__ T, Soa A,
+                                                const double* __restrict__ pres,
+                                                const double* __restrict__ gx,
+                                                const double* __restrict__ gy,
+                                                const double* __restrict__ gz,
+                                                const double* __restrict__ pa,
                                                 const int* __restrict__ nbr,
                                                 const int* __restrict__ ncount,
-                                                const int* __restrict__ ida,
-                                                double4* __restrict__ force,
-                                                double4* __restrict__ acc,
-                                                double4* __restrict__ xb, double4* __restrict__ vb,
-                                                int* __restrict__ idb)
+                                                double4* __restrict__ force, double4* __restrict__ acc,
+                                                Soa B)
 {
     __shared__ double s_ratio[kTypes * kTypes];
     __shared__ double s_mu[kTypes * kTypes];
@@ -451,111 +581,70 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
     }
     __syncthreads();
     const int i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    if (i >= P.n) return;
-    const double4 xi = x[i];
-    const double4 pvi = pv[i];
-    const int ti = (int)xi.w;
+    const bool live = i < P.n;
+    const int ii = live ? i : P.n - 1;
+    const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
+    const bool fast = wave_interior(P, live, xi, yi, zi);
+    if (!live) return;
+    const double vxi = A.vx[i], vyi = A.vy[i], vzi = A.vz[i];
+    const double pi = pres[i];
+    const int ti = A.type[i];
     const bool solid = dev_is_struct(ti);
     const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
     const int* row = ell_row(nbr, i);
     double f0 = 0.0, f1 = 0.0, f2 = 0.0;
-    double4 gi = make_double4(0.0, 0.0, 0.0, 0.0);
-    double ai = 0.0;
+    double gxi = 0.0, gyi = 0.0, gzi = 0.0, pai = 0.0, ai = 0.0;
     if (SURF) {
-        gi = gca[i];
+        gxi = gx[i]; gyi = gy[i]; gzi = gz[i]; pai = pa[i];
         ai = T->cofa[ti] * P.cofk * P.cofk;
     }
-    const double dscale = P.rg / P.r2g * (P.vol / P.dx);
-    for (int k = 0; k < cnt; ++k) {
-        const int j = row[k * kTile];
-        const double4 xj = x[j];
-        const int tj = (int)xj.w;
-        if (solid && dev_is_struct(tj)) continue;
-        const double q0 = image_exact(xj.x - xi.x, P.dw[0], P.hw[0], P.w075[0]);
-        const double q1 = image_exact(xj.y - xi.y, P.dw[1], P.hw[1], P.w075[1]);
-        const double q2 = image_exact(xj.z - xi.z, P.dw[2], P.hw[2], P.w075[2]);
-        const double r2 = r2_exact(q0, q1, q2);
-        const double4 pvj = pv[j];
-        const double r = sqrt(r2);
-        const double ir = 1.0 / r;
-        double c = 0.0;
-        if (r2 < P.rp2) {
-            const double dw = P.cdp * (1.0 - r * P.inv_rp);
-            c += (pvi.w + pvj.w) * dw * ir * P.vol;
-        }
-        if (!solid) {
-            if (SURF) {
-                const double4 gj = gca[j];
-                const double rij = s_ratio[ti * kTypes + tj];
-                const double rji = s_ratio[tj * kTypes + ti];
-                if (r2 < P.ra2) {
-                    const double t = r * P.inv_ra;
-                    const double dwa = P.cda * (1.0 - t) * (1.0 - 3.0 * t);
-                    c += (gi.w * rij + gj.w * rji) * dwa * ir * P.vol;
-                }
-                if (r2 < P.rg2) {
-                    const double omt = 1.0 - r * P.inv_rg;
-                    const double wg = P.cg * omt * omt;
-                    const double dwg = P.cdg * omt;
-                    const double wij = rij * wg, wji = rji * wg;
-                    f0 -= (ai * gj.x * wji - ai * gi.x * wij) * dscale;
-                    f1 -= (ai * gj.y * wji - ai * gi.y * wij) * dscale;
-                    f2 -= (ai * gj.z * wji - ai * gi.z * wij) * dscale;
-                    const double dwij = rij * dwg, dwji = rji * dwg;
-                    const double gr = (ai * gj.x * dwji - ai * gi.x * dwij) * q0 +
-                                      (ai * gj.y * dwji - ai * gi.y * dwij) * q1 +
-                                      (ai * gj.z * dwji - ai * gi.z * dwij) * q2;
-                    c -= gr * ir * dscale;
-                }
-            }
-            if (r2 < P.rv2) {
-                const double dwij = -P.cdv * (1.0 - r * P.inv_rv);
-                const double dot = (pvj.x - pvi.x) * q0 + (pvj.y - pvi.y) * q1 + (pvj.z - pvi.z) * q2;
-                c += P.cvis * s_mu[ti * kTypes + tj] * dot * dwij * (ir * ir * ir) * P.vol;
-            }
-        }
-        f0 += c * q0;
-        f1 += c * q1;
-        f2 += c * q2;
-    }
-    double4 vo = make_double4(pvi.x, pvi.y, pvi.z, 0.0);
-    double4 xo = xi;
+    if (fast)
+        pass_b_loop<true, SURF, DIM>(P, s_ratio, s_mu, A, pres, gx, gy, gz, pa, row, cnt, ti, solid, xi,
+                                     yi, zi, vxi, vyi, vzi, pi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
+    else
+        pass_b_loop<false, SURF, DIM>(P, s_ratio, s_mu, A, pres, gx, gy, gz, pa, row, cnt, ti, solid, xi,
+                                      yi, zi, vxi, vyi, vzi, pi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
+    double vo0 = vxi, vo1 = vyi, vo2 = vzi;
+    double xo0 = xi, xo1 = yi, xo2 = zi;
     double4 ao = make_double4(0.0, 0.0, 0.0, 0.0);
     if (dev_is_fluid(ti) || solid) {
         const double m = T->mass[ti], im = T->inv_mass[ti];
         f0 += m * P.gravity[0];
         f1 += m * P.gravity[1];
         f2 += m * P.gravity[2];
-        vo.x += f0 * im * P.dt;
-        vo.y += f1 * im * P.dt;
-        vo.z += f2 * im * P.dt;
+        vo0 += f0 * im * P.dt;
+        vo1 += f1 * im * P.dt;
+        vo2 += f2 * im * P.dt;
         if (!solid) {
             ao = make_double4(f0 * im, f1 * im, f2 * im, 0.0);
-            xo.x += vo.x * P.dt;
-            xo.y += vo.y * P.dt;
-            xo.z += vo.z * P.dt;
+            xo0 += vo0 * P.dt;
+            xo1 += vo1 * P.dt;
+            xo2 += vo2 * P.dt;
         }
     }
     force[i] = make_double4(f0, f1, f2, 0.0);
     acc[i] = ao;
-    xb[i] = xo;
-    vb[i] = vo;
-    idb[i] = ida[i];
+    B.x[i] = xo0;
+    B.y[i] = xo1;
+    B.z[i] = xo2;
+    B.vx[i] = vo0;
+    B.vy[i] = vo1;
+    B.vz[i] = vo2;
+    B.type[i] = ti;
+    B.id[i] = A.id[i];
 }
 
 // ------------------------------------------------------------------------ elastic solid ----
 
 __global__ __launch_bounds__(256) void k_struct_gather(int ns, const int* __restrict__ sorig,
-                                                       const int* __restrict__ rank_of,
-                                                       const double4* __restrict__ xb,
-                                                       const double4* __restrict__ vb,
+                                                       const int* __restrict__ rank_of, Soa B,
                                                        double4* __restrict__ sx, double4* __restrict__ sv)
 {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= ns) return;
     const int r = rank_of[sorig[s]];
-    sx[s] = xb[r];
-    sv[s] = vb[r];
+    sx[s] = make_double4(B.x[r], B.y[r], B.z[r], (double)B.type[r]);
+    sv[s] = make_double4(B.vx[r], B.vy[r], B.vz[r], 0.0);
 }
 
 // calculateElasticDeformationVector (2673-2754) + calculateStress (2756-2809) + the first
@@ -576,9 +665,9 @@ __global__ __launch_bounds__(256) void k_struct_stress(DevParams P, int ns,
     if (s >= ns) return;
     const double4 xi = sx[s], x0i = sx0[s];
     double ui[3];
-    ui[0] = image_exact(xi.x - x0i.x, P.dw[0], P.hw[0], P.w075[0]);
-    ui[1] = image_exact(xi.y - x0i.y, P.dw[1], P.hw[1], P.w075[1]);
-    ui[2] = image_exact(xi.z - x0i.z, P.dw[2], P.hw[2], P.w075[2]);
+    ui[0] = image_exact<false>(xi.x - x0i.x, P.dw[0], P.hw[0], P.w075[0]);
+    ui[1] = image_exact<false>(xi.y - x0i.y, P.dw[1], P.hw[1], P.w075[1]);
+    ui[2] = image_exact<false>(xi.z - x0i.z, P.dw[2], P.hw[2], P.w075[2]);
     double Fr[DIM][DIM];
 #pragma unroll
     for (int a = 0; a < DIM; ++a)
@@ -589,9 +678,9 @@ __global__ __launch_bounds__(256) void k_struct_stress(DevParams P, int ns,
         const double4 pr = pair[k];
         const double4 xj = sx[t], x0j = sx0[t];
         const double x0ij[3] = {pr.x, pr.y, pr.z};
-        const double uj[3] = {image_exact(xj.x - x0j.x, P.dw[0], P.hw[0], P.w075[0]),
-                              image_exact(xj.y - x0j.y, P.dw[1], P.hw[1], P.w075[1]),
-                              image_exact(xj.z - x0j.z, P.dw[2], P.hw[2], P.w075[2])};
+        const double uj[3] = {image_exact<false>(xj.x - x0j.x, P.dw[0], P.hw[0], P.w075[0]),
+                              image_exact<false>(xj.y - x0j.y, P.dw[1], P.hw[1], P.w075[1]),
+                              image_exact<false>(xj.z - x0j.z, P.dw[2], P.hw[2], P.w075[2])};
 #pragma unroll
         for (int a = 0; a < DIM; ++a) {
             const double xa = x0ij[a] + (uj[a] - ui[a]);
@@ -732,27 +821,21 @@ __global__ __launch_bounds__(256) void k_struct_scatter(int ns, const int* __res
                                                         const int* __restrict__ rank_of,
                                                         const int* __restrict__ clamp,
                                                         const double4* __restrict__ sx,
-                                                        const double4* __restrict__ sv,
-                                                        double4* __restrict__ xb, double4* __restrict__ vb,
+                                                        const double4* __restrict__ sv, Soa B,
                                                         double4* __restrict__ force)
 {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= ns) return;
     const int r = rank_of[sorig[s]];
-    xb[r] = sx[s];
-    vb[r] = sv[s];
+    const double4 x = sx[s], v = sv[s];
+    B.x[r] = x.x; B.y[r] = x.y; B.z[r] = x.z;
+    B.vx[r] = v.x; B.vy[r] = v.y; B.vz[r] = v.z;
     if (clamp[s] == 1) force[r] = make_double4(0.0, 0.0, 0.0, 0.0);
 }
 
 // ---------------------------------------------------------------------------- launchers -----
 
 static inline int blocks(int n, int t) { return (n + t - 1) / t; }
-
-#define MPH_LAUNCH(name, grid, block, stream, ...)                                  \
-    do {                                                                            \
-        ProfScope _ps(prof, name, stream);                                          \
-        hipLaunchKernelGGL(__VA_ARGS__);                                            \
-    } while (0)
 
 struct ProfScope {
     Profiler* p;
@@ -768,24 +851,30 @@ struct ProfScope {
     }
 };
 
+#define MPH_LAUNCH(name, stream, ...)                                               \
+    do {                                                                            \
+        ProfScope _ps(prof, name, stream);                                          \
+        hipLaunchKernelGGL(__VA_ARGS__);                                            \
+    } while (0)
+
 void launch_sort(const Launch& L, int mode)
 {
     Profiler* prof = L.prof;
     const DevParams& P = *L.P;
     const int n = P.n;
     if (n == 0) return;
-    MPH_LAUNCH("prep", 0, 0, L.stream, k_prep, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st,
-               L.xb, L.vb, L.key, L.slot, L.cnt, mode);
+    MPH_LAUNCH("prep", L.stream, k_prep, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.B,
+               L.key, L.slot, L.cnt, mode);
     const int nb = blocks(P.ncell, kScanBlock);
-    MPH_LAUNCH("scan_reduce", 0, 0, L.stream, k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, L.stream,
-               L.cnt, P.ncell, L.bsum);
-    MPH_LAUNCH("scan_top", 0, 0, L.stream, k_scan_top, dim3(1), dim3(1024), 0, L.stream, L.bsum, nb);
-    MPH_LAUNCH("scan_down", 0, 0, L.stream, k_scan_down, dim3(nb), dim3(kScanThreads), 0, L.stream,
-               L.cnt, P.ncell, L.bsum, L.start, n);
-    MPH_LAUNCH("place", 0, 0, L.stream, k_place, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st,
-               L.key, L.slot, L.start, L.tmp, mode);
-    MPH_LAUNCH("rank_scatter", 0, 0, L.stream, k_rank_scatter, dim3(blocks(n, 256)), dim3(256), 0,
-               L.stream, P, L.key, L.start, L.tmp, L.xb, L.vb, L.idb, L.xa, L.va, L.ida, L.rank_of);
+    MPH_LAUNCH("scan_reduce", L.stream, k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt,
+               P.ncell, L.bsum);
+    MPH_LAUNCH("scan_top", L.stream, k_scan_top, dim3(1), dim3(1024), 0, L.stream, L.bsum, nb);
+    MPH_LAUNCH("scan_down", L.stream, k_scan_down, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt,
+               P.ncell, L.bsum, L.start, n);
+    MPH_LAUNCH("place", L.stream, k_place, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.key,
+               L.slot, L.start, L.tmp, mode);
+    MPH_LAUNCH("rank_scatter", L.stream, k_rank_scatter, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P,
+               L.key, L.start, L.tmp, L.B, L.A, L.rank_of);
 }
 
 void launch_neighbors(const Launch& L)
@@ -794,11 +883,11 @@ void launch_neighbors(const Launch& L)
     const DevParams& P = *L.P;
     if (P.n == 0) return;
     if (P.dim == 3)
-        MPH_LAUNCH("neighbors", 0, 0, L.stream, k_neighbors<3>, dim3(blocks(P.n, 256)), dim3(256), 0,
-                   L.stream, P, L.xa, L.start, L.nbr, L.ncount, L.st);
+        MPH_LAUNCH("neighbors", L.stream, k_neighbors<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P,
+                   L.A, L.start, L.nbr, L.ncount, L.st);
     else
-        MPH_LAUNCH("neighbors", 0, 0, L.stream, k_neighbors<2>, dim3(blocks(P.n, 256)), dim3(256), 0,
-                   L.stream, P, L.xa, L.start, L.nbr, L.ncount, L.st);
+        MPH_LAUNCH("neighbors", L.stream, k_neighbors<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P,
+                   L.A, L.start, L.nbr, L.ncount, L.st);
 }
 
 void launch_pass_a(const Launch& L)
@@ -806,12 +895,12 @@ void launch_pass_a(const Launch& L)
     Profiler* prof = L.prof;
     const DevParams& P = *L.P;
     if (P.n == 0) return;
-    if (P.surface)
-        MPH_LAUNCH("pass_a", 0, 0, L.stream, k_pass_a<true>, dim3(blocks(P.n, 256)), dim3(256), 0,
-                   L.stream, P, L.T, L.xa, L.va, L.nbr, L.ncount, L.pv, L.gca, L.dens_a, L.vstrain, L.divp);
+    if (P.dim == 3)
+        MPH_LAUNCH("pass_a", L.stream, k_pass_a<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T,
+                   L.A, L.nbr, L.ncount, L.pres, L.gx, L.gy, L.gz, L.pa, L.dens_a, L.vstrain, L.divp);
     else
-        MPH_LAUNCH("pass_a", 0, 0, L.stream, k_pass_a<false>, dim3(blocks(P.n, 256)), dim3(256), 0,
-                   L.stream, P, L.T, L.xa, L.va, L.nbr, L.ncount, L.pv, L.gca, L.dens_a, L.vstrain, L.divp);
+        MPH_LAUNCH("pass_a", L.stream, k_pass_a<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T,
+                   L.A, L.nbr, L.ncount, L.pres, L.gx, L.gy, L.gz, L.pa, L.dens_a, L.vstrain, L.divp);
 }
 
 void launch_pass_b(const Launch& L)
@@ -819,14 +908,15 @@ void launch_pass_b(const Launch& L)
     Profiler* prof = L.prof;
     const DevParams& P = *L.P;
     if (P.n == 0) return;
-    if (P.surface)
-        MPH_LAUNCH("pass_b", 0, 0, L.stream, k_pass_b<true>, dim3(blocks(P.n, 256)), dim3(256), 0,
-                   L.stream, P, L.T, L.xa, L.pv, L.gca, L.nbr, L.ncount, L.ida, L.force, L.acc, L.xb,
-                   L.vb, L.idb);
-    else
-        MPH_LAUNCH("pass_b", 0, 0, L.stream, k_pass_b<false>, dim3(blocks(P.n, 256)), dim3(256), 0,
-                   L.stream, P, L.T, L.xa, L.pv, L.gca, L.nbr, L.ncount, L.ida, L.force, L.acc, L.xb,
-                   L.vb, L.idb);
+#define MPH_PASS_B(S, D)                                                                            \
+    MPH_LAUNCH("pass_b", L.stream, (k_pass_b<S, D>), dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, \
+               L.T, L.A, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, L.force, L.acc, L.B)
+    if (P.surface) {
+        if (P.dim == 3) MPH_PASS_B(true, 3); else MPH_PASS_B(true, 2);
+    } else {
+        if (P.dim == 3) MPH_PASS_B(false, 3); else MPH_PASS_B(false, 2);
+    }
+#undef MPH_PASS_B
 }
 
 void launch_structure(const Launch& L)
@@ -836,25 +926,25 @@ void launch_structure(const Launch& L)
     const int ns = P.n_struct;
     if (ns == 0) return;
     const StructDev& S = *L.S;
-    MPH_LAUNCH("struct_gather", 0, 0, L.stream, k_struct_gather, dim3(blocks(ns, 256)), dim3(256), 0,
-               L.stream, ns, S.orig, L.rank_of, L.xb, L.vb, S.x, S.v);
+    MPH_LAUNCH("struct_gather", L.stream, k_struct_gather, dim3(blocks(ns, 256)), dim3(256), 0, L.stream, ns,
+               S.orig, L.rank_of, L.B, S.x, S.v);
     for (int sub = 0; sub < P.substeps; ++sub) {
         if (P.dim == 3) {
-            MPH_LAUNCH("struct_stress", 0, 0, L.stream, k_struct_stress<3>, dim3(blocks(ns, 256)), dim3(256),
-                       0, L.stream, P, ns, S.x, S.x0, S.off, S.nb, S.pair_out, S.L, S.lame, S.P, S.F, S.E, S.S);
-            MPH_LAUNCH("struct_velocity", 0, 0, L.stream, k_struct_velocity<3>, dim3(blocks(ns, 256)),
-                       dim3(256), 0, L.stream, P, ns, S.off, S.pair_out, S.in_off, S.in_nb, S.pair_in, S.P,
-                       S.inv_rho, S.clamp, S.x0, S.x, S.v);
+            MPH_LAUNCH("struct_stress", L.stream, k_struct_stress<3>, dim3(blocks(ns, 256)), dim3(256), 0,
+                       L.stream, P, ns, S.x, S.x0, S.off, S.nb, S.pair_out, S.L, S.lame, S.P, S.F, S.E, S.S);
+            MPH_LAUNCH("struct_velocity", L.stream, k_struct_velocity<3>, dim3(blocks(ns, 256)), dim3(256), 0,
+                       L.stream, P, ns, S.off, S.pair_out, S.in_off, S.in_nb, S.pair_in, S.P, S.inv_rho,
+                       S.clamp, S.x0, S.x, S.v);
         } else {
-            MPH_LAUNCH("struct_stress", 0, 0, L.stream, k_struct_stress<2>, dim3(blocks(ns, 256)), dim3(256),
-                       0, L.stream, P, ns, S.x, S.x0, S.off, S.nb, S.pair_out, S.L, S.lame, S.P, S.F, S.E, S.S);
-            MPH_LAUNCH("struct_velocity", 0, 0, L.stream, k_struct_velocity<2>, dim3(blocks(ns, 256)),
-                       dim3(256), 0, L.stream, P, ns, S.off, S.pair_out, S.in_off, S.in_nb, S.pair_in, S.P,
-                       S.inv_rho, S.clamp, S.x0, S.x, S.v);
+            MPH_LAUNCH("struct_stress", L.stream, k_struct_stress<2>, dim3(blocks(ns, 256)), dim3(256), 0,
+                       L.stream, P, ns, S.x, S.x0, S.off, S.nb, S.pair_out, S.L, S.lame, S.P, S.F, S.E, S.S);
+            MPH_LAUNCH("struct_velocity", L.stream, k_struct_velocity<2>, dim3(blocks(ns, 256)), dim3(256), 0,
+                       L.stream, P, ns, S.off, S.pair_out, S.in_off, S.in_nb, S.pair_in, S.P, S.inv_rho,
+                       S.clamp, S.x0, S.x, S.v);
         }
     }
-    MPH_LAUNCH("struct_scatter", 0, 0, L.stream, k_struct_scatter, dim3(blocks(ns, 256)), dim3(256), 0,
-               L.stream, ns, S.orig, L.rank_of, S.clamp, S.x, S.v, L.xb, L.vb, L.force);
+    MPH_LAUNCH("struct_scatter", L.stream, k_struct_scatter, dim3(blocks(ns, 256)), dim3(256), 0, L.stream,
+               ns, S.orig, L.rank_of, S.clamp, S.x, S.v, L.B, L.force);
 }
 
 }  // namespace mph

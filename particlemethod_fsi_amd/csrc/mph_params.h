@@ -28,6 +28,9 @@ struct DevParams {
     int gc[3];         // GPU linked-cell grid (gc[2] == 1 in 2-D)
     int ncell;         // gc[0]*gc[1]*gc[2]
     int substeps;      // (int)(Dt/Elastic_Dt + 0.5), main.cpp:653
+    int fast_ok;       // every active axis has > 12 GPU cells: interior waves may skip the
+                       // periodic branch of the minimum image (see k_neighbors)
+    double inner_lo[3], inner_hi[3];   // interior box: >= 3 GPU cells from every periodic face
     double dmin[3], dw[3], hw[3], w075[3];   // domain min / width / half width / 0.75 width
     double ginv[3];    // 1 / GPU cell width per axis
     double rc2;        // (MaxRadius + MARGIN)^2, main.cpp:1765

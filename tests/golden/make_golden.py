@@ -46,6 +46,10 @@ PLAN = {  # case -> steps (cumulative) to snapshot; the first is the full-field 
     "bar2d": [1, 10, 100],
     "box3d": [1, 10],
     "gate3d": [1, 10],
+    "dam2d_st": [1, 10, 100],
+    "box3d_st": [1, 10],
+    "gate2d_sub": [1, 10, 100],
+    "gate3d_sub": [1, 10, 50],
 }
 
 

@@ -8,7 +8,8 @@ import os
 import numpy as np
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-CASES = ["dam2d", "gate2d", "bar2d", "box3d", "gate3d"]
+CASES = ["dam2d", "gate2d", "bar2d", "box3d", "gate3d", "dam2d_st", "box3d_st", "gate2d_sub",
+         "gate3d_sub"]
 
 
 class Golden:
