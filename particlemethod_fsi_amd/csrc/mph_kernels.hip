@@ -407,29 +407,44 @@ struct PassA {
     double da = 0.0, g0 = 0.0, g1 = 0.0, g2 = 0.0, vs = 0.0, dv = 0.0;
 };
 
-template <bool FAST, int DIM>
+// Neighbour loops gather U neighbours' fields before the first use (all loads in flight at once):
+// the loops are memory-latency bound (profiles/r01: 90% of wave time in s_waitcnt).
+template <bool FAST, int DIM, int U = 4>
 __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_ratio, const Soa& A,
                                             const int* row, int cnt, int ti, bool solid, double xi,
                                             double yi, double zi, double vxi, double vyi, double vzi,
                                             PassA& o)
 {
     const double gscale = P.rg / P.r2g;
-    for (int k = 0; k < cnt; ++k) {
-        const int j = row[k * kTile];
-        const double q0 = image_exact<FAST>(A.x[j] - xi, P.dw[0], P.hw[0], P.w075[0]);
-        const double q1 = image_exact<FAST>(A.y[j] - yi, P.dw[1], P.hw[1], P.w075[1]);
-        const double q2 = image_exact<FAST || DIM == 2>(A.z[j] - zi, P.dw[2], P.hw[2], P.w075[2]);
+    for (int k0 = 0; k0 < cnt; k0 += U) {
+        int jj[U];
+        double X[U], Y[U], Z[U], VX[U], VY[U], VZ[U];
+        int TT[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) jj[u] = row[(k0 + u < cnt ? k0 + u : cnt - 1) * kTile];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            X[u] = A.x[jj[u]]; Y[u] = A.y[jj[u]]; Z[u] = A.z[jj[u]];
+            VX[u] = A.vx[jj[u]]; VY[u] = A.vy[jj[u]]; VZ[u] = A.vz[jj[u]];
+            TT[u] = A.type[jj[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+        if (k0 + u >= cnt) break;
+        const double q0 = image_exact<FAST>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
+        const double q1 = image_exact<FAST>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
+        const double q2 = image_exact<FAST || DIM == 2>(Z[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
         const double r2 = r2_exact(q0, q1, q2);
         double r, ir;
         rsqrt_pair(r2, r, ir);
         if (r2 <= P.rp2) {
             const double omt = 1.0 - r * P.inv_rp;
             o.vs += P.cp * omt * omt;
-            const double dot = (A.vx[j] - vxi) * q0 + (A.vy[j] - vyi) * q1 + (A.vz[j] - vzi) * q2;
+            const double dot = (VX[u] - vxi) * q0 + (VY[u] - vyi) * q1 + (VZ[u] - vzi) * q2;
             o.dv -= dot * ir * (P.cdp * omt);
         }
         if (!solid) {
-            const double ratio = s_ratio[ti * kTypes + A.type[j]];
+            const double ratio = s_ratio[ti * kTypes + TT[u]];
             if (r2 <= P.ra2) {
                 const double t = r * P.inv_ra;
                 const double omt = 1.0 - t;
@@ -442,6 +457,7 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
                 o.g1 += q1 * w;
                 o.g2 += q2 * w;
             }
+        }
         }
     }
 }
@@ -495,7 +511,7 @@ __global__ __launch_bounds__(256) void k_pass_a(DevParams P, const DevTables* __
 
 // ---------------------------------------------------------------------------- pass B -------
 
-template <bool FAST, bool SURF, int DIM>
+template <bool FAST, bool SURF, int DIM, int U = 4>
 __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_ratio, const double* s_mu,
                                             const Soa& A, const double* pres, const double* gx,
                                             const double* gy, const double* gz, const double* pa,
@@ -505,15 +521,30 @@ __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_
                                             double ai, double& f0, double& f1, double& f2)
 {
     const double dscale = P.rg / P.r2g * (P.vol / P.dx);
-    for (int k = 0; k < cnt; ++k) {
-        const int j = row[k * kTile];
-        const int tj = A.type[j];
+    for (int k0 = 0; k0 < cnt; k0 += U) {
+        int jj[U];
+        double X[U], Y[U], Z[U], VX[U], VY[U], VZ[U], PJ[U];
+        int TT[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) jj[u] = row[(k0 + u < cnt ? k0 + u : cnt - 1) * kTile];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            X[u] = A.x[jj[u]]; Y[u] = A.y[jj[u]]; Z[u] = A.z[jj[u]];
+            VX[u] = A.vx[jj[u]]; VY[u] = A.vy[jj[u]]; VZ[u] = A.vz[jj[u]];
+            PJ[u] = pres[jj[u]];
+            TT[u] = A.type[jj[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+        if (k0 + u >= cnt) break;
+        const int j = jj[u];
+        const int tj = TT[u];
         if (solid && dev_is_struct(tj)) continue;
-        const double q0 = image_exact<FAST>(A.x[j] - xi, P.dw[0], P.hw[0], P.w075[0]);
-        const double q1 = image_exact<FAST>(A.y[j] - yi, P.dw[1], P.hw[1], P.w075[1]);
-        const double q2 = image_exact<FAST || DIM == 2>(A.z[j] - zi, P.dw[2], P.hw[2], P.w075[2]);
+        const double q0 = image_exact<FAST>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
+        const double q1 = image_exact<FAST>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
+        const double q2 = image_exact<FAST || DIM == 2>(Z[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
         const double r2 = r2_exact(q0, q1, q2);
-        const double pj = pres[j];
+        const double pj = PJ[u];
         double r, ir;
         rsqrt_pair(r2, r, ir);
         double c = 0.0;
@@ -548,13 +579,14 @@ __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_
             }
             if (r2 < P.rv2) {
                 const double dwij = -P.cdv * (1.0 - r * P.inv_rv);
-                const double dot = (A.vx[j] - vxi) * q0 + (A.vy[j] - vyi) * q1 + (A.vz[j] - vzi) * q2;
+                const double dot = (VX[u] - vxi) * q0 + (VY[u] - vyi) * q1 + (VZ[u] - vzi) * q2;
                 c += P.cvis * s_mu[ti * kTypes + tj] * dot * dwij * (ir * ir * ir) * P.vol;
             }
         }
         f0 += c * q0;
         f1 += c * q1;
         f2 += c * q2;
+        }
     }
 }
 
