@@ -10,8 +10,10 @@ neighbour search, density/pressure sums, pressure/surface/viscous forces, gravit
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--case d1m] [--no-cpu-baseline]
 
-For N > 1 (torchrun, one rank per GPU) every rank runs the slab decomposition of a dam whose
-z-extent is N times D1M's, so the per-GPU work stays fixed (weak scaling).
+For N > 1 (torchrun, one rank per GPU) the ranks run the slab decomposition (z slabs, RCCL
+halo exchange; csrc/mph_dist.hip) of the D1M tank extended N-fold along z, so the per-GPU work
+stays about one D1M (weak scaling); `value` counts every particle of the whole job per step.
+MPH_SLAB_TRANSPORT=host switches the halo transport to host staging over gloo (diagnostics).
 
 Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel's algorithmic HBM bytes per
 launch (SURVEY 8d per-particle figures) over its HIP-event-timed average
@@ -36,6 +38,7 @@ FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector spec
 # algorithmic bytes per particle per launch
 ALG_BYTES = {"pass_a": 92.0, "pass_b": 140.0, "sort": 140.0}
 B_ALG_STEP = 372.0          # grid build 140 + pass 1 92 + pass 2 140
+SLAB_AXIS = 2               # z slabs for the dam workloads
 
 
 def dist_env():
@@ -107,25 +110,40 @@ def main():
     args = ap.parse_args()
 
     rank, world, local = dist_env()
-    import numpy as np
+    device = int(os.environ.get("MPH_BENCH_DEVICE", local))   # rehearsals: ranks sharing a GPU
     from particlemethod_fsi_amd import MphSolver, cases
 
     dist = None
+    case_name = args.case
     if world > 1:
+        # one process per GPU; torch.distributed (gloo) is only the control plane (rendezvous,
+        # RCCL unique id, timing reduction).  Particle data moves over the library's own RCCL
+        # communicator (ncclSend/Recv with the two slab neighbours, csrc/mph_dist.hip).
         import torch
         import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(device)
+        tdist.init_process_group("gloo")
         dist = tdist
+        if case_name == "d1m":
+            case_name = "d1m_x%d" % world
 
-    case = cases.get(args.case)
+    case = cases.get(case_name)
     cfg, parts = case.build()
-    solver = MphSolver(cfg, parts, device=local)
     n_total = parts.n
+    if dist is not None:
+        from particlemethod_fsi_amd.dist import gloo_slab, rccl_slab
+        mk = gloo_slab if os.environ.get("MPH_SLAB_TRANSPORT") == "host" else rccl_slab
+        solver = MphSolver(cfg, parts, device=device, slab=mk(rank, world, SLAB_AXIS))
+        n_local = len(solver.owned_ids())
+    else:
+        solver = MphSolver(cfg, parts, device=device)
+        n_local = n_total
 
     def barrier():
         solver.synchronize()
         if dist is not None:
+            import torch
+            torch.cuda.synchronize()
             dist.barrier()
 
     solver.step(args.warmup)
@@ -136,16 +154,16 @@ def main():
     elapsed = time.perf_counter() - t0
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    value = n_total * world * args.steps / elapsed   # replicas: every rank advances its own set
+    value = n_total * args.steps / elapsed   # every particle of the whole job, once per step
 
     mean_nb, max_nb = solver.neighbor_stats()
     prof = solver.profile(args.profile_steps)
     dom = max((k for k in prof if k in ALG_BYTES), key=lambda k: prof[k]["avg_ms"])
     step_ms = sum(v["avg_ms"] * v["launches"] for v in prof.values()) / args.profile_steps
-    alg_bytes = ALG_BYTES[dom] * parts.n
+    alg_bytes = ALG_BYTES[dom] * n_local
     achieved = alg_bytes / (prof[dom]["avg_ms"] * 1e-3) / 1e9
     traffic = load_pmc_traffic(dom)
     out = {
@@ -161,9 +179,12 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (reference generator algorithm + results/Dam/dam.data parameters)",
-        "config": {"workload": "%s: 3-D dam break (SURVEY 8d D1M), %d particles per GPU" % (args.case, parts.n),
-                   "particles": n_total * world, "dim": case.dim, "module": case.module,
-                   "dt": cfg.dt, "parallelism": "replicas" if world > 1 else "single"},
+        "config": {"workload": "%s: 3-D dam break (SURVEY 8d D1M%s), %d particles, ~%d per GPU"
+                               % (case_name, "" if world == 1 else " extended %dx along z" % world,
+                                  n_total, n_total // world),
+                   "particles": n_total, "dim": case.dim, "module": case.module, "dt": cfg.dt,
+                   "parallelism": "single" if world == 1 else "slab%d-z (%s halo exchange)" % (
+                       world, "host-staged" if os.environ.get("MPH_SLAB_TRANSPORT") == "host" else "RCCL")},
         "achieved_hbm_gbps_alg": B_ALG_STEP * value / 1e9,
         "neighbors": {"mean": mean_nb, "max": max_nb},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS,

@@ -32,6 +32,8 @@
 #ifndef MPH_GPU_H_INCLUDED
 #define MPH_GPU_H_INCLUDED
 
+#include <stddef.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -61,7 +63,9 @@ typedef enum MphStatus {
     MPH_ERR_RCCL = -6,
     MPH_ERR_DOMAIN = -7,             /* domain too small for the cell stencil        */
     MPH_ERR_UNSUPPORTED = -8,
-    MPH_ERR_NONFINITE = -9
+    MPH_ERR_NONFINITE = -9,
+    MPH_ERR_TRANSPORT = -10,         /* slab mode: host exchange callback failed                  */
+    MPH_ERR_CAPACITY = -11           /* slab mode: local arrays full, or a particle jumped a slab */
 } MphStatus;
 
 /* Everything the reference reads from its .data file (main.cpp:743-767) and .grid header
@@ -180,6 +184,8 @@ double mph_time(const MphCtx* ctx);
 int mph_get_scalars(const MphCtx* ctx, double* out36);
 int mph_write_prof(MphCtx* ctx, const char* path);
 int mph_write_vtk(MphCtx* ctx, const char* path);
+/* Message of the last failure on ctx; with ctx == NULL, of the last failed mph_create* on the
+ * calling thread (the context is destroyed on failure).                                        */
 const char* mph_last_error(const MphCtx* ctx);
 void mph_destroy(MphCtx* ctx);
 
@@ -195,15 +201,49 @@ int mph_neighbor_stats(MphCtx* ctx, double* mean, int* max);
 
 /* ---- multi-GPU slab decomposition (one process per GPU, RCCL over xGMI) ------------------ */
 
+/* The reference runs one process over all particles (OpenMP/OpenACC, main.cpp:597-686); it has
+ * no domain decomposition.  These entry points add one: the periodic domain is cut into
+ * `nranks` equal slabs along `axis`; each rank owns the particles inside its slab, mirrors the
+ * ones within one cutoff of a face to that neighbour as ghosts, and hands particles that crossed
+ * a face to the neighbour at the start of the next step.  Per step: one exchange of
+ * (x, v, type, id) for migrants + ghosts before the cell sort, one of the pass-A values
+ * (PressureP [, GravityCenter, PressureA]) of the ghosts before the force pass.
+ * Elastic-solid particles (types 2, 3) are not supported in slab mode (MPH_ERR_UNSUPPORTED).
+ *
+ * mph_get in slab mode fills only the entries of the particles this rank owns (indexed by the
+ * original particle index, arrays of mph_particle_count() = the global count); the other
+ * entries are left untouched, so a caller can merge the ranks' arrays.                        */
+
 /* 128-byte RCCL unique id generated on rank 0 and shared out of band by the caller.          */
 int mph_dist_unique_id(char* out128);
 /* Same as mph_create, but this rank owns only the particles whose slab (along `axis`) is
- * `rank` of `nranks`; all ranks pass the full particle set (any rank may pass it).           */
+ * `rank` of `nranks`; all ranks pass the full particle set.  Transport: RCCL (ncclSend/Recv
+ * with the two periodic neighbours, on the context's stream).                                */
 int mph_create_dist(MphCtx** ctx, const MphConfig* cfg, int n, const int* property,
                     const double* pos, const double* pos0, const double* vel, int device,
                     int rank, int nranks, const char* unique_id128, int axis);
-/* Particles currently owned by this rank (after migration).                                  */
+/* Host-staged transport for the same protocol: the context copies each message to pinned host
+ * memory and calls `fn`, which must deliver send_l to the left neighbour (received there as
+ * its recv_r) and send_r to the right neighbour (its recv_l), with the byte counts given.
+ * Used to run several ranks on one GPU (tests) or where RCCL is unavailable.  Returns 0 on
+ * success.                                                                                     */
+typedef int (*mph_host_exchange_fn)(void* user, const void* send_l, size_t bytes_send_l,
+                                    const void* send_r, size_t bytes_send_r, void* recv_l,
+                                    size_t bytes_recv_l, void* recv_r, size_t bytes_recv_r);
+int mph_create_dist_host(MphCtx** ctx, const MphConfig* cfg, int n, const int* property,
+                         const double* pos, const double* pos0, const double* vel, int device,
+                         int rank, int nranks, int axis, mph_host_exchange_fn fn, void* user);
+/* One-rank RCCL communicator on `device` whose two neighbours are itself: checks that the
+ * exchange delivers each message to the right buffer (the per-peer ordering nranks == 2 relies
+ * on) without a second GPU.  Returns 0 on success.                                            */
+int mph_dist_selftest(int device);
+/* Particles currently owned by this rank (after the last migration); their original indices.  */
 int mph_owned_count(const MphCtx* ctx);
+int mph_owned_ids(MphCtx* ctx, int* out_ids);
+/* Host-only: the slab bounds [lo, hi) of `rank` and the halo width along `axis` that
+ * mph_create_dist would use (out3 = {lo, hi, h}), and whether a rank owns coordinate c.      */
+int mph_slab_bounds(const MphConfig* cfg, int rank, int nranks, int axis, double* out3);
+int mph_slab_owner(const MphConfig* cfg, int nranks, int axis, double c);
 
 #ifdef __cplusplus
 }

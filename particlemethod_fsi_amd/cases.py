@@ -198,5 +198,42 @@ _reg(Case("gate3d_sub", 3, "dam", 0.001, CASES["gate3d"].lower, CASES["gate3d"].
           CASES["gate3d"].cuboids, data_changes={"ElasticDt": [2.5e-5]}, note="gate3d, 4 substeps"))
 
 
+# Slab-decomposition (multi-GPU) parity cases: a fluid layer over a floor, periodic along the
+# slab axis and streaming along it at 0.5 m/s, so that within ~20 steps every face-adjacent
+# layer migrates to the next slab and the periodic seam is crossed (nothing moves far enough
+# in the dam cases).  Slab axis: z (3-D), x (2-D).
+_U = 0.5
+_reg(Case("channel3d", 3, "dam", 0.001, (-0.01, 0.0, 0.0), (0.025, 0.04, 0.036), [
+    Cuboid(1, (0.0, 0.003, 0.0), (0.012, 0.015, 0.036), 0.001, (0.0, 0.0, _U)),
+    Cuboid(4, (-0.003, 0.0, 0.0), (0.015, 0.003, 0.036), 0.001),
+    Cuboid(4, (-0.003, 0.003, 0.0), (0.0, 0.02, 0.036), 0.001),
+    Cuboid(4, (0.012, 0.003, 0.0), (0.015, 0.02, 0.036), 0.001),
+], note="periodic 3-D channel flow (slab tests)"))
+_reg(Case("channel2d", 2, "dam", 0.001, (0.0, 0.0, 0.0), (0.04, 0.03, 0.001), [
+    Cuboid(1, (0.0, 0.003, 0.0), (0.04, 0.015, 0.001), 0.001, (_U, 0.0, 0.0)),
+    Cuboid(4, (0.0, 0.0, 0.0), (0.04, 0.003, 0.001), 0.001),
+], note="periodic 2-D channel flow (slab tests)"))
+_reg(Case("channel3d_st", 3, "dam", 0.001, CASES["channel3d"].lower, CASES["channel3d"].upper,
+          CASES["channel3d"].cuboids, data_changes=_ST, note="channel3d with surface tension"))
+
+
+def d1m_weak(nranks: int) -> Case:
+    """Weak-scaling workload of bench.py --gpus N: the D1M tank extended N-fold
+    along z (slab axis), so each of N slabs holds about one D1M (N = 1 is D1M itself)."""
+    if nranks == 1:
+        return CASES["d1m"]
+    zl = 0.1 * nranks
+    return Case("d1m_x%d" % nranks, 3, "dam", 0.001, (-0.01, 0.0, -0.01), (0.21, 0.40, zl + 0.01), [
+        Cuboid(1, (0.0, 0.003, 0.0), (0.1, 0.1, zl), 0.001),
+        Cuboid(4, (0.0, 0.0, 0.0), (0.2, 0.003, zl), 0.001),
+        Cuboid(4, (0.2, 0.0, 0.0), (0.203, 0.2, zl), 0.001),
+        Cuboid(4, (-0.003, 0.0, 0.0), (0.0, 0.2, zl), 0.001),
+        Cuboid(4, (-0.003, 0.0, -0.003), (0.203, 0.2, 0.0), 0.001),
+        Cuboid(4, (-0.003, 0.0, zl), (0.203, 0.2, zl + 0.003), 0.001),
+    ], note="D1M extended %dx along z" % nranks)
+
+
 def get(name: str) -> Case:
+    if name.startswith("d1m_x"):
+        return d1m_weak(int(name[5:]))
     return CASES[name]

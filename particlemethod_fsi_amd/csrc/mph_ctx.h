@@ -1,0 +1,115 @@
+// mph_ctx.h -- the device context behind the C ABI (include/mph_gpu.h), shared by the single-GPU
+// implementation (mph_ctx.hip) and the slab-decomposed multi-GPU step (mph_dist.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "mph_internal.h"
+#include "mph_kernels.h"
+
+// Multi-GPU state of one rank (one process per GPU).  Local particle arrays hold
+// [owned | ghosts] in cell order; see mph_dist.hip for the step protocol.
+struct MphDist {
+    int rank = 0, nranks = 1, left = 0, right = 0;
+    mph::SlabGeom g{};
+    int cap = 0;                  // capacity of every local per-particle array
+    int msg_cap = 0;              // capacity (particles) of one exchange message
+    int n_own = 0;                // owned particles after the last redistribution
+    // segment sizes of the last redistribution (kMigR..kMigL) and of the two received messages
+    int seg[mph::kSlabClasses] = {0};
+    int from_l_mig = 0, from_l_band = 0, from_r_band = 0, from_r_mig = 0;
+    mph::Soa C;                   // redistributed state (pre-sort order)
+    int* cls = nullptr;           // class of every B entry
+    int* bcnt = nullptr;          // per (class, block) counts -> offsets
+    int* boff = nullptr;
+    int* bsum = nullptr;
+    int* dseg = nullptr;          // device copy of the class segment starts (7 ints)
+    int* hseg = nullptr;          // pinned host mirror
+    char *send_l = nullptr, *send_r = nullptr, *recv_l = nullptr, *recv_r = nullptr;  // device
+    int *cnt_send = nullptr, *cnt_recv = nullptr;    // device count messages (4 ints each way)
+    // transport: RCCL communicator, or a host callback (tests / hosts without RCCL)
+    bool rccl = false;
+    char uid[128] = {0};          // ncclUniqueId
+    void* comm = nullptr;         // ncclComm_t
+    mph_host_exchange_fn host_fn = nullptr;
+    void* host_user = nullptr;
+    char* host_stage = nullptr;   // pinned staging for the host transport (4 messages)
+    int* hcnt = nullptr;          // pinned count messages (send 4, recv 4)
+};
+
+struct MphCtx {
+    int device = 0;
+    int n = 0;                   // particles held on the device (single GPU: all; slab: owned+ghosts)
+    int n_glob = 0;              // particles of the whole problem (length of mph_get arrays)
+    MphConfig cfg{};
+    mph::HostDerived h{};
+    mph::DevParams P{};
+    mph::DevTables T{};
+    std::string err;
+    double time = 0.0;           // host mirror of Time (same additions as the device)
+    bool stepped = false;
+    hipStream_t stream = nullptr;
+    hipGraphExec_t graph1 = nullptr, graph8 = nullptr;
+    // host copies (original order)
+    std::vector<int> prop;
+    std::vector<double> pos0;
+    mph::StructureInit S;
+    // device
+    mph::DevTables* dT = nullptr;
+    mph::DevState* dst = nullptr;
+    mph::Soa A, B;               // sorted current state / integrated state (see mph_kernels.h)
+    int* rank_of = nullptr;
+    int *key = nullptr, *slot = nullptr, *tmp = nullptr, *cnt = nullptr, *start = nullptr, *bsum = nullptr;
+    int *nbr = nullptr, *ncount = nullptr;
+    double *pres = nullptr, *gx = nullptr, *gy = nullptr, *gz = nullptr, *pa = nullptr;
+    double4 *force = nullptr, *acc = nullptr;
+    double *dens_a = nullptr, *vstrain = nullptr, *divp = nullptr;
+    mph::StructDev Sd;
+    std::vector<void*> allocs;
+    mph::Launch L;
+    MphDist* dist = nullptr;     // non-null in slab mode
+};
+
+namespace mph {
+
+int ctx_fail(MphCtx* c, int code, const std::string& msg);
+int ctx_hip_fail(MphCtx* c, hipError_t e, const char* what);
+void* ctx_alloc(MphCtx* c, size_t bytes, int* status);
+
+template <typename T>
+int ctx_dalloc(MphCtx* c, T** p, size_t count)
+{
+    int st = MPH_OK;
+    *p = (T*)ctx_alloc(c, (count ? count : 1) * sizeof(T), &st);
+    return st;
+}
+
+void ctx_fill_launch(MphCtx* c);
+
+void ctx_set_global_error(const std::string& msg);   // mph_last_error(NULL)
+int ctx_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, const double* pos,
+               const double* pos0, const double* vel, int device, MphDist* dist);
+
+// slab mode (mph_dist.hip)
+int dist_setup(MphCtx* c, const double* pos, std::vector<int>& owned);   // geometry + owned set
+int dist_alloc(MphCtx* c);                                               // exchange buffers
+int dist_init(MphCtx* c);                                                // first exchange + init sums
+int dist_step(MphCtx* c, int nsteps, Profiler* prof = nullptr);
+void dist_free(MphCtx* c);
+
+}  // namespace mph
+
+#define MPH_HIP_OK(ctx, expr)                                                \
+    do {                                                                     \
+        hipError_t _e = (expr);                                              \
+        if (_e != hipSuccess) return mph::ctx_hip_fail(ctx, _e, #expr);      \
+    } while (0)
+
+#define MPH_CK(expr)                   \
+    do {                               \
+        int _r = (expr);               \
+        if (_r != MPH_OK) return _r;   \
+    } while (0)

@@ -12,80 +12,39 @@
 #include <string>
 #include <vector>
 
-#include "mph_internal.h"
-#include "mph_kernels.h"
+#include "mph_ctx.h"
 
 using namespace mph;
 
-struct MphCtx {
-    int device = 0;
-    int n = 0;
-    MphConfig cfg{};
-    HostDerived h{};
-    DevParams P{};
-    DevTables T{};
-    std::string err;
-    double time = 0.0;           // host mirror of Time (same additions as the device)
-    bool stepped = false;
-    hipStream_t stream = nullptr;
-    hipGraphExec_t graph1 = nullptr, graph8 = nullptr;
-    // host copies (original order)
-    std::vector<int> prop;
-    std::vector<double> pos0;
-    StructureInit S;
-    // device
-    DevTables* dT = nullptr;
-    DevState* dst = nullptr;
-    Soa A, B;                    // sorted current state / integrated state (see mph_kernels.h)
-    int* rank_of = nullptr;
-    int *key = nullptr, *slot = nullptr, *tmp = nullptr, *cnt = nullptr, *start = nullptr, *bsum = nullptr;
-    int *nbr = nullptr, *ncount = nullptr;
-    double *pres = nullptr, *gx = nullptr, *gy = nullptr, *gz = nullptr, *pa = nullptr;
-    double4 *force = nullptr, *acc = nullptr;
-    double *dens_a = nullptr, *vstrain = nullptr, *divp = nullptr;
-    StructDev Sd;
-    std::vector<void*> allocs;
-    Launch L;
-};
+namespace mph {
 
-namespace {
-
-int fail(MphCtx* c, int code, const std::string& msg)
+int ctx_fail(MphCtx* c, int code, const std::string& msg)
 {
     if (c) c->err = msg;
     return code;
 }
 
-#define HIP_OK(ctx, expr)                                                                       \
-    do {                                                                                        \
-        hipError_t _e = (expr);                                                                 \
-        if (_e != hipSuccess)                                                                   \
-            return fail(ctx, _e == hipErrorOutOfMemory ? MPH_ERR_DEVICE_OOM : MPH_ERR_HIP,      \
-                        std::string(#expr) + ": " + hipGetErrorString(_e));                     \
-    } while (0)
-
-template <typename T>
-int dalloc(MphCtx* c, T** p, size_t count)
+int ctx_hip_fail(MphCtx* c, hipError_t e, const char* what)
 {
-    *p = nullptr;
-    if (count == 0) count = 1;
-    void* q = nullptr;
-    hipError_t e = hipMalloc(&q, count * sizeof(T));
-    if (e != hipSuccess)
-        return fail(c, e == hipErrorOutOfMemory ? MPH_ERR_DEVICE_OOM : MPH_ERR_HIP,
-                    "hipMalloc(" + std::to_string(count * sizeof(T)) + " B): " + hipGetErrorString(e));
-    c->allocs.push_back(q);
-    *p = (T*)q;
-    return MPH_OK;
+    return ctx_fail(c, e == hipErrorOutOfMemory ? MPH_ERR_DEVICE_OOM : MPH_ERR_HIP,
+                    std::string(what) + ": " + hipGetErrorString(e));
 }
 
-#define CK(expr)                       \
-    do {                               \
-        int _r = (expr);               \
-        if (_r != MPH_OK) return _r;   \
-    } while (0)
+void* ctx_alloc(MphCtx* c, size_t bytes, int* status)
+{
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, bytes);
+    if (e != hipSuccess) {
+        *status = ctx_fail(c, e == hipErrorOutOfMemory ? MPH_ERR_DEVICE_OOM : MPH_ERR_HIP,
+                           "hipMalloc(" + std::to_string(bytes) + " B): " + hipGetErrorString(e));
+        return nullptr;
+    }
+    c->allocs.push_back(q);
+    *status = MPH_OK;
+    return q;
+}
 
-void fill_launch(MphCtx* c)
+void ctx_fill_launch(MphCtx* c)
 {
     Launch& L = c->L;
     L.P = &c->P;
@@ -93,7 +52,7 @@ void fill_launch(MphCtx* c)
     L.st = c->dst;
     L.stream = c->stream;
     L.prof = nullptr;
-    L.A = c->A; L.B = c->B; L.rank_of = c->rank_of;
+    L.A = c->A; L.B = c->B; L.rank_of = c->rank_of; L.dst_of = nullptr;
     L.key = c->key; L.slot = c->slot; L.tmp = c->tmp; L.cnt = c->cnt; L.start = c->start; L.bsum = c->bsum;
     L.nbr = c->nbr; L.ncount = c->ncount;
     L.pres = c->pres; L.gx = c->gx; L.gy = c->gy; L.gz = c->gz; L.pa = c->pa;
@@ -101,6 +60,23 @@ void fill_launch(MphCtx* c)
     L.dens_a = c->dens_a; L.vstrain = c->vstrain; L.divp = c->divp;
     L.S = &c->Sd;
 }
+
+}  // namespace mph
+
+namespace {
+
+int fail(MphCtx* c, int code, const std::string& msg) { return ctx_fail(c, code, msg); }
+
+#define HIP_OK(ctx, expr) MPH_HIP_OK(ctx, expr)
+#define CK(expr) MPH_CK(expr)
+
+template <typename T>
+int dalloc(MphCtx* c, T** p, size_t count)
+{
+    return ctx_dalloc(c, p, count);
+}
+
+void fill_launch(MphCtx* c) { ctx_fill_launch(c); }
 
 void enqueue_step(const Launch& L)
 {
@@ -132,6 +108,7 @@ int download_vec(MphCtx* c, const double4* d, const int* ids, double* out, int w
     HIP_OK(c, hipMemcpyAsync(id.data(), ids, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipStreamSynchronize(c->stream));
     for (int i = 0; i < n; ++i) {
+        if (id[i] < 0) continue;   // slab mode: ghost
         double* o = out + (size_t)width * id[i];
         o[0] = h[i].x;
         if (width > 1) { o[1] = h[i].y; o[2] = h[i].z; }
@@ -148,7 +125,8 @@ int download_scalar(MphCtx* c, const T* d, const int* ids, T* out)
     HIP_OK(c, hipMemcpyAsync(h.data(), d, sizeof(T) * n, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipMemcpyAsync(id.data(), ids, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipStreamSynchronize(c->stream));
-    for (int i = 0; i < n; ++i) out[id[i]] = h[i];
+    for (int i = 0; i < n; ++i)
+        if (id[i] >= 0) out[id[i]] = h[i];
     return MPH_OK;
 }
 
@@ -166,7 +144,8 @@ int download_soa3(MphCtx* c, const double* dx, const double* dy, const double* d
     HIP_OK(c, hipMemcpyAsync(id.data(), ids, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipStreamSynchronize(c->stream));
     for (int i = 0; i < n; ++i)
-        for (int k = 0; k < 3; ++k) out[3 * (size_t)id[i] + k] = h[(size_t)k * n + i];
+        if (id[i] >= 0)
+            for (int k = 0; k < 3; ++k) out[3 * (size_t)id[i] + k] = h[(size_t)k * n + i];
     return MPH_OK;
 }
 
@@ -178,14 +157,15 @@ int download_w(MphCtx* c, const double4* d, const int* ids, double* out)
     HIP_OK(c, hipMemcpyAsync(h.data(), d, sizeof(double4) * n, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipMemcpyAsync(id.data(), ids, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipStreamSynchronize(c->stream));
-    for (int i = 0; i < n; ++i) out[id[i]] = h[i].w;
+    for (int i = 0; i < n; ++i)
+        if (id[i] >= 0) out[id[i]] = h[i].w;
     return MPH_OK;
 }
 
 int download_struct_m33(MphCtx* c, const double* d, double* out)
 {
     const int ns = (int)c->S.orig.size();
-    std::memset(out, 0, sizeof(double) * 9 * (size_t)c->n);
+    std::memset(out, 0, sizeof(double) * 9 * (size_t)c->n_glob);
     if (ns == 0) return MPH_OK;
     std::vector<double> h((size_t)ns * 9);
     HIP_OK(c, hipMemcpyAsync(h.data(), d, sizeof(double) * 9 * ns, hipMemcpyDeviceToHost, c->stream));
@@ -217,13 +197,17 @@ struct EventProfiler final : Profiler {
 
 extern "C" {
 
-int mph_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, const double* pos,
-               const double* pos0, const double* vel, int device)
+}  // extern "C"
+
+namespace mph {
+
+// Shared body of mph_create (dist == nullptr) and the slab-mode constructors of mph_dist.hip
+// (dist != nullptr: only this rank's particles are uploaded, the cell grid covers its window).
+static thread_local std::string g_create_error;   // mph_last_error(NULL) after a failed create
+
+static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property, const double* pos,
+                    const double* pos0, const double* vel, int device)
 {
-    if (!out || !cfg || n < 0 || (n > 0 && (!property || !pos || !pos0 || !vel))) return MPH_ERR_ARG;
-    *out = nullptr;
-    std::unique_ptr<MphCtx> up(new MphCtx());
-    MphCtx* c = up.get();
     if (cfg->dim != 2 && cfg->dim != 3) return MPH_ERR_ARG;
     if (cfg->module < 0 || cfg->module > MPH_MODULE_NONE) return MPH_ERR_ARG;
     if (!(cfg->particle_spacing > 0.0) || !(cfg->dt > 0.0) || !(cfg->elastic_dt > 0.0)) return MPH_ERR_ARG;
@@ -231,15 +215,22 @@ int mph_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, c
         if (property[i] < 0 || property[i] >= kTypes) return MPH_ERR_ARG;
     c->cfg = *cfg;
     c->n = n;
+    c->n_glob = n;
     c->device = device;
     c->time = cfg->time;
-    HIP_OK(nullptr, hipSetDevice(device));
-    HIP_OK(nullptr, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIP_OK(c, hipSetDevice(device));
+    HIP_OK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     derive_constants(c->cfg, c->h);
     c->prop.assign(property, property + n);
     c->pos0.assign(pos0, pos0 + 3 * (size_t)n);
     std::string err;
-    CK(fail(c, build_structure(c->cfg, c->h, n, property, pos0, c->S, err), err));
+    if (c->dist) {
+        for (int i = 0; i < n; ++i)
+            if (is_struct(property[i]))
+                return fail(c, MPH_ERR_UNSUPPORTED, "slab mode does not support elastic-solid particles");
+    } else {
+        CK(fail(c, build_structure(c->cfg, c->h, n, property, pos0, c->S, err), err));
+    }
     const int ns = (int)c->S.orig.size();
     make_dev_params(c->cfg, c->h, n, ns, c->P);
     const double rc = std::sqrt(c->P.rc2);
@@ -247,7 +238,6 @@ int mph_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, c
         int r = choose_grid(c->h, cfg->dim, rc, c->P.gc, c->P.ginv, err);
         if (r != MPH_OK) return fail(c, r, err);
     }
-    c->P.ncell = c->P.gc[0] * c->P.gc[1] * c->P.gc[2];
     // interior box for the wave-uniform fast minimum image (k_neighbors / passes): >= 3 cells
     // (+1e-9 relative margin) from every periodic face; needs > 12 cells on every active axis
     c->P.fast_ok = 1;
@@ -258,6 +248,16 @@ int mph_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, c
         c->P.inner_lo[d] = c->h.dmin[d] + 3.0 * cw * (1.0 + 1e-9);
         c->P.inner_hi[d] = c->h.dmax[d] - 3.0 * cw * (1.0 + 1e-9);
     }
+    // slab mode: owned subset, local window grid along the slab axis, array capacity
+    std::vector<int> owned;
+    int cap = n;
+    if (c->dist) {
+        CK(dist_setup(c, pos, owned));
+        cap = c->dist->cap;
+        c->n = (int)owned.size();
+        c->P.n = c->n;
+    }
+    c->P.ncell = c->P.gc[0] * c->P.gc[1] * c->P.gc[2];
     // tables
     for (int t = 0; t < kTypes; ++t) {
         for (int u = 0; u < kTypes; ++u) {
@@ -270,26 +270,26 @@ int mph_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, c
         c->T.bulk[t] = c->P.bulk[t];
         c->T.bulk_visc[t] = c->P.bulk_visc[t];
     }
-    // device allocations
-    const size_t ntile = ((size_t)n + kTile - 1) / kTile;
+    // device allocations (capacity `cap` per particle array)
+    const size_t ntile = ((size_t)cap + kTile - 1) / kTile;
     CK(dalloc(c, &c->dT, 1));
     CK(dalloc(c, &c->dst, 1));
     for (Soa* s : {&c->A, &c->B}) {
-        CK(dalloc(c, &s->x, n)); CK(dalloc(c, &s->y, n)); CK(dalloc(c, &s->z, n));
-        CK(dalloc(c, &s->vx, n)); CK(dalloc(c, &s->vy, n)); CK(dalloc(c, &s->vz, n));
-        CK(dalloc(c, &s->type, n)); CK(dalloc(c, &s->id, n));
+        CK(dalloc(c, &s->x, cap)); CK(dalloc(c, &s->y, cap)); CK(dalloc(c, &s->z, cap));
+        CK(dalloc(c, &s->vx, cap)); CK(dalloc(c, &s->vy, cap)); CK(dalloc(c, &s->vz, cap));
+        CK(dalloc(c, &s->type, cap)); CK(dalloc(c, &s->id, cap));
     }
-    CK(dalloc(c, &c->rank_of, n));
-    CK(dalloc(c, &c->key, n)); CK(dalloc(c, &c->slot, n)); CK(dalloc(c, &c->tmp, n));
+    CK(dalloc(c, &c->rank_of, cap));
+    CK(dalloc(c, &c->key, cap)); CK(dalloc(c, &c->slot, cap)); CK(dalloc(c, &c->tmp, cap));
     CK(dalloc(c, &c->cnt, c->P.ncell)); CK(dalloc(c, &c->start, (size_t)c->P.ncell + 1));
     CK(dalloc(c, &c->bsum, (size_t)c->P.ncell / 4096 + 2));
-    CK(dalloc(c, &c->nbr, ntile * kTile * kMaxNeighbor)); CK(dalloc(c, &c->ncount, n));
-    CK(dalloc(c, &c->pres, n)); CK(dalloc(c, &c->gx, n)); CK(dalloc(c, &c->gy, n)); CK(dalloc(c, &c->gz, n));
-    CK(dalloc(c, &c->pa, n)); CK(dalloc(c, &c->force, n)); CK(dalloc(c, &c->acc, n));
-    CK(dalloc(c, &c->dens_a, n)); CK(dalloc(c, &c->vstrain, n)); CK(dalloc(c, &c->divp, n));
+    CK(dalloc(c, &c->nbr, ntile * kTile * kMaxNeighbor)); CK(dalloc(c, &c->ncount, cap));
+    CK(dalloc(c, &c->pres, cap)); CK(dalloc(c, &c->gx, cap)); CK(dalloc(c, &c->gy, cap)); CK(dalloc(c, &c->gz, cap));
+    CK(dalloc(c, &c->pa, cap)); CK(dalloc(c, &c->force, cap)); CK(dalloc(c, &c->acc, cap));
+    CK(dalloc(c, &c->dens_a, cap)); CK(dalloc(c, &c->vstrain, cap)); CK(dalloc(c, &c->divp, cap));
     HIP_OK(c, hipMemsetAsync(c->cnt, 0, sizeof(int) * c->P.ncell, c->stream));
-    HIP_OK(c, hipMemsetAsync(c->force, 0, sizeof(double4) * std::max(n, 1), c->stream));
-    HIP_OK(c, hipMemsetAsync(c->acc, 0, sizeof(double4) * std::max(n, 1), c->stream));
+    HIP_OK(c, hipMemsetAsync(c->force, 0, sizeof(double4) * std::max(cap, 1), c->stream));
+    HIP_OK(c, hipMemsetAsync(c->acc, 0, sizeof(double4) * std::max(cap, 1), c->stream));
     HIP_OK(c, hipMemcpyAsync(c->dT, &c->T, sizeof(DevTables), hipMemcpyHostToDevice, c->stream));
     DevState st{};
     st.time = cfg->time;
@@ -303,17 +303,20 @@ int mph_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, c
     HIP_OK(c, hipMemcpyAsync(c->dst, &st, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
     {
         // upload into the B set (original order, id = file index); the init sort reorders it
-        std::vector<double> comp(n);
-        std::vector<int> ids(n);
+        const int m = c->n;
+        std::vector<int> sel(m);
+        for (int i = 0; i < m; ++i) sel[i] = c->dist ? owned[i] : i;
+        std::vector<double> comp(m);
+        std::vector<int> ids(m), types(m);
         double* dstc[6] = {c->B.x, c->B.y, c->B.z, c->B.vx, c->B.vy, c->B.vz};
         for (int k = 0; k < 6; ++k) {
             const double* src = k < 3 ? pos : vel;
-            for (int i = 0; i < n; ++i) comp[i] = src[3 * i + (k % 3)];
-            HIP_OK(c, hipMemcpy(dstc[k], comp.data(), sizeof(double) * n, hipMemcpyHostToDevice));
+            for (int i = 0; i < m; ++i) comp[i] = src[3 * (size_t)sel[i] + (k % 3)];
+            HIP_OK(c, hipMemcpy(dstc[k], comp.data(), sizeof(double) * m, hipMemcpyHostToDevice));
         }
-        for (int i = 0; i < n; ++i) ids[i] = i;
-        HIP_OK(c, hipMemcpy(c->B.type, property, sizeof(int) * n, hipMemcpyHostToDevice));
-        HIP_OK(c, hipMemcpy(c->B.id, ids.data(), sizeof(int) * n, hipMemcpyHostToDevice));
+        for (int i = 0; i < m; ++i) { ids[i] = sel[i]; types[i] = property[sel[i]]; }
+        HIP_OK(c, hipMemcpy(c->B.type, types.data(), sizeof(int) * m, hipMemcpyHostToDevice));
+        HIP_OK(c, hipMemcpy(c->B.id, ids.data(), sizeof(int) * m, hipMemcpyHostToDevice));
     }
     // elastic solid
     if (ns > 0) {
@@ -373,25 +376,66 @@ int mph_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, c
         HIP_OK(c, hipStreamSynchronize(c->stream));
     }
     fill_launch(c);
-    // initialisation sums, main.cpp:565-568 (calculateNeighbor, DensityA, GravityCenter, DensityP)
-    launch_sort(c->L, 0);
-    launch_neighbors(c->L);
-    launch_pass_a(c->L);
+    if (c->dist) {
+        // slab mode: allocations of the exchange, then the initial ghost exchange + init sums
+        CK(dist_alloc(c));
+        CK(dist_init(c));
+    } else {
+        // initialisation sums, main.cpp:565-568 (calculateNeighbor, DensityA, GravityCenter, DensityP)
+        launch_sort(c->L, 0);
+        launch_neighbors(c->L);
+        launch_pass_a(c->L);
+    }
     HIP_OK(c, hipGetLastError());
     HIP_OK(c, hipStreamSynchronize(c->stream));
     {
         DevState hs;
         HIP_OK(c, hipMemcpy(&hs, c->dst, sizeof(DevState), hipMemcpyDeviceToHost));
-        if (hs.overflow) return fail(c, MPH_ERR_NEIGHBOR_OVERFLOW, "a particle has more than 512 neighbours");
+        if (hs.overflow & 1) return fail(c, MPH_ERR_NEIGHBOR_OVERFLOW, "a particle has more than 512 neighbours");
+        if (hs.overflow & 2) return fail(c, MPH_ERR_CAPACITY, "a particle moved past a neighbouring slab");
     }
-    *out = up.release();
     return MPH_OK;
+}
+
+void ctx_set_global_error(const std::string& msg) { g_create_error = msg; }
+
+int ctx_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, const double* pos,
+               const double* pos0, const double* vel, int device, MphDist* dist)
+{
+    g_create_error.clear();
+    if (!out || !cfg || n < 0 || (n > 0 && (!property || !pos || !pos0 || !vel))) {
+        delete dist;
+        g_create_error = "invalid argument";
+        return MPH_ERR_ARG;
+    }
+    *out = nullptr;
+    MphCtx* c = new MphCtx();
+    c->dist = dist;
+    const int r = ctx_init(c, cfg, n, property, pos, pos0, vel, device);
+    if (r != MPH_OK) {
+        g_create_error = c->err.empty() ? "mph_create failed with status " + std::to_string(r) : c->err;
+        mph_destroy(c);
+        return r;
+    }
+    *out = c;
+    return MPH_OK;
+}
+
+}  // namespace mph
+
+extern "C" {
+
+int mph_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, const double* pos,
+               const double* pos0, const double* vel, int device)
+{
+    return ctx_create(out, cfg, n, property, pos, pos0, vel, device, nullptr);
 }
 
 int mph_step(MphCtx* c, int nsteps)
 {
     if (!c || nsteps < 0) return MPH_ERR_ARG;
     HIP_OK(c, hipSetDevice(c->device));
+    if (c->dist) return dist_step(c, nsteps);
     if (nsteps == 0 || c->n == 0) {
         for (int k = 0; k < nsteps; ++k) c->time += c->cfg.dt;
         return MPH_OK;
@@ -417,9 +461,9 @@ int mph_synchronize(MphCtx* c)
     return MPH_OK;
 }
 
-int mph_particle_count(const MphCtx* c) { return c ? c->n : -1; }
+int mph_particle_count(const MphCtx* c) { return c ? c->n_glob : -1; }
 double mph_time(const MphCtx* c) { return c ? c->time : 0.0; }
-const char* mph_last_error(const MphCtx* c) { return c ? c->err.c_str() : "null context"; }
+const char* mph_last_error(const MphCtx* c) { return c ? c->err.c_str() : g_create_error.c_str(); }
 
 int mph_get_scalars(const MphCtx* c, double* out)
 {
@@ -432,7 +476,7 @@ int mph_get(MphCtx* c, int field, void* out)
 {
     if (!c || !out) return MPH_ERR_ARG;
     HIP_OK(c, hipSetDevice(c->device));
-    const int n = c->n;
+    const int n = c->n_glob;
     double* o = (double*)out;
     int* oi = (int*)out;
     const int ns = (int)c->S.orig.size();
@@ -454,7 +498,7 @@ int mph_get(MphCtx* c, int field, void* out)
         return MPH_OK;
     case MPH_FIELD_KAPPA: {
         // initializeFluid (1317-1319) before the first step, calculatePhysicalCoefficients after
-        std::vector<double> vs(n);
+        std::vector<double> vs(n, 0.0);
         if (c->stepped) CK(download_scalar(c, c->vstrain, c->A.id, vs.data()));
         for (int i = 0; i < n; ++i)
             o[i] = (c->stepped && vs[i] < 0.0) ? 0.0 : c->cfg.bulk_modulus[c->prop[i]];
@@ -504,7 +548,7 @@ int mph_set(MphCtx* c, int field, const void* in)
     double* dst[3] = {c->B.x, c->B.y, c->B.z};
     if (field == MPH_FIELD_VELOCITY) { dst[0] = c->B.vx; dst[1] = c->B.vy; dst[2] = c->B.vz; }
     for (int k = 0; k < 3; ++k) {
-        for (int i = 0; i < n; ++i) h[i] = v[3 * (size_t)id[i] + k];
+        for (int i = 0; i < n; ++i) h[i] = id[i] >= 0 ? v[3 * (size_t)id[i] + k] : 0.0;
         HIP_OK(c, hipMemcpy(dst[k], h.data(), sizeof(double) * n, hipMemcpyHostToDevice));
     }
     return MPH_OK;
@@ -513,7 +557,8 @@ int mph_set(MphCtx* c, int field, const void* in)
 int mph_write_prof(MphCtx* c, const char* path)
 {
     if (!c || !path) return MPH_ERR_ARG;
-    const int n = c->n;
+    if (c->dist) return fail(c, MPH_ERR_UNSUPPORTED, "slab mode: gather the owned entries (mph_get) and use mph_write_prof_arrays");
+    const int n = c->n_glob;
     std::vector<double> pos(3 * (size_t)n), vel(3 * (size_t)n);
     CK(mph_get(c, MPH_FIELD_POSITION, pos.data()));
     CK(mph_get(c, MPH_FIELD_VELOCITY, vel.data()));
@@ -524,7 +569,8 @@ int mph_write_prof(MphCtx* c, const char* path)
 int mph_write_vtk(MphCtx* c, const char* path)
 {
     if (!c || !path) return MPH_ERR_ARG;
-    const size_t n = (size_t)c->n;
+    if (c->dist) return fail(c, MPH_ERR_UNSUPPORTED, "slab mode: gather the owned entries (mph_get) and use mph_write_vtk_arrays");
+    const size_t n = (size_t)c->n_glob;
     std::vector<double> pos(3 * n), vel(3 * n), acc(3 * n), force(3 * n), stress(9 * n), strain(9 * n);
     std::vector<int> isnc(n), nc(n);
     CK(mph_get(c, MPH_FIELD_POSITION, pos.data()));
@@ -535,7 +581,7 @@ int mph_write_vtk(MphCtx* c, const char* path)
     CK(mph_get(c, MPH_FIELD_STRAIN, strain.data()));
     CK(mph_get(c, MPH_FIELD_INITIAL_STRUCTURE_NEIGHBOR_COUNT, isnc.data()));
     CK(mph_get(c, MPH_FIELD_NEIGHBOR_COUNT, nc.data()));
-    return mph_write_vtk_arrays(path, c->n, c->prop.data(), pos.data(), c->pos0.data(), vel.data(),
+    return mph_write_vtk_arrays(path, c->n_glob, c->prop.data(), pos.data(), c->pos0.data(), vel.data(),
                                 acc.data(), force.data(), stress.data(), strain.data(), isnc.data(), nc.data());
 }
 
@@ -544,13 +590,17 @@ int mph_profile_steps(MphCtx* c, int nsteps, double* avg_ms, int* launches, char
     if (!c || nsteps <= 0 || !avg_ms || !launches || !names32) return MPH_ERR_ARG;
     HIP_OK(c, hipSetDevice(c->device));
     EventProfiler prof;
-    Launch L = c->L;
-    L.prof = &prof;
-    for (int k = 0; k < nsteps; ++k) enqueue_step(L);
-    HIP_OK(c, hipGetLastError());
-    HIP_OK(c, hipStreamSynchronize(c->stream));
-    for (int k = 0; k < nsteps; ++k) c->time += c->cfg.dt;
-    c->stepped = true;
+    if (c->dist) {
+        CK(dist_step(c, nsteps, &prof));
+    } else {
+        Launch L = c->L;
+        L.prof = &prof;
+        for (int k = 0; k < nsteps; ++k) enqueue_step(L);
+        HIP_OK(c, hipGetLastError());
+        HIP_OK(c, hipStreamSynchronize(c->stream));
+        for (int k = 0; k < nsteps; ++k) c->time += c->cfg.dt;
+        c->stepped = true;
+    }
     std::vector<std::string> order;
     std::map<std::string, std::pair<double, int>> acc;
     for (auto& r : prof.recs) {
@@ -592,6 +642,7 @@ void mph_destroy(MphCtx* c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->graph1) (void)hipGraphExecDestroy(c->graph1);
     if (c->graph8) (void)hipGraphExecDestroy(c->graph8);
+    if (c->dist) dist_free(c);
     for (void* p : c->allocs) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;

@@ -1,29 +1,521 @@
-// mph_dist.hip -- multi-GPU slab decomposition entry points (one process per GPU, RCCL).
+// mph_dist.hip -- multi-GPU slab decomposition of the hot path (one process per GPU, RCCL).
+//
+// The reference has no domain decomposition (one OpenMP/OpenACC process, main.cpp:597-686).  The
+// update of a particle depends only on neighbours within the cutoff rc = MaxRadius + MARGIN
+// (main.cpp:1765), so the periodic domain is cut into `nranks` equal slabs along one axis
+// (SURVEY 8e).  Each rank holds
+//
+//   owned   particles inside its slab [lo, hi)                (computed, returned by mph_get)
+//   ghosts  copies of the neighbours' particles within h >= rc of a face, and of its own
+//           particles that crossed a face this step (now owned next door)
+//
+// One step (this file, dist_step), all on the context's stream:
+//
+//   1. k_dist_classify: wall motion + periodic wrap (calculateWall / calculatePeriodicBoundary
+//      exactly as the single-GPU k_prep), then the slab class of every owned particle; ghosts of
+//      the previous step are dropped.
+//   2. stable partition into C = [migR | bandR | inner | bandL | migL]     (scan + scatter)
+//   3. exchange: to the left neighbour [bandL | migL], to the right [migR | bandR] (56 B per
+//      particle, preceded by a 2-int count message); received messages are appended to C:
+//      [.. | from left: their migR (ours now), their bandR (ghosts) | from right: their bandL
+//      (ghosts), their migL (ours now)].  Our own migrants stay in C as ghosts.
+//   4. cell sort of C (owned + ghosts) into A, neighbour search, pass A -- the single-GPU kernels
+//      on the local window grid (DevParams.corg / gc along the slab axis).
+//   5. halo exchange of the pass-A values every neighbour's ghosts need in pass B: PressureP
+//      (+ GravityCenter, PressureA with surface tension), 8 or 40 B per ghost.
+//   6. pass B (forces, kick, drift) into B.
+//
+// Owned particles see every neighbour (band width h >= rc), run the same FP64 expressions as
+// the single-GPU path, and get bit-identical neighbour sets; sums may be ordered differently
+// (local cell grid), so values agree with the single-GPU run to reassociation roundoff.
+// Transport: RCCL ncclSend/ncclRecv (xGMI) or a host callback (tests, mph_create_dist_host).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstring>
+#include <string>
+#include <vector>
 
-#include "../../include/mph_gpu.h"
+#include "mph_ctx.h"
+
+using namespace mph;
+
+namespace {
+
+constexpr size_t kMsgBytes = 56;   // per particle, k_dist_pack layout
+
+#define RCCL_OK(ctx, expr)                                                                     \
+    do {                                                                                       \
+        ncclResult_t _r = (expr);                                                              \
+        if (_r != ncclSuccess)                                                                 \
+            return ctx_fail(ctx, MPH_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+    } while (0)
+
+// Slab of `rank`: equal widths along `axis`; hi(r) and lo(r+1) are the same expression.
+void slab_of(const HostDerived& h, int axis, int rank, int nranks, double& lo, double& hi)
+{
+    const double W = h.dw[axis];
+    lo = rank == 0 ? h.dmin[axis] : h.dmin[axis] + W * rank / nranks;
+    hi = rank == nranks - 1 ? h.dmax[axis] : h.dmin[axis] + W * (rank + 1) / nranks;
+}
+
+SlabGeom make_geom(const HostDerived& h, int axis, int rank, int nranks, double halo)
+{
+    SlabGeom g{};
+    g.axis = axis;
+    const int l = (rank + nranks - 1) % nranks, r = (rank + 1) % nranks;
+    slab_of(h, axis, rank, nranks, g.lo, g.hi);
+    slab_of(h, axis, l, nranks, g.llo, g.lhi);
+    slab_of(h, axis, r, nranks, g.rlo, g.rhi);
+    g.first = rank == 0; g.last = rank == nranks - 1;
+    g.lfirst = l == 0; g.llast = l == nranks - 1;
+    g.rfirst = r == 0; g.rlast = r == nranks - 1;
+    g.h = halo;
+    return g;
+}
+
+double wrap_coord(const HostDerived& h, int axis, double x)
+{
+#pragma clang fp contract(off)
+    const double w = h.dw[axis];
+    const double u = x - h.dmin[axis];
+    return u - w * std::floor(u / w) + h.dmin[axis];
+}
+
+double halo_width(const DevParams& P) { return std::sqrt(P.rc2) * (1.0 + 1e-6); }
+
+int check_geometry(const MphConfig& cfg, int nranks, int axis, std::string& err)
+{
+    if (nranks < 2) { err = "slab mode needs nranks >= 2 (use mph_create)"; return MPH_ERR_ARG; }
+    if (axis < 0 || axis > 2 || (cfg.dim == 2 && axis == 2)) { err = "invalid slab axis"; return MPH_ERR_ARG; }
+    return MPH_OK;
+}
+
+int copy_soa(MphCtx* c, const Soa& dst, const Soa& src, int n)
+{
+    double* dd[6] = {dst.x, dst.y, dst.z, dst.vx, dst.vy, dst.vz};
+    const double* sd[6] = {src.x, src.y, src.z, src.vx, src.vy, src.vz};
+    for (int k = 0; k < 6; ++k)
+        MPH_HIP_OK(c, hipMemcpyAsync(dd[k], sd[k], sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream));
+    MPH_HIP_OK(c, hipMemcpyAsync(dst.type, src.type, sizeof(int) * n, hipMemcpyDeviceToDevice, c->stream));
+    MPH_HIP_OK(c, hipMemcpyAsync(dst.id, src.id, sizeof(int) * n, hipMemcpyDeviceToDevice, c->stream));
+    return MPH_OK;
+}
+
+// -- transport ----------------------------------------------------------------------------------
+
+// send_l -> left neighbour (arrives there as its recv_r), send_r -> right neighbour (its recv_l)
+int exchange(MphCtx* c, const void* send_l, size_t bsl, const void* send_r, size_t bsr, void* recv_l,
+             size_t brl, void* recv_r, size_t brr)
+{
+    MphDist& D = *c->dist;
+    if (D.rccl) {
+        ncclComm_t comm = (ncclComm_t)D.comm;
+        RCCL_OK(c, ncclGroupStart());
+        // per-peer order: first the left-going message, then the right-going one (matters when
+        // left == right, nranks == 2): a rank's first receive from a peer matches that peer's
+        // first send, i.e. its left-going message = our from-right message
+        if (bsl) RCCL_OK(c, ncclSend(send_l, bsl, ncclChar, D.left, comm, c->stream));
+        if (brr) RCCL_OK(c, ncclRecv(recv_r, brr, ncclChar, D.right, comm, c->stream));
+        if (bsr) RCCL_OK(c, ncclSend(send_r, bsr, ncclChar, D.right, comm, c->stream));
+        if (brl) RCCL_OK(c, ncclRecv(recv_l, brl, ncclChar, D.left, comm, c->stream));
+        RCCL_OK(c, ncclGroupEnd());
+        return MPH_OK;
+    }
+    const size_t region = (size_t)D.msg_cap * kMsgBytes;
+    char* hs_l = D.host_stage;
+    char* hs_r = D.host_stage + region;
+    char* hr_l = D.host_stage + 2 * region;
+    char* hr_r = D.host_stage + 3 * region;
+    if (bsl) MPH_HIP_OK(c, hipMemcpyAsync(hs_l, send_l, bsl, hipMemcpyDeviceToHost, c->stream));
+    if (bsr) MPH_HIP_OK(c, hipMemcpyAsync(hs_r, send_r, bsr, hipMemcpyDeviceToHost, c->stream));
+    MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
+    if (D.host_fn(D.host_user, hs_l, bsl, hs_r, bsr, hr_l, brl, hr_r, brr) != 0)
+        return ctx_fail(c, MPH_ERR_TRANSPORT, "host exchange callback failed");
+    if (brl) MPH_HIP_OK(c, hipMemcpyAsync(recv_l, hr_l, brl, hipMemcpyHostToDevice, c->stream));
+    if (brr) MPH_HIP_OK(c, hipMemcpyAsync(recv_r, hr_r, brr, hipMemcpyHostToDevice, c->stream));
+    return MPH_OK;
+}
+
+// Steps 1-3 of the protocol: classify, partition, exchange migrants + ghosts.  Leaves the new
+// local set (n entries, owned and ghosts) in D.C.
+int redistribute(MphCtx* c, bool move, Profiler* prof)
+{
+    MphDist& D = *c->dist;
+    Launch L = c->L;
+    L.prof = prof;
+    const int n_prev = c->n;
+    const int nb = dist_blocks(n_prev);
+    launch_dist_classify(L, D.g, n_prev, move ? 1 : 0, D.cls, D.bcnt);
+    launch_scan(D.bcnt, kSlabClasses * nb, D.bsum, D.boff, n_prev, c->stream, prof);
+    launch_dist_scatter(L, n_prev, D.cls, D.boff, D.C, D.dseg);
+    MPH_HIP_OK(c, hipMemcpyAsync(D.hseg, D.dseg, sizeof(int) * (kSlabClasses + 1), hipMemcpyDeviceToHost,
+                                 c->stream));
+    MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
+    for (int k = 0; k < kSlabClasses; ++k) D.seg[k] = D.hseg[k + 1] - D.hseg[k];
+    const int mR = D.seg[kMigR], bR = D.seg[kBandR], bL = D.seg[kBandL], mL = D.seg[kMigL];
+    const int nc = D.hseg[kSlabDrop];                 // kept entries (classes 0..4)
+    // count messages: left-going {bandL, migL}, right-going {migR, bandR}
+    int* hc = D.hcnt;
+    hc[0] = bL; hc[1] = mL; hc[2] = mR; hc[3] = bR;
+    MPH_HIP_OK(c, hipMemcpyAsync(D.cnt_send, hc, sizeof(int) * 4, hipMemcpyHostToDevice, c->stream));
+    MPH_CK(exchange(c, D.cnt_send, 2 * sizeof(int), D.cnt_send + 2, 2 * sizeof(int), D.cnt_recv,
+                    2 * sizeof(int), D.cnt_recv + 2, 2 * sizeof(int)));
+    MPH_HIP_OK(c, hipMemcpyAsync(hc + 4, D.cnt_recv, sizeof(int) * 4, hipMemcpyDeviceToHost, c->stream));
+    MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
+    D.from_l_mig = hc[4]; D.from_l_band = hc[5];     // their {migR, bandR}
+    D.from_r_band = hc[6]; D.from_r_mig = hc[7];     // their {bandL, migL}
+    const int fl = D.from_l_mig + D.from_l_band, fr = D.from_r_band + D.from_r_mig;
+    const int n_new = nc + fl + fr;
+    if (n_new > D.cap || fl > D.msg_cap || fr > D.msg_cap)
+        return ctx_fail(c, MPH_ERR_CAPACITY, "slab mode: local particle capacity " + std::to_string(D.cap) +
+                                                 " exceeded (" + std::to_string(n_new) + ")");
+    launch_dist_pack(L, D.C, D.hseg[kBandL], bL + mL, D.send_l);
+    launch_dist_pack(L, D.C, 0, mR + bR, D.send_r);
+    MPH_CK(exchange(c, D.send_l, kMsgBytes * (bL + mL), D.send_r, kMsgBytes * (mR + bR), D.recv_l,
+                    kMsgBytes * fl, D.recv_r, kMsgBytes * fr));
+    launch_dist_unpack(L, D.recv_l, fl, D.C, nc);
+    launch_dist_unpack(L, D.recv_r, fr, D.C, nc + fl);
+    c->n = n_new;
+    c->P.n = n_new;
+    D.n_own = bR + D.seg[kInner] + bL + D.from_l_mig + D.from_r_mig;
+    return MPH_OK;
+}
+
+// cell sort of C into A (slab-local grid), recording dst_of = pre-sort -> sorted index
+void sort_local(MphCtx* c, int mode, Profiler* prof)
+{
+    Launch L = c->L;
+    L.prof = prof;
+    L.B = c->dist->C;
+    L.dst_of = c->rank_of;
+    launch_sort(L, mode);
+}
+
+HaloFields halo_fields(MphCtx* c)
+{
+    HaloFields F{};
+    F.f[0] = c->pres;
+    F.nf = 1;
+    if (c->P.surface) {
+        F.f[1] = c->gx; F.f[2] = c->gy; F.f[3] = c->gz; F.f[4] = c->pa;
+        F.nf = 5;
+    }
+    return F;
+}
+
+// Step 5: the pass-A values of every neighbour's ghosts.
+int halo_exchange(MphCtx* c, Profiler* prof)
+{
+    MphDist& D = *c->dist;
+    Launch L = c->L;
+    L.prof = prof;
+    const HaloFields F = halo_fields(c);
+    const int nc = D.hseg[kSlabDrop];
+    const int fl = D.from_l_mig + D.from_l_band;
+    // to left: the left neighbour's migrants we now own, then our band-left particles
+    const int l1 = nc, ln1 = D.from_l_mig, l2 = D.hseg[kBandL], ln2 = D.seg[kBandL];
+    // to right: the right neighbour's migrants we now own, then our band-right particles
+    const int r1 = nc + fl + D.from_r_band, rn1 = D.from_r_mig, r2 = D.hseg[kBandR], rn2 = D.seg[kBandR];
+    // from left: values of our migL ghosts, then of the left neighbour's bandR ghosts
+    const int fl1 = D.hseg[kMigL], fln1 = D.seg[kMigL], fl2 = nc + D.from_l_mig, fln2 = D.from_l_band;
+    // from right: values of our migR ghosts, then of the right neighbour's bandL ghosts
+    const int fr1 = D.hseg[kMigR], frn1 = D.seg[kMigR], fr2 = nc + fl, frn2 = D.from_r_band;
+    double* sl = (double*)D.send_l;
+    double* sr = (double*)D.send_r;
+    double* rl = (double*)D.recv_l;
+    double* rr = (double*)D.recv_r;
+    launch_halo_pack(L, c->rank_of, l1, ln1, l2, ln2, F, sl);
+    launch_halo_pack(L, c->rank_of, r1, rn1, r2, rn2, F, sr);
+    const size_t b = sizeof(double) * F.nf;
+    MPH_CK(exchange(c, sl, b * (ln1 + ln2), sr, b * (rn1 + rn2), rl, b * (fln1 + fln2), rr, b * (frn1 + frn2)));
+    launch_halo_unpack(L, rl, c->rank_of, fl1, fln1, fl2, fln2, F);
+    launch_halo_unpack(L, rr, c->rank_of, fr1, frn1, fr2, frn2, F);
+    return MPH_OK;
+}
+
+int check_state(MphCtx* c)
+{
+    DevState hs;
+    MPH_HIP_OK(c, hipMemcpyAsync(&hs, c->dst, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
+    MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
+    if (hs.overflow & 1) return ctx_fail(c, MPH_ERR_NEIGHBOR_OVERFLOW, "a particle has more than 512 neighbours");
+    if (hs.overflow & 2) return ctx_fail(c, MPH_ERR_CAPACITY, "a particle moved past a neighbouring slab");
+    return MPH_OK;
+}
+
+}  // namespace
+
+namespace mph {
+
+int dist_setup(MphCtx* c, const double* pos, std::vector<int>& owned)
+{
+    MphDist& D = *c->dist;
+    const HostDerived& h = c->h;
+    const int axis = D.g.axis;
+    std::string err;
+    MPH_CK(ctx_fail(c, check_geometry(c->cfg, D.nranks, axis, err), err));
+    D.left = (D.rank + D.nranks - 1) % D.nranks;
+    D.right = (D.rank + 1) % D.nranks;
+    const double halo = halo_width(c->P);
+    D.g = make_geom(h, axis, D.rank, D.nranks, halo);
+    const double W = h.dw[axis];
+    const double cw = W / c->P.gc[axis];
+    // slabs must be wider than two halos plus a migration margin, so that a band particle is
+    // mirrored to one neighbour only and a migrant reaches only the adjacent slab
+    if (W / D.nranks < 2.0 * halo + 2.0 * h.dx)
+        return ctx_fail(c, MPH_ERR_DOMAIN, "slab width " + std::to_string(W / D.nranks) +
+                                               " below two halo widths (" + std::to_string(2.0 * halo) + ")");
+    // local window grid along the slab axis: [lo - h - cw, hi + h + cw)
+    const double wlo = D.g.lo - halo - cw, whi = D.g.hi + halo + cw;
+    const int gloc = (int)std::ceil((whi - wlo) / cw);
+    if (gloc < 5) return ctx_fail(c, MPH_ERR_DOMAIN, "slab window narrower than 5 cells");
+    c->P.corg[axis] = wlo;
+    c->P.gc[axis] = std::min(gloc, c->P.gc[axis] + 1);
+    // fast-path interior: >= 3 cells inside both the window and the periodic domain
+    c->P.inner_lo[axis] = std::max(wlo, h.dmin[axis]) + 3.0 * cw * (1.0 + 1e-9);
+    c->P.inner_hi[axis] = std::min(whi, h.dmax[axis]) - 3.0 * cw * (1.0 + 1e-9);
+    // initial owned set and a capacity for owned + ghosts (+ headroom for migration imbalance)
+    owned.clear();
+    size_t near = 0;
+    for (int i = 0; i < c->n_glob; ++i) {
+        const double a = wrap_coord(h, axis, pos[3 * (size_t)i + axis]);
+        if (slab_owns(a, D.g.lo, D.g.hi, D.g.first, D.g.last)) {
+            owned.push_back(i);
+        } else {
+            // within h + 2 dx outside a face (periodic distance): a ghost candidate
+            double dl = D.g.lo - a, dh = a - D.g.hi;
+            dl -= W * std::floor(dl / W);
+            dh -= W * std::floor(dh / W);
+            if (std::min(dl, dh) <= halo + 2.0 * h.dx) ++near;
+        }
+    }
+    const size_t want = (size_t)((owned.size() + near) * 1.25) + 65536;
+    D.cap = (int)std::min<size_t>(want, (size_t)c->n_glob);
+    D.msg_cap = D.cap;
+    D.n_own = (int)owned.size();
+    return MPH_OK;
+}
+
+int dist_alloc(MphCtx* c)
+{
+    MphDist& D = *c->dist;
+    const int cap = D.cap;
+    Soa& C = D.C;
+    MPH_CK(ctx_dalloc(c, &C.x, cap)); MPH_CK(ctx_dalloc(c, &C.y, cap)); MPH_CK(ctx_dalloc(c, &C.z, cap));
+    MPH_CK(ctx_dalloc(c, &C.vx, cap)); MPH_CK(ctx_dalloc(c, &C.vy, cap)); MPH_CK(ctx_dalloc(c, &C.vz, cap));
+    MPH_CK(ctx_dalloc(c, &C.type, cap)); MPH_CK(ctx_dalloc(c, &C.id, cap));
+    MPH_CK(ctx_dalloc(c, &D.cls, cap));
+    const size_t nslots = (size_t)kSlabClasses * dist_blocks(cap);
+    MPH_CK(ctx_dalloc(c, &D.bcnt, nslots + 1));
+    MPH_CK(ctx_dalloc(c, &D.boff, nslots + 1));
+    MPH_CK(ctx_dalloc(c, &D.bsum, nslots / 4096 + 2));
+    MPH_CK(ctx_dalloc(c, &D.dseg, kSlabClasses + 2));
+    MPH_CK(ctx_dalloc(c, &D.cnt_send, 4));
+    MPH_CK(ctx_dalloc(c, &D.cnt_recv, 4));
+    const size_t region = (size_t)D.msg_cap * kMsgBytes;
+    MPH_CK(ctx_dalloc(c, &D.send_l, region)); MPH_CK(ctx_dalloc(c, &D.send_r, region));
+    MPH_CK(ctx_dalloc(c, &D.recv_l, region)); MPH_CK(ctx_dalloc(c, &D.recv_r, region));
+    MPH_HIP_OK(c, hipHostMalloc((void**)&D.hseg, sizeof(int) * (kSlabClasses + 2), hipHostMallocDefault));
+    MPH_HIP_OK(c, hipHostMalloc((void**)&D.hcnt, sizeof(int) * 8, hipHostMallocDefault));
+    if (D.rccl) {
+        ncclUniqueId id;
+        std::memcpy(&id, D.uid, sizeof(id));
+        ncclComm_t comm = nullptr;
+        RCCL_OK(c, ncclCommInitRank(&comm, D.nranks, id, D.rank));
+        D.comm = comm;
+    } else {
+        MPH_HIP_OK(c, hipHostMalloc((void**)&D.host_stage, 4 * region, hipHostMallocDefault));
+    }
+    return MPH_OK;
+}
+
+int dist_init(MphCtx* c)
+{
+    // calculateNeighbor, DensityA, GravityCenter, DensityP of the initialisation (main.cpp:565-568)
+    // on owned + ghosts (no motion, no time advance)
+    MPH_CK(redistribute(c, false, nullptr));
+    sort_local(c, 0, nullptr);
+    launch_neighbors(c->L);
+    launch_pass_a(c->L);
+    // the integrated-state set B starts as the sorted local set (owned + ghosts, ids signed)
+    MPH_CK(copy_soa(c, c->B, c->A, c->n));
+    MPH_HIP_OK(c, hipGetLastError());
+    return check_state(c);
+}
+
+int dist_step(MphCtx* c, int nsteps, Profiler* prof)
+{
+    Launch L = c->L;
+    L.prof = prof;
+    for (int k = 0; k < nsteps; ++k) {
+        MPH_CK(redistribute(c, true, prof));
+        sort_local(c, 2, prof);
+        launch_neighbors(L);
+        launch_pass_a(L);
+        MPH_CK(halo_exchange(c, prof));
+        launch_pass_b(L);
+        MPH_HIP_OK(c, hipGetLastError());
+        c->time += c->cfg.dt;
+        c->stepped = true;
+    }
+    return check_state(c);
+}
+
+void dist_free(MphCtx* c)
+{
+    MphDist* D = c->dist;
+    if (!D) return;
+    if (D->comm) (void)ncclCommDestroy((ncclComm_t)D->comm);
+    if (D->hseg) (void)hipHostFree(D->hseg);
+    if (D->hcnt) (void)hipHostFree(D->hcnt);
+    if (D->host_stage) (void)hipHostFree(D->host_stage);
+    delete D;
+    c->dist = nullptr;
+}
+
+}  // namespace mph
 
 extern "C" {
 
 int mph_dist_unique_id(char* out128)
 {
     if (!out128) return MPH_ERR_ARG;
-    std::memset(out128, 0, 128);
-    return MPH_ERR_UNSUPPORTED;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return MPH_ERR_RCCL;
+    static_assert(sizeof(id) == 128, "ncclUniqueId size");
+    std::memcpy(out128, &id, sizeof(id));
+    return MPH_OK;
 }
 
 int mph_create_dist(MphCtx** ctx, const MphConfig* cfg, int n, const int* property, const double* pos,
                     const double* pos0, const double* vel, int device, int rank, int nranks,
                     const char* unique_id128, int axis)
 {
-    (void)cfg; (void)n; (void)property; (void)pos; (void)pos0; (void)vel; (void)device;
-    (void)rank; (void)nranks; (void)unique_id128; (void)axis;
-    if (ctx) *ctx = nullptr;
-    return MPH_ERR_UNSUPPORTED;
+    if (!unique_id128 || rank < 0 || rank >= nranks) return MPH_ERR_ARG;
+    MphDist* D = new MphDist();
+    D->rank = rank;
+    D->nranks = nranks;
+    D->g.axis = axis;
+    D->rccl = true;
+    std::memcpy(D->uid, unique_id128, sizeof(D->uid));
+    return ctx_create(ctx, cfg, n, property, pos, pos0, vel, device, D);
 }
 
-int mph_owned_count(const MphCtx* ctx) { return mph_particle_count(ctx); }
+int mph_create_dist_host(MphCtx** ctx, const MphConfig* cfg, int n, const int* property, const double* pos,
+                         const double* pos0, const double* vel, int device, int rank, int nranks, int axis,
+                         mph_host_exchange_fn fn, void* user)
+{
+    if (!fn || rank < 0 || rank >= nranks) return MPH_ERR_ARG;
+    MphDist* D = new MphDist();
+    D->rank = rank;
+    D->nranks = nranks;
+    D->g.axis = axis;
+    D->host_fn = fn;
+    D->host_user = user;
+    return ctx_create(ctx, cfg, n, property, pos, pos0, vel, device, D);
+}
+
+int mph_dist_selftest(int device)
+{
+    // one-rank RCCL communicator whose left and right neighbour are itself: exercises the
+    // group send/recv of exchange() including the per-peer message order that nranks == 2
+    // relies on (our first receive from a peer = its first, left-going, send)
+    MphCtx c;
+    MphDist* D = new MphDist();
+    c.dist = D;
+    D->rccl = true;
+    D->nranks = 1;
+    int status = MPH_OK;
+    auto run = [&]() -> int {
+        MPH_HIP_OK(&c, hipSetDevice(device));
+        MPH_HIP_OK(&c, hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+        ncclUniqueId id;
+        RCCL_OK(&c, ncclGetUniqueId(&id));
+        ncclComm_t comm = nullptr;
+        RCCL_OK(&c, ncclCommInitRank(&comm, 1, id, 0));
+        D->comm = comm;
+        const size_t nl = 1000, nr = 37;
+        std::vector<char> hl(nl), hr(nr), gl(nr), gr(nl);
+        for (size_t i = 0; i < nl; ++i) hl[i] = (char)(i * 7 + 1);
+        for (size_t i = 0; i < nr; ++i) hr[i] = (char)(i * 5 + 2);
+        char *sl, *sr, *rl, *rr;
+        MPH_CK(ctx_dalloc(&c, &sl, nl)); MPH_CK(ctx_dalloc(&c, &sr, nr));
+        MPH_CK(ctx_dalloc(&c, &rl, nr)); MPH_CK(ctx_dalloc(&c, &rr, nl));
+        MPH_HIP_OK(&c, hipMemcpy(sl, hl.data(), nl, hipMemcpyHostToDevice));
+        MPH_HIP_OK(&c, hipMemcpy(sr, hr.data(), nr, hipMemcpyHostToDevice));
+        // left-going (sl) must arrive as from-right (rr); right-going (sr) as from-left (rl)
+        MPH_CK(exchange(&c, sl, nl, sr, nr, rl, nr, rr, nl));
+        // a zero-byte direction is skipped on both sides
+        MPH_CK(exchange(&c, sl, 0, sr, nr, rl, nr, rr, 0));
+        MPH_HIP_OK(&c, hipStreamSynchronize(c.stream));
+        MPH_HIP_OK(&c, hipMemcpy(gl.data(), rl, nr, hipMemcpyDeviceToHost));
+        MPH_HIP_OK(&c, hipMemcpy(gr.data(), rr, nl, hipMemcpyDeviceToHost));
+        if (gl != hr || gr != hl) return ctx_fail(&c, MPH_ERR_RCCL, "RCCL self-exchange delivered wrong bytes");
+        return MPH_OK;
+    };
+    status = run();
+    ctx_set_global_error(c.err);
+    (void)hipStreamSynchronize(c.stream);
+    dist_free(&c);
+    for (void* p : c.allocs) (void)hipFree(p);
+    if (c.stream) (void)hipStreamDestroy(c.stream);
+    return status;
+}
+
+int mph_owned_count(const MphCtx* c)
+{
+    if (!c) return -1;
+    return c->dist ? c->dist->n_own : c->n_glob;
+}
+
+int mph_owned_ids(MphCtx* c, int* out)
+{
+    if (!c || !out) return MPH_ERR_ARG;
+    if (!c->dist) {
+        for (int i = 0; i < c->n_glob; ++i) out[i] = i;
+        return MPH_OK;
+    }
+    MPH_HIP_OK(c, hipSetDevice(c->device));
+    std::vector<int> id(c->n);
+    MPH_HIP_OK(c, hipMemcpyAsync(id.data(), c->B.id, sizeof(int) * c->n, hipMemcpyDeviceToHost, c->stream));
+    MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
+    int k = 0;
+    for (int i = 0; i < c->n; ++i)
+        if (id[i] >= 0) {
+            if (k >= c->dist->n_own) return ctx_fail(c, MPH_ERR_CAPACITY, "owned id count mismatch");
+            out[k++] = id[i];
+        }
+    std::sort(out, out + k);
+    return k == c->dist->n_own ? MPH_OK : ctx_fail(c, MPH_ERR_CAPACITY, "owned id count mismatch");
+}
+
+int mph_slab_bounds(const MphConfig* cfg, int rank, int nranks, int axis, double* out3)
+{
+    if (!cfg || !out3 || nranks < 1 || rank < 0 || rank >= nranks || axis < 0 || axis > 2) return MPH_ERR_ARG;
+    HostDerived h{};
+    derive_constants(*cfg, h);
+    DevParams P{};
+    make_dev_params(*cfg, h, 0, 0, P);
+    slab_of(h, axis, rank, nranks, out3[0], out3[1]);
+    out3[2] = halo_width(P);
+    return MPH_OK;
+}
+
+int mph_slab_owner(const MphConfig* cfg, int nranks, int axis, double x)
+{
+    if (!cfg || nranks < 1 || axis < 0 || axis > 2) return MPH_ERR_ARG;
+    HostDerived h{};
+    derive_constants(*cfg, h);
+    const double a = wrap_coord(h, axis, x);
+    for (int r = 0; r < nranks; ++r) {
+        double lo, hi;
+        slab_of(h, axis, r, nranks, lo, hi);
+        if (slab_owns(a, lo, hi, r == 0, r == nranks - 1)) return r;
+    }
+    return MPH_ERR_DOMAIN;
+}
 
 }  // extern "C"

@@ -391,6 +391,7 @@ void make_dev_params(const MphConfig& c, const HostDerived& h, int n, int n_stru
     P.substeps = (int)(c.dt / c.elastic_dt + 0.5);
     for (int d = 0; d < 3; ++d) {
         P.dmin[d] = h.dmin[d];
+        P.corg[d] = h.dmin[d];
         P.dw[d] = h.dw[d];
         P.hw[d] = 0.5 * h.dw[d];
         P.w075[d] = 0.75 * h.dw[d];

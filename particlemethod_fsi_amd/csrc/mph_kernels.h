@@ -55,6 +55,7 @@ struct Launch {
     // B set: integrated state in the previous order; A set: cell-sorted current order
     Soa A, B;
     int* rank_of = nullptr;
+    int* dst_of = nullptr;        // slab mode: pre-sort index -> sorted index (else rank_of[id])
     int *key = nullptr, *slot = nullptr, *tmp = nullptr, *cnt = nullptr, *start = nullptr, *bsum = nullptr;
     int *nbr = nullptr, *ncount = nullptr;
     // pass A products (A order): pressure values, gravity centre (GC, PressureA), sums
@@ -64,10 +65,26 @@ struct Launch {
     const StructDev* S = nullptr;
 };
 
-void launch_sort(const Launch& L, int mode);   // mode 0 init, 1 step
+void launch_sort(const Launch& L, int mode);   // mode 0 init, 1 step, 2 step (motion done)
 void launch_neighbors(const Launch& L);
 void launch_pass_a(const Launch& L);
 void launch_pass_b(const Launch& L);
 void launch_structure(const Launch& L);
+
+// slab decomposition (mph_dist.hip)
+struct HaloFields {
+    double* f[5];
+    int nf;
+};
+void launch_scan(int* cnt, int ncell, int* bsum, int* start, int total, hipStream_t stream, Profiler* prof);
+int dist_blocks(int n);
+void launch_dist_classify(const Launch& L, const SlabGeom& g, int n, int move, int* cls, int* bcnt);
+void launch_dist_scatter(const Launch& L, int n, const int* cls, const int* boff, const Soa& C, int* dseg);
+void launch_dist_pack(const Launch& L, const Soa& C, int off, int m, char* buf);
+void launch_dist_unpack(const Launch& L, const char* buf, int m, const Soa& C, int off);
+void launch_halo_pack(const Launch& L, const int* dst_of, int o1, int n1, int o2, int n2, const HaloFields& F,
+                      double* buf);
+void launch_halo_unpack(const Launch& L, const double* buf, const int* dst_of, int o1, int n1, int o2, int n2,
+                        const HaloFields& F);
 
 }  // namespace mph

@@ -81,20 +81,24 @@ __device__ __forceinline__ int wrap_cell(int c, int g)
     return c >= g ? c - g : c;
 }
 
-__device__ __forceinline__ int cell_axis(double x, double dmin, double ginv, int g)
+// Cell index along one axis.  The offset from the grid origin is wrapped once into [0, w) (w =
+// periodic domain width), so a slab window that straddles the periodic seam (multi-GPU) sees its
+// ghosts from the far side at the right place; for the full-domain grid the wrap changes nothing.
+// Out-of-window offsets clamp into the edge cells (only far ghosts, never needed as neighbours).
+__device__ __forceinline__ int cell_axis(double x, double org, double w, double ginv, int g)
 {
-    int c = (int)floor((x - dmin) * ginv);
-    c = c < 0 ? c + g : c;
-    c = c >= g ? c - g : c;
+    double u = x - org;
+    u = u < 0.0 ? u + w : (u >= w ? u - w : u);
+    int c = (int)floor(u * ginv);
     c = c < 0 ? 0 : c;
     return c >= g ? g - 1 : c;
 }
 
 __device__ __forceinline__ int cell_id(const DevParams& P, double x, double y, double z)
 {
-    const int cx = cell_axis(x, P.dmin[0], P.ginv[0], P.gc[0]);
-    const int cy = cell_axis(y, P.dmin[1], P.ginv[1], P.gc[1]);
-    const int cz = P.dim == 3 ? cell_axis(z, P.dmin[2], P.ginv[2], P.gc[2]) : 0;
+    const int cx = cell_axis(x, P.corg[0], P.dw[0], P.ginv[0], P.gc[0]);
+    const int cy = cell_axis(y, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
+    const int cz = P.dim == 3 ? cell_axis(z, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
     return (cx * P.gc[1] + cy) * P.gc[2] + cz;
 }
 
@@ -129,7 +133,38 @@ __device__ __forceinline__ const int* ell_row(const int* nbr, int i)
 // ------------------------------------------------------------------------- sort phase -------
 
 // calculateWall (main.cpp:3031-3060) + calculatePeriodicBoundary (3322-3333) + cell histogram.
-// mode 0: initialisation (no motion), 1: time step.
+// mode 0: initialisation (no motion), 1: time step, 2: time step whose motion was already applied
+// (slab mode, k_dist_prep).
+// calculateWall (3031-3060) then calculatePeriodicBoundary (3322-3333) for particle p of B.
+__device__ __forceinline__ void move_and_wrap(const DevParams& P, const DevState* st, Soa& B, int p,
+                                              double& x, double& y, double& z)
+{
+#pragma clang fp contract(off)
+    const int t = B.type[p];
+    if (dev_is_wall(t) && st->time < 0.2) {
+        const double* C = st->wall_c[t];
+        const double* V = st->wall_vel[t];
+        const double* w = st->wall_omega[t];
+        const double (*R)[3] = st->wall_rot[t];
+        const double r0 = x - C[0], r1 = y - C[1], r2 = z - C[2];
+        const double a0 = R[0][0] * r0 + R[0][1] * r1 + R[0][2] * r2;
+        const double a1 = R[1][0] * r0 + R[1][1] * r1 + R[1][2] * r2;
+        const double a2 = R[2][0] * r0 + R[2][1] * r1 + R[2][2] * r2;
+        B.vx[p] = w[1] * a2 - w[2] * a1 + V[0];
+        B.vy[p] = w[2] * a0 - w[0] * a2 + V[1];
+        B.vz[p] = w[0] * a1 - w[1] * a0 + V[2];
+        x = a0 + C[0] + V[0] * P.dt;
+        y = a1 + C[1] + V[1] * P.dt;
+        z = a2 + C[2] + V[2] * P.dt;
+    }
+    x = mod_exact(x - P.dmin[0], P.dw[0]) + P.dmin[0];
+    y = mod_exact(y - P.dmin[1], P.dw[1]) + P.dmin[1];
+    z = mod_exact(z - P.dmin[2], P.dw[2]) + P.dmin[2];
+    B.x[p] = x;
+    B.y[p] = y;
+    B.z[p] = z;
+}
+
 __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __restrict__ st, Soa B,
                                               int* __restrict__ key, int* __restrict__ slot,
                                               int* __restrict__ cnt, int mode)
@@ -137,32 +172,7 @@ __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __res
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P.n) return;
     double x = B.x[p], y = B.y[p], z = B.z[p];
-    if (mode) {
-#pragma clang fp contract(off)
-        const int t = B.type[p];
-        if (dev_is_wall(t) && st->time < 0.2) {
-            const double* C = st->wall_c[t];
-            const double* V = st->wall_vel[t];
-            const double* w = st->wall_omega[t];
-            const double (*R)[3] = st->wall_rot[t];
-            const double r0 = x - C[0], r1 = y - C[1], r2 = z - C[2];
-            const double a0 = R[0][0] * r0 + R[0][1] * r1 + R[0][2] * r2;
-            const double a1 = R[1][0] * r0 + R[1][1] * r1 + R[1][2] * r2;
-            const double a2 = R[2][0] * r0 + R[2][1] * r1 + R[2][2] * r2;
-            B.vx[p] = w[1] * a2 - w[2] * a1 + V[0];
-            B.vy[p] = w[2] * a0 - w[0] * a2 + V[1];
-            B.vz[p] = w[0] * a1 - w[1] * a0 + V[2];
-            x = a0 + C[0] + V[0] * P.dt;
-            y = a1 + C[1] + V[1] * P.dt;
-            z = a2 + C[2] + V[2] * P.dt;
-        }
-        x = mod_exact(x - P.dmin[0], P.dw[0]) + P.dmin[0];
-        y = mod_exact(y - P.dmin[1], P.dw[1]) + P.dmin[1];
-        z = mod_exact(z - P.dmin[2], P.dw[2]) + P.dmin[2];
-        B.x[p] = x;
-        B.y[p] = y;
-        B.z[p] = z;
-    }
+    if (mode == 1) move_and_wrap(P, st, B, p, x, y, z);
     const int k = cell_id(P, x, y, z);
     key[p] = k;
     slot[p] = atomicAdd(&cnt[k], 1);
@@ -282,7 +292,7 @@ __global__ __launch_bounds__(256) void k_place(DevParams P, DevState* __restrict
 __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __restrict__ key,
                                                       const int* __restrict__ start,
                                                       const int* __restrict__ tmp, Soa B, Soa A,
-                                                      int* __restrict__ rank_of)
+                                                      int* __restrict__ rank_of, int* __restrict__ dst_of)
 {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P.n) return;
@@ -300,7 +310,8 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
     A.type[dst] = B.type[p];
     const int id = B.id[p];
     A.id[dst] = id;
-    rank_of[id] = dst;
+    if (dst_of) dst_of[p] = dst;   // slab mode: ids are global (ghosts negative)
+    else rank_of[id] = dst;
 }
 
 // ---------------------------------------------------------------------- neighbour search ----
@@ -377,9 +388,9 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int
     const bool fast = wave_interior(P, live, xi, yi, zi);
     int cnt = 0;
     if (live) {
-        const int cx = cell_axis(xi, P.dmin[0], P.ginv[0], P.gc[0]);
-        const int cy = cell_axis(yi, P.dmin[1], P.ginv[1], P.gc[1]);
-        const int cz = DIM == 3 ? cell_axis(zi, P.dmin[2], P.ginv[2], P.gc[2]) : 0;
+        const int cx = cell_axis(xi, P.corg[0], P.dw[0], P.ginv[0], P.gc[0]);
+        const int cy = cell_axis(yi, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
+        const int cz = DIM == 3 ? cell_axis(zi, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
         int* out = nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
         cnt = fast ? scan_candidates<DIM, true>(P, A, start, i, xi, yi, zi, cx, cy, cz, out)
                    : scan_candidates<DIM, false>(P, A, start, i, xi, yi, zi, cx, cy, cz, out);
@@ -865,6 +876,127 @@ __global__ __launch_bounds__(256) void k_struct_scatter(int ns, const int* __res
     if (clamp[s] == 1) force[r] = make_double4(0.0, 0.0, 0.0, 0.0);
 }
 
+// ------------------------------------------------------------------ slab decomposition -----
+// Multi-GPU redistribution (mph_dist.hip).  Every B entry is classified by its slab coordinate
+// after this step's wall motion + periodic wrap; a stable partition then writes the owned and
+// outgoing particles into C as [migrate R | band R | inner | band L | migrate L] (ghosts of the
+// previous step are dropped).  Migrants keep a copy here as ghosts (id -> -1-id).
+
+__device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << (threadIdx.x & 63)) - 1ull; }
+
+__global__ __launch_bounds__(256) void k_dist_classify(DevParams P, DevState* __restrict__ st, SlabGeom g,
+                                                       Soa B, int n, int move, int* __restrict__ cls,
+                                                       int* __restrict__ bcnt, int nb)
+{
+    __shared__ int wc[4][kSlabClasses];
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    int c = -1;
+    if (p < n) {
+        if (B.id[p] < 0) {
+            c = kSlabDrop;
+        } else {
+            double x = B.x[p], y = B.y[p], z = B.z[p];
+            if (move) move_and_wrap(P, st, B, p, x, y, z);
+            const double a = g.axis == 0 ? x : (g.axis == 1 ? y : z);
+            c = slab_class(g, a);
+            if (c == kSlabLost) {
+                atomicOr(&st->overflow, 2);
+                c = kInner;
+            }
+        }
+        cls[p] = c;
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < kSlabClasses; ++k) {
+        const unsigned long long m = __ballot(c == k);
+        if (lane == 0) wc[wave][k] = __popcll(m);
+    }
+    __syncthreads();
+    if (threadIdx.x < kSlabClasses) {
+        int t = 0;
+        for (int w = 0; w < 4; ++w) t += wc[w][threadIdx.x];
+        bcnt[threadIdx.x * nb + blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_dist_scatter(Soa B, int n, const int* __restrict__ cls,
+                                                      const int* __restrict__ boff, int nb, Soa C,
+                                                      int* __restrict__ dseg)
+{
+    __shared__ int wc[4][kSlabClasses];
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int c = p < n ? cls[p] : -1;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int rank = 0;
+#pragma unroll
+    for (int k = 0; k < kSlabClasses; ++k) {
+        const unsigned long long m = __ballot(c == k);
+        if (c == k) rank = __popcll(m & lanemask_lt());
+        if (lane == 0) wc[wave][k] = __popcll(m);
+    }
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x <= kSlabClasses) dseg[threadIdx.x] = boff[threadIdx.x * nb];
+    if (c < 0 || c == kSlabDrop) return;
+    int o = boff[c * nb + blockIdx.x] + rank;
+    for (int w = 0; w < wave; ++w) o += wc[w][c];
+    C.x[o] = B.x[p]; C.y[o] = B.y[p]; C.z[o] = B.z[p];
+    C.vx[o] = B.vx[p]; C.vy[o] = B.vy[p]; C.vz[o] = B.vz[p];
+    C.type[o] = B.type[p];
+    const int id = B.id[p];
+    C.id[o] = (c == kMigR || c == kMigL) ? -1 - id : id;
+}
+
+// message layout: x[m] y[m] z[m] vx[m] vy[m] vz[m] (double) type[m] id[m] (int) = 56 B/particle
+__global__ __launch_bounds__(256) void k_dist_pack(Soa C, int off, int m, char* __restrict__ buf)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    double* d = (double*)buf;
+    int* q = (int*)(d + 6 * (size_t)m);
+    const int s = off + k;
+    d[k] = C.x[s]; d[m + k] = C.y[s]; d[2 * m + k] = C.z[s];
+    d[3 * m + k] = C.vx[s]; d[4 * m + k] = C.vy[s]; d[5 * m + k] = C.vz[s];
+    q[k] = C.type[s];
+    q[m + k] = C.id[s];
+}
+
+// received message -> C[off, off+m); ownership flips (their migrants are ours, their band
+// particles are our ghosts): id -> -1-id for every entry.
+__global__ __launch_bounds__(256) void k_dist_unpack(const char* __restrict__ buf, int m, Soa C, int off)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    const double* d = (const double*)buf;
+    const int* q = (const int*)(d + 6 * (size_t)m);
+    const int s = off + k;
+    C.x[s] = d[k]; C.y[s] = d[m + k]; C.z[s] = d[2 * m + k];
+    C.vx[s] = d[3 * m + k]; C.vy[s] = d[4 * m + k]; C.vz[s] = d[5 * m + k];
+    C.type[s] = q[k];
+    C.id[s] = -1 - q[m + k];
+}
+
+// pass-A values of two C-index ranges, read at their sorted position dst_of[c]
+__global__ __launch_bounds__(256) void k_halo_pack(const int* __restrict__ dst_of, int o1, int n1, int o2,
+                                                   int n2, HaloFields F, double* __restrict__ buf)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int m = n1 + n2;
+    if (k >= m) return;
+    const int a = dst_of[k < n1 ? o1 + k : o2 + (k - n1)];
+    for (int f = 0; f < F.nf; ++f) buf[(size_t)f * m + k] = F.f[f][a];
+}
+
+__global__ __launch_bounds__(256) void k_halo_unpack(const double* __restrict__ buf, const int* __restrict__ dst_of,
+                                                     int o1, int n1, int o2, int n2, HaloFields F)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int m = n1 + n2;
+    if (k >= m) return;
+    const int a = dst_of[k < n1 ? o1 + k : o2 + (k - n1)];
+    for (int f = 0; f < F.nf; ++f) F.f[f][a] = buf[(size_t)f * m + k];
+}
+
 // ---------------------------------------------------------------------------- launchers -----
 
 static inline int blocks(int n, int t) { return (n + t - 1) / t; }
@@ -906,7 +1038,7 @@ void launch_sort(const Launch& L, int mode)
     MPH_LAUNCH("place", L.stream, k_place, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.key,
                L.slot, L.start, L.tmp, mode);
     MPH_LAUNCH("rank_scatter", L.stream, k_rank_scatter, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P,
-               L.key, L.start, L.tmp, L.B, L.A, L.rank_of);
+               L.key, L.start, L.tmp, L.B, L.A, L.rank_of, L.dst_of);
 }
 
 void launch_neighbors(const Launch& L)
@@ -977,6 +1109,66 @@ void launch_structure(const Launch& L)
     }
     MPH_LAUNCH("struct_scatter", L.stream, k_struct_scatter, dim3(blocks(ns, 256)), dim3(256), 0, L.stream,
                ns, S.orig, L.rank_of, S.clamp, S.x, S.v, L.B, L.force);
+}
+
+void launch_scan(int* cnt, int ncell, int* bsum, int* start, int total, hipStream_t stream, Profiler* prof)
+{
+    const int nb = blocks(ncell, kScanBlock);
+    MPH_LAUNCH("scan_reduce", stream, k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, stream, cnt, ncell, bsum);
+    MPH_LAUNCH("scan_top", stream, k_scan_top, dim3(1), dim3(1024), 0, stream, bsum, nb);
+    MPH_LAUNCH("scan_down", stream, k_scan_down, dim3(nb), dim3(kScanThreads), 0, stream, cnt, ncell, bsum,
+               start, total);
+}
+
+int dist_blocks(int n) { return blocks(n > 0 ? n : 1, 256); }
+
+void launch_dist_classify(const Launch& L, const SlabGeom& g, int n, int move, int* cls, int* bcnt)
+{
+    Profiler* prof = L.prof;
+    const int nb = dist_blocks(n);
+    MPH_LAUNCH("dist_classify", L.stream, k_dist_classify, dim3(nb), dim3(256), 0, L.stream, *L.P, L.st, g,
+               L.B, n, move, cls, bcnt, nb);
+}
+
+void launch_dist_scatter(const Launch& L, int n, const int* cls, const int* boff, const Soa& C, int* dseg)
+{
+    Profiler* prof = L.prof;
+    const int nb = dist_blocks(n);
+    MPH_LAUNCH("dist_scatter", L.stream, k_dist_scatter, dim3(nb), dim3(256), 0, L.stream, L.B, n, cls, boff,
+               nb, C, dseg);
+}
+
+void launch_dist_pack(const Launch& L, const Soa& C, int off, int m, char* buf)
+{
+    Profiler* prof = L.prof;
+    if (m <= 0) return;
+    MPH_LAUNCH("dist_pack", L.stream, k_dist_pack, dim3(blocks(m, 256)), dim3(256), 0, L.stream, C, off, m, buf);
+}
+
+void launch_dist_unpack(const Launch& L, const char* buf, int m, const Soa& C, int off)
+{
+    Profiler* prof = L.prof;
+    if (m <= 0) return;
+    MPH_LAUNCH("dist_unpack", L.stream, k_dist_unpack, dim3(blocks(m, 256)), dim3(256), 0, L.stream, buf, m, C,
+               off);
+}
+
+void launch_halo_pack(const Launch& L, const int* dst_of, int o1, int n1, int o2, int n2, const HaloFields& F,
+                      double* buf)
+{
+    Profiler* prof = L.prof;
+    if (n1 + n2 <= 0) return;
+    MPH_LAUNCH("halo_pack", L.stream, k_halo_pack, dim3(blocks(n1 + n2, 256)), dim3(256), 0, L.stream, dst_of,
+               o1, n1, o2, n2, F, buf);
+}
+
+void launch_halo_unpack(const Launch& L, const double* buf, const int* dst_of, int o1, int n1, int o2, int n2,
+                        const HaloFields& F)
+{
+    Profiler* prof = L.prof;
+    if (n1 + n2 <= 0) return;
+    MPH_LAUNCH("halo_unpack", L.stream, k_halo_unpack, dim3(blocks(n1 + n2, 256)), dim3(256), 0, L.stream, buf,
+               dst_of, o1, n1, o2, n2, F);
 }
 
 }  // namespace mph

@@ -32,6 +32,7 @@ struct DevParams {
                        // periodic branch of the minimum image (see k_neighbors)
     double inner_lo[3], inner_hi[3];   // interior box: >= 3 GPU cells from every periodic face
     double dmin[3], dw[3], hw[3], w075[3];   // domain min / width / half width / 0.75 width
+    double corg[3];    // origin of the GPU cell grid (dmin, or the slab window's lower edge)
     double ginv[3];    // 1 / GPU cell width per axis
     double rc2;        // (MaxRadius + MARGIN)^2, main.cpp:1765
     double ra, rg, rp, rv;                   // radii (main.cpp:1195-1198)
@@ -64,6 +65,46 @@ struct DevState {
     int max_count;               // max neighbour count of the last search
     unsigned long long sum_count;
 };
+
+#if defined(__HIPCC__)
+#define MPH_HD __host__ __device__
+#else
+#define MPH_HD
+#endif
+
+// Slab decomposition along one axis (multi-GPU, mph_dist.hip).  Rank r owns the particles whose
+// (periodically wrapped) coordinate c satisfies lo <= c < hi, with the first/last rank also
+// owning any roundoff spill below dmin / above dmax.  `h` is the halo width (>= the neighbour
+// cutoff): owned particles within h of a face are mirrored to that neighbour as ghosts.
+struct SlabGeom {
+    int axis;
+    int first, last, lfirst, llast, rfirst, rlast;   // first/last-rank flags: me, left, right
+    double lo, hi, llo, lhi, rlo, rhi;               // slabs of me and my periodic neighbours
+    double h;
+};
+
+// Particle classes of one step's redistribution, in the order of their segment in the local
+// arrays: [migrate right | band right | inner | band left | migrate left]; kSlabDrop marks ghosts
+// of the previous step, kSlabLost a particle that jumped past a neighbour's slab.
+enum SlabClass { kMigR = 0, kBandR = 1, kInner = 2, kBandL = 3, kMigL = 4, kSlabDrop = 5,
+                 kSlabClasses = 6, kSlabLost = 7 };
+
+MPH_HD inline bool slab_owns(double c, double lo, double hi, int first, int last)
+{
+    return (first || c >= lo) && (last || c < hi);
+}
+
+MPH_HD inline int slab_class(const SlabGeom& g, double c)
+{
+    if (slab_owns(c, g.lo, g.hi, g.first, g.last)) {
+        if (c - g.lo < g.h) return kBandL;
+        if (g.hi - c <= g.h) return kBandR;
+        return kInner;
+    }
+    if (slab_owns(c, g.llo, g.lhi, g.lfirst, g.llast)) return kMigL;
+    if (slab_owns(c, g.rlo, g.rhi, g.rfirst, g.rlast)) return kMigR;
+    return kSlabLost;
+}
 
 // Per-type tables read with per-lane type indices (device memory; staged through LDS where hot).
 struct DevTables {

@@ -1,0 +1,88 @@
+"""Multi-process glue for the slab decomposition (include/mph_gpu.h, csrc/mph_dist.hip).
+
+One process per GPU, launched by torchrun / torch.multiprocessing; `torch.distributed` is the
+control plane only (rendezvous, the RCCL unique id, result gathering).  The particle data path
+between neighbouring slabs is the library's own: RCCL ncclSend/ncclRecv on the context's stream
+(`rccl_slab`), or -- to run several ranks on one GPU, or without RCCL -- the host-staged
+transport driven by `GlooExchange` over a gloo process group.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import solver
+
+
+class GlooExchange:
+    """mph_host_exchange_fn over torch.distributed point-to-point (gloo, CPU tensors).
+
+    send_l goes to the left neighbour, which receives it as its recv_r; send_r goes right
+    (received as recv_l).  Tags keep the two directions apart when left == right (2 ranks)."""
+
+    TAG_LEFTWARD = 17
+    TAG_RIGHTWARD = 23
+
+    def __init__(self, rank: int, nranks: int, group=None):
+        self.rank, self.nranks, self.group = rank, nranks, group
+        self.left = (rank - 1) % nranks
+        self.right = (rank + 1) % nranks
+
+    def __call__(self, send_l, send_r, recv_l, recv_r):
+        import torch
+        import torch.distributed as dist
+
+        def t(mv):
+            return torch.from_numpy(np.frombuffer(mv, dtype=np.uint8))
+
+        reqs = []
+        if len(send_l):
+            reqs.append(dist.isend(t(send_l), self.left, group=self.group, tag=self.TAG_LEFTWARD))
+        if len(send_r):
+            reqs.append(dist.isend(t(send_r), self.right, group=self.group, tag=self.TAG_RIGHTWARD))
+        bufs = []
+        if len(recv_r):
+            b = torch.empty(len(recv_r), dtype=torch.uint8)
+            reqs.append(dist.irecv(b, self.right, group=self.group, tag=self.TAG_LEFTWARD))
+            bufs.append((b, recv_r))
+        if len(recv_l):
+            b = torch.empty(len(recv_l), dtype=torch.uint8)
+            reqs.append(dist.irecv(b, self.left, group=self.group, tag=self.TAG_RIGHTWARD))
+            bufs.append((b, recv_l))
+        for r in reqs:
+            r.wait()
+        for b, mv in bufs:
+            np.frombuffer(mv, dtype=np.uint8)[:] = b.numpy()
+
+
+def rccl_slab(rank: int, nranks: int, axis: int, group=None) -> solver.Slab:
+    """Slab options with an RCCL communicator: rank 0 makes the unique id, everyone receives it
+    through torch.distributed (any backend)."""
+    import torch.distributed as dist
+    obj = [solver.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    return solver.Slab(rank, nranks, axis, uid=obj[0])
+
+
+def gloo_slab(rank: int, nranks: int, axis: int, group=None) -> solver.Slab:
+    return solver.Slab(rank, nranks, axis, exchange=GlooExchange(rank, nranks, group))
+
+
+def gather_field(s: solver.MphSolver, name: str, group=None) -> np.ndarray:
+    """Merge a field over all ranks (owned entries of each) into the full original-order array,
+    returned on every rank."""
+    import torch.distributed as dist
+    mine_ids = s.owned_ids()
+    vals = s.get(name)[mine_ids]
+    parts = [None] * dist.get_world_size(group)
+    dist.all_gather_object(parts, (mine_ids, vals), group=group)
+    fid, w, dt = solver.FIELDS[name]
+    shape = (s.n,) if w == 1 else ((s.n, 3) if w == 3 else (s.n, 3, 3))
+    out = np.zeros(shape, dt)
+    seen = np.zeros(s.n, np.int32)
+    for ids, v in parts:
+        out[ids] = v
+        seen[ids] += 1
+    if not np.all(seen == 1):
+        raise RuntimeError("slab ownership is not a partition: %d missing, %d duplicated"
+                           % (int((seen == 0).sum()), int((seen > 1).sum())))
+    return out

@@ -41,7 +41,8 @@ FIELDS = {
 
 STATUS = {0: "MPH_OK", -1: "MPH_ERR_ARG", -2: "MPH_ERR_IO", -3: "MPH_ERR_NEIGHBOR_OVERFLOW",
           -4: "MPH_ERR_DEVICE_OOM", -5: "MPH_ERR_HIP", -6: "MPH_ERR_RCCL", -7: "MPH_ERR_DOMAIN",
-          -8: "MPH_ERR_UNSUPPORTED", -9: "MPH_ERR_NONFINITE"}
+          -8: "MPH_ERR_UNSUPPORTED", -9: "MPH_ERR_NONFINITE", -10: "MPH_ERR_TRANSPORT",
+          -11: "MPH_ERR_CAPACITY"}
 
 EXPORTED_SYMBOLS = [
     "mph_config_default", "mph_read_data_file", "mph_read_grid_header", "mph_read_grid_particles",
@@ -49,8 +50,14 @@ EXPORTED_SYMBOLS = [
     "mph_get", "mph_set", "mph_particle_count", "mph_time", "mph_get_scalars", "mph_write_prof",
     "mph_write_vtk", "mph_last_error", "mph_destroy", "mph_profile_steps", "mph_neighbor_stats",
     "mph_dist_unique_id", "mph_create_dist", "mph_owned_count", "mph_derive_scalars",
-    "mph_structure_init",
+    "mph_structure_init", "mph_create_dist_host", "mph_owned_ids", "mph_slab_bounds",
+    "mph_slab_owner", "mph_dist_selftest",
 ]
+
+# mph_host_exchange_fn (include/mph_gpu.h): (user, send_l, n, send_r, n, recv_l, n, recv_r, n)
+HOST_EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                    ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                                    ctypes.c_void_p, ctypes.c_size_t)
 
 
 class MphError(RuntimeError):
@@ -106,6 +113,12 @@ def load_library() -> ctypes.CDLL:
         "mph_dist_unique_id": (ip, [vp]),
         "mph_create_dist": (ip, [ctypes.POINTER(vp), cfgp, ip, vp, vp, vp, vp, ip, ip, ip, vp, ip]),
         "mph_owned_count": (ip, [vp]),
+        "mph_create_dist_host": (ip, [ctypes.POINTER(vp), cfgp, ip, vp, vp, vp, vp, ip, ip, ip, ip,
+                                      HOST_EXCHANGE_FN, vp]),
+        "mph_owned_ids": (ip, [vp, vp]),
+        "mph_slab_bounds": (ip, [cfgp, ip, ip, ip, vp]),
+        "mph_slab_owner": (ip, [cfgp, ip, ip, dp]),
+        "mph_dist_selftest": (ip, [ip]),
         "mph_derive_scalars": (ip, [cfgp, vp]),
         "mph_structure_init": (ip, [cfgp, ip, vp, vp, vp, vp, vp, vp]),
     }
@@ -150,23 +163,65 @@ def _check(rc, ctx=None):
     return rc
 
 
-class MphSolver:
-    """One MI355X context running the reference hot path (see module docstring)."""
+def slab_bounds(cfg: mphio.MphConfig, rank: int, nranks: int, axis: int):
+    """(lo, hi, halo) of a rank's slab, as mph_create_dist computes them (host only)."""
+    out = np.zeros(3)
+    _check(load_library().mph_slab_bounds(ctypes.byref(cfg), rank, nranks, axis, out.ctypes.data))
+    return float(out[0]), float(out[1]), float(out[2])
 
-    def __init__(self, cfg: mphio.MphConfig, parts: mphio.Particles, device: int = 0):
+
+def slab_owner(cfg: mphio.MphConfig, nranks: int, axis: int, x: float) -> int:
+    return _check(load_library().mph_slab_owner(ctypes.byref(cfg), nranks, axis, float(x)))
+
+
+class Slab:
+    """Slab-mode options of MphSolver: this process is `rank` of `nranks`, slabs along `axis`.
+    Transport: RCCL with the 128-byte unique id `uid` (mph_create_dist), or a host callback
+    `exchange(send_l, send_r, recv_l, recv_r)` over memoryviews (mph_create_dist_host)."""
+
+    def __init__(self, rank: int, nranks: int, axis: int, uid: bytes | None = None, exchange=None):
+        if (uid is None) == (exchange is None):
+            raise ValueError("Slab needs exactly one of uid (RCCL) or exchange (host transport)")
+        self.rank, self.nranks, self.axis, self.uid, self.exchange = rank, nranks, axis, uid, exchange
+
+
+def unique_id() -> bytes:
+    """A fresh RCCL unique id (rank 0 calls this and shares it with the other ranks)."""
+    buf = ctypes.create_string_buffer(128)
+    _check(load_library().mph_dist_unique_id(buf))
+    return buf.raw
+
+
+class MphSolver:
+    """One MI355X context running the reference hot path (see module docstring).  With
+    `slab=Slab(...)` the context is one rank of the multi-GPU slab decomposition: get() then fills
+    only the entries of the particles this rank owns (see owned_ids())."""
+
+    def __init__(self, cfg: mphio.MphConfig, parts: mphio.Particles, device: int = 0,
+                 slab: Slab | None = None):
         L = load_library()
         self._L = L
         self.cfg = cfg.copy()
         self.n = parts.n
+        self.slab = slab
         self._arrays = [np.ascontiguousarray(parts.property, np.int32),
                         np.ascontiguousarray(parts.position, np.float64),
                         np.ascontiguousarray(parts.initial_position, np.float64),
                         np.ascontiguousarray(parts.velocity, np.float64)]
         h = ctypes.c_void_p()
-        rc = L.mph_create(ctypes.byref(h), ctypes.byref(self.cfg), self.n,
-                          *[a.ctypes.data for a in self._arrays], int(device))
+        ptrs = [a.ctypes.data for a in self._arrays]
+        if slab is None:
+            rc = L.mph_create(ctypes.byref(h), ctypes.byref(self.cfg), self.n, *ptrs, int(device))
+        elif slab.uid is not None:
+            uid = ctypes.create_string_buffer(bytes(slab.uid), 128)
+            rc = L.mph_create_dist(ctypes.byref(h), ctypes.byref(self.cfg), self.n, *ptrs, int(device),
+                                   slab.rank, slab.nranks, uid, slab.axis)
+        else:
+            self._cb = HOST_EXCHANGE_FN(_host_exchange_adapter(slab.exchange))
+            rc = L.mph_create_dist_host(ctypes.byref(h), ctypes.byref(self.cfg), self.n, *ptrs,
+                                        int(device), slab.rank, slab.nranks, slab.axis, self._cb, None)
         if rc < 0:
-            msg = (L.mph_last_error(h) or b"").decode() if h.value else ""
+            msg = (L.mph_last_error(None) or b"").decode()
             raise MphError(rc, msg or "mph_create failed")
         self._h = h
 
@@ -243,8 +298,34 @@ class MphSolver:
             out[nm] = {"avg_ms": float(avg[i]), "launches": int(cnt[i])}
         return out
 
+    def owned_ids(self) -> np.ndarray:
+        """Original indices of the particles this context owns (all of them without a slab)."""
+        k = self._L.mph_owned_count(self._h)
+        out = np.zeros(max(self.n, 1), np.int32)
+        _check(self._L.mph_owned_ids(self._h, out.ctypes.data), self._h)
+        return out[:k].copy()
+
     def neighbor_stats(self):
         m = ctypes.c_double()
         x = ctypes.c_int()
         _check(self._L.mph_neighbor_stats(self._h, ctypes.byref(m), ctypes.byref(x)), self._h)
         return m.value, x.value
+
+
+def _host_exchange_adapter(fn):
+    """Wrap a Python exchange(send_l, send_r, recv_l, recv_r) over writable memoryviews as an
+    mph_host_exchange_fn; exceptions become a nonzero return (MPH_ERR_TRANSPORT)."""
+    def view(ptr, n):
+        if not n:
+            return memoryview(bytearray(0))
+        return memoryview((ctypes.c_uint8 * n).from_address(ptr)).cast("B")
+
+    def cb(user, sl, nsl, sr, nsr, rl, nrl, rr, nrr):
+        try:
+            fn(view(sl, nsl), view(sr, nsr), view(rl, nrl), view(rr, nrr))
+            return 0
+        except Exception as e:  # reported through the status code
+            import sys
+            print("mph host exchange failed: %r" % (e,), file=sys.stderr)
+            return 1
+    return cb

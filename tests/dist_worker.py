@@ -1,0 +1,128 @@
+"""Worker processes of the slab-decomposition tests (tests/test_dist_cpu.py, test_gpu_dist.py).
+
+Each worker is one rank: it joins a gloo process group on 127.0.0.1 and either runs a GPU slab
+context (host-staged transport over gloo, several ranks sharing one GPU) or, on CPU, exercises
+the exchange routing and the halo-band rule of the decomposition.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+SLAB_AXIS = {"channel3d": 2, "channel3d_st": 2, "channel2d": 0, "dam2d": 0, "box3d": 0}
+
+
+def _init(rank, world, port):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def gpu_worker(rank, world, port, case, checkpoints, fields, out_path):
+    """Run `case` as rank `rank` of `world` on cuda:0; at every checkpoint (cumulative step
+    count) gather `fields` over the ranks; rank 0 saves them to out_path (.npz)."""
+    dist = _init(rank, world, port)
+    from particlemethod_fsi_amd import MphSolver, cases
+    from particlemethod_fsi_amd.dist import gather_field, gloo_slab
+    c = cases.get(case)
+    cfg, parts = c.build()
+    res = {}
+    with MphSolver(cfg, parts, device=0, slab=gloo_slab(rank, world, SLAB_AXIS[case])) as s:
+        def owner_map():
+            parts_ = [None] * world
+            dist.all_gather_object(parts_, s.owned_ids())
+            m = np.full(s.n, -1, np.int32)
+            for r, ids in enumerate(parts_):
+                m[ids] = r
+            return m
+
+        res["owner0"] = owner_map()
+        done = 0
+        for k in checkpoints:
+            s.step(k - done)
+            done = k
+            for f in fields:
+                res["s%d/%s" % (k, f)] = gather_field(s, f)
+            res["s%d/owner" % k] = owner_map()
+    if rank == 0:
+        np.savez(out_path, **res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def exchange_worker(rank, world, port, out_path):
+    """CPU: route tagged messages through GlooExchange and record what arrived."""
+    dist = _init(rank, world, port)
+    from particlemethod_fsi_amd.dist import GlooExchange
+    ex = GlooExchange(rank, world)
+    left, right = (rank - 1) % world, (rank + 1) % world
+    # message sizes depend on (sender, direction) so a mis-route shows up as a size/content error
+    def msg(src, direction):
+        n = 8 + 3 * src + (5 if direction == "L" else 0)
+        return bytearray([(src * 7 + (1 if direction == "L" else 2) + i) % 251 for i in range(n)])
+    send_l, send_r = msg(rank, "L"), msg(rank, "R")
+    recv_l = bytearray(len(msg(left, "R")))
+    recv_r = bytearray(len(msg(right, "L")))
+    ex(memoryview(send_l), memoryview(send_r), memoryview(recv_l), memoryview(recv_r))
+    ok = recv_l == msg(left, "R") and recv_r == msg(right, "L")
+    flags = [None] * world
+    dist.all_gather_object(flags, bool(ok))
+    if rank == 0:
+        np.save(out_path, np.array(flags))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def band_worker(rank, world, port, case, out_path):
+    """CPU: each rank selects its owned particles and the band particles it sends to its two
+    neighbours (the rule of mph_params.h slab_class, via the library's host functions), ships the
+    bands through GlooExchange, and checks that owned + received ghosts contain every reference
+    neighbour (golden lists) of every owned particle."""
+    dist = _init(rank, world, port)
+    from golden_utils import Golden
+    from particlemethod_fsi_amd import solver, cases
+    from particlemethod_fsi_amd.dist import GlooExchange
+    c = cases.get(case)
+    cfg, _ = c.build()
+    g = Golden(case)
+    pos = g.get(1, "Position")
+    off, ids = g.get(1, "nbr_offsets"), g.get(1, "nbr_ids")
+    axis = SLAB_AXIS[case]
+    lo, hi, h = solver.slab_bounds(cfg, rank, world, axis)
+    owner = np.array([solver.slab_owner(cfg, world, axis, x) for x in pos[:, axis]])
+    mine = np.nonzero(owner == rank)[0]
+    a = pos[mine, axis]
+    band_l = mine[(a - lo) < h]          # -> left neighbour
+    band_r = mine[(hi - a) <= h]         # -> right neighbour
+    ex = GlooExchange(rank, world)
+    # sizes first (fixed 8-byte messages), then the index lists
+    sl = np.array([len(band_l)], np.int64).tobytes()
+    sr = np.array([len(band_r)], np.int64).tobytes()
+    rl, rr = bytearray(8), bytearray(8)
+    ex(memoryview(bytearray(sl)), memoryview(bytearray(sr)), memoryview(rl), memoryview(rr))
+    nl, nr = int(np.frombuffer(rl, np.int64)[0]), int(np.frombuffer(rr, np.int64)[0])
+    bl, br = bytearray(4 * nl), bytearray(4 * nr)
+    ex(memoryview(bytearray(band_l.astype(np.int32).tobytes())),
+       memoryview(bytearray(band_r.astype(np.int32).tobytes())), memoryview(bl), memoryview(br))
+    ghosts = np.concatenate([np.frombuffer(bl, np.int32), np.frombuffer(br, np.int32)])
+    have = np.zeros(len(pos), bool)
+    have[mine] = True
+    have[ghosts] = True
+    missing = 0
+    for i in mine:
+        nb = ids[off[i]:off[i + 1]]
+        missing += int((~have[nb]).sum())
+    res = [None] * world
+    dist.all_gather_object(res, (len(mine), missing, int(len(ghosts))))
+    if rank == 0:
+        np.save(out_path, np.array(res))
+    dist.barrier()
+    dist.destroy_process_group()

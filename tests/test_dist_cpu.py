@@ -1,0 +1,77 @@
+"""CPU tests of the multi-GPU slab decomposition (no device): slab geometry of the library's
+host functions, and world-size 2/3 gloo runs of the neighbour exchange routing and of the
+halo-band rule (every reference neighbour of an owned particle is owned or a received ghost)."""
+import multiprocessing as mp
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from particlemethod_fsi_amd import cases, solver
+
+import dist_worker
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn(target, world, *args):
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    ps = [ctx.Process(target=target, args=(r, world, port) + args) for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(180)
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+
+
+@pytest.mark.parametrize("case,axis", [("channel3d", 2), ("d1m", 2), ("dam2d", 0)])
+@pytest.mark.parametrize("nranks", [2, 3, 5])
+def test_slab_bounds_partition_domain(case, axis, nranks):
+    cfg, parts = cases.get(case).build()
+    b = [solver.slab_bounds(cfg, r, nranks, axis) for r in range(nranks)]
+    assert b[0][0] == cfg.domain_min[axis]
+    assert b[-1][1] == cfg.domain_max[axis]
+    for r in range(nranks - 1):
+        assert b[r][1] == b[r + 1][0]          # same expression -> no gap, no overlap
+    h = b[0][2]
+    assert h > 0 and all(x[2] == h for x in b)
+    # every particle has exactly one owner, the one whose [lo, hi) holds it
+    xs = parts.position[:: max(1, parts.n // 4000), axis]
+    for x in xs:
+        r = solver.slab_owner(cfg, nranks, axis, x)
+        assert b[r][0] <= x < b[r][1] or (r == nranks - 1 and x >= b[r][0]) or (r == 0 and x < b[0][1])
+
+
+def test_slab_halo_covers_cutoff():
+    cfg, _ = cases.get("d1m").build()
+    lo, hi, h = solver.slab_bounds(cfg, 0, 2, 2)
+    scal = solver.derive_scalars(cfg)
+    # halo = (MaxRadius + MARGIN) * (1 + 1e-6) >= the acceptance radius of calculateNeighbor
+    assert h >= 2.5 * cfg.particle_spacing
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_exchange_routing(tmp_path, world):
+    out = str(tmp_path / "flags.npy")
+    _spawn(dist_worker.exchange_worker, world, out)
+    assert np.load(out).all()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_halo_band_contains_all_neighbours(tmp_path, world):
+    out = str(tmp_path / "band.npy")
+    _spawn(dist_worker.band_worker, world, "dam2d", out)
+    res = np.load(out)
+    n = cases.get("dam2d").build()[1].n
+    assert res[:, 0].sum() == n             # ownership is a partition
+    assert (res[:, 1] == 0).all(), res       # no owned particle misses a neighbour
+    assert (res[:, 2] > 0).all()             # dam2d's fluid spans the slab faces

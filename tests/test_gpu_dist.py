@@ -1,0 +1,109 @@
+"""GPU: the slab-decomposed multi-rank path against the CPU oracle and the single-GPU path.
+
+2-4 ranks share the one GPU of the test box (one process each, host-staged transport over gloo,
+csrc/mph_dist.hip); the RCCL transport differs only in who moves the message bytes.  The
+channel cases stream at 0.5 m/s along the slab axis, so every face-adjacent layer migrates and
+the periodic seam is crossed within the checked steps.
+
+Tolerances: NeighborCount exact (bit-identical acceptance on owned particles); positions 1e-12 m,
+velocities 1e-9 m/s; other fields relative 1e-8 of the field's max plus the roundoff floors of
+test_gpu_parity (the slab's local cell grid orders neighbour sums differently from the oracle).
+"""
+import multiprocessing as mp
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from particlemethod_fsi_amd import MphSolver, cases
+
+import dist_worker
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ["Position", "Velocity", "PressureP", "NeighborCount", "Force", "VolStrainP", "DivergenceP",
+          "DensityA", "GravityCenter", "PressureA", "Acceleration"]
+FLOOR = {"PressureP": 1e-9, "PressureA": 1e-9, "Force": 1e-15, "Acceleration": 1e-12,
+         "VolStrainP": 1e-13, "DivergenceP": 1e-12, "DensityA": 1e-13, "GravityCenter": 1e-16}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_slab(case, world, checkpoints, out):
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    ps = [ctx.Process(target=dist_worker.gpu_worker, args=(r, world, port, case, checkpoints, FIELDS, out))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(300)
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    return np.load(out)
+
+
+def close(f, a, b):
+    if f == "NeighborCount":
+        return np.array_equal(a, b), int((a != b).sum())
+    err = float(np.max(np.abs(a - b))) if a.size else 0.0
+    if f == "Position":
+        t = 1e-12
+    elif f == "Velocity":
+        t = 1e-9
+    else:
+        t = 1e-8 * float(np.max(np.abs(b))) + FLOOR.get(f, 1e-12)
+    return err <= t, (err, t)
+
+
+@pytest.mark.parametrize("case,world", [("channel3d", 2), ("channel3d", 3), ("channel2d", 4),
+                                        ("channel3d_st", 2), ("dam2d", 2)])
+def test_slab_ranks_match_oracle(tmp_path, case, world):
+    from oracle_bindings import OracleSolver
+    checkpoints = [1, 5, 20]
+    r = run_slab(case, world, checkpoints, str(tmp_path / "slab.npz"))
+    cfg, parts = cases.get(case).build()
+    assert (r["owner0"] >= 0).all()
+    o = OracleSolver(cfg, parts)
+    o.init()
+    done = 0
+    moved = False
+    for k in checkpoints:
+        o.step(k - done)
+        done = k
+        owner = r["s%d/owner" % k]
+        assert (owner >= 0).all()
+        if not np.array_equal(owner, r["owner0"]):
+            moved = True
+        for f in FIELDS:
+            ok, info = close(f, r["s%d/%s" % (k, f)], o.get(f))
+            assert ok, (case, world, k, f, info)
+    if case.startswith("channel"):
+        assert moved, "no particle migrated between slabs"
+
+
+def test_slab_matches_single_gpu(tmp_path):
+    """Same case, 2 slabs vs one context: identical neighbour counts, values within roundoff."""
+    r = run_slab("channel3d", 2, [10], str(tmp_path / "slab.npz"))
+    cfg, parts = cases.get("channel3d").build()
+    with MphSolver(cfg, parts) as s:
+        s.step(10)
+        for f in FIELDS:
+            ok, info = close(f, r["s10/%s" % f], s.get(f))
+            assert ok, (f, info)
+
+
+def test_rccl_exchange_selftest():
+    """The RCCL transport on a one-rank communicator (left = right = self): message routing and
+    the per-peer ordering that two ranks rely on."""
+    from particlemethod_fsi_amd.solver import load_library
+    L = load_library()
+    rc = L.mph_dist_selftest(0)
+    assert rc == 0, (rc, (L.mph_last_error(None) or b"").decode())
