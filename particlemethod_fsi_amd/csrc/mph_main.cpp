@@ -58,7 +58,13 @@ int main(int argc, char** argv)
     MphConfig cfg;
     mph_config_default(&cfg, 2, MPH_MODULE_BAR);
     if (const char* d = std::getenv("MPH_DIM")) cfg.dim = std::atoi(d);
-    if (const char* m = std::getenv("MPH_MODULE")) cfg.module = std::atoi(m);
+    if (const char* m = std::getenv("MPH_MODULE")) {
+        // the module #define of main.cpp:54-59 by name (or MphModule number)
+        static const char* names[] = {"bar", "dam", "turek_hron", "rolling1", "hydroelastic", "none"};
+        cfg.module = std::atoi(m);
+        for (int k = 0; k < 6; ++k)
+            if (std::strcmp(m, names[k]) == 0) cfg.module = k;
+    }
     int rc = mph_read_data_file(data.c_str(), &cfg);
     if (rc) die(nullptr, rc, "reading the data file");
     int n = 0;
