@@ -36,7 +36,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector spec
 # algorithmic bytes per particle per launch
-ALG_BYTES = {"pass_a": 92.0, "pass_b": 140.0, "sort": 140.0}
+ALG_BYTES = {"pass_a": 92.0, "neighbors_pass_a": 92.0, "pass_b": 140.0, "sort": 140.0}
 B_ALG_STEP = 372.0          # grid build 140 + pass 1 92 + pass 2 140
 SLAB_AXIS = 2               # z slabs for the dam workloads
 

@@ -28,6 +28,8 @@
 // 32-byte records); SoA makes consecutive lanes gather consecutive doubles.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "mph_kernels.h"
 #include "mph_params.h"
 
@@ -314,31 +316,139 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
     else rank_of[id] = dst;
 }
 
+// ----------------------------------------------------------------------------- pass A sums --
+
+struct PassA {
+    double da = 0.0, g0 = 0.0, g1 = 0.0, g2 = 0.0, vs = 0.0, dv = 0.0;
+};
+
+// One neighbour's contribution to DensityA (2141-2171), GravityCenter (2174-2210), DensityP
+// (2314-2341) and DivergenceP (2343-2379); (dvx, dvy, dvz) = v_j - v_i.
+__device__ __forceinline__ void pass_a_term(const DevParams& P, const double* s_ratio, int ti, int tj, bool solid,
+                                            double q0, double q1, double q2, double r2, double dvx, double dvy,
+                                            double dvz, PassA& o)
+{
+    double r, ir;
+    rsqrt_pair(r2, r, ir);
+    if (r2 <= P.rp2) {
+        const double omt = 1.0 - r * P.inv_rp;
+        o.vs += P.cp * omt * omt;
+        const double dot = dvx * q0 + dvy * q1 + dvz * q2;
+        o.dv -= dot * ir * (P.cdp * omt);
+    }
+    if (!solid) {
+        const double ratio = s_ratio[ti * kTypes + tj];
+        if (r2 <= P.ra2) {
+            const double t = r * P.inv_ra;
+            const double omt = 1.0 - t;
+            o.da += ratio * (P.ca * t * omt * omt);
+        }
+        if (r2 <= P.rg2) {
+            const double omt = 1.0 - r * P.inv_rg;
+            const double w = ratio * (P.cg * omt * omt) * (P.rg / P.r2g);
+            o.g0 += q0 * w;
+            o.g1 += q1 * w;
+            o.g2 += q2 * w;
+        }
+    }
+}
+
+// Epilogue: PhysicalCoefficients (2099-2137) and the pressure values of calculatePressureP
+// (2384-2392) and calculatePressureA (2218-2223).
+struct PassAOut {
+    double *pres, *gx, *gy, *gz, *pa, *dens_a, *vstrain, *divp;
+};
+
+__device__ __forceinline__ void pass_a_finish(const DevParams& P, const DevTables* T, int ti, int i,
+                                              const PassA& o, const PassAOut& out)
+{
+    const double vstr = o.vs - P.n0p;
+    const double kappa = vstr < 0.0 ? 0.0 : T->bulk[ti];
+    double p = -T->bulk_visc[ti] * o.dv;
+    if (vstr > 0.0) p += kappa * vstr;
+    double pa = T->cofa[ti] * (o.da - P.n0a) / P.dx;
+    if (P.n0a <= o.da) pa = 0.0;
+    out.pres[i] = p;
+    out.gx[i] = o.g0;
+    out.gy[i] = o.g1;
+    out.gz[i] = o.g2;
+    out.pa[i] = pa;
+    out.dens_a[i] = o.da;
+    out.vstrain[i] = vstr;
+    out.divp[i] = o.dv;
+}
+
 // ---------------------------------------------------------------------- neighbour search ----
 
 // calculateNeighbor (main.cpp:1743-1810).  The reference scans (2*3+1)^d cells of width dx; here
 // cells are >= rc/2 wide, so a +-2 stencil covers the acceptance sphere: 25 columns (3-D) or 5
 // (2-D) along which the cells of the last axis are contiguous in memory.  Acceptance is the
 // reference's own test  q0^2+q1^2+q2^2 <= (MaxRadius+MARGIN)^2  with the Mod-based minimum image.
-template <int DIM, bool FAST>
+// With FUSE the pass-A sums of every accepted neighbour are accumulated on the spot (same
+// neighbour order as the list, so the same sums as a separate list pass), saving pass A's list
+// read and gathers.
+struct FuseA {
+    const double* s_ratio;
+    int ti;
+    bool solid;
+    double vxi, vyi, vzi;
+};
+
+// Offset of x from the grid origin, wrapped once into [0, w) (as cell_axis).
+__device__ __forceinline__ double grid_offset(double x, double org, double w)
+{
+    const double u = x - org;
+    return u < 0.0 ? u + w : (u >= w ? u - w : u);
+}
+
+// Gap between grid offset u (inside cell c) and cell c + d along one axis (0 for d == 0).
+__device__ __forceinline__ double cell_gap(double u, int c, int d, double cw)
+{
+    const double g = d > 0 ? (c + d) * cw - u : (d < 0 ? u - (c + d + 1) * cw : 0.0);
+    return g > 0.0 ? g : 0.0;
+}
+
+template <int DIM, bool FAST, bool FUSE>
 __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A, const int* start,
                                                int i, double xi, double yi, double zi, int cx,
-                                               int cy, int cz, int* out)
+                                               int cy, int cz, int* out, const FuseA& F, PassA& o)
 {
     int cnt = 0;
     constexpr int NCOL = DIM == 3 ? 25 : 5;
     const int gca = DIM == 3 ? P.gc[2] : P.gc[1];   // contiguous axis
     const int cca = DIM == 3 ? cz : cy;
+    // Column trimming: skip the cells of a column (and whole columns) that lie entirely beyond
+    // the cutoff.  Conservative (cutoff enlarged by 1e-6 relative, far above the roundoff of the
+    // cell geometry), so the accepted set and its order are unchanged.
+    const double rcm2 = P.rc2 * (1.0 + 4e-6);
+    const double cw0 = 1.0 / P.ginv[0], cw1 = 1.0 / P.ginv[1];
+    const double ux = grid_offset(xi, P.corg[0], P.dw[0]);
+    const double uy = grid_offset(yi, P.corg[1], P.dw[1]);
+    const double uz = DIM == 3 ? grid_offset(zi, P.corg[2], P.dw[2]) : 0.0;
+    const double ua = DIM == 3 ? uz : uy;             // offset along the contiguous axis
+    const double ginva = DIM == 3 ? P.ginv[2] : P.ginv[1];
     for (int col = 0; col < NCOL; ++col) {
         int base;
+        double d2;
         if (DIM == 3) {
-            const int jx = FAST ? cx + col / 5 - 2 : wrap_cell(cx + col / 5 - 2, P.gc[0]);
-            const int jy = FAST ? cy + col % 5 - 2 : wrap_cell(cy + col % 5 - 2, P.gc[1]);
+            const int dxc = col / 5 - 2, dyc = col % 5 - 2;
+            const double gx = cell_gap(ux, cx, dxc, cw0), gy = cell_gap(uy, cy, dyc, cw1);
+            d2 = gx * gx + gy * gy;
+            if (d2 > rcm2) continue;
+            const int jx = FAST ? cx + dxc : wrap_cell(cx + dxc, P.gc[0]);
+            const int jy = FAST ? cy + dyc : wrap_cell(cy + dyc, P.gc[1]);
             base = (jx * P.gc[1] + jy) * P.gc[2];
         } else {
-            base = (FAST ? cx + col - 2 : wrap_cell(cx + col - 2, P.gc[0])) * P.gc[1];
+            const int dxc = col - 2;
+            const double gx = cell_gap(ux, cx, dxc, cw0);
+            d2 = gx * gx;
+            if (d2 > rcm2) continue;
+            base = (FAST ? cx + dxc : wrap_cell(cx + dxc, P.gc[0])) * P.gc[1];
         }
-        const int lo = cca - 2, hi = cca + 2;
+        const double ra = sqrt(rcm2 - d2);
+        int lo = (int)floor((ua - ra) * ginva), hi = (int)floor((ua + ra) * ginva);
+        lo = lo < cca - 2 ? cca - 2 : lo;
+        hi = hi > cca + 2 ? cca + 2 : hi;
         int seg_a[2], seg_b[2], nseg;
         if (FAST) { seg_a[0] = lo; seg_b[0] = hi; seg_a[1] = 0; seg_b[1] = -1; nseg = 1; }
         else if (lo < 0) { seg_a[0] = lo + gca; seg_b[0] = gca - 1; seg_a[1] = 0; seg_b[1] = hi; nseg = 2; }
@@ -358,15 +468,39 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
                     ys[u] = A.y[j];
                     zs[u] = A.z[j];
                 }
+                double q0[4], q1[4], q2[4], r2[4];
+                bool acc[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int j = j0 + u;
-                    const double q0 = image_exact<FAST>(xs[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
-                    const double q1 = image_exact<FAST>(ys[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
-                    const double q2 = image_exact<FAST || DIM == 2>(zs[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
-                    const double r2 = r2_exact(q0, q1, q2);
-                    if (j < je && r2 <= P.rc2 && j != i) {
-                        if (cnt < kMaxNeighbor) out[cnt * kTile] = j;
+                    q0[u] = image_exact<FAST>(xs[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
+                    q1[u] = image_exact<FAST>(ys[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
+                    q2[u] = image_exact<FAST || DIM == 2>(zs[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
+                    r2[u] = r2_exact(q0[u], q1[u], q2[u]);
+                    acc[u] = j < je && r2[u] <= P.rc2 && j != i;
+                }
+                if (FUSE) {
+                    // velocities / types of the accepted candidates, all loads in flight at once
+                    double vx[4], vy[4], vz[4];
+                    int tj[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int j = acc[u] ? j0 + u : i;
+                        vx[u] = A.vx[j];
+                        vy[u] = A.vy[j];
+                        vz[u] = A.vz[j];
+                        tj[u] = A.type[j];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (acc[u])
+                            pass_a_term(P, F.s_ratio, F.ti, tj[u], F.solid, q0[u], q1[u], q2[u], r2[u],
+                                        vx[u] - F.vxi, vy[u] - F.vyi, vz[u] - F.vzi, o);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (acc[u]) {
+                        if (cnt < kMaxNeighbor) out[cnt * kTile] = j0 + u;
                         ++cnt;
                     }
                 }
@@ -376,11 +510,17 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
     return cnt;
 }
 
-template <int DIM>
-__global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int* __restrict__ start,
-                                                   int* __restrict__ nbr, int* __restrict__ ncount,
-                                                   DevState* __restrict__ st)
+template <int DIM, bool FUSE>
+__global__ __launch_bounds__(256) void k_neighbors(DevParams P, const DevTables* __restrict__ T, Soa A,
+                                                   const int* __restrict__ start, int* __restrict__ nbr,
+                                                   int* __restrict__ ncount, DevState* __restrict__ st,
+                                                   PassAOut pout)
 {
+    __shared__ double s_ratio[kTypes * kTypes];
+    if (FUSE) {
+        if (threadIdx.x < kTypes * kTypes) s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
+        __syncthreads();
+    }
     const int i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     const bool live = i < P.n;
     const int ii = live ? i : P.n - 1;
@@ -392,18 +532,27 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int
         const int cy = cell_axis(yi, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
         const int cz = DIM == 3 ? cell_axis(zi, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
         int* out = nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
-        cnt = fast ? scan_candidates<DIM, true>(P, A, start, i, xi, yi, zi, cx, cy, cz, out)
-                   : scan_candidates<DIM, false>(P, A, start, i, xi, yi, zi, cx, cy, cz, out);
+        FuseA F{};
+        PassA o;
+        if (FUSE) {
+            F.s_ratio = s_ratio;
+            F.ti = A.type[i];
+            F.solid = dev_is_struct(F.ti);
+            F.vxi = A.vx[i]; F.vyi = A.vy[i]; F.vzi = A.vz[i];
+        }
+        cnt = fast ? scan_candidates<DIM, true, FUSE>(P, A, start, i, xi, yi, zi, cx, cy, cz, out, F, o)
+                   : scan_candidates<DIM, false, FUSE>(P, A, start, i, xi, yi, zi, cx, cy, cz, out, F, o);
         ncount[i] = cnt;
+        if (FUSE) pass_a_finish(P, T, F.ti, i, o, pout);
     }
     // wave reduction of the statistics (mean/max neighbours, overflow flag)
     int mx = cnt;
     unsigned long long sm = (unsigned long long)cnt;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const int m2 = __shfl_xor(mx, o, 64);
+    for (int o2 = 32; o2 > 0; o2 >>= 1) {
+        const int m2 = __shfl_xor(mx, o2, 64);
         mx = m2 > mx ? m2 : mx;
-        sm += __shfl_xor(sm, o, 64);
+        sm += __shfl_xor(sm, o2, 64);
     }
     if ((threadIdx.x & 63) == 0) {
         atomicMax(&st->max_count, mx);
@@ -414,19 +563,14 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int
 
 // ---------------------------------------------------------------------------- pass A -------
 
-struct PassA {
-    double da = 0.0, g0 = 0.0, g1 = 0.0, g2 = 0.0, vs = 0.0, dv = 0.0;
-};
-
-// Neighbour loops gather U neighbours' fields before the first use (all loads in flight at once):
-// the loops are memory-latency bound (profiles/r01: 90% of wave time in s_waitcnt).
+// Separate list pass (MPH_UNFUSED=1 diagnostics): neighbour loops gather U neighbours' fields
+// before the first use (all loads in flight at once; the loops are memory-latency bound).
 template <bool FAST, int DIM, int U = 4>
 __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_ratio, const Soa& A,
                                             const int* row, int cnt, int ti, bool solid, double xi,
                                             double yi, double zi, double vxi, double vyi, double vzi,
                                             PassA& o)
 {
-    const double gscale = P.rg / P.r2g;
     for (int k0 = 0; k0 < cnt; k0 += U) {
         int jj[U];
         double X[U], Y[U], Z[U], VX[U], VY[U], VZ[U];
@@ -441,51 +585,20 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-        if (k0 + u >= cnt) break;
-        const double q0 = image_exact<FAST>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
-        const double q1 = image_exact<FAST>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
-        const double q2 = image_exact<FAST || DIM == 2>(Z[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
-        const double r2 = r2_exact(q0, q1, q2);
-        double r, ir;
-        rsqrt_pair(r2, r, ir);
-        if (r2 <= P.rp2) {
-            const double omt = 1.0 - r * P.inv_rp;
-            o.vs += P.cp * omt * omt;
-            const double dot = (VX[u] - vxi) * q0 + (VY[u] - vyi) * q1 + (VZ[u] - vzi) * q2;
-            o.dv -= dot * ir * (P.cdp * omt);
-        }
-        if (!solid) {
-            const double ratio = s_ratio[ti * kTypes + TT[u]];
-            if (r2 <= P.ra2) {
-                const double t = r * P.inv_ra;
-                const double omt = 1.0 - t;
-                o.da += ratio * (P.ca * t * omt * omt);
-            }
-            if (r2 <= P.rg2) {
-                const double omt = 1.0 - r * P.inv_rg;
-                const double w = ratio * (P.cg * omt * omt) * gscale;
-                o.g0 += q0 * w;
-                o.g1 += q1 * w;
-                o.g2 += q2 * w;
-            }
-        }
+            if (k0 + u >= cnt) break;
+            const double q0 = image_exact<FAST>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
+            const double q1 = image_exact<FAST>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
+            const double q2 = image_exact<FAST || DIM == 2>(Z[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
+            pass_a_term(P, s_ratio, ti, TT[u], solid, q0, q1, q2, r2_exact(q0, q1, q2), VX[u] - vxi,
+                        VY[u] - vyi, VZ[u] - vzi, o);
         }
     }
 }
 
-// DensityA (2141-2171), GravityCenter (2174-2210), DensityP (2314-2341), DivergenceP
-// (2343-2379); epilogue: PhysicalCoefficients (2099-2137) and the pressure values of
-// calculatePressureP (2384-2392) and calculatePressureA (2218-2223).
 template <int DIM>
 __global__ __launch_bounds__(256) void k_pass_a(DevParams P, const DevTables* __restrict__ T, Soa A,
                                                 const int* __restrict__ nbr,
-                                                const int* __restrict__ ncount,
-                                                double* __restrict__ pres, double* __restrict__ gx,
-                                                double* __restrict__ gy, double* __restrict__ gz,
-                                                double* __restrict__ pa_out,
-                                                double* __restrict__ dens_a,
-                                                double* __restrict__ vstrain,
-                                                double* __restrict__ divp)
+                                                const int* __restrict__ ncount, PassAOut pout)
 {
     __shared__ double s_ratio[kTypes * kTypes];
     if (threadIdx.x < kTypes * kTypes) s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
@@ -504,20 +617,7 @@ __global__ __launch_bounds__(256) void k_pass_a(DevParams P, const DevTables* __
     PassA o;
     if (fast) pass_a_loop<true, DIM>(P, s_ratio, A, row, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
     else pass_a_loop<false, DIM>(P, s_ratio, A, row, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
-    const double vstr = o.vs - P.n0p;
-    const double kappa = vstr < 0.0 ? 0.0 : T->bulk[ti];
-    double p = -T->bulk_visc[ti] * o.dv;
-    if (vstr > 0.0) p += kappa * vstr;
-    double pa = T->cofa[ti] * (o.da - P.n0a) / P.dx;
-    if (P.n0a <= o.da) pa = 0.0;
-    pres[i] = p;
-    gx[i] = o.g0;
-    gy[i] = o.g1;
-    gz[i] = o.g2;
-    pa_out[i] = pa;
-    dens_a[i] = o.da;
-    vstrain[i] = vstr;
-    divp[i] = o.dv;
+    pass_a_finish(P, T, ti, i, o, pout);
 }
 
 // ---------------------------------------------------------------------------- pass B -------
@@ -1041,30 +1141,49 @@ void launch_sort(const Launch& L, int mode)
                L.key, L.start, L.tmp, L.B, L.A, L.rank_of, L.dst_of);
 }
 
+static bool fused_pass_a()
+{
+    static const bool fused = [] {
+        const char* e = std::getenv("MPH_UNFUSED");
+        return !(e && e[0] == '1');
+    }();
+    return fused;
+}
+
+static PassAOut pass_a_out(const Launch& L)
+{
+    return PassAOut{L.pres, L.gx, L.gy, L.gz, L.pa, L.dens_a, L.vstrain, L.divp};
+}
+
 void launch_neighbors(const Launch& L)
 {
     Profiler* prof = L.prof;
     const DevParams& P = *L.P;
     if (P.n == 0) return;
-    if (P.dim == 3)
-        MPH_LAUNCH("neighbors", L.stream, k_neighbors<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P,
-                   L.A, L.start, L.nbr, L.ncount, L.st);
-    else
-        MPH_LAUNCH("neighbors", L.stream, k_neighbors<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P,
-                   L.A, L.start, L.nbr, L.ncount, L.st);
+    const PassAOut po = pass_a_out(L);
+#define MPH_NB(D, F) \
+    MPH_LAUNCH(F ? "neighbors_pass_a" : "neighbors", L.stream, (k_neighbors<D, F>), dim3(blocks(P.n, 256)), \
+               dim3(256), 0, L.stream, P, L.T, L.A, L.start, L.nbr, L.ncount, L.st, po)
+    if (fused_pass_a()) {
+        if (P.dim == 3) MPH_NB(3, true); else MPH_NB(2, true);
+    } else {
+        if (P.dim == 3) MPH_NB(3, false); else MPH_NB(2, false);
+    }
+#undef MPH_NB
 }
 
 void launch_pass_a(const Launch& L)
 {
     Profiler* prof = L.prof;
     const DevParams& P = *L.P;
-    if (P.n == 0) return;
+    if (P.n == 0 || fused_pass_a()) return;   // fused into the neighbour search
+    const PassAOut po = pass_a_out(L);
     if (P.dim == 3)
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, L.pres, L.gx, L.gy, L.gz, L.pa, L.dens_a, L.vstrain, L.divp);
+                   L.A, L.nbr, L.ncount, po);
     else
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, L.pres, L.gx, L.gy, L.gz, L.pa, L.dens_a, L.vstrain, L.divp);
+                   L.A, L.nbr, L.ncount, po);
 }
 
 void launch_pass_b(const Launch& L)
