@@ -88,6 +88,7 @@ int ctx_dalloc(MphCtx* c, T** p, size_t count)
 }
 
 void ctx_fill_launch(MphCtx* c);
+int ctx_state_status(MphCtx* c, const DevState& hs);   // kernel error flags -> MphStatus
 
 void ctx_set_global_error(const std::string& msg);   // mph_last_error(NULL)
 int ctx_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, const double* pos,

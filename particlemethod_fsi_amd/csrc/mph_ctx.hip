@@ -44,6 +44,17 @@ void* ctx_alloc(MphCtx* c, size_t bytes, int* status)
     return q;
 }
 
+// Error flags raised by the kernels (DevState.overflow bits).
+int ctx_state_status(MphCtx* c, const DevState& hs)
+{
+    if (hs.overflow & 4)
+        return ctx_fail(c, MPH_ERR_NONFINITE, "non-finite particle position (diverged state)");
+    if (hs.overflow & 1)
+        return ctx_fail(c, MPH_ERR_NEIGHBOR_OVERFLOW, "a particle has more than 512 neighbours");
+    if (hs.overflow & 2) return ctx_fail(c, MPH_ERR_CAPACITY, "a particle moved past a neighbouring slab");
+    return MPH_OK;
+}
+
 void ctx_fill_launch(MphCtx* c)
 {
     Launch& L = c->L;
@@ -391,8 +402,7 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     {
         DevState hs;
         HIP_OK(c, hipMemcpy(&hs, c->dst, sizeof(DevState), hipMemcpyDeviceToHost));
-        if (hs.overflow & 1) return fail(c, MPH_ERR_NEIGHBOR_OVERFLOW, "a particle has more than 512 neighbours");
-        if (hs.overflow & 2) return fail(c, MPH_ERR_CAPACITY, "a particle moved past a neighbouring slab");
+        CK(ctx_state_status(c, hs));
     }
     return MPH_OK;
 }
@@ -450,7 +460,7 @@ int mph_step(MphCtx* c, int nsteps)
     DevState hs;
     HIP_OK(c, hipMemcpyAsync(&hs, c->dst, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipStreamSynchronize(c->stream));
-    if (hs.overflow) return fail(c, MPH_ERR_NEIGHBOR_OVERFLOW, "a particle has more than 512 neighbours");
+    CK(ctx_state_status(c, hs));
     return MPH_OK;
 }
 
@@ -620,7 +630,7 @@ int mph_profile_steps(MphCtx* c, int nsteps, double* avg_ms, int* launches, char
     }
     DevState hs;
     HIP_OK(c, hipMemcpy(&hs, c->dst, sizeof(DevState), hipMemcpyDeviceToHost));
-    if (hs.overflow) return fail(c, MPH_ERR_NEIGHBOR_OVERFLOW, "a particle has more than 512 neighbours");
+    CK(ctx_state_status(c, hs));
     return k;
 }
 

@@ -241,9 +241,7 @@ int check_state(MphCtx* c)
     DevState hs;
     MPH_HIP_OK(c, hipMemcpyAsync(&hs, c->dst, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
     MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
-    if (hs.overflow & 1) return ctx_fail(c, MPH_ERR_NEIGHBOR_OVERFLOW, "a particle has more than 512 neighbours");
-    if (hs.overflow & 2) return ctx_fail(c, MPH_ERR_CAPACITY, "a particle moved past a neighbouring slab");
-    return MPH_OK;
+    return ctx_state_status(c, hs);
 }
 
 }  // namespace

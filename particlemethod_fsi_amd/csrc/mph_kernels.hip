@@ -91,9 +91,10 @@ __device__ __forceinline__ int cell_axis(double x, double org, double w, double 
 {
     double u = x - org;
     u = u < 0.0 ? u + w : (u >= w ? u - w : u);
-    int c = (int)floor(u * ginv);
-    c = c < 0 ? 0 : c;
-    return c >= g ? g - 1 : c;
+    // clamp before the conversion: a NaN / infinite coordinate (diverged input) maps to cell 0
+    // instead of an undefined float->int conversion
+    const double t = fmin(fmax(floor(u * ginv), 0.0), (double)(g - 1));
+    return (int)t;
 }
 
 __device__ __forceinline__ int cell_id(const DevParams& P, double x, double y, double z)
@@ -175,6 +176,7 @@ __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __res
     if (p >= P.n) return;
     double x = B.x[p], y = B.y[p], z = B.z[p];
     if (mode == 1) move_and_wrap(P, st, B, p, x, y, z);
+    if (!isfinite(x + y + z)) atomicOr(const_cast<int*>(&st->overflow), 4);   // MPH_ERR_NONFINITE
     const int k = cell_id(P, x, y, z);
     key[p] = k;
     slot[p] = atomicAdd(&cnt[k], 1);
@@ -446,9 +448,8 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
             base = (FAST ? cx + dxc : wrap_cell(cx + dxc, P.gc[0])) * P.gc[1];
         }
         const double ra = sqrt(rcm2 - d2);
-        int lo = (int)floor((ua - ra) * ginva), hi = (int)floor((ua + ra) * ginva);
-        lo = lo < cca - 2 ? cca - 2 : lo;
-        hi = hi > cca + 2 ? cca + 2 : hi;
+        const int lo = (int)fmax(floor((ua - ra) * ginva), (double)(cca - 2));
+        const int hi = (int)fmin(floor((ua + ra) * ginva), (double)(cca + 2));
         int seg_a[2], seg_b[2], nseg;
         if (FAST) { seg_a[0] = lo; seg_b[0] = hi; seg_a[1] = 0; seg_b[1] = -1; nseg = 1; }
         else if (lo < 0) { seg_a[0] = lo + gca; seg_b[0] = gca - 1; seg_a[1] = 0; seg_b[1] = hi; nseg = 2; }
@@ -565,7 +566,13 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, const DevTables*
 
 // Separate list pass (the default; see fused_pass_a): neighbour loops gather U neighbours' fields
 // before the first use (all loads in flight at once; the loops are memory-latency bound).
-template <bool FAST, int DIM, int U = 4>
+#ifndef MPH_UA
+#define MPH_UA 4
+#endif
+#ifndef MPH_UB
+#define MPH_UB 4
+#endif
+template <bool FAST, int DIM, int U = MPH_UA>
 __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_ratio, const Soa& A,
                                             const int* row, int cnt, int ti, bool solid, double xi,
                                             double yi, double zi, double vxi, double vyi, double vzi,
@@ -622,7 +629,7 @@ __global__ __launch_bounds__(256) void k_pass_a(DevParams P, const DevTables* __
 
 // ---------------------------------------------------------------------------- pass B -------
 
-template <bool FAST, bool SURF, int DIM, int U = 4>
+template <bool FAST, bool SURF, int DIM, int U = MPH_UB>
 __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_ratio, const double* s_mu,
                                             const Soa& A, const double* pres, const double* gx,
                                             const double* gy, const double* gz, const double* pa,

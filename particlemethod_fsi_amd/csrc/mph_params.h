@@ -61,7 +61,8 @@ struct DevState {
     double wall_vel[kTypes][3];  // WallVelocity
     double wall_omega[kTypes][3];// WallOmega
     double wall_rot[kTypes][3][3];  // WallRotation (initializeWall)
-    int overflow;                // some particle reached MAX_NEIGHBOR_COUNT
+    int overflow;                // error bits: 1 neighbour overflow (> MAX_NEIGHBOR_COUNT),
+                                 // 2 slab jump (mph_dist), 4 non-finite position
     int max_count;               // max neighbour count of the last search
     unsigned long long sum_count;
 };

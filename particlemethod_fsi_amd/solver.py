@@ -20,7 +20,7 @@ from . import mphio
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(PKG_DIR, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libmph_gpu.so")
+LIB_PATH = os.environ.get("MPH_GPU_LIB") or os.path.join(LIB_DIR, "libmph_gpu.so")   # env: A/B builds
 CSRC_DIR = os.path.join(PKG_DIR, "csrc")
 
 # MphField (include/mph_gpu.h) keyed by the reference's array names (main.cpp:102-197)

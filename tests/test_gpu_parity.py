@@ -156,3 +156,19 @@ def test_gpu_graph_chunking_equivalence():
             b.step(1)
         assert np.array_equal(a.get("Position"), b.get("Position"))
         assert np.array_equal(a.get("Velocity"), b.get("Velocity"))
+
+
+def test_gpu_nonfinite_state_is_an_error_not_a_fault():
+    """A diverged state (NaN position) is reported as MPH_ERR_NONFINITE by the next step; every
+    index the kernels derive from it stays in range (no device fault)."""
+    from particlemethod_fsi_amd.solver import MphError
+    cfg, parts = cases.get("dam2d").build()
+    with MphSolver(cfg, parts) as s:
+        s.step(2)
+        pos = s.get("Position")
+        pos[100, 0] = np.nan
+        pos[200, 1] = np.inf
+        s.set("Position", pos)
+        with pytest.raises(MphError) as e:
+            s.step(1)
+        assert e.value.code == -9
