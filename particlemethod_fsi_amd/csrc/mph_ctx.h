@@ -30,6 +30,8 @@ struct MphDist {
     int* hseg = nullptr;          // pinned host mirror
     char *send_l = nullptr, *send_r = nullptr, *recv_l = nullptr, *recv_r = nullptr;  // device
     int *cnt_send = nullptr, *cnt_recv = nullptr;    // device count messages (4 ints each way)
+    hipStream_t stream2 = nullptr;                   // halo exchange beside the inner pass B
+    hipEvent_t ev_a = nullptr, ev_h = nullptr;       // pass A done / halo landed
     // transport: RCCL communicator, or a host callback (tests / hosts without RCCL)
     bool rccl = false;
     char uid[128] = {0};          // ncclUniqueId

@@ -107,8 +107,8 @@ int copy_soa(MphCtx* c, const Soa& dst, const Soa& src, int n)
 // -- transport ----------------------------------------------------------------------------------
 
 // send_l -> left neighbour (arrives there as its recv_r), send_r -> right neighbour (its recv_l)
-int exchange(MphCtx* c, const void* send_l, size_t bsl, const void* send_r, size_t bsr, void* recv_l,
-             size_t brl, void* recv_r, size_t brr)
+int exchange(MphCtx* c, hipStream_t stream, const void* send_l, size_t bsl, const void* send_r, size_t bsr,
+             void* recv_l, size_t brl, void* recv_r, size_t brr)
 {
     MphDist& D = *c->dist;
     if (D.rccl) {
@@ -117,10 +117,10 @@ int exchange(MphCtx* c, const void* send_l, size_t bsl, const void* send_r, size
         // per-peer order: first the left-going message, then the right-going one (matters when
         // left == right, nranks == 2): a rank's first receive from a peer matches that peer's
         // first send, i.e. its left-going message = our from-right message
-        if (bsl) RCCL_OK(c, ncclSend(send_l, bsl, ncclChar, D.left, comm, c->stream));
-        if (brr) RCCL_OK(c, ncclRecv(recv_r, brr, ncclChar, D.right, comm, c->stream));
-        if (bsr) RCCL_OK(c, ncclSend(send_r, bsr, ncclChar, D.right, comm, c->stream));
-        if (brl) RCCL_OK(c, ncclRecv(recv_l, brl, ncclChar, D.left, comm, c->stream));
+        if (bsl) RCCL_OK(c, ncclSend(send_l, bsl, ncclChar, D.left, comm, stream));
+        if (brr) RCCL_OK(c, ncclRecv(recv_r, brr, ncclChar, D.right, comm, stream));
+        if (bsr) RCCL_OK(c, ncclSend(send_r, bsr, ncclChar, D.right, comm, stream));
+        if (brl) RCCL_OK(c, ncclRecv(recv_l, brl, ncclChar, D.left, comm, stream));
         RCCL_OK(c, ncclGroupEnd());
         return MPH_OK;
     }
@@ -129,13 +129,13 @@ int exchange(MphCtx* c, const void* send_l, size_t bsl, const void* send_r, size
     char* hs_r = D.host_stage + region;
     char* hr_l = D.host_stage + 2 * region;
     char* hr_r = D.host_stage + 3 * region;
-    if (bsl) MPH_HIP_OK(c, hipMemcpyAsync(hs_l, send_l, bsl, hipMemcpyDeviceToHost, c->stream));
-    if (bsr) MPH_HIP_OK(c, hipMemcpyAsync(hs_r, send_r, bsr, hipMemcpyDeviceToHost, c->stream));
-    MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
+    if (bsl) MPH_HIP_OK(c, hipMemcpyAsync(hs_l, send_l, bsl, hipMemcpyDeviceToHost, stream));
+    if (bsr) MPH_HIP_OK(c, hipMemcpyAsync(hs_r, send_r, bsr, hipMemcpyDeviceToHost, stream));
+    MPH_HIP_OK(c, hipStreamSynchronize(stream));
     if (D.host_fn(D.host_user, hs_l, bsl, hs_r, bsr, hr_l, brl, hr_r, brr) != 0)
         return ctx_fail(c, MPH_ERR_TRANSPORT, "host exchange callback failed");
-    if (brl) MPH_HIP_OK(c, hipMemcpyAsync(recv_l, hr_l, brl, hipMemcpyHostToDevice, c->stream));
-    if (brr) MPH_HIP_OK(c, hipMemcpyAsync(recv_r, hr_r, brr, hipMemcpyHostToDevice, c->stream));
+    if (brl) MPH_HIP_OK(c, hipMemcpyAsync(recv_l, hr_l, brl, hipMemcpyHostToDevice, stream));
+    if (brr) MPH_HIP_OK(c, hipMemcpyAsync(recv_r, hr_r, brr, hipMemcpyHostToDevice, stream));
     return MPH_OK;
 }
 
@@ -151,20 +151,19 @@ int redistribute(MphCtx* c, bool move, Profiler* prof)
     launch_dist_classify(L, D.g, n_prev, move ? 1 : 0, D.cls, D.bcnt);
     launch_scan(D.bcnt, kSlabClasses * nb, D.bsum, D.boff, n_prev, c->stream, prof);
     launch_dist_scatter(L, n_prev, D.cls, D.boff, D.C, D.dseg);
+    // count messages straight from the device segment table; one host sync for both the local
+    // segment sizes and the neighbours' counts
+    launch_dist_counts(L, D.dseg, D.cnt_send);
+    MPH_CK(exchange(c, c->stream, D.cnt_send, 2 * sizeof(int), D.cnt_send + 2, 2 * sizeof(int), D.cnt_recv,
+                    2 * sizeof(int), D.cnt_recv + 2, 2 * sizeof(int)));
+    int* hc = D.hcnt;
     MPH_HIP_OK(c, hipMemcpyAsync(D.hseg, D.dseg, sizeof(int) * (kSlabClasses + 1), hipMemcpyDeviceToHost,
                                  c->stream));
+    MPH_HIP_OK(c, hipMemcpyAsync(hc + 4, D.cnt_recv, sizeof(int) * 4, hipMemcpyDeviceToHost, c->stream));
     MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
     for (int k = 0; k < kSlabClasses; ++k) D.seg[k] = D.hseg[k + 1] - D.hseg[k];
     const int mR = D.seg[kMigR], bR = D.seg[kBandR], bL = D.seg[kBandL], mL = D.seg[kMigL];
     const int nc = D.hseg[kSlabDrop];                 // kept entries (classes 0..4)
-    // count messages: left-going {bandL, migL}, right-going {migR, bandR}
-    int* hc = D.hcnt;
-    hc[0] = bL; hc[1] = mL; hc[2] = mR; hc[3] = bR;
-    MPH_HIP_OK(c, hipMemcpyAsync(D.cnt_send, hc, sizeof(int) * 4, hipMemcpyHostToDevice, c->stream));
-    MPH_CK(exchange(c, D.cnt_send, 2 * sizeof(int), D.cnt_send + 2, 2 * sizeof(int), D.cnt_recv,
-                    2 * sizeof(int), D.cnt_recv + 2, 2 * sizeof(int)));
-    MPH_HIP_OK(c, hipMemcpyAsync(hc + 4, D.cnt_recv, sizeof(int) * 4, hipMemcpyDeviceToHost, c->stream));
-    MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
     D.from_l_mig = hc[4]; D.from_l_band = hc[5];     // their {migR, bandR}
     D.from_r_band = hc[6]; D.from_r_mig = hc[7];     // their {bandL, migL}
     const int fl = D.from_l_mig + D.from_l_band, fr = D.from_r_band + D.from_r_mig;
@@ -174,7 +173,7 @@ int redistribute(MphCtx* c, bool move, Profiler* prof)
                                                  " exceeded (" + std::to_string(n_new) + ")");
     launch_dist_pack(L, D.C, D.hseg[kBandL], bL + mL, D.send_l);
     launch_dist_pack(L, D.C, 0, mR + bR, D.send_r);
-    MPH_CK(exchange(c, D.send_l, kMsgBytes * (bL + mL), D.send_r, kMsgBytes * (mR + bR), D.recv_l,
+    MPH_CK(exchange(c, c->stream, D.send_l, kMsgBytes * (bL + mL), D.send_r, kMsgBytes * (mR + bR), D.recv_l,
                     kMsgBytes * fl, D.recv_r, kMsgBytes * fr));
     launch_dist_unpack(L, D.recv_l, fl, D.C, nc);
     launch_dist_unpack(L, D.recv_r, fr, D.C, nc + fl);
@@ -207,11 +206,12 @@ HaloFields halo_fields(MphCtx* c)
 }
 
 // Step 5: the pass-A values of every neighbour's ghosts.
-int halo_exchange(MphCtx* c, Profiler* prof)
+int halo_exchange(MphCtx* c, Profiler* prof, hipStream_t stream)
 {
     MphDist& D = *c->dist;
     Launch L = c->L;
     L.prof = prof;
+    L.stream = stream;
     const HaloFields F = halo_fields(c);
     const int nc = D.hseg[kSlabDrop];
     const int fl = D.from_l_mig + D.from_l_band;
@@ -230,7 +230,8 @@ int halo_exchange(MphCtx* c, Profiler* prof)
     launch_halo_pack(L, c->rank_of, l1, ln1, l2, ln2, F, sl);
     launch_halo_pack(L, c->rank_of, r1, rn1, r2, rn2, F, sr);
     const size_t b = sizeof(double) * F.nf;
-    MPH_CK(exchange(c, sl, b * (ln1 + ln2), sr, b * (rn1 + rn2), rl, b * (fln1 + fln2), rr, b * (frn1 + frn2)));
+    MPH_CK(exchange(c, stream, sl, b * (ln1 + ln2), sr, b * (rn1 + rn2), rl, b * (fln1 + fln2), rr,
+                    b * (frn1 + frn2)));
     launch_halo_unpack(L, rl, c->rank_of, fl1, fln1, fl2, fln2, F);
     launch_halo_unpack(L, rr, c->rank_of, fr1, frn1, fr2, frn2, F);
     return MPH_OK;
@@ -271,6 +272,10 @@ int dist_setup(MphCtx* c, const double* pos, std::vector<int>& owned)
     const int gloc = (int)std::ceil((whi - wlo) / cw);
     if (gloc < 5) return ctx_fail(c, MPH_ERR_DOMAIN, "slab window narrower than 5 cells");
     c->P.corg[axis] = wlo;
+    c->P.slab_axis = axis;
+    c->P.slab_lo = D.g.lo;
+    c->P.slab_hi = D.g.hi;
+    c->P.slab_h = halo;
     c->P.gc[axis] = std::min(gloc, c->P.gc[axis] + 1);
     // fast-path interior: >= 3 cells inside both the window and the periodic domain
     c->P.inner_lo[axis] = std::max(wlo, h.dmin[axis]) + 3.0 * cw * (1.0 + 1e-9);
@@ -316,6 +321,9 @@ int dist_alloc(MphCtx* c)
     const size_t region = (size_t)D.msg_cap * kMsgBytes;
     MPH_CK(ctx_dalloc(c, &D.send_l, region)); MPH_CK(ctx_dalloc(c, &D.send_r, region));
     MPH_CK(ctx_dalloc(c, &D.recv_l, region)); MPH_CK(ctx_dalloc(c, &D.recv_r, region));
+    MPH_HIP_OK(c, hipStreamCreateWithFlags(&D.stream2, hipStreamNonBlocking));
+    MPH_HIP_OK(c, hipEventCreateWithFlags(&D.ev_a, hipEventDisableTiming));
+    MPH_HIP_OK(c, hipEventCreateWithFlags(&D.ev_h, hipEventDisableTiming));
     MPH_HIP_OK(c, hipHostMalloc((void**)&D.hseg, sizeof(int) * (kSlabClasses + 2), hipHostMallocDefault));
     MPH_HIP_OK(c, hipHostMalloc((void**)&D.hcnt, sizeof(int) * 8, hipHostMallocDefault));
     if (D.rccl) {
@@ -353,8 +361,18 @@ int dist_step(MphCtx* c, int nsteps, Profiler* prof)
         sort_local(c, 2, prof);
         launch_neighbors(L);
         launch_pass_a(L);
-        MPH_CK(halo_exchange(c, prof));
-        launch_pass_b(L);
+        // the pass-A halo travels on stream2 while pass B runs the particles that have no
+        // ghost neighbours; the near-face particles follow once the halo has landed
+        // (inner pass B is enqueued first, so that a host-staged exchange, which blocks the host,
+        // also overlaps with it)
+        MphDist& D = *c->dist;
+        MPH_HIP_OK(c, hipEventRecord(D.ev_a, c->stream));
+        launch_pass_b(L, 1);
+        MPH_HIP_OK(c, hipStreamWaitEvent(D.stream2, D.ev_a, 0));
+        MPH_CK(halo_exchange(c, prof, D.stream2));
+        MPH_HIP_OK(c, hipEventRecord(D.ev_h, D.stream2));
+        MPH_HIP_OK(c, hipStreamWaitEvent(c->stream, D.ev_h, 0));
+        launch_pass_b(L, 2);
         MPH_HIP_OK(c, hipGetLastError());
         c->time += c->cfg.dt;
         c->stepped = true;
@@ -366,7 +384,11 @@ void dist_free(MphCtx* c)
 {
     MphDist* D = c->dist;
     if (!D) return;
+    if (D->stream2) (void)hipStreamSynchronize(D->stream2);
     if (D->comm) (void)ncclCommDestroy((ncclComm_t)D->comm);
+    if (D->ev_a) (void)hipEventDestroy(D->ev_a);
+    if (D->ev_h) (void)hipEventDestroy(D->ev_h);
+    if (D->stream2) (void)hipStreamDestroy(D->stream2);
     if (D->hseg) (void)hipHostFree(D->hseg);
     if (D->hcnt) (void)hipHostFree(D->hcnt);
     if (D->host_stage) (void)hipHostFree(D->host_stage);
@@ -445,9 +467,9 @@ int mph_dist_selftest(int device)
         MPH_HIP_OK(&c, hipMemcpy(sl, hl.data(), nl, hipMemcpyHostToDevice));
         MPH_HIP_OK(&c, hipMemcpy(sr, hr.data(), nr, hipMemcpyHostToDevice));
         // left-going (sl) must arrive as from-right (rr); right-going (sr) as from-left (rl)
-        MPH_CK(exchange(&c, sl, nl, sr, nr, rl, nr, rr, nl));
+        MPH_CK(exchange(&c, c.stream, sl, nl, sr, nr, rl, nr, rr, nl));
         // a zero-byte direction is skipped on both sides
-        MPH_CK(exchange(&c, sl, 0, sr, nr, rl, nr, rr, 0));
+        MPH_CK(exchange(&c, c.stream, sl, 0, sr, nr, rl, nr, rr, 0));
         MPH_HIP_OK(&c, hipStreamSynchronize(c.stream));
         MPH_HIP_OK(&c, hipMemcpy(gl.data(), rl, nr, hipMemcpyDeviceToHost));
         MPH_HIP_OK(&c, hipMemcpy(gr.data(), rr, nl, hipMemcpyDeviceToHost));

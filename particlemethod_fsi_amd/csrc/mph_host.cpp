@@ -385,6 +385,7 @@ void make_dev_params(const MphConfig& c, const HostDerived& h, int n, int n_stru
 {
     std::memset(&P, 0, sizeof(P));
     P.n = n;
+    P.slab_axis = -1;
     P.dim = c.dim;
     P.module = c.module;
     P.n_struct = n_struct;

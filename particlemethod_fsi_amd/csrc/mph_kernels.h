@@ -68,7 +68,7 @@ struct Launch {
 void launch_sort(const Launch& L, int mode);   // mode 0 init, 1 step, 2 step (motion done)
 void launch_neighbors(const Launch& L);
 void launch_pass_a(const Launch& L);
-void launch_pass_b(const Launch& L);
+void launch_pass_b(const Launch& L, int phase = 0);   // phase: 0 all, 1/2 slab inner/near-face
 void launch_structure(const Launch& L);
 
 // slab decomposition (mph_dist.hip)
@@ -80,6 +80,7 @@ void launch_scan(int* cnt, int ncell, int* bsum, int* start, int total, hipStrea
 int dist_blocks(int n);
 void launch_dist_classify(const Launch& L, const SlabGeom& g, int n, int move, int* cls, int* bcnt);
 void launch_dist_scatter(const Launch& L, int n, const int* cls, const int* boff, const Soa& C, int* dseg);
+void launch_dist_counts(const Launch& L, const int* dseg, int* cnt_send);
 void launch_dist_pack(const Launch& L, const Soa& C, int off, int m, char* buf);
 void launch_dist_unpack(const Launch& L, const char* buf, int m, const Soa& C, int off);
 void launch_halo_pack(const Launch& L, const int* dst_of, int o1, int n1, int o2, int n2, const HaloFields& F,

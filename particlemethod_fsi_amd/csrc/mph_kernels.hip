@@ -567,7 +567,7 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, const DevTables*
 // Separate list pass (the default; see fused_pass_a): neighbour loops gather U neighbours' fields
 // before the first use (all loads in flight at once; the loops are memory-latency bound).
 #ifndef MPH_UA
-#define MPH_UA 4
+#define MPH_UA 8
 #endif
 #ifndef MPH_UB
 #define MPH_UB 4
@@ -721,7 +721,7 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
                                                 const int* __restrict__ nbr,
                                                 const int* __restrict__ ncount,
                                                 double4* __restrict__ force, double4* __restrict__ acc,
-                                                Soa B)
+                                                Soa B, int phase)
 {
     __shared__ double s_ratio[kTypes * kTypes];
     __shared__ double s_mu[kTypes * kTypes];
@@ -731,9 +731,16 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
     }
     __syncthreads();
     const int i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    const bool live = i < P.n;
-    const int ii = live ? i : P.n - 1;
+    const int ii = i < P.n ? i : P.n - 1;
     const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
+    bool live = i < P.n;
+    if (phase) {
+        // slab mode: phase 1 = particles whose neighbours are all owned (run while the halo of
+        // pass-A values is in flight), phase 2 = the rest (after the halo arrived)
+        const double c = P.slab_axis == 0 ? xi : (P.slab_axis == 1 ? yi : zi);
+        const bool inner = c - P.slab_lo > P.slab_h && P.slab_hi - c > P.slab_h;
+        live = live && (phase == 1 ? inner : !inner);
+    }
     const bool fast = wave_interior(P, live, xi, yi, zi);
     if (!live) return;
     const double vxi = A.vx[i], vyi = A.vy[i], vzi = A.vz[i];
@@ -1054,6 +1061,16 @@ __global__ __launch_bounds__(256) void k_dist_scatter(Soa B, int n, const int* _
     C.id[o] = (c == kMigR || c == kMigL) ? -1 - id : id;
 }
 
+// count messages from the segment starts: left-going {bandL, migL}, right-going {migR, bandR}
+__global__ void k_dist_counts(const int* __restrict__ dseg, int* __restrict__ cnt_send)
+{
+    if (threadIdx.x != 0) return;
+    cnt_send[0] = dseg[kBandL + 1] - dseg[kBandL];
+    cnt_send[1] = dseg[kMigL + 1] - dseg[kMigL];
+    cnt_send[2] = dseg[kMigR + 1] - dseg[kMigR];
+    cnt_send[3] = dseg[kBandR + 1] - dseg[kBandR];
+}
+
 // message layout: x[m] y[m] z[m] vx[m] vy[m] vz[m] (double) type[m] id[m] (int) = 56 B/particle
 __global__ __launch_bounds__(256) void k_dist_pack(Soa C, int off, int m, char* __restrict__ buf)
 {
@@ -1195,14 +1212,14 @@ void launch_pass_a(const Launch& L)
                    L.A, L.nbr, L.ncount, po);
 }
 
-void launch_pass_b(const Launch& L)
+void launch_pass_b(const Launch& L, int phase)
 {
     Profiler* prof = L.prof;
     const DevParams& P = *L.P;
     if (P.n == 0) return;
 #define MPH_PASS_B(S, D)                                                                            \
     MPH_LAUNCH("pass_b", L.stream, (k_pass_b<S, D>), dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, \
-               L.T, L.A, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, L.force, L.acc, L.B)
+               L.T, L.A, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, L.force, L.acc, L.B, phase)
     if (P.surface) {
         if (P.dim == 3) MPH_PASS_B(true, 3); else MPH_PASS_B(true, 2);
     } else {
@@ -1264,6 +1281,12 @@ void launch_dist_scatter(const Launch& L, int n, const int* cls, const int* boff
     const int nb = dist_blocks(n);
     MPH_LAUNCH("dist_scatter", L.stream, k_dist_scatter, dim3(nb), dim3(256), 0, L.stream, L.B, n, cls, boff,
                nb, C, dseg);
+}
+
+void launch_dist_counts(const Launch& L, const int* dseg, int* cnt_send)
+{
+    Profiler* prof = L.prof;
+    MPH_LAUNCH("dist_counts", L.stream, k_dist_counts, dim3(1), dim3(64), 0, L.stream, dseg, cnt_send);
 }
 
 void launch_dist_pack(const Launch& L, const Soa& C, int off, int m, char* buf)

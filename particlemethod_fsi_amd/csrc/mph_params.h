@@ -34,6 +34,10 @@ struct DevParams {
     double dmin[3], dw[3], hw[3], w075[3];   // domain min / width / half width / 0.75 width
     double corg[3];    // origin of the GPU cell grid (dmin, or the slab window's lower edge)
     double ginv[3];    // 1 / GPU cell width per axis
+    // slab mode: particles within slab_h of a slab face may have ghost neighbours (pass B runs
+    // them after the halo exchange); slab_axis = -1 outside slab mode
+    int slab_axis;
+    double slab_lo, slab_hi, slab_h;
     double rc2;        // (MaxRadius + MARGIN)^2, main.cpp:1765
     double ra, rg, rp, rv;                   // radii (main.cpp:1195-1198)
     double ra2, rg2, rp2, rv2;               // radius*radius as the reference compares them
