@@ -90,6 +90,12 @@ int ctx_dalloc(MphCtx* c, T** p, size_t count)
 }
 
 void ctx_fill_launch(MphCtx* c);
+// cells between a fast-path interior particle and a grid face along axis d: stencil half-width + 1
+inline int stencil_margin(const DevParams& P, int d)
+{
+    const int ca = P.dim == 3 ? 2 : 1;
+    return (d == ca ? P.sa : 2) + 1;
+}
 int ctx_state_status(MphCtx* c, const DevState& hs);   // kernel error flags -> MphStatus
 
 void ctx_set_global_error(const std::string& msg);   // mph_last_error(NULL)

@@ -246,18 +246,22 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     make_dev_params(c->cfg, c->h, n, ns, c->P);
     const double rc = std::sqrt(c->P.rc2);
     {
-        int r = choose_grid(c->h, cfg->dim, rc, c->P.gc, c->P.ginv, err);
+        int r = choose_grid(c->h, cfg->dim, rc, kContigSub, c->P.gc, c->P.ginv, err);
         if (r != MPH_OK) return fail(c, r, err);
     }
     // interior box for the wave-uniform fast minimum image (k_neighbors / passes): >= 3 cells
     // (+1e-9 relative margin) from every periodic face; needs > 12 cells on every active axis
+    // (stencil half-width + 1 cells from every periodic face; the candidate offsets then stay
+    // below a quarter of the domain width, which needs > 4 x that many cells on every axis)
+    c->P.sa = 2 * kContigSub;
     c->P.fast_ok = 1;
     for (int d = 0; d < 3; ++d) {
         if (d == 2 && cfg->dim == 2) { c->P.inner_lo[d] = -1e300; c->P.inner_hi[d] = 1e300; continue; }
-        if (c->P.gc[d] <= 12) c->P.fast_ok = 0;
+        const int m = stencil_margin(c->P, d);
+        if (c->P.gc[d] <= 4 * m) c->P.fast_ok = 0;
         const double cw = c->h.dw[d] / c->P.gc[d];
-        c->P.inner_lo[d] = c->h.dmin[d] + 3.0 * cw * (1.0 + 1e-9);
-        c->P.inner_hi[d] = c->h.dmax[d] - 3.0 * cw * (1.0 + 1e-9);
+        c->P.inner_lo[d] = c->h.dmin[d] + m * cw * (1.0 + 1e-9);
+        c->P.inner_hi[d] = c->h.dmax[d] - m * cw * (1.0 + 1e-9);
     }
     // slab mode: owned subset, local window grid along the slab axis, array capacity
     std::vector<int> owned;

@@ -270,7 +270,8 @@ int dist_setup(MphCtx* c, const double* pos, std::vector<int>& owned)
     // local window grid along the slab axis: [lo - h - cw, hi + h + cw)
     const double wlo = D.g.lo - halo - cw, whi = D.g.hi + halo + cw;
     const int gloc = (int)std::ceil((whi - wlo) / cw);
-    if (gloc < 5) return ctx_fail(c, MPH_ERR_DOMAIN, "slab window narrower than 5 cells");
+    const int m = stencil_margin(c->P, axis);
+    if (gloc < 2 * m - 1) return ctx_fail(c, MPH_ERR_DOMAIN, "slab window narrower than the cell stencil");
     c->P.corg[axis] = wlo;
     c->P.slab_axis = axis;
     c->P.slab_lo = D.g.lo;
@@ -278,8 +279,8 @@ int dist_setup(MphCtx* c, const double* pos, std::vector<int>& owned)
     c->P.slab_h = halo;
     c->P.gc[axis] = std::min(gloc, c->P.gc[axis] + 1);
     // fast-path interior: >= 3 cells inside both the window and the periodic domain
-    c->P.inner_lo[axis] = std::max(wlo, h.dmin[axis]) + 3.0 * cw * (1.0 + 1e-9);
-    c->P.inner_hi[axis] = std::min(whi, h.dmax[axis]) - 3.0 * cw * (1.0 + 1e-9);
+    c->P.inner_lo[axis] = std::max(wlo, h.dmin[axis]) + m * cw * (1.0 + 1e-9);
+    c->P.inner_hi[axis] = std::min(whi, h.dmax[axis]) - m * cw * (1.0 + 1e-9);
     // initial owned set and a capacity for owned + ghosts (+ headroom for migration imbalance)
     owned.clear();
     size_t near = 0;

@@ -363,16 +363,21 @@ void fill_scalars(const HostDerived& h, const MphConfig& c, double* o)
     o[33] = h.cell_n[0]; o[34] = h.cell_n[1]; o[35] = h.cell_n[2];
 }
 
-// GPU linked-cell grid: cells of width >= rc/2 along every active axis so that a +-2-cell
-// stencil covers the acceptance sphere; the cell count divides the periodic width exactly.
-int choose_grid(const HostDerived& h, int dim, double rc, int gc[3], double ginv[3], std::string& err)
+// GPU linked-cell grid: cells of width >= rc/2 along the two outer axes (a +-2-cell stencil
+// covers the acceptance sphere) and >= rc/(2 sub) along the contiguous axis (z in 3-D, y in 2-D;
+// a +-2 sub stencil, scanned as one contiguous index range per column, so thinner cells there
+// only sharpen the cutoff trimming of each column).  Cell counts divide the periodic width
+// exactly; every axis needs enough cells that the stencil never visits a cell twice.
+int choose_grid(const HostDerived& h, int dim, double rc, int sub, int gc[3], double ginv[3], std::string& err)
 {
-    const double target = 0.5 * rc * (1.0 + 1e-6);
+    const int ca = dim == 3 ? 2 : 1;
     for (int d = 0; d < 3; ++d) {
         if (d == 2 && dim == 2) { gc[d] = 1; ginv[d] = 1.0 / h.dw[d]; continue; }
+        const int s = d == ca ? sub : 1;
+        const double target = 0.5 * rc / s * (1.0 + 1e-6);
         const int nc = (int)std::floor(h.dw[d] / target);
-        if (nc < 5) {
-            err = "domain axis " + std::to_string(d) + " narrower than 5 GPU cells (2.5 x cutoff)";
+        if (nc < 4 * s + 1) {
+            err = "domain axis " + std::to_string(d) + " narrower than 2.5 x cutoff";
             return MPH_ERR_DOMAIN;
         }
         gc[d] = nc;

@@ -22,7 +22,7 @@ struct StructureInit {
 
 void derive_constants(const MphConfig& c, HostDerived& h);
 void fill_scalars(const HostDerived& h, const MphConfig& c, double* out36);
-int choose_grid(const HostDerived& h, int dim, double rc, int gc[3], double ginv[3], std::string& err);
+int choose_grid(const HostDerived& h, int dim, double rc, int sub, int gc[3], double ginv[3], std::string& err);
 void make_dev_params(const MphConfig& c, const HostDerived& h, int n, int n_struct, DevParams& P);
 int build_structure(const MphConfig& c, const HostDerived& h, int n, const int* prop,
                     const double* pos0, StructureInit& S, std::string& err);

@@ -211,14 +211,33 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int* lds, int& total)
     return wsum + x - v;
 }
 
+// 16 consecutive counts of one thread: four 16-byte loads when the run is inside the array
+// (cell arrays are 16-int aligned per thread), element loads at the tail.
+__device__ __forceinline__ void load16(const int* __restrict__ a, int base, int n, int (&v)[kScanItems])
+{
+    if (base + kScanItems <= n) {
+        const int4* q = reinterpret_cast<const int4*>(a + base);
+#pragma unroll
+        for (int k = 0; k < kScanItems / 4; ++k) {
+            const int4 t = q[k];
+            v[4 * k] = t.x; v[4 * k + 1] = t.y; v[4 * k + 2] = t.z; v[4 * k + 3] = t.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kScanItems; ++k) v[k] = base + k < n ? a[base + k] : 0;
+    }
+}
+
 __global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const int* __restrict__ cnt, int ncell,
                                                               int* __restrict__ bsum)
 {
     __shared__ int lds[kScanThreads / 64];
     const int base = blockIdx.x * kScanBlock + threadIdx.x * kScanItems;
+    int v[kScanItems];
+    load16(cnt, base, ncell, v);
     int s = 0;
 #pragma unroll
-    for (int k = 0; k < kScanItems; ++k) s += (base + k < ncell) ? cnt[base + k] : 0;
+    for (int k = 0; k < kScanItems; ++k) s += v[k];
     int total;
     block_exclusive_scan(s, lds, total);
     if (threadIdx.x == 0) bsum[blockIdx.x] = total;
@@ -250,21 +269,33 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_down(int* __restrict__ cn
     __shared__ int lds[kScanThreads / 64];
     const int base = blockIdx.x * kScanBlock + threadIdx.x * kScanItems;
     int v[kScanItems];
+    load16(cnt, base, ncell, v);
     int s = 0;
 #pragma unroll
-    for (int k = 0; k < kScanItems; ++k) {
-        v[k] = (base + k < ncell) ? cnt[base + k] : 0;
-        s += v[k];
-    }
+    for (int k = 0; k < kScanItems; ++k) s += v[k];
     int total;
     int run = block_exclusive_scan(s, lds, total) + bsum[blockIdx.x];
+    int o[kScanItems];
 #pragma unroll
     for (int k = 0; k < kScanItems; ++k) {
-        if (base + k < ncell) {
-            start[base + k] = run;
-            cnt[base + k] = 0;   // histogram ready for the next step
-        }
+        o[k] = run;
         run += v[k];
+    }
+    if (base + kScanItems <= ncell) {
+        int4* st = reinterpret_cast<int4*>(start + base);
+        int4* ct = reinterpret_cast<int4*>(cnt + base);
+#pragma unroll
+        for (int k = 0; k < kScanItems / 4; ++k) {
+            st[k] = make_int4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+            ct[k] = make_int4(0, 0, 0, 0);   // histogram ready for the next step
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kScanItems; ++k)
+            if (base + k < ncell) {
+                start[base + k] = o[k];
+                cnt[base + k] = 0;
+            }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) start[ncell] = n;
 }
@@ -448,8 +479,8 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
             base = (FAST ? cx + dxc : wrap_cell(cx + dxc, P.gc[0])) * P.gc[1];
         }
         const double ra = sqrt(rcm2 - d2);
-        const int lo = (int)fmax(floor((ua - ra) * ginva), (double)(cca - 2));
-        const int hi = (int)fmin(floor((ua + ra) * ginva), (double)(cca + 2));
+        const int lo = (int)fmax(floor((ua - ra) * ginva), (double)(cca - P.sa));
+        const int hi = (int)fmin(floor((ua + ra) * ginva), (double)(cca + P.sa));
         int seg_a[2], seg_b[2], nseg;
         if (FAST) { seg_a[0] = lo; seg_b[0] = hi; seg_a[1] = 0; seg_b[1] = -1; nseg = 1; }
         else if (lo < 0) { seg_a[0] = lo + gca; seg_b[0] = gca - 1; seg_a[1] = 0; seg_b[1] = hi; nseg = 2; }

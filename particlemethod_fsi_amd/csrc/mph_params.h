@@ -11,6 +11,7 @@ namespace mph {
 constexpr int kTypes = MPH_TYPE_COUNT;
 constexpr int kMaxNeighbor = MPH_MAX_NEIGHBOR_COUNT;
 constexpr int kTile = 64;  // ELL neighbour-list tile = one wavefront of i-particles
+constexpr int kContigSub = 2;   // cells along the contiguous axis are 1/kContigSub as wide
 
 inline bool is_fluid(int t) { return t >= 0 && t < 2; }   // main.cpp:69-70
 inline bool is_struct(int t) { return t >= 2 && t < 4; }  // main.cpp:71-72
@@ -28,6 +29,7 @@ struct DevParams {
     int gc[3];         // GPU linked-cell grid (gc[2] == 1 in 2-D)
     int ncell;         // gc[0]*gc[1]*gc[2]
     int substeps;      // (int)(Dt/Elastic_Dt + 0.5), main.cpp:653
+    int sa;            // stencil half-width (cells) along the contiguous axis (2 * kContigSub)
     int fast_ok;       // every active axis has > 12 GPU cells: interior waves may skip the
                        // periodic branch of the minimum image (see k_neighbors)
     double inner_lo[3], inner_hi[3];   // interior box: >= 3 GPU cells from every periodic face
