@@ -67,7 +67,7 @@ struct MphCtx {
     int *key = nullptr, *slot = nullptr, *tmp = nullptr, *cnt = nullptr, *start = nullptr, *bsum = nullptr;
     int *nbr = nullptr, *ncount = nullptr;
     double *pres = nullptr, *gx = nullptr, *gy = nullptr, *gz = nullptr, *pa = nullptr;
-    double4 *force = nullptr, *acc = nullptr;
+    double4 *force = nullptr, *acc = nullptr, *fpart = nullptr, *rec = nullptr;
     double *dens_a = nullptr, *vstrain = nullptr, *divp = nullptr;
     mph::StructDev Sd;
     std::vector<void*> allocs;

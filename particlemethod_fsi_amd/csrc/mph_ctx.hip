@@ -67,7 +67,7 @@ void ctx_fill_launch(MphCtx* c)
     L.key = c->key; L.slot = c->slot; L.tmp = c->tmp; L.cnt = c->cnt; L.start = c->start; L.bsum = c->bsum;
     L.nbr = c->nbr; L.ncount = c->ncount;
     L.pres = c->pres; L.gx = c->gx; L.gy = c->gy; L.gz = c->gz; L.pa = c->pa;
-    L.force = c->force; L.acc = c->acc;
+    L.force = c->force; L.acc = c->acc; L.fpart = c->fpart; L.rec = c->rec;
     L.dens_a = c->dens_a; L.vstrain = c->vstrain; L.divp = c->divp;
     L.S = &c->Sd;
 }
@@ -294,6 +294,7 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         CK(dalloc(c, &s->vx, cap)); CK(dalloc(c, &s->vy, cap)); CK(dalloc(c, &s->vz, cap));
         CK(dalloc(c, &s->type, cap)); CK(dalloc(c, &s->id, cap));
     }
+    CK(dalloc(c, &c->A.pt, cap)); CK(dalloc(c, &c->A.pv, cap));
     CK(dalloc(c, &c->rank_of, cap));
     CK(dalloc(c, &c->key, cap)); CK(dalloc(c, &c->slot, cap)); CK(dalloc(c, &c->tmp, cap));
     CK(dalloc(c, &c->cnt, c->P.ncell)); CK(dalloc(c, &c->start, (size_t)c->P.ncell + 1));
@@ -301,6 +302,7 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     CK(dalloc(c, &c->nbr, ntile * kTile * kMaxNeighbor)); CK(dalloc(c, &c->ncount, cap));
     CK(dalloc(c, &c->pres, cap)); CK(dalloc(c, &c->gx, cap)); CK(dalloc(c, &c->gy, cap)); CK(dalloc(c, &c->gz, cap));
     CK(dalloc(c, &c->pa, cap)); CK(dalloc(c, &c->force, cap)); CK(dalloc(c, &c->acc, cap));
+    CK(dalloc(c, &c->fpart, cap)); CK(dalloc(c, &c->rec, cap));
     CK(dalloc(c, &c->dens_a, cap)); CK(dalloc(c, &c->vstrain, cap)); CK(dalloc(c, &c->divp, cap));
     HIP_OK(c, hipMemsetAsync(c->cnt, 0, sizeof(int) * c->P.ncell, c->stream));
     HIP_OK(c, hipMemsetAsync(c->force, 0, sizeof(double4) * std::max(cap, 1), c->stream));

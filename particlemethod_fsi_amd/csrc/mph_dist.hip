@@ -198,6 +198,7 @@ HaloFields halo_fields(MphCtx* c)
     HaloFields F{};
     F.f[0] = c->pres;
     F.nf = 1;
+    F.rec = c->rec;
     if (c->P.surface) {
         F.f[1] = c->gx; F.f[2] = c->gy; F.f[3] = c->gz; F.f[4] = c->pa;
         F.nf = 5;

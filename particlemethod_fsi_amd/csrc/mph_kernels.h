@@ -43,6 +43,11 @@ struct Soa {
     double *x = nullptr, *y = nullptr, *z = nullptr;
     double *vx = nullptr, *vy = nullptr, *vz = nullptr;
     int *type = nullptr, *id = nullptr;
+    // gather records of the sorted set A (null for B/C): {x, y, z, type} and {vx, vy, vz, 0}.
+    // A neighbour's fields then arrive with two 16-byte loads per record instead of one 8-byte
+    // load per field: the neighbour loops are bound by the number of gather instructions
+    // (profiles/r01: pass B 0.46 ms with 4 SoA loads vs 0.38 ms with one 32-byte record).
+    double4 *pt = nullptr, *pv = nullptr;
 };
 
 // Everything one launch sequence needs.
@@ -61,6 +66,8 @@ struct Launch {
     // pass A products (A order): pressure values, gravity centre (GC, PressureA), sums
     double *pres = nullptr, *gx = nullptr, *gy = nullptr, *gz = nullptr, *pa = nullptr;
     double *dens_a = nullptr, *vstrain = nullptr, *divp = nullptr;
+    double4 *fpart = nullptr;   // pass A: P_i half of the pressure force + viscous force
+    double4 *rec = nullptr;     // pass A: {x, y, z, PressureP}, the pass-B gather record
     double4 *force = nullptr, *acc = nullptr;   // outputs (A order)
     const StructDev* S = nullptr;
 };
@@ -75,6 +82,7 @@ void launch_structure(const Launch& L);
 struct HaloFields {
     double* f[5];
     int nf;
+    double4* rec;   // f[0] (PressureP) is also the .w of the pass-B record
 };
 void launch_scan(int* cnt, int ncell, int* bsum, int* start, int total, hipStream_t stream, Profiler* prof);
 int dist_blocks(int n);

@@ -33,6 +33,17 @@
 #include "mph_kernels.h"
 #include "mph_params.h"
 
+// Tuning switches (A/B builds: tools/ab.sh): pass A gathers from the AoS records of A (1) or from
+// the SoA arrays (0); the search reads its candidates from the SoA arrays (0) or the records (1);
+// batch widths of the pass-A / pass-B neighbour loops (MPH_UA / MPH_UB below).  Defaults are the
+// D1M measurements of profiles/r01.
+#ifndef MPH_AOS_GATHER
+#define MPH_AOS_GATHER 1
+#endif
+#ifndef MPH_AOS_SEARCH
+#define MPH_AOS_SEARCH 0
+#endif
+
 namespace mph {
 
 // ------------------------------------------------------------------------------ helpers ------
@@ -345,6 +356,10 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
     A.type[dst] = B.type[p];
     const int id = B.id[p];
     A.id[dst] = id;
+    if (A.pt) {
+        A.pt[dst] = make_double4(B.x[p], B.y[p], B.z[p], (double)B.type[p]);
+        A.pv[dst] = make_double4(B.vx[p], B.vy[p], B.vz[p], 0.0);
+    }
     if (dst_of) dst_of[p] = dst;   // slab mode: ids are global (ghosts negative)
     else rank_of[id] = dst;
 }
@@ -353,21 +368,34 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
 
 struct PassA {
     double da = 0.0, g0 = 0.0, g1 = 0.0, g2 = 0.0, vs = 0.0, dv = 0.0;
+    // force sums that need no pass-A value of j: S = sum_j [r<RP] dwp(r)/r V q_ij (the P_i half
+    // of calculatePressureP's (P_i+P_j) term, 2394-2424) and the viscous force (2478-2522)
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, v0 = 0.0, v1 = 0.0, v2 = 0.0;
 };
 
 // One neighbour's contribution to DensityA (2141-2171), GravityCenter (2174-2210), DensityP
-// (2314-2341) and DivergenceP (2343-2379); (dvx, dvy, dvz) = v_j - v_i.
-__device__ __forceinline__ void pass_a_term(const DevParams& P, const double* s_ratio, int ti, int tj, bool solid,
-                                            double q0, double q1, double q2, double r2, double dvx, double dvy,
-                                            double dvz, PassA& o)
+// (2314-2341), DivergenceP (2343-2379), and (FORCE) the P_i half of the pressure force and the
+// viscous force; (dvx, dvy, dvz) = v_j - v_i.
+template <bool FORCE>
+__device__ __forceinline__ void pass_a_term(const DevParams& P, const double* s_ratio, const double* s_mu, int ti,
+                                            int tj, bool solid, double q0, double q1, double q2, double r2,
+                                            double dvx, double dvy, double dvz, PassA& o)
 {
     double r, ir;
     rsqrt_pair(r2, r, ir);
+    const double dot = dvx * q0 + dvy * q1 + dvz * q2;
     if (r2 <= P.rp2) {
         const double omt = 1.0 - r * P.inv_rp;
         o.vs += P.cp * omt * omt;
-        const double dot = dvx * q0 + dvy * q1 + dvz * q2;
         o.dv -= dot * ir * (P.cdp * omt);
+        // strict test of the force loops (2402), and structure i sees only non-structure j
+        // (InterfaceForce 2439-2472)
+        if (FORCE && r2 < P.rp2 && !(solid && dev_is_struct(tj))) {
+            const double c = P.cdp * omt * ir * P.vol;
+            o.s0 += c * q0;
+            o.s1 += c * q1;
+            o.s2 += c * q2;
+        }
     }
     if (!solid) {
         const double ratio = s_ratio[ti * kTypes + tj];
@@ -383,17 +411,27 @@ __device__ __forceinline__ void pass_a_term(const DevParams& P, const double* s_
             o.g1 += q1 * w;
             o.g2 += q2 * w;
         }
+        if (FORCE && r2 < P.rv2) {
+            const double dwij = -P.cdv * (1.0 - r * P.inv_rv);
+            const double c = P.cvis * s_mu[ti * kTypes + tj] * dot * dwij * (ir * ir * ir) * P.vol;
+            o.v0 += c * q0;
+            o.v1 += c * q1;
+            o.v2 += c * q2;
+        }
     }
 }
 
 // Epilogue: PhysicalCoefficients (2099-2137) and the pressure values of calculatePressureP
-// (2384-2392) and calculatePressureA (2218-2223).
+// (2384-2392) and calculatePressureA (2218-2223); with fpart, the neighbour-independent part of
+// the force P_i S_i + viscous force, and the pass-B gather record {x, y, z, P}.
 struct PassAOut {
     double *pres, *gx, *gy, *gz, *pa, *dens_a, *vstrain, *divp;
+    double4 *fpart, *rec;
 };
 
 __device__ __forceinline__ void pass_a_finish(const DevParams& P, const DevTables* T, int ti, int i,
-                                              const PassA& o, const PassAOut& out)
+                                              const PassA& o, const PassAOut& out, double xi = 0.0,
+                                              double yi = 0.0, double zi = 0.0)
 {
     const double vstr = o.vs - P.n0p;
     const double kappa = vstr < 0.0 ? 0.0 : T->bulk[ti];
@@ -409,6 +447,10 @@ __device__ __forceinline__ void pass_a_finish(const DevParams& P, const DevTable
     out.dens_a[i] = o.da;
     out.vstrain[i] = vstr;
     out.divp[i] = o.dv;
+    if (out.fpart) {
+        out.fpart[i] = make_double4(p * o.s0 + o.v0, p * o.s1 + o.v1, p * o.s2 + o.v2, 0.0);
+        out.rec[i] = make_double4(xi, yi, zi, p);
+    }
 }
 
 // ---------------------------------------------------------------------- neighbour search ----
@@ -422,6 +464,7 @@ __device__ __forceinline__ void pass_a_finish(const DevParams& P, const DevTable
 // read and gathers.
 struct FuseA {
     const double* s_ratio;
+    const double* s_mu;
     int ti;
     bool solid;
     double vxi, vyi, vzi;
@@ -496,9 +539,14 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int j = j0 + u < je ? j0 + u : je - 1;
-                    xs[u] = A.x[j];
-                    ys[u] = A.y[j];
-                    zs[u] = A.z[j];
+                    if (MPH_AOS_SEARCH) {
+                        const double4 t = A.pt[j];
+                        xs[u] = t.x; ys[u] = t.y; zs[u] = t.z;
+                    } else {
+                        xs[u] = A.x[j];
+                        ys[u] = A.y[j];
+                        zs[u] = A.z[j];
+                    }
                 }
                 double q0[4], q1[4], q2[4], r2[4];
                 bool acc[4];
@@ -526,7 +574,7 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
 #pragma unroll
                     for (int u = 0; u < 4; ++u)
                         if (acc[u])
-                            pass_a_term(P, F.s_ratio, F.ti, tj[u], F.solid, q0[u], q1[u], q2[u], r2[u],
+                            pass_a_term<true>(P, F.s_ratio, F.s_mu, F.ti, tj[u], F.solid, q0[u], q1[u], q2[u], r2[u],
                                         vx[u] - F.vxi, vy[u] - F.vyi, vz[u] - F.vzi, o);
                 }
 #pragma unroll
@@ -549,8 +597,12 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, const DevTables*
                                                    PassAOut pout)
 {
     __shared__ double s_ratio[kTypes * kTypes];
+    __shared__ double s_mu[kTypes * kTypes];
     if (FUSE) {
-        if (threadIdx.x < kTypes * kTypes) s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
+        if (threadIdx.x < kTypes * kTypes) {
+            s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
+            s_mu[threadIdx.x] = T->mu_ij[threadIdx.x];
+        }
         __syncthreads();
     }
     const int i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
@@ -568,6 +620,7 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, const DevTables*
         PassA o;
         if (FUSE) {
             F.s_ratio = s_ratio;
+            F.s_mu = s_mu;
             F.ti = A.type[i];
             F.solid = dev_is_struct(F.ti);
             F.vxi = A.vx[i]; F.vyi = A.vy[i]; F.vzi = A.vz[i];
@@ -575,7 +628,7 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, const DevTables*
         cnt = fast ? scan_candidates<DIM, true, FUSE>(P, A, start, i, xi, yi, zi, cx, cy, cz, out, F, o)
                    : scan_candidates<DIM, false, FUSE>(P, A, start, i, xi, yi, zi, cx, cy, cz, out, F, o);
         ncount[i] = cnt;
-        if (FUSE) pass_a_finish(P, T, F.ti, i, o, pout);
+        if (FUSE) pass_a_finish(P, T, F.ti, i, o, pout, xi, yi, zi);
     }
     // wave reduction of the statistics (mean/max neighbours, overflow flag)
     int mx = cnt;
@@ -601,10 +654,11 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, const DevTables*
 #define MPH_UA 8
 #endif
 #ifndef MPH_UB
-#define MPH_UB 4
+#define MPH_UB 8
 #endif
 template <bool FAST, int DIM, int U = MPH_UA>
-__device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_ratio, const Soa& A,
+__device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_ratio, const double* s_mu,
+                                            const Soa& A,
                                             const int* row, int cnt, int ti, bool solid, double xi,
                                             double yi, double zi, double vxi, double vyi, double vzi,
                                             PassA& o)
@@ -617,9 +671,15 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
         for (int u = 0; u < U; ++u) jj[u] = row[(k0 + u < cnt ? k0 + u : cnt - 1) * kTile];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            X[u] = A.x[jj[u]]; Y[u] = A.y[jj[u]]; Z[u] = A.z[jj[u]];
-            VX[u] = A.vx[jj[u]]; VY[u] = A.vy[jj[u]]; VZ[u] = A.vz[jj[u]];
-            TT[u] = A.type[jj[u]];
+            if (MPH_AOS_GATHER) {
+                const double4 t = A.pt[jj[u]], v = A.pv[jj[u]];
+                X[u] = t.x; Y[u] = t.y; Z[u] = t.z; TT[u] = (int)t.w;
+                VX[u] = v.x; VY[u] = v.y; VZ[u] = v.z;
+            } else {
+                X[u] = A.x[jj[u]]; Y[u] = A.y[jj[u]]; Z[u] = A.z[jj[u]];
+                VX[u] = A.vx[jj[u]]; VY[u] = A.vy[jj[u]]; VZ[u] = A.vz[jj[u]];
+                TT[u] = A.type[jj[u]];
+            }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -627,19 +687,31 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
             const double q0 = image_exact<FAST>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
             const double q1 = image_exact<FAST>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
             const double q2 = image_exact<FAST || DIM == 2>(Z[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
-            pass_a_term(P, s_ratio, ti, TT[u], solid, q0, q1, q2, r2_exact(q0, q1, q2), VX[u] - vxi,
-                        VY[u] - vyi, VZ[u] - vzi, o);
+            pass_a_term<true>(P, s_ratio, s_mu, ti, TT[u], solid, q0, q1, q2, r2_exact(q0, q1, q2), VX[u] - vxi,
+                              VY[u] - vyi, VZ[u] - vzi, o);
         }
     }
 }
 
+#ifndef MPH_PA_WPE
+#define MPH_PA_WPE 0
+#endif
+#if MPH_PA_WPE
+#define MPH_PA_ATTR __attribute__((amdgpu_waves_per_eu(MPH_PA_WPE)))
+#else
+#define MPH_PA_ATTR
+#endif
 template <int DIM>
-__global__ __launch_bounds__(256) void k_pass_a(DevParams P, const DevTables* __restrict__ T, Soa A,
+__global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const DevTables* __restrict__ T, Soa A,
                                                 const int* __restrict__ nbr,
                                                 const int* __restrict__ ncount, PassAOut pout)
 {
     __shared__ double s_ratio[kTypes * kTypes];
-    if (threadIdx.x < kTypes * kTypes) s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
+    __shared__ double s_mu[kTypes * kTypes];
+    if (threadIdx.x < kTypes * kTypes) {
+        s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
+        s_mu[threadIdx.x] = T->mu_ij[threadIdx.x];
+    }
     __syncthreads();
     const int i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     const bool live = i < P.n;
@@ -653,84 +725,94 @@ __global__ __launch_bounds__(256) void k_pass_a(DevParams P, const DevTables* __
     const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
     const int* row = ell_row(nbr, i);
     PassA o;
-    if (fast) pass_a_loop<true, DIM>(P, s_ratio, A, row, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
-    else pass_a_loop<false, DIM>(P, s_ratio, A, row, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
-    pass_a_finish(P, T, ti, i, o, pout);
+    if (fast) pass_a_loop<true, DIM>(P, s_ratio, s_mu, A, row, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+    else pass_a_loop<false, DIM>(P, s_ratio, s_mu, A, row, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+    pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
 }
 
 // ---------------------------------------------------------------------------- pass B -------
 
+// Pass B needs, per neighbour, only what pass A could not know: P_j (and, with surface tension,
+// GC_j and PA_j).  The P_i half of the pressure force and the viscous force were summed in pass A
+// (fpart), so the default gather per neighbour is one 32-byte record {x, y, z, P} (MPH_PB_REC=1)
+// or four SoA doubles (MPH_PB_REC=0); the type of j only for structure i (InterfaceForce) or
+// surface tension.
+#ifndef MPH_PB_REC
+#define MPH_PB_REC 1
+#endif
 template <bool FAST, bool SURF, int DIM, int U = MPH_UB>
-__device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_ratio, const double* s_mu,
-                                            const Soa& A, const double* pres, const double* gx,
+__device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_ratio, const Soa& A,
+                                            const double4* rec, const double* pres, const double* gx,
                                             const double* gy, const double* gz, const double* pa,
                                             const int* row, int cnt, int ti, bool solid, double xi,
-                                            double yi, double zi, double vxi, double vyi, double vzi,
-                                            double pi, double gxi, double gyi, double gzi, double pai,
-                                            double ai, double& f0, double& f1, double& f2)
+                                            double yi, double zi, double gxi, double gyi, double gzi,
+                                            double pai, double ai, double& f0, double& f1, double& f2)
 {
     const double dscale = P.rg / P.r2g * (P.vol / P.dx);
+    const double cpv = P.cdp * P.vol;
     for (int k0 = 0; k0 < cnt; k0 += U) {
         int jj[U];
-        double X[U], Y[U], Z[U], VX[U], VY[U], VZ[U], PJ[U];
+        double X[U], Y[U], Z[U], PJ[U];
         int TT[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) jj[u] = row[(k0 + u < cnt ? k0 + u : cnt - 1) * kTile];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            X[u] = A.x[jj[u]]; Y[u] = A.y[jj[u]]; Z[u] = A.z[jj[u]];
-            VX[u] = A.vx[jj[u]]; VY[u] = A.vy[jj[u]]; VZ[u] = A.vz[jj[u]];
-            PJ[u] = pres[jj[u]];
-            TT[u] = A.type[jj[u]];
+            if (MPH_PB_REC) {
+                const double4 r4 = rec[jj[u]];
+                X[u] = r4.x; Y[u] = r4.y; Z[u] = r4.z; PJ[u] = r4.w;
+            } else {
+                X[u] = A.x[jj[u]]; Y[u] = A.y[jj[u]]; Z[u] = A.z[jj[u]];
+                PJ[u] = pres[jj[u]];
+            }
+            TT[u] = (SURF || solid) ? A.type[jj[u]] : 0;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
         if (k0 + u >= cnt) break;
-        const int j = jj[u];
         const int tj = TT[u];
         if (solid && dev_is_struct(tj)) continue;
         const double q0 = image_exact<FAST>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
         const double q1 = image_exact<FAST>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
         const double q2 = image_exact<FAST || DIM == 2>(Z[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
         const double r2 = r2_exact(q0, q1, q2);
-        const double pj = PJ[u];
+        if (!SURF || solid) {
+            if (r2 < P.rp2) {
+                double r, ir;
+                rsqrt_pair(r2, r, ir);
+                const double c = PJ[u] * (cpv * (1.0 - r * P.inv_rp)) * ir;
+                f0 += c * q0;
+                f1 += c * q1;
+                f2 += c * q2;
+            }
+            continue;
+        }
+        const int j = jj[u];
         double r, ir;
         rsqrt_pair(r2, r, ir);
         double c = 0.0;
-        if (r2 < P.rp2) {
-            const double dw = P.cdp * (1.0 - r * P.inv_rp);
-            c += (pi + pj) * dw * ir * P.vol;
+        if (r2 < P.rp2) c += PJ[u] * (cpv * (1.0 - r * P.inv_rp)) * ir;
+        const double rij = s_ratio[ti * kTypes + tj];
+        const double rji = s_ratio[tj * kTypes + ti];
+        const double gxj = gx[j], gyj = gy[j], gzj = gz[j], paj = pa[j];
+        if (r2 < P.ra2) {
+            const double t = r * P.inv_ra;
+            const double dwa = P.cda * (1.0 - t) * (1.0 - 3.0 * t);
+            c += (pai * rij + paj * rji) * dwa * ir * P.vol;
         }
-        if (!solid) {
-            if (SURF) {
-                const double rij = s_ratio[ti * kTypes + tj];
-                const double rji = s_ratio[tj * kTypes + ti];
-                const double gxj = gx[j], gyj = gy[j], gzj = gz[j], paj = pa[j];
-                if (r2 < P.ra2) {
-                    const double t = r * P.inv_ra;
-                    const double dwa = P.cda * (1.0 - t) * (1.0 - 3.0 * t);
-                    c += (pai * rij + paj * rji) * dwa * ir * P.vol;
-                }
-                if (r2 < P.rg2) {
-                    const double omt = 1.0 - r * P.inv_rg;
-                    const double wg = P.cg * omt * omt;
-                    const double dwg = P.cdg * omt;
-                    const double wij = rij * wg, wji = rji * wg;
-                    f0 -= (ai * gxj * wji - ai * gxi * wij) * dscale;
-                    f1 -= (ai * gyj * wji - ai * gyi * wij) * dscale;
-                    f2 -= (ai * gzj * wji - ai * gzi * wij) * dscale;
-                    const double dwij = rij * dwg, dwji = rji * dwg;
-                    const double gr = (ai * gxj * dwji - ai * gxi * dwij) * q0 +
-                                      (ai * gyj * dwji - ai * gyi * dwij) * q1 +
-                                      (ai * gzj * dwji - ai * gzi * dwij) * q2;
-                    c -= gr * ir * dscale;
-                }
-            }
-            if (r2 < P.rv2) {
-                const double dwij = -P.cdv * (1.0 - r * P.inv_rv);
-                const double dot = (VX[u] - vxi) * q0 + (VY[u] - vyi) * q1 + (VZ[u] - vzi) * q2;
-                c += P.cvis * s_mu[ti * kTypes + tj] * dot * dwij * (ir * ir * ir) * P.vol;
-            }
+        if (r2 < P.rg2) {
+            const double omt = 1.0 - r * P.inv_rg;
+            const double wg = P.cg * omt * omt;
+            const double dwg = P.cdg * omt;
+            const double wij = rij * wg, wji = rji * wg;
+            f0 -= (ai * gxj * wji - ai * gxi * wij) * dscale;
+            f1 -= (ai * gyj * wji - ai * gyi * wij) * dscale;
+            f2 -= (ai * gzj * wji - ai * gzi * wij) * dscale;
+            const double dwij = rij * dwg, dwji = rji * dwg;
+            const double gr = (ai * gxj * dwji - ai * gxi * dwij) * q0 +
+                              (ai * gyj * dwji - ai * gyi * dwij) * q1 +
+                              (ai * gzj * dwji - ai * gzi * dwij) * q2;
+            c -= gr * ir * dscale;
         }
         f0 += c * q0;
         f1 += c * q1;
@@ -741,9 +823,12 @@ __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_
 
 // Pair forces of PressureP (2394-2424), PressureA (2225-2258), DiffuseInterface (2261-2312),
 // ViscosityV (2478-2522) for non-structure i; InterfaceForce (2439-2472) for structure i; then
-// Gravity (2917-2936), Acceleration/kick (2938-2956) and Convection/drift (1892-1907).
+// Gravity (2917-2936), Acceleration/kick (2938-2956) and Convection/drift (1892-1907).  The sums
+// start from pass A's fpart (P_i half of the pressure force + viscous force).
 template <bool SURF, int DIM>
 __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __restrict__ T, Soa A,
+                                                const double4* __restrict__ rec,
+                                                const double4* __restrict__ fpart,
                                                 const double* __restrict__ pres,
                                                 const double* __restrict__ gx,
                                                 const double* __restrict__ gy,
@@ -755,12 +840,10 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
                                                 Soa B, int phase)
 {
     __shared__ double s_ratio[kTypes * kTypes];
-    __shared__ double s_mu[kTypes * kTypes];
-    if (threadIdx.x < kTypes * kTypes) {
-        s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
-        s_mu[threadIdx.x] = T->mu_ij[threadIdx.x];
+    if (SURF) {
+        if (threadIdx.x < kTypes * kTypes) s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
+        __syncthreads();
     }
-    __syncthreads();
     const int i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     const int ii = i < P.n ? i : P.n - 1;
     const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
@@ -774,24 +857,24 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
     }
     const bool fast = wave_interior(P, live, xi, yi, zi);
     if (!live) return;
-    const double vxi = A.vx[i], vyi = A.vy[i], vzi = A.vz[i];
-    const double pi = pres[i];
     const int ti = A.type[i];
     const bool solid = dev_is_struct(ti);
     const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
     const int* row = ell_row(nbr, i);
-    double f0 = 0.0, f1 = 0.0, f2 = 0.0;
+    const double4 fp = fpart[i];
+    double f0 = fp.x, f1 = fp.y, f2 = fp.z;
     double gxi = 0.0, gyi = 0.0, gzi = 0.0, pai = 0.0, ai = 0.0;
     if (SURF) {
         gxi = gx[i]; gyi = gy[i]; gzi = gz[i]; pai = pa[i];
         ai = T->cofa[ti] * P.cofk * P.cofk;
     }
     if (fast)
-        pass_b_loop<true, SURF, DIM>(P, s_ratio, s_mu, A, pres, gx, gy, gz, pa, row, cnt, ti, solid, xi,
-                                     yi, zi, vxi, vyi, vzi, pi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
+        pass_b_loop<true, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, row, cnt, ti, solid, xi, yi, zi,
+                                     gxi, gyi, gzi, pai, ai, f0, f1, f2);
     else
-        pass_b_loop<false, SURF, DIM>(P, s_ratio, s_mu, A, pres, gx, gy, gz, pa, row, cnt, ti, solid, xi,
-                                      yi, zi, vxi, vyi, vzi, pi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
+        pass_b_loop<false, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, row, cnt, ti, solid, xi, yi, zi,
+                                      gxi, gyi, gzi, pai, ai, f0, f1, f2);
+    const double vxi = A.vx[i], vyi = A.vy[i], vzi = A.vz[i];
     double vo0 = vxi, vo1 = vyi, vo2 = vzi;
     double xo0 = xi, xo1 = yi, xo2 = zi;
     double4 ao = make_double4(0.0, 0.0, 0.0, 0.0);
@@ -1150,6 +1233,7 @@ __global__ __launch_bounds__(256) void k_halo_unpack(const double* __restrict__ 
     if (k >= m) return;
     const int a = dst_of[k < n1 ? o1 + k : o2 + (k - n1)];
     for (int f = 0; f < F.nf; ++f) F.f[f][a] = buf[(size_t)f * m + k];
+    if (F.rec) F.rec[a].w = buf[k];
 }
 
 // ---------------------------------------------------------------------------- launchers -----
@@ -1209,7 +1293,7 @@ static bool fused_pass_a()
 
 static PassAOut pass_a_out(const Launch& L)
 {
-    return PassAOut{L.pres, L.gx, L.gy, L.gz, L.pa, L.dens_a, L.vstrain, L.divp};
+    return PassAOut{L.pres, L.gx, L.gy, L.gz, L.pa, L.dens_a, L.vstrain, L.divp, L.fpart, L.rec};
 }
 
 void launch_neighbors(const Launch& L)
@@ -1250,7 +1334,7 @@ void launch_pass_b(const Launch& L, int phase)
     if (P.n == 0) return;
 #define MPH_PASS_B(S, D)                                                                            \
     MPH_LAUNCH("pass_b", L.stream, (k_pass_b<S, D>), dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, \
-               L.T, L.A, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, L.force, L.acc, L.B, phase)
+               L.T, L.A, L.rec, L.fpart, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, L.force, L.acc, L.B, phase)
     if (P.surface) {
         if (P.dim == 3) MPH_PASS_B(true, 3); else MPH_PASS_B(true, 2);
     } else {
