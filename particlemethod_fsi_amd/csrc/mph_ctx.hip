@@ -290,9 +290,10 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     CK(dalloc(c, &c->dT, 1));
     CK(dalloc(c, &c->dst, 1));
     for (Soa* s : {&c->A, &c->B}) {
-        CK(dalloc(c, &s->x, cap)); CK(dalloc(c, &s->y, cap)); CK(dalloc(c, &s->z, cap));
-        CK(dalloc(c, &s->vx, cap)); CK(dalloc(c, &s->vy, cap)); CK(dalloc(c, &s->vz, cap));
-        CK(dalloc(c, &s->type, cap)); CK(dalloc(c, &s->id, cap));
+        const size_t m = (size_t)cap + kPad;
+        CK(dalloc(c, &s->x, m)); CK(dalloc(c, &s->y, m)); CK(dalloc(c, &s->z, m));
+        CK(dalloc(c, &s->vx, m)); CK(dalloc(c, &s->vy, m)); CK(dalloc(c, &s->vz, m));
+        CK(dalloc(c, &s->type, m)); CK(dalloc(c, &s->id, m));
     }
     CK(dalloc(c, &c->A.pt, cap)); CK(dalloc(c, &c->A.pv, cap));
     CK(dalloc(c, &c->rank_of, cap));
@@ -644,10 +645,14 @@ int mph_neighbor_stats(MphCtx* c, double* mean, int* mx)
 {
     if (!c || !mean || !mx) return MPH_ERR_ARG;
     HIP_OK(c, hipSetDevice(c->device));
-    DevState hs;
-    HIP_OK(c, hipMemcpy(&hs, c->dst, sizeof(DevState), hipMemcpyDeviceToHost));
-    *mean = c->n ? (double)hs.sum_count / c->n : 0.0;
-    *mx = hs.max_count;
+    // NeighborCount of the particles held here (slab mode: owned + ghosts), reduced on the host
+    std::vector<int> h(c->n);
+    if (c->n) HIP_OK(c, hipMemcpy(h.data(), c->ncount, sizeof(int) * c->n, hipMemcpyDeviceToHost));
+    long long sum = 0;
+    int m = 0;
+    for (int v : h) { sum += v; m = v > m ? v : m; }
+    *mean = c->n ? (double)sum / c->n : 0.0;
+    *mx = m;
     return MPH_OK;
 }
 

@@ -34,17 +34,32 @@
 #include "mph_params.h"
 
 // Tuning switches (A/B builds: tools/ab.sh): pass A gathers from the AoS records of A (1) or from
-// the SoA arrays (0); the search reads its candidates from the SoA arrays (0) or the records (1);
+// the SoA arrays (0); the search of interior waves stages each stencil column's candidates in LDS
+// (1) or gathers them per lane from global memory (0);
 // batch widths of the pass-A / pass-B neighbour loops (MPH_UA / MPH_UB below).  Defaults are the
 // D1M measurements of profiles/r01.
 #ifndef MPH_AOS_GATHER
 #define MPH_AOS_GATHER 1
 #endif
-#ifndef MPH_AOS_SEARCH
-#define MPH_AOS_SEARCH 0
+#ifndef MPH_DIAG_SEARCH
+#define MPH_DIAG_SEARCH 0   // diagnostic builds only: 1 = stage but test nothing, 2 = no staging,
+                            // 4 = waves near a periodic face do nothing
+#endif
+#ifndef MPH_DIAG_NOSTORE
+#define MPH_DIAG_NOSTORE 0   // diagnostic builds only: the search counts but stores no list
+#endif
+#ifndef MPH_SB
+#define MPH_SB 4   // candidates per batch in the search
+#endif
+#ifndef MPH_SEARCH_LDS
+#define MPH_SEARCH_LDS 1
+#endif
+#ifndef MPH_LDS_CAP
+#define MPH_LDS_CAP 192   // candidates staged per wave and stencil column
 #endif
 
 namespace mph {
+
 
 // ------------------------------------------------------------------------------ helpers ------
 
@@ -312,7 +327,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_down(int* __restrict__ cn
 }
 
 // Unordered placement; block 0 also advances Time and WallCenter (main.cpp:685, 3066-3070)
-// after k_prep consumed them, and clears the neighbour statistics of the coming search.
+// after k_prep consumed them.
 __global__ __launch_bounds__(256) void k_place(DevParams P, DevState* __restrict__ st,
                                                const int* __restrict__ key, const int* __restrict__ slot,
                                                const int* __restrict__ start, int* __restrict__ tmp,
@@ -326,8 +341,6 @@ __global__ __launch_bounds__(256) void k_place(DevParams P, DevState* __restrict
                 for (int d = 0; d < 3; ++d) st->wall_c[t][d] += st->wall_vel[t][d] * P.dt;
             st->time += P.dt;
         }
-        st->max_count = 0;
-        st->sum_count = 0;
     }
     if (p >= P.n) return;
     tmp[start[key[p]] + slot[p]] = p;
@@ -459,17 +472,6 @@ __device__ __forceinline__ void pass_a_finish(const DevParams& P, const DevTable
 // cells are >= rc/2 wide, so a +-2 stencil covers the acceptance sphere: 25 columns (3-D) or 5
 // (2-D) along which the cells of the last axis are contiguous in memory.  Acceptance is the
 // reference's own test  q0^2+q1^2+q2^2 <= (MaxRadius+MARGIN)^2  with the Mod-based minimum image.
-// With FUSE the pass-A sums of every accepted neighbour are accumulated on the spot (same
-// neighbour order as the list, so the same sums as a separate list pass), saving pass A's list
-// read and gathers.
-struct FuseA {
-    const double* s_ratio;
-    const double* s_mu;
-    int ti;
-    bool solid;
-    double vxi, vyi, vzi;
-};
-
 // Offset of x from the grid origin, wrapped once into [0, w) (as cell_axis).
 __device__ __forceinline__ double grid_offset(double x, double org, double w)
 {
@@ -484,10 +486,28 @@ __device__ __forceinline__ double cell_gap(double u, int c, int d, double cw)
     return g > 0.0 ? g : 0.0;
 }
 
-template <int DIM, bool FAST, bool FUSE>
+// calculateNeighbor's acceptance (main.cpp:1760-1765) for an interior pair, bit-exact but cheap:
+// r2 from the raw difference d = x_j - x_i (FMA) differs from the reference's
+// q = (d + W/2) - W/2, r2 = q0^2+q1^2+q2^2 by < 1e-13 relative, so outside a +-1e-10 band
+// around rc^2 the answer is decided; inside it (rare) the reference expression is evaluated.
+__device__ __forceinline__ bool accept_interior(const DevParams& P, double dx, double dy, double dz,
+                                                double lo2, double hi2)
+{
+    const double r2a = fma(dx, dx, fma(dy, dy, dz * dz));
+    bool a = r2a <= lo2;
+    if (r2a > lo2 && r2a <= hi2) {
+        const double q0 = image_exact<true>(dx, P.dw[0], P.hw[0], P.w075[0]);
+        const double q1 = image_exact<true>(dy, P.dw[1], P.hw[1], P.w075[1]);
+        const double q2 = image_exact<true>(dz, P.dw[2], P.hw[2], P.w075[2]);
+        a = r2_exact(q0, q1, q2) <= P.rc2;
+    }
+    return a;
+}
+
+template <int DIM, bool FAST, int SB = MPH_SB>
 __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A, const int* start,
                                                int i, double xi, double yi, double zi, int cx,
-                                               int cy, int cz, int* out, const FuseA& F, PassA& o)
+                                               int cy, int cz, int* out)
 {
     int cnt = 0;
     constexpr int NCOL = DIM == 3 ? 25 : 5;
@@ -502,6 +522,7 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
     const double uy = grid_offset(yi, P.corg[1], P.dw[1]);
     const double uz = DIM == 3 ? grid_offset(zi, P.corg[2], P.dw[2]) : 0.0;
     const double ua = DIM == 3 ? uz : uy;             // offset along the contiguous axis
+    const double lo2 = P.rc2 * (1.0 - 1e-10), hi2 = P.rc2 * (1.0 + 1e-10);
     const double ginva = DIM == 3 ? P.ginv[2] : P.ginv[1];
     for (int col = 0; col < NCOL; ++col) {
         int base;
@@ -532,55 +553,33 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
         for (int sg = 0; sg < nseg; ++sg) {
             const int jb = start[base + seg_a[sg]];
             const int je = start[base + seg_b[sg] + 1];
-            // batches of 4 candidates: all 12 loads issued before the first test (memory-level
-            // parallelism; the loop is latency-bound, not ALU-bound)
-            for (int j0 = jb; j0 < je; j0 += 4) {
-                double xs[4], ys[4], zs[4];
+            // batches of SB candidates: all loads issued before the first test (memory-level
+            // parallelism; the loop is bound by the gathers, not by the FP64 arithmetic)
+            for (int j0 = jb; j0 < je; j0 += SB) {
+                double xs[SB], ys[SB], zs[SB];
+                {
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int j = j0 + u < je ? j0 + u : je - 1;
-                    if (MPH_AOS_SEARCH) {
-                        const double4 t = A.pt[j];
-                        xs[u] = t.x; ys[u] = t.y; zs[u] = t.z;
-                    } else {
+                    for (int u = 0; u < SB; ++u) {
+                        const int j = j0 + u < je ? j0 + u : je - 1;
                         xs[u] = A.x[j];
                         ys[u] = A.y[j];
                         zs[u] = A.z[j];
                     }
                 }
-                double q0[4], q1[4], q2[4], r2[4];
-                bool acc[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < SB; ++u) {
                     const int j = j0 + u;
-                    q0[u] = image_exact<FAST>(xs[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
-                    q1[u] = image_exact<FAST>(ys[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
-                    q2[u] = image_exact<FAST || DIM == 2>(zs[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
-                    r2[u] = r2_exact(q0[u], q1[u], q2[u]);
-                    acc[u] = j < je && r2[u] <= P.rc2 && j != i;
-                }
-                if (FUSE) {
-                    // velocities / types of the accepted candidates, all loads in flight at once
-                    double vx[4], vy[4], vz[4];
-                    int tj[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int j = acc[u] ? j0 + u : i;
-                        vx[u] = A.vx[j];
-                        vy[u] = A.vy[j];
-                        vz[u] = A.vz[j];
-                        tj[u] = A.type[j];
+                    bool a;
+                    if (FAST) {
+                        a = accept_interior(P, xs[u] - xi, ys[u] - yi, zs[u] - zi, lo2, hi2);
+                    } else {
+                        const double q0 = image_exact<false>(xs[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
+                        const double q1 = image_exact<false>(ys[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
+                        const double q2 = image_exact<DIM == 2>(zs[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
+                        a = r2_exact(q0, q1, q2) <= P.rc2;
                     }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        if (acc[u])
-                            pass_a_term<true>(P, F.s_ratio, F.s_mu, F.ti, tj[u], F.solid, q0[u], q1[u], q2[u], r2[u],
-                                        vx[u] - F.vxi, vy[u] - F.vyi, vz[u] - F.vzi, o);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    if (acc[u]) {
-                        if (cnt < kMaxNeighbor) out[cnt * kTile] = j0 + u;
+                    if (a && j < je && j != i) {
+                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) out[cnt * kTile] = j;
                         ++cnt;
                     }
                 }
@@ -590,65 +589,161 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
     return cnt;
 }
 
-template <int DIM, bool FUSE>
-__global__ __launch_bounds__(256) void k_neighbors(DevParams P, const DevTables* __restrict__ T, Soa A,
-                                                   const int* __restrict__ start, int* __restrict__ nbr,
-                                                   int* __restrict__ ncount, DevState* __restrict__ st,
-                                                   PassAOut pout)
+__device__ __forceinline__ int wave_min(int v)
 {
-    __shared__ double s_ratio[kTypes * kTypes];
-    __shared__ double s_mu[kTypes * kTypes];
-    if (FUSE) {
-        if (threadIdx.x < kTypes * kTypes) {
-            s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
-            s_mu[threadIdx.x] = T->mu_ij[threadIdx.x];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ int wave_max(int v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// The search of a wave whose particles are all interior (FAST): per stencil column the union of
+// the 64 lanes' candidate ranges is one short index range (the lanes are consecutive in cell
+// order, mostly inside one or two cell columns), so the wave stages it in LDS with coalesced
+// loads and every lane then tests its own candidates from LDS.  The global gathers of the
+// per-lane loop cost ~19 L1 tag lookups per load instruction (PMC, profiles/r01) and the
+// texture-address unit was the bound; a staged column costs 4.  Same candidates, same order,
+// same FP64 test as scan_candidates, so the list is identical.  Every lane of the wave must call
+// this (act = live particle); the column loop and the staging are wave-uniform.
+template <int DIM, int SB = MPH_SB, int CAP = MPH_LDS_CAP>
+__device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa& A, const int* start,
+                                                   int i, bool act, double xi, double yi, double zi,
+                                                   int cx, int cy, int cz, int* out, double* sx)
+{
+    double* sy = sx + (CAP + SB);
+    double* sz = sx + 2 * (CAP + SB);
+    const int lane = threadIdx.x & 63;
+    const double lo2 = P.rc2 * (1.0 - 1e-10), hi2 = P.rc2 * (1.0 + 1e-10);
+    int cnt = 0;
+    constexpr int NCOL = DIM == 3 ? 25 : 5;
+    const int cca = DIM == 3 ? cz : cy;
+    const double rcm2 = P.rc2 * (1.0 + 4e-6);
+    const double cw0 = 1.0 / P.ginv[0], cw1 = 1.0 / P.ginv[1];
+    const double ux = grid_offset(xi, P.corg[0], P.dw[0]);
+    const double uy = grid_offset(yi, P.corg[1], P.dw[1]);
+    const double uz = DIM == 3 ? grid_offset(zi, P.corg[2], P.dw[2]) : 0.0;
+    const double ua = DIM == 3 ? uz : uy;
+    const double ginva = DIM == 3 ? P.ginv[2] : P.ginv[1];
+    for (int col = 0; col < NCOL; ++col) {
+        int base;
+        double d2;
+        if (DIM == 3) {
+            const int dxc = col / 5 - 2, dyc = col % 5 - 2;
+            const double gx = cell_gap(ux, cx, dxc, cw0), gy = cell_gap(uy, cy, dyc, cw1);
+            d2 = gx * gx + gy * gy;
+            base = ((cx + dxc) * P.gc[1] + cy + dyc) * P.gc[2];
+        } else {
+            const int dxc = col - 2;
+            const double gx = cell_gap(ux, cx, dxc, cw0);
+            d2 = gx * gx;
+            base = (cx + dxc) * P.gc[1];
         }
-        __syncthreads();
+        int jb = 0, je = 0;
+        if (act && d2 <= rcm2) {
+            const double ra = sqrt(rcm2 - d2);
+            const int lo = (int)fmax(floor((ua - ra) * ginva), (double)(cca - P.sa));
+            const int hi = (int)fmin(floor((ua + ra) * ginva), (double)(cca + P.sa));
+            jb = start[base + lo];
+            je = start[base + hi + 1];
+        }
+        const bool any = je > jb;
+        const int mn = wave_min(any ? jb : 0x7fffffff);
+        const int mx = wave_max(any ? je : -1);
+        if (mx <= mn) continue;   // wave-uniform: no lane has candidates in this column
+        const int span = mx - mn;
+        if (MPH_DIAG_SEARCH & 2) { cnt += span & 1; continue; }
+        if (span <= CAP) {
+            for (int t = lane; t < span; t += 64) {
+                sx[t] = A.x[mn + t];
+                sy[t] = A.y[mn + t];
+                sz[t] = A.z[mn + t];
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (MPH_DIAG_SEARCH & 1) { cnt += sx[lane] > 0.0; continue; }
+            // the staging arrays are padded by SB entries, so a batch may read past je (masked)
+            for (int j0 = jb; j0 < je; j0 += SB) {
+                double xs[SB], ys[SB], zs[SB];
+                const int k0 = j0 - mn;
+#pragma unroll
+                for (int u = 0; u < SB; ++u) {
+                    xs[u] = sx[k0 + u];
+                    ys[u] = sy[k0 + u];
+                    zs[u] = sz[k0 + u];
+                }
+#pragma unroll
+                for (int u = 0; u < SB; ++u) {
+                    const int j = j0 + u;
+                    if (accept_interior(P, xs[u] - xi, ys[u] - yi, zs[u] - zi, lo2, hi2) && j < je && j != i) {
+                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) out[cnt * kTile] = j;
+                        ++cnt;
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();   // every lane done reading before the next staging
+        } else {
+            for (int j0 = jb; j0 < je; j0 += SB) {
+                double xs[SB], ys[SB], zs[SB];
+#pragma unroll
+                for (int u = 0; u < SB; ++u) {
+                    const int j = j0 + u < je ? j0 + u : je - 1;
+                    xs[u] = A.x[j];
+                    ys[u] = A.y[j];
+                    zs[u] = A.z[j];
+                }
+#pragma unroll
+                for (int u = 0; u < SB; ++u) {
+                    const int j = j0 + u;
+                    if (accept_interior(P, xs[u] - xi, ys[u] - yi, zs[u] - zi, lo2, hi2) && j < je && j != i) {
+                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) out[cnt * kTile] = j;
+                        ++cnt;
+                    }
+                }
+            }
+        }
     }
+    return cnt;
+}
+
+template <int DIM>
+__global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int* __restrict__ start,
+                                                   int* __restrict__ nbr, int* __restrict__ ncount,
+                                                   DevState* __restrict__ st)
+{
     const int i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     const bool live = i < P.n;
     const int ii = live ? i : P.n - 1;
     const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
     const bool fast = wave_interior(P, live, xi, yi, zi);
     int cnt = 0;
-    if (live) {
-        const int cx = cell_axis(xi, P.corg[0], P.dw[0], P.ginv[0], P.gc[0]);
-        const int cy = cell_axis(yi, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
-        const int cz = DIM == 3 ? cell_axis(zi, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
-        int* out = nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
-        FuseA F{};
-        PassA o;
-        if (FUSE) {
-            F.s_ratio = s_ratio;
-            F.s_mu = s_mu;
-            F.ti = A.type[i];
-            F.solid = dev_is_struct(F.ti);
-            F.vxi = A.vx[i]; F.vyi = A.vy[i]; F.vzi = A.vz[i];
-        }
-        cnt = fast ? scan_candidates<DIM, true, FUSE>(P, A, start, i, xi, yi, zi, cx, cy, cz, out, F, o)
-                   : scan_candidates<DIM, false, FUSE>(P, A, start, i, xi, yi, zi, cx, cy, cz, out, F, o);
+    const int cx = cell_axis(xi, P.corg[0], P.dw[0], P.ginv[0], P.gc[0]);
+    const int cy = cell_axis(yi, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
+    const int cz = DIM == 3 ? cell_axis(zi, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
+    int* out = nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
+    if (MPH_SEARCH_LDS && fast) {
+        __shared__ double stage[4][3 * (MPH_LDS_CAP + MPH_SB)];
+        cnt = scan_candidates_lds<DIM>(P, A, start, i, live, xi, yi, zi, cx, cy, cz, out,
+                                       stage[threadIdx.x >> 6]);
+        if (live) ncount[i] = cnt;
+    } else if (live && !(MPH_DIAG_SEARCH & 4)) {
+        cnt = fast ? scan_candidates<DIM, true>(P, A, start, i, xi, yi, zi, cx, cy, cz, out)
+                   : scan_candidates<DIM, false>(P, A, start, i, xi, yi, zi, cx, cy, cz, out);
         ncount[i] = cnt;
-        if (FUSE) pass_a_finish(P, T, F.ti, i, o, pout, xi, yi, zi);
     }
-    // wave reduction of the statistics (mean/max neighbours, overflow flag)
-    int mx = cnt;
-    unsigned long long sm = (unsigned long long)cnt;
-#pragma unroll
-    for (int o2 = 32; o2 > 0; o2 >>= 1) {
-        const int m2 = __shfl_xor(mx, o2, 64);
-        mx = m2 > mx ? m2 : mx;
-        sm += __shfl_xor(sm, o2, 64);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        atomicMax(&st->max_count, mx);
-        atomicAdd(&st->sum_count, sm);
-        if (mx > kMaxNeighbor) atomicOr(&st->overflow, 1);
-    }
+    // overflow flag (main.cpp:1766-1768 is the reference's limit).  No per-step statistics here:
+    // one same-address device atomic per wave serialises at ~11 ns each (21.8k waves at D1M took
+    // 0.5 ms); mph_neighbor_stats reduces ncount on demand.
+    if (cnt > kMaxNeighbor) atomicOr(&st->overflow, 1);
 }
 
 // ---------------------------------------------------------------------------- pass A -------
 
-// Separate list pass (the default; see fused_pass_a): neighbour loops gather U neighbours' fields
+// List pass: the neighbour loops gather U neighbours' fields
 // before the first use (all loads in flight at once; the loops are memory-latency bound).
 #ifndef MPH_UA
 #define MPH_UA 8
@@ -1280,17 +1375,6 @@ void launch_sort(const Launch& L, int mode)
                L.key, L.start, L.tmp, L.B, L.A, L.rank_of, L.dst_of);
 }
 
-// Pass A fused into the search (MPH_FUSED=1) is an A/B option: on D1M it measured 1.34 ms against
-// 0.67 + 0.64 ms for the separate kernels (the fused kernel needs 123 VGPRs -> half the occupancy).
-static bool fused_pass_a()
-{
-    static const bool fused = [] {
-        const char* e = std::getenv("MPH_FUSED");
-        return e && e[0] == '1';
-    }();
-    return fused;
-}
-
 static PassAOut pass_a_out(const Launch& L)
 {
     return PassAOut{L.pres, L.gx, L.gy, L.gz, L.pa, L.dens_a, L.vstrain, L.divp, L.fpart, L.rec};
@@ -1301,23 +1385,19 @@ void launch_neighbors(const Launch& L)
     Profiler* prof = L.prof;
     const DevParams& P = *L.P;
     if (P.n == 0) return;
-    const PassAOut po = pass_a_out(L);
-#define MPH_NB(D, F) \
-    MPH_LAUNCH(F ? "neighbors_pass_a" : "neighbors", L.stream, (k_neighbors<D, F>), dim3(blocks(P.n, 256)), \
-               dim3(256), 0, L.stream, P, L.T, L.A, L.start, L.nbr, L.ncount, L.st, po)
-    if (fused_pass_a()) {
-        if (P.dim == 3) MPH_NB(3, true); else MPH_NB(2, true);
-    } else {
-        if (P.dim == 3) MPH_NB(3, false); else MPH_NB(2, false);
-    }
-#undef MPH_NB
+    if (P.dim == 3)
+        MPH_LAUNCH("neighbors", L.stream, k_neighbors<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.A,
+                   L.start, L.nbr, L.ncount, L.st);
+    else
+        MPH_LAUNCH("neighbors", L.stream, k_neighbors<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.A,
+                   L.start, L.nbr, L.ncount, L.st);
 }
 
 void launch_pass_a(const Launch& L)
 {
     Profiler* prof = L.prof;
     const DevParams& P = *L.P;
-    if (P.n == 0 || fused_pass_a()) return;   // fused into the neighbour search
+    if (P.n == 0) return;
     const PassAOut po = pass_a_out(L);
     if (P.dim == 3)
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T,

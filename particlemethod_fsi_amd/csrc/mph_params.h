@@ -12,6 +12,7 @@ constexpr int kTypes = MPH_TYPE_COUNT;
 constexpr int kMaxNeighbor = MPH_MAX_NEIGHBOR_COUNT;
 constexpr int kTile = 64;  // ELL neighbour-list tile = one wavefront of i-particles
 constexpr int kContigSub = 2;   // cells along the contiguous axis are 1/kContigSub as wide
+constexpr int kPad = 8;         // extra elements behind every per-particle array (vector over-reads)
 
 inline bool is_fluid(int t) { return t >= 0 && t < 2; }   // main.cpp:69-70
 inline bool is_struct(int t) { return t >= 2 && t < 4; }  // main.cpp:71-72
@@ -69,8 +70,6 @@ struct DevState {
     double wall_rot[kTypes][3][3];  // WallRotation (initializeWall)
     int overflow;                // error bits: 1 neighbour overflow (> MAX_NEIGHBOR_COUNT),
                                  // 2 slab jump (mph_dist), 4 non-finite position
-    int max_count;               // max neighbour count of the last search
-    unsigned long long sum_count;
 };
 
 #if defined(__HIPCC__)
