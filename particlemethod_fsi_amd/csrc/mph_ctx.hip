@@ -272,6 +272,9 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         c->n = (int)owned.size();
         c->P.n = c->n;
     }
+    if (cap > kIndexMask)
+        return fail(c, MPH_ERR_UNSUPPORTED, "more than 2^28 particles in one context (neighbour-list entries "
+                                            "carry the type in their top bits)");
     c->P.ncell = c->P.gc[0] * c->P.gc[1] * c->P.gc[2];
     // tables
     for (int t = 0; t < kTypes; ++t) {
@@ -295,7 +298,7 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         CK(dalloc(c, &s->vx, m)); CK(dalloc(c, &s->vy, m)); CK(dalloc(c, &s->vz, m));
         CK(dalloc(c, &s->type, m)); CK(dalloc(c, &s->id, m));
     }
-    CK(dalloc(c, &c->A.pt, cap)); CK(dalloc(c, &c->A.pv, cap));
+    CK(dalloc(c, &c->A.p6, 3 * (size_t)cap));
     CK(dalloc(c, &c->rank_of, cap));
     CK(dalloc(c, &c->key, cap)); CK(dalloc(c, &c->slot, cap)); CK(dalloc(c, &c->tmp, cap));
     CK(dalloc(c, &c->cnt, c->P.ncell)); CK(dalloc(c, &c->start, (size_t)c->P.ncell + 1));

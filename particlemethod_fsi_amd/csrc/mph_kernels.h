@@ -43,11 +43,11 @@ struct Soa {
     double *x = nullptr, *y = nullptr, *z = nullptr;
     double *vx = nullptr, *vy = nullptr, *vz = nullptr;
     int *type = nullptr, *id = nullptr;
-    // gather records of the sorted set A (null for B/C): {x, y, z, type} and {vx, vy, vz, 0}.
-    // A neighbour's fields then arrive with two 16-byte loads per record instead of one 8-byte
-    // load per field: the neighbour loops are bound by the number of gather instructions
-    // (profiles/r01: pass B 0.46 ms with 4 SoA loads vs 0.38 ms with one 32-byte record).
-    double4 *pt = nullptr, *pv = nullptr;
+    // gather record of the sorted set A (null for B/C): {x, y, z, vx, vy, vz}, 48 bytes, read
+    // with three 16-byte loads.  The neighbour loops are bound by the texture-address/data path
+    // (profiles/r01: TA ~64 % busy in pass A); the type of j travels in the list entry instead
+    // (kTypeShift), so a neighbour costs 48 gathered bytes instead of 64.
+    double2* p6 = nullptr;
 };
 
 // Everything one launch sequence needs.

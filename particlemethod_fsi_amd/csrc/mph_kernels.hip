@@ -154,6 +154,8 @@ __device__ __forceinline__ int xcd_block(int b, int nb)
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
 }
 
+__device__ __forceinline__ int nbr_entry(int j, int type) { return j | (type << kTypeShift); }
+
 __device__ __forceinline__ const int* ell_row(const int* nbr, int i)
 {
     return nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
@@ -369,9 +371,11 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
     A.type[dst] = B.type[p];
     const int id = B.id[p];
     A.id[dst] = id;
-    if (A.pt) {
-        A.pt[dst] = make_double4(B.x[p], B.y[p], B.z[p], (double)B.type[p]);
-        A.pv[dst] = make_double4(B.vx[p], B.vy[p], B.vz[p], 0.0);
+    if (A.p6) {
+        double2* q = A.p6 + 3 * (size_t)dst;
+        q[0] = make_double2(B.x[p], B.y[p]);
+        q[1] = make_double2(B.z[p], B.vx[p]);
+        q[2] = make_double2(B.vy[p], B.vz[p]);
     }
     if (dst_of) dst_of[p] = dst;   // slab mode: ids are global (ghosts negative)
     else rank_of[id] = dst;
@@ -579,7 +583,7 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
                         a = r2_exact(q0, q1, q2) <= P.rc2;
                     }
                     if (a && j < je && j != i) {
-                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) out[cnt * kTile] = j;
+                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) out[cnt * kTile] = nbr_entry(j, A.type[j]);
                         ++cnt;
                     }
                 }
@@ -618,6 +622,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
 {
     double* sy = sx + (CAP + SB);
     double* sz = sx + 2 * (CAP + SB);
+    int* st = reinterpret_cast<int*>(sx + 3 * (CAP + SB));
     const int lane = threadIdx.x & 63;
     const double lo2 = P.rc2 * (1.0 - 1e-10), hi2 = P.rc2 * (1.0 + 1e-10);
     int cnt = 0;
@@ -663,6 +668,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                 sx[t] = A.x[mn + t];
                 sy[t] = A.y[mn + t];
                 sz[t] = A.z[mn + t];
+                st[t] = A.type[mn + t];
             }
             __builtin_amdgcn_wave_barrier();
             if (MPH_DIAG_SEARCH & 1) { cnt += sx[lane] > 0.0; continue; }
@@ -680,7 +686,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                 for (int u = 0; u < SB; ++u) {
                     const int j = j0 + u;
                     if (accept_interior(P, xs[u] - xi, ys[u] - yi, zs[u] - zi, lo2, hi2) && j < je && j != i) {
-                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) out[cnt * kTile] = j;
+                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) out[cnt * kTile] = nbr_entry(j, st[k0 + u]);
                         ++cnt;
                     }
                 }
@@ -700,7 +706,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                 for (int u = 0; u < SB; ++u) {
                     const int j = j0 + u;
                     if (accept_interior(P, xs[u] - xi, ys[u] - yi, zs[u] - zi, lo2, hi2) && j < je && j != i) {
-                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) out[cnt * kTile] = j;
+                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) out[cnt * kTile] = nbr_entry(j, A.type[j]);
                         ++cnt;
                     }
                 }
@@ -726,7 +732,7 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int
     const int cz = DIM == 3 ? cell_axis(zi, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
     int* out = nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
     if (MPH_SEARCH_LDS && fast) {
-        __shared__ double stage[4][3 * (MPH_LDS_CAP + MPH_SB)];
+        __shared__ double stage[4][3 * (MPH_LDS_CAP + MPH_SB) + (MPH_LDS_CAP + MPH_SB + 1) / 2];
         cnt = scan_candidates_lds<DIM>(P, A, start, i, live, xi, yi, zi, cx, cy, cz, out,
                                        stage[threadIdx.x >> 6]);
         if (live) ncount[i] = cnt;
@@ -763,17 +769,21 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
         double X[U], Y[U], Z[U], VX[U], VY[U], VZ[U];
         int TT[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) jj[u] = row[(k0 + u < cnt ? k0 + u : cnt - 1) * kTile];
+        for (int u = 0; u < U; ++u) {
+            const int e = row[(k0 + u < cnt ? k0 + u : cnt - 1) * kTile];
+            jj[u] = e & kIndexMask;
+            TT[u] = e >> kTypeShift;
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (MPH_AOS_GATHER) {
-                const double4 t = A.pt[jj[u]], v = A.pv[jj[u]];
-                X[u] = t.x; Y[u] = t.y; Z[u] = t.z; TT[u] = (int)t.w;
-                VX[u] = v.x; VY[u] = v.y; VZ[u] = v.z;
+                const double2* q = A.p6 + 3 * (size_t)jj[u];
+                const double2 a = q[0], b = q[1], c = q[2];
+                X[u] = a.x; Y[u] = a.y; Z[u] = b.x;
+                VX[u] = b.y; VY[u] = c.x; VZ[u] = c.y;
             } else {
                 X[u] = A.x[jj[u]]; Y[u] = A.y[jj[u]]; Z[u] = A.z[jj[u]];
                 VX[u] = A.vx[jj[u]]; VY[u] = A.vy[jj[u]]; VZ[u] = A.vz[jj[u]];
-                TT[u] = A.type[jj[u]];
             }
         }
 #pragma unroll
@@ -850,7 +860,11 @@ __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_
         double X[U], Y[U], Z[U], PJ[U];
         int TT[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) jj[u] = row[(k0 + u < cnt ? k0 + u : cnt - 1) * kTile];
+        for (int u = 0; u < U; ++u) {
+            const int e = row[(k0 + u < cnt ? k0 + u : cnt - 1) * kTile];
+            jj[u] = e & kIndexMask;
+            TT[u] = e >> kTypeShift;
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (MPH_PB_REC) {
@@ -860,7 +874,6 @@ __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_
                 X[u] = A.x[jj[u]]; Y[u] = A.y[jj[u]]; Z[u] = A.z[jj[u]];
                 PJ[u] = pres[jj[u]];
             }
-            TT[u] = (SURF || solid) ? A.type[jj[u]] : 0;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {

@@ -12,6 +12,10 @@ constexpr int kTypes = MPH_TYPE_COUNT;
 constexpr int kMaxNeighbor = MPH_MAX_NEIGHBOR_COUNT;
 constexpr int kTile = 64;  // ELL neighbour-list tile = one wavefront of i-particles
 constexpr int kContigSub = 2;   // cells along the contiguous axis are 1/kContigSub as wide
+// ELL list entry = sorted index | (type << kTypeShift): pass A reads the neighbour's type with
+// its index instead of gathering it (requires fewer than 2^28 particles per context)
+constexpr int kTypeShift = 28;
+constexpr int kIndexMask = (1 << kTypeShift) - 1;
 constexpr int kPad = 8;         // extra elements behind every per-particle array (vector over-reads)
 
 inline bool is_fluid(int t) { return t >= 0 && t < 2; }   // main.cpp:69-70

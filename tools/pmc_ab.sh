@@ -1,0 +1,11 @@
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+G1="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY"
+G2="SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_WAIT_ANY TA_BUSY_avr TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE"
+for v in old c128u2; do
+  export MPH_GPU_LIB=$PWD/particlemethod_fsi_amd/lib_$v/libmph_gpu.so
+  mkdir -p gpurun_out/pmc_$v
+  bash tools/pmc.sh "$G1" "$G2" || exit 30
+  mv gpurun_out/pmc/* gpurun_out/pmc_$v/
+  python tools/pmc_summary.py gpurun_out/pmc_$v > gpurun_out/pmc_$v.txt
+done
