@@ -37,6 +37,12 @@ HBM_PEAK_GBPS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level
 FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector spec
 # algorithmic bytes per particle per launch
 ALG_BYTES = {"pass_a": 92.0, "neighbors_pass_a": 92.0, "pass_b": 140.0, "sort": 140.0}
+# elastic substep kernels, per structure particle and launch (SURVEY 8d "500 + 8 n_s" split by
+# kernel; n_s = mean InitialStructureNeighborCount; output-only DeformGradient/Strain/Stress
+# excluded as for the fluid passes):
+#   struct_stress   read x, x0 (48), L (72), Lame (16), list (4 n_s); write P (72)
+#   struct_velocity read P (72), v, x (48), out- and in-lists (8 n_s); write v, x (48)
+STRUCT_BYTES = {"struct_stress": (208.0, 4.0), "struct_velocity": (168.0, 8.0)}
 B_ALG_STEP = 372.0          # grid build 140 + pass 1 92 + pass 2 140
 SLAB_AXIS = 2               # z slabs for the dam workloads
 
@@ -161,9 +167,25 @@ def main():
 
     mean_nb, max_nb = solver.neighbor_stats()
     prof = solver.profile(args.profile_steps)
-    dom = max((k for k in prof if k in ALG_BYTES), key=lambda k: prof[k]["avg_ms"])
+    ns, mean_ns = 0, 0.0
+    if any(k in prof for k in STRUCT_BYTES):
+        isnc = solver.get("InitialStructureNeighborCount")
+        prop = solver.get("Property")
+        smask = (prop == 2) | (prop == 3)
+        ns = int(smask.sum())
+        mean_ns = float(isnc[smask].mean()) if ns else 0.0
+
+    def alg_bytes_of(k):
+        if k in STRUCT_BYTES:
+            a, b = STRUCT_BYTES[k]
+            return (a + b * mean_ns) * ns
+        return ALG_BYTES[k] * n_local
+
+    # dominant kernel by total time per step among those with an algorithmic byte count
+    dom = max((k for k in prof if k in ALG_BYTES or k in STRUCT_BYTES),
+              key=lambda k: prof[k]["avg_ms"] * prof[k]["launches"])
     step_ms = sum(v["avg_ms"] * v["launches"] for v in prof.values()) / args.profile_steps
-    alg_bytes = ALG_BYTES[dom] * n_local
+    alg_bytes = alg_bytes_of(dom)
     achieved = alg_bytes / (prof[dom]["avg_ms"] * 1e-3) / 1e9
     traffic = load_pmc_traffic(dom)
     out = {
@@ -179,9 +201,8 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (reference generator algorithm + results/Dam/dam.data parameters)",
-        "config": {"workload": "%s: 3-D dam break (SURVEY 8d D1M%s), %d particles, ~%d per GPU"
-                               % (case_name, "" if world == 1 else " extended %dx along z" % world,
-                                  n_total, n_total // world),
+        "config": {"workload": "%s: %s, %d particles, ~%d per GPU"
+                               % (case_name, case.describe(), n_total, n_total // world),
                    "particles": n_total, "dim": case.dim, "module": case.module, "dt": cfg.dt,
                    "parallelism": "single" if world == 1 else "slab%d-z (%s halo exchange)" % (
                        world, "host-staged" if os.environ.get("MPH_SLAB_TRANSPORT") == "host" else "RCCL")},

@@ -55,6 +55,10 @@ class Case:
     data_changes: dict = field(default_factory=dict)
     note: str = ""
 
+    def describe(self) -> str:
+        """One-line description for bench.py's config.workload."""
+        return self.note or "%d-D %s-module case" % (self.dim, self.module)
+
     def data(self) -> dict:
         d = dict(DAM_DATA)
         d.update(self.data_changes)
@@ -111,7 +115,7 @@ _reg(Case("d1m", 3, "dam", 0.001, (-0.01, 0.0, -0.01), (0.21, 0.40, 0.11), [
     Cuboid(4, (-0.003, 0.0, 0.0), (0.0, 0.2, 0.1), 0.001),
     Cuboid(4, (-0.003, 0.0, -0.003), (0.203, 0.2, 0.0), 0.001),
     Cuboid(4, (-0.003, 0.0, 0.1), (0.203, 0.2, 0.103), 0.001),
-]))
+], note="3-D dam break (SURVEY 8d D1M, BASELINE configs[1])"))
 
 # 3-D dam break, dx 4e-4, 16,205,500 particles, Dt = ElasticDt = 4e-5
 _reg(Case("d16m", 3, "dam", 0.0004, (-0.004, 0.0, -0.004), (0.208, 0.40, 0.108), [
@@ -121,7 +125,8 @@ _reg(Case("d16m", 3, "dam", 0.0004, (-0.004, 0.0, -0.004), (0.208, 0.40, 0.108),
     Cuboid(4, (-0.0012, 0.0, 0.0), (0.0, 0.2, 0.1), 0.0004),
     Cuboid(4, (-0.0012, 0.0, -0.0012), (0.2012, 0.2, 0.0), 0.0004),
     Cuboid(4, (-0.0012, 0.0, 0.1), (0.2012, 0.2, 0.1012), 0.0004),
-], data_changes={"Dt": [4e-5], "ElasticDt": [4e-5]}))
+], data_changes={"Dt": [4e-5], "ElasticDt": [4e-5]},
+   note="3-D dam break, dx 0.4 mm (SURVEY 8d D16M, BASELINE configs[4] on one GPU)"))
 
 # SURVEY 8d FSI: 3-D dam break onto an elastic gate, DAM_Module, 2,259,700 particles
 _reg(Case("fsi3d", 3, "dam", 0.001, (-0.01, 0.0, -0.01), (0.31, 0.40, 0.11), [
@@ -133,7 +138,7 @@ _reg(Case("fsi3d", 3, "dam", 0.001, (-0.01, 0.0, -0.01), (0.31, 0.40, 0.11), [
     Cuboid(4, (-0.003, 0.0, 0.0), (0.0, 0.2, 0.1), 0.001),
     Cuboid(4, (-0.003, 0.0, -0.003), (0.303, 0.2, 0.0), 0.001),
     Cuboid(4, (-0.003, 0.0, 0.1), (0.303, 0.2, 0.103), 0.001),
-]))
+], note="3-D dam break onto an elastic gate, coupled FSI (SURVEY 8d FSI, BASELINE configs[3])"))
 
 # SURVEY 8d Bar (parity size): 2-D cantilever, Bar_Module, 4,000 structure particles
 _reg(Case("bar2d", 2, "bar", 0.001, (-0.01, -0.1, 0.0), (0.25, 0.1, 0.001), [
@@ -143,7 +148,8 @@ _reg(Case("bar2d", 2, "bar", 0.001, (-0.01, -0.1, 0.0), (0.25, 0.1, 0.001), [
 # SURVEY 8d Bar (perf size): dx 1e-4, 400,000 structure particles, Dt = ElasticDt = 1e-5
 _reg(Case("bar2d_400k", 2, "bar", 0.0001, (-0.001, -0.05, 0.0), (0.25, 0.05, 0.0001), [
     Cuboid(2, (0.0, -0.01, 0.0), (0.2, 0.01, 0.0001), 0.0001),
-], data_changes={"Dt": [1e-5], "ElasticDt": [1e-5]}))
+], data_changes={"Dt": [1e-5], "ElasticDt": [1e-5]},
+   note="2-D elastic cantilever, total-Lagrangian solid (SURVEY 8d Bar, BASELINE configs[2])"))
 
 # 2-D dam break onto an elastic gate (DAM_Module), 7,035 particles = 4,850 + 400 + 1,785
 _reg(Case("gate2d", 2, "dam", 0.001, (-0.01, 0.0, 0.0), (0.21, 0.40, 0.001), [
@@ -230,7 +236,7 @@ def d1m_weak(nranks: int) -> Case:
         Cuboid(4, (-0.003, 0.0, 0.0), (0.0, 0.2, zl), 0.001),
         Cuboid(4, (-0.003, 0.0, -0.003), (0.203, 0.2, 0.0), 0.001),
         Cuboid(4, (-0.003, 0.0, zl), (0.203, 0.2, zl + 0.003), 0.001),
-    ], note="D1M extended %dx along z" % nranks)
+    ], note="3-D dam break, D1M extended %dx along z (weak scaling)" % nranks)
 
 
 def get(name: str) -> Case:

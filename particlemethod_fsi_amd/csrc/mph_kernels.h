@@ -7,15 +7,19 @@
 
 namespace mph {
 
-// Device arrays of the elastic solid, in structure-slot order (see StructureInit).
+// Device arrays of the elastic solid, in structure-slot order (see StructureInit).  The fixed
+// Lagrangian lists are stored ELL-tiled like the fluid list: entry k of slot s at
+// [(s >> 6) * W + k][s & 63], so the 64 lanes of a wavefront read entry k with one coalesced load.
 struct StructDev {
     int* orig = nullptr;          // slot -> original particle index
-    int* off = nullptr;           // CSR offsets of the fixed neighbour list
-    int* nb = nullptr;
-    int* in_off = nullptr;        // transpose
-    int* in_nb = nullptr;
-    double4* pair_out = nullptr;  // {x0_ij, w_ij}
-    double4* pair_in = nullptr;   // {x0_is, w_is} of the sender i
+    int wo = 0, wi = 0;           // ELL widths (max out / in count)
+    int* ocnt = nullptr;          // InitialStructureNeighborCount per slot
+    int* icnt = nullptr;          // in-degree (how many slots list s)
+    int* eo_nb = nullptr;         // out-list neighbour slots, ELL [ntile * wo][64]
+    double4* eo_pair = nullptr;   // {x0_ij, w_ij}, ELL
+    int* ei_nb = nullptr;         // in-list (senders i of the reference's scatter), ELL [ntile * wi][64]
+    double4* ei_pair = nullptr;   // {x0_is, w_is} of the sender i, ELL
+    double4* wx0 = nullptr;       // sum_j w_sj x0_sj (the P_s half of StressForce, fixed)
     double* L = nullptr;          // Normalizer [ns][9]
     double2* lame = nullptr;      // (LambdaLames, MuLames)
     double* inv_rho = nullptr;    // 1/Density[type]
@@ -23,7 +27,8 @@ struct StructDev {
     double4* x0 = nullptr;        // InitialPosition
     double4* x = nullptr;         // current position (valid during the substeps)
     double4* v = nullptr;
-    double* P = nullptr;          // first Piola-Kirchhoff F S L [ns][9]
+    double4* u = nullptr;         // displacement Mod(x - x0) (main.cpp:2700-2712), per substep
+    double4* P = nullptr;         // first Piola-Kirchhoff F S L, 3 rows of double4 (xyz, 0)
     double* F = nullptr;          // DeformGradient [ns][9]
     double* E = nullptr;          // Strain
     double* S = nullptr;          // Stress

@@ -1015,56 +1015,86 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
 
 // ------------------------------------------------------------------------ elastic solid ----
 
-__global__ __launch_bounds__(256) void k_struct_gather(int ns, const int* __restrict__ sorig,
+// Displacement u = Mod(x - x0 + W/2, W) - W/2 of calculateElasticDeformationVector (2700-2712),
+// computed once per slot and substep instead of once per pair (same expression, same bits).
+__device__ __forceinline__ double4 struct_disp(const DevParams& P, double4 x, double4 x0)
+{
+    return make_double4(image_exact<false>(x.x - x0.x, P.dw[0], P.hw[0], P.w075[0]),
+                        image_exact<false>(x.y - x0.y, P.dw[1], P.hw[1], P.w075[1]),
+                        image_exact<false>(x.z - x0.z, P.dw[2], P.hw[2], P.w075[2]), 0.0);
+}
+
+__global__ __launch_bounds__(256) void k_struct_gather(DevParams P, int ns, const int* __restrict__ sorig,
                                                        const int* __restrict__ rank_of, Soa B,
-                                                       double4* __restrict__ sx, double4* __restrict__ sv)
+                                                       const double4* __restrict__ sx0,
+                                                       double4* __restrict__ sx, double4* __restrict__ sv,
+                                                       double4* __restrict__ su)
 {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= ns) return;
     const int r = rank_of[sorig[s]];
-    sx[s] = make_double4(B.x[r], B.y[r], B.z[r], (double)B.type[r]);
+    const double4 x = make_double4(B.x[r], B.y[r], B.z[r], (double)B.type[r]);
+    sx[s] = x;
     sv[s] = make_double4(B.vx[r], B.vy[r], B.vz[r], 0.0);
+    su[s] = struct_disp(P, x, sx0[s]);
+}
+
+#ifndef MPH_US
+#define MPH_US 4   // batch width of the elastic list loops
+#endif
+
+// ELL entry k of slot s (tile width w)
+__device__ __forceinline__ size_t sell(int s, int w, int k)
+{
+    return ((size_t)(s >> 6) * w + k) * 64 + (s & 63);
 }
 
 // calculateElasticDeformationVector (2673-2754) + calculateStress (2756-2809) + the first
-// Piola-Kirchhoff tensor P = F S L of calculateStressForce (2837-2852).
-template <int DIM>
-__global__ __launch_bounds__(256) void k_struct_stress(DevParams P, int ns,
-                                                       const double4* __restrict__ sx,
-                                                       const double4* __restrict__ sx0,
-                                                       const int* __restrict__ off,
-                                                       const int* __restrict__ nb,
-                                                       const double4* __restrict__ pair,
+// Piola-Kirchhoff tensor P = F S L of calculateStressForce (2837-2852).  One lane per structure
+// slot; the fixed list is read ELL-tiled (coalesced) in batches of MPH_US, and per neighbour only
+// the 32-byte displacement record u_j is gathered.
+template <int DIM, int U = MPH_US>
+__global__ __launch_bounds__(256) void k_struct_stress(int ns, int wo, const int* __restrict__ ocnt,
+                                                       const int* __restrict__ eo_nb,
+                                                       const double4* __restrict__ eo_pair,
+                                                       const double4* __restrict__ su,
                                                        const double* __restrict__ L,
                                                        const double2* __restrict__ lame,
-                                                       double* __restrict__ sP, double* __restrict__ sF,
+                                                       double4* __restrict__ sP, double* __restrict__ sF,
                                                        double* __restrict__ sE, double* __restrict__ sS)
 {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= ns) return;
-    const double4 xi = sx[s], x0i = sx0[s];
-    double ui[3];
-    ui[0] = image_exact<false>(xi.x - x0i.x, P.dw[0], P.hw[0], P.w075[0]);
-    ui[1] = image_exact<false>(xi.y - x0i.y, P.dw[1], P.hw[1], P.w075[1]);
-    ui[2] = image_exact<false>(xi.z - x0i.z, P.dw[2], P.hw[2], P.w075[2]);
+    const double4 u4 = su[s];
+    const double ui[3] = {u4.x, u4.y, u4.z};
     double Fr[DIM][DIM];
 #pragma unroll
     for (int a = 0; a < DIM; ++a)
 #pragma unroll
         for (int b = 0; b < DIM; ++b) Fr[a][b] = 0.0;
-    for (int k = off[s]; k < off[s + 1]; ++k) {
-        const int t = nb[k];
-        const double4 pr = pair[k];
-        const double4 xj = sx[t], x0j = sx0[t];
-        const double x0ij[3] = {pr.x, pr.y, pr.z};
-        const double uj[3] = {image_exact<false>(xj.x - x0j.x, P.dw[0], P.hw[0], P.w075[0]),
-                              image_exact<false>(xj.y - x0j.y, P.dw[1], P.hw[1], P.w075[1]),
-                              image_exact<false>(xj.z - x0j.z, P.dw[2], P.hw[2], P.w075[2])};
+    const int cnt = ocnt[s];
+    for (int k0 = 0; k0 < cnt; k0 += U) {
+        int t[U];
+        double4 pr[U], uj[U];
 #pragma unroll
-        for (int a = 0; a < DIM; ++a) {
-            const double xa = x0ij[a] + (uj[a] - ui[a]);
+        for (int u = 0; u < U; ++u) {
+            const size_t e = sell(s, wo, k0 + u < cnt ? k0 + u : cnt - 1);
+            t[u] = eo_nb[e];
+            pr[u] = eo_pair[e];
+        }
 #pragma unroll
-            for (int b = 0; b < DIM; ++b) Fr[a][b] += pr.w * xa * x0ij[b];
+        for (int u = 0; u < U; ++u) uj[u] = su[t[u]];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (k0 + u >= cnt) break;
+            const double x0ij[3] = {pr[u].x, pr[u].y, pr[u].z};
+            const double ujv[3] = {uj[u].x, uj[u].y, uj[u].z};
+#pragma unroll
+            for (int a = 0; a < DIM; ++a) {
+                const double xa = x0ij[a] + (ujv[a] - ui[a]);
+#pragma unroll
+                for (int b = 0; b < DIM; ++b) Fr[a][b] += pr[u].w * xa * x0ij[b];
+            }
         }
     }
     double Lm[DIM][DIM], F[DIM][DIM], E[DIM][DIM], S[DIM][DIM], PK[DIM][DIM];
@@ -1109,7 +1139,9 @@ __global__ __launch_bounds__(256) void k_struct_stress(DevParams P, int ns,
                 for (int l = 0; l < DIM; ++l) acc += F[a][k] * S[k][l] * Lm[l][b];
             PK[a][b] = acc;
         }
-    double* oP = sP + (size_t)s * 9;
+#pragma unroll
+    for (int a = 0; a < DIM; ++a)
+        sP[(size_t)s * DIM + a] = make_double4(PK[a][0], PK[a][1], DIM == 3 ? PK[a][DIM - 1] : 0.0, 0.0);
     double* oF = sF + (size_t)s * 9;
     double* oE = sE + (size_t)s * 9;
     double* oS = sS + (size_t)s * 9;
@@ -1118,62 +1150,72 @@ __global__ __launch_bounds__(256) void k_struct_stress(DevParams P, int ns,
 #pragma unroll
         for (int b = 0; b < 3; ++b) {
             const bool in = a < DIM && b < DIM;
-            oP[3 * a + b] = in ? PK[a < DIM ? a : 0][b < DIM ? b : 0] : 0.0;
             oF[3 * a + b] = in ? F[a < DIM ? a : 0][b < DIM ? b : 0] : 0.0;
             oE[3 * a + b] = in ? E[a < DIM ? a : 0][b < DIM ? b : 0] : 0.0;
             oS[3 * a + b] = in ? S[a < DIM ? a : 0][b < DIM ? b : 0] : 0.0;
         }
 }
 
-// calculateStressForce (2854-2887) in gather form: v_s += dt_e/rho_s * [sum_j w_sj P_s x0_sj -
-// sum_{i lists s} w_is P_i x0_is] (exactly the reference's scatter, regrouped by receiver),
-// followed by updateElasticPosition (1910-2082): module clamp, then the always-compiled second
-// drift of 2070-2079 (free particles drift twice per substep; structure acceleration is zero).
-template <int DIM>
-__global__ __launch_bounds__(256) void k_struct_velocity(DevParams P, int ns,
-                                                         const int* __restrict__ off,
-                                                         const double4* __restrict__ pair_out,
-                                                         const int* __restrict__ in_off,
-                                                         const int* __restrict__ in_nb,
-                                                         const double4* __restrict__ pair_in,
-                                                         const double* __restrict__ sP,
+// calculateStressForce (2854-2887) in gather form: v_s += dt_e/rho_s * [P_s sum_j w_sj x0_sj -
+// sum_{i lists s} w_is P_i x0_is] (the reference's scatter regrouped by receiver; the first sum is
+// fixed, wx0), followed by updateElasticPosition (1910-2082): module clamp, then the always-
+// compiled second drift of 2070-2079 (free particles drift twice per substep; structure
+// acceleration is zero).  Also refreshes the displacement u for the next substep.
+template <int DIM, int U = MPH_US>
+__global__ __launch_bounds__(256) void k_struct_velocity(DevParams P, int ns, int wi,
+                                                         const int* __restrict__ icnt,
+                                                         const int* __restrict__ ei_nb,
+                                                         const double4* __restrict__ ei_pair,
+                                                         const double4* __restrict__ wx0,
+                                                         const double4* __restrict__ sP,
                                                          const double* __restrict__ inv_rho,
                                                          const int* __restrict__ clamp,
                                                          const double4* __restrict__ sx0,
-                                                         double4* __restrict__ sx, double4* __restrict__ sv)
+                                                         double4* __restrict__ sx, double4* __restrict__ sv,
+                                                         double4* __restrict__ su)
 {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= ns) return;
-    double Ps[DIM][DIM];
-#pragma unroll
-    for (int a = 0; a < DIM; ++a)
-#pragma unroll
-        for (int b = 0; b < DIM; ++b) Ps[a][b] = sP[(size_t)s * 9 + 3 * a + b];
     double dv[DIM];
-#pragma unroll
-    for (int a = 0; a < DIM; ++a) dv[a] = 0.0;
-    for (int k = off[s]; k < off[s + 1]; ++k) {
-        const double4 pr = pair_out[k];
-        const double x0[3] = {pr.x, pr.y, pr.z};
+    {
+        const double4 c = wx0[s];
+        const double cv[3] = {c.x, c.y, c.z};
 #pragma unroll
         for (int a = 0; a < DIM; ++a) {
+            const double4 r = sP[(size_t)s * DIM + a];
+            const double pr[3] = {r.x, r.y, r.z};
             double f = 0.0;
 #pragma unroll
-            for (int b = 0; b < DIM; ++b) f += Ps[a][b] * x0[b];
-            dv[a] += f * pr.w;
+            for (int b = 0; b < DIM; ++b) f += pr[b] * cv[b];
+            dv[a] = f;
         }
     }
-    for (int k = in_off[s]; k < in_off[s + 1]; ++k) {
-        const int i = in_nb[k];
-        const double4 pr = pair_in[k];
-        const double x0[3] = {pr.x, pr.y, pr.z};
-        const double* Pi = sP + (size_t)i * 9;
+    const int cnt = icnt[s];
+    for (int k0 = 0; k0 < cnt; k0 += U) {
+        int t[U];
+        double4 pr[U], Pi[U][DIM];
 #pragma unroll
-        for (int a = 0; a < DIM; ++a) {
-            double f = 0.0;
+        for (int u = 0; u < U; ++u) {
+            const size_t e = sell(s, wi, k0 + u < cnt ? k0 + u : cnt - 1);
+            t[u] = ei_nb[e];
+            pr[u] = ei_pair[e];
+        }
 #pragma unroll
-            for (int b = 0; b < DIM; ++b) f += Pi[3 * a + b] * x0[b];
-            dv[a] -= f * pr.w;
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int a = 0; a < DIM; ++a) Pi[u][a] = sP[(size_t)t[u] * DIM + a];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (k0 + u >= cnt) break;
+            const double x0[3] = {pr[u].x, pr[u].y, pr[u].z};
+#pragma unroll
+            for (int a = 0; a < DIM; ++a) {
+                const double row[3] = {Pi[u][a].x, Pi[u][a].y, Pi[u][a].z};
+                double f = 0.0;
+#pragma unroll
+                for (int b = 0; b < DIM; ++b) f += row[b] * x0[b];
+                dv[a] -= f * pr[u].w;
+            }
         }
     }
     double4 v = sv[s];
@@ -1184,16 +1226,18 @@ __global__ __launch_bounds__(256) void k_struct_velocity(DevParams P, int ns,
     for (int a = 0; a < DIM; ++a) vv[a] += ir * dv[a] * P.edt;
     double xx[3] = {xo.x, xo.y, xo.z};
     const int cl = clamp[s];
+    const double4 x0s = sx0[s];
     if (cl) {
-        const double4 x0 = sx0[s];
-        xx[0] = x0.x; xx[1] = x0.y; xx[2] = x0.z;
+        xx[0] = x0s.x; xx[1] = x0s.y; xx[2] = x0s.z;
         vv[0] = vv[1] = vv[2] = 0.0;
     } else if (P.module != MPH_MODULE_NONE) {
         for (int d = 0; d < 3; ++d) xx[d] += vv[d] * P.edt;
     }
     for (int d = 0; d < 3; ++d) xx[d] += vv[d] * P.edt;
     sv[s] = make_double4(vv[0], vv[1], vv[2], 0.0);
-    sx[s] = make_double4(xx[0], xx[1], xx[2], xo.w);
+    const double4 xn = make_double4(xx[0], xx[1], xx[2], xo.w);
+    sx[s] = xn;
+    su[s] = struct_disp(P, xn, x0s);
 }
 
 __global__ __launch_bounds__(256) void k_struct_scatter(int ns, const int* __restrict__ sorig,
@@ -1443,21 +1487,21 @@ void launch_structure(const Launch& L)
     const int ns = P.n_struct;
     if (ns == 0) return;
     const StructDev& S = *L.S;
-    MPH_LAUNCH("struct_gather", L.stream, k_struct_gather, dim3(blocks(ns, 256)), dim3(256), 0, L.stream, ns,
-               S.orig, L.rank_of, L.B, S.x, S.v);
+    MPH_LAUNCH("struct_gather", L.stream, k_struct_gather, dim3(blocks(ns, 256)), dim3(256), 0, L.stream, P, ns,
+               S.orig, L.rank_of, L.B, S.x0, S.x, S.v, S.u);
     for (int sub = 0; sub < P.substeps; ++sub) {
         if (P.dim == 3) {
             MPH_LAUNCH("struct_stress", L.stream, k_struct_stress<3>, dim3(blocks(ns, 256)), dim3(256), 0,
-                       L.stream, P, ns, S.x, S.x0, S.off, S.nb, S.pair_out, S.L, S.lame, S.P, S.F, S.E, S.S);
+                       L.stream, ns, S.wo, S.ocnt, S.eo_nb, S.eo_pair, S.u, S.L, S.lame, S.P, S.F, S.E, S.S);
             MPH_LAUNCH("struct_velocity", L.stream, k_struct_velocity<3>, dim3(blocks(ns, 256)), dim3(256), 0,
-                       L.stream, P, ns, S.off, S.pair_out, S.in_off, S.in_nb, S.pair_in, S.P, S.inv_rho,
-                       S.clamp, S.x0, S.x, S.v);
+                       L.stream, P, ns, S.wi, S.icnt, S.ei_nb, S.ei_pair, S.wx0, S.P, S.inv_rho, S.clamp, S.x0,
+                       S.x, S.v, S.u);
         } else {
             MPH_LAUNCH("struct_stress", L.stream, k_struct_stress<2>, dim3(blocks(ns, 256)), dim3(256), 0,
-                       L.stream, P, ns, S.x, S.x0, S.off, S.nb, S.pair_out, S.L, S.lame, S.P, S.F, S.E, S.S);
+                       L.stream, ns, S.wo, S.ocnt, S.eo_nb, S.eo_pair, S.u, S.L, S.lame, S.P, S.F, S.E, S.S);
             MPH_LAUNCH("struct_velocity", L.stream, k_struct_velocity<2>, dim3(blocks(ns, 256)), dim3(256), 0,
-                       L.stream, P, ns, S.off, S.pair_out, S.in_off, S.in_nb, S.pair_in, S.P, S.inv_rho,
-                       S.clamp, S.x0, S.x, S.v);
+                       L.stream, P, ns, S.wi, S.icnt, S.ei_nb, S.ei_pair, S.wx0, S.P, S.inv_rho, S.clamp, S.x0,
+                       S.x, S.v, S.u);
         }
     }
     MPH_LAUNCH("struct_scatter", L.stream, k_struct_scatter, dim3(blocks(ns, 256)), dim3(256), 0, L.stream,
