@@ -48,6 +48,10 @@
 #ifndef MPH_DIAG_NOSTORE
 #define MPH_DIAG_NOSTORE 0   // diagnostic builds only: the search counts but stores no list
 #endif
+#ifndef MPH_DIAG_GATHER
+#define MPH_DIAG_GATHER 0   // diagnostic builds only: 1 = list passes gather a coalesced dummy
+                            // neighbour (j = lane id ^ 1) instead of the listed one, 2 = gathers only
+#endif
 #ifndef MPH_SB
 #define MPH_SB 4   // candidates per batch in the search
 #endif
@@ -773,6 +777,7 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
             const int e = row[(k0 + u < cnt ? k0 + u : cnt - 1) * kTile];
             jj[u] = e & kIndexMask;
             TT[u] = e >> kTypeShift;
+            if (MPH_DIAG_GATHER == 1) jj[u] = min((int)(blockIdx.x * blockDim.x + threadIdx.x) ^ 1, P.n - 1);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -789,6 +794,7 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (k0 + u >= cnt) break;
+            if (MPH_DIAG_GATHER == 2) { o.da += X[u] + Y[u] + Z[u] + VX[u] + VY[u] + VZ[u] + TT[u]; continue; }
             const double q0 = image_exact<FAST>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
             const double q1 = image_exact<FAST>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
             const double q2 = image_exact<FAST || DIM == 2>(Z[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
@@ -864,6 +870,7 @@ __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_
             const int e = row[(k0 + u < cnt ? k0 + u : cnt - 1) * kTile];
             jj[u] = e & kIndexMask;
             TT[u] = e >> kTypeShift;
+            if (MPH_DIAG_GATHER == 1) jj[u] = min((int)(blockIdx.x * blockDim.x + threadIdx.x) ^ 1, P.n - 1);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -878,6 +885,7 @@ __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_
 #pragma unroll
         for (int u = 0; u < U; ++u) {
         if (k0 + u >= cnt) break;
+        if (MPH_DIAG_GATHER == 2) { f0 += X[u] + Y[u] + Z[u] + PJ[u] + TT[u]; continue; }
         const int tj = TT[u];
         if (solid && dev_is_struct(tj)) continue;
         const double q0 = image_exact<FAST>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
