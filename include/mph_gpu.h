@@ -127,7 +127,9 @@ typedef enum MphField {
     MPH_FIELD_NORMALIZER = 21,        /* double[n][3][3] */
     MPH_FIELD_LAMBDA_LAMES = 22,      /* double[n] */
     MPH_FIELD_MU_LAMES = 23,          /* double[n] */
-    MPH_FIELD_COUNT = 24
+    MPH_FIELD_VIRIAL_STRESS = 24,     /* double[n][3][3], VirialStressAtParticle (mph_compute_virial) */
+    MPH_FIELD_VIRIAL_PRESSURE = 25,   /* double[n], VirialPressureAtParticle (mph_compute_virial) */
+    MPH_FIELD_COUNT = 26
 } MphField;
 
 typedef struct MphCtx MphCtx;
@@ -188,6 +190,14 @@ int mph_write_vtk(MphCtx* ctx, const char* path);
  * calling thread (the context is destroyed on failure).                                        */
 const char* mph_last_error(const MphCtx* ctx);
 void mph_destroy(MphCtx* ctx);
+
+/* calculateVirialStressAtParticle (main.cpp:3077-3318), which the reference runs after the
+ * physics of every VTK output step (main.cpp:672-673): per-particle virial stress of the
+ * pressure (PressureP, PressureA), viscous and diffuse-interface pair forces over the step's
+ * neighbour list at the post-step positions and velocities, and VirialPressureAtParticle
+ * = -tr/dim.  Results are read with mph_get(MPH_FIELD_VIRIAL_STRESS / _PRESSURE); zeros until
+ * the first call.  Single-context mode only (slab mode: MPH_ERR_UNSUPPORTED).             */
+int mph_compute_virial(MphCtx* ctx);
 
 /* ---- measurement ---------------------------------------------------------------------------- */
 

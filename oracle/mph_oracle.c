@@ -52,6 +52,8 @@ struct OrcState {
     double *mass, *kappa, *lambda, *mu, *young, *dens_a, *pres_a, *vstrain, *div_p, *pres_p;
     double *lame_l, *lame_m;
     m33 *normalizer, *deform, *strain, *stress;
+    m33 *virial;              /* VirialStressAtParticle */
+    double *vpres;            /* VirialPressureAtParticle */
     int *ncount, *nlist;     /* [n][MAXN] like main.cpp:877-878 */
     int *sncount, *snlist;   /* InitialStructureNeighbor */
     int *cell_index, *cell_particle, *cell_begin, *cell_end;
@@ -849,6 +851,118 @@ static void orc_update_elastic(OrcState* s)
 
 /* ---------------------------------------------------------------- driver ------------------- */
 
+/* calculateVirialStressAtParticle, main.cpp:3077-3318: four pair loops, each accumulating its
+ * own stress[3][3] per particle and adding it to VirialStressAtParticle, then the pressure. */
+static void orc_virial_add(OrcState* s, int i, double st[3][3])
+{
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) s->virial[i][a][b] += st[a][b];
+}
+
+static void orc_virial(OrcState* s)
+{
+    const double cvis = s->dim == 2 ? 8.0 : 10.0;
+    memset(s->virial, 0, sizeof(m33) * (size_t)s->n);   /* 3083-3093 */
+    #pragma omp parallel for
+    for (int i = 0; i < s->n; ++i) {   /* pressureP, 3095-3125 */
+        double st[3][3] = {{0.0}};
+        for (int k = 0; k < s->ncount[i]; ++k) {
+            const int j = s->nlist[(size_t)i * MAXN + k];
+            double xij[3], r2;
+            orc_pair(s, i, j, xij, &r2);
+            if (s->rp * s->rp - r2 > 0) {
+                const double r = sqrt(r2);
+                const double dwij = k_dwp(s, r, s->rp);
+                const double gradw[3] = {dwij * xij[0] / r, dwij * xij[1] / r, dwij * xij[2] / r};
+                double fij[3];
+                for (int d = 0; d < 3; ++d) fij[d] = (s->pres_p[i]) * gradw[d] * s->vol;
+                for (int a = 0; a < 3; ++a)
+                    for (int b = 0; b < 3; ++b) st[a][b] += 1.0 * fij[a] * xij[b] / s->vol;
+            }
+        }
+        orc_virial_add(s, i, st);
+    }
+    #pragma omp parallel for
+    for (int i = 0; i < s->n; ++i) {   /* pressureA, 3127-3163 */
+        double st[3][3] = {{0.0}};
+        for (int k = 0; k < s->ncount[i]; ++k) {
+            const int j = s->nlist[(size_t)i * MAXN + k];
+            double xij[3], r2;
+            orc_pair(s, i, j, xij, &r2);
+            if (s->ra * s->ra - r2 > 0) {
+                const double ratio = s->c.interaction_ratio[s->prop[i]][s->prop[j]];
+                const double r = sqrt(r2);
+                const double dwij = ratio * k_dwa(s, r, s->ra);
+                const double gradw[3] = {dwij * xij[0] / r, dwij * xij[1] / r, dwij * xij[2] / r};
+                double fij[3];
+                for (int d = 0; d < 3; ++d) fij[d] = (s->pres_a[i]) * gradw[d] * s->vol;
+                for (int a = 0; a < 3; ++a)
+                    for (int b = 0; b < 3; ++b) st[a][b] += 1.0 * fij[a] * xij[b] / s->vol;
+            }
+        }
+        orc_virial_add(s, i, st);
+    }
+    #pragma omp parallel for
+    for (int i = 0; i < s->n; ++i) {   /* viscosity, 3165-3206 */
+        double st[3][3] = {{0.0}};
+        for (int k = 0; k < s->ncount[i]; ++k) {
+            const int j = s->nlist[(size_t)i * MAXN + k];
+            double xij[3], r2;
+            orc_pair(s, i, j, xij, &r2);
+            if (s->rv * s->rv - r2 > 0) {
+                const double r = sqrt(r2);
+                const double dwij = -k_dwv(s, r, s->rv);
+                const double e[3] = {xij[0] / r, xij[1] / r, xij[2] / r};
+                const double u[3] = {s->v[j][0] - s->v[i][0], s->v[j][1] - s->v[i][1], s->v[j][2] - s->v[i][2]};
+                const double muij = 2.0 * (s->mu[i] * s->mu[j]) / (s->mu[i] + s->mu[j]);
+                double fij[3];
+                for (int d = 0; d < 3; ++d)
+                    fij[d] = cvis * muij * (u[0] * e[0] + u[1] * e[1] + u[2] * e[2]) * e[d] * dwij / r * s->vol;
+                for (int a = 0; a < 3; ++a)
+                    for (int b = 0; b < 3; ++b) st[a][b] += 0.5 * fij[a] * xij[b] / s->vol;
+            }
+        }
+        orc_virial_add(s, i, st);
+    }
+    #pragma omp parallel for
+    for (int i = 0; i < s->n; ++i) {   /* diffuse interface, 3208-3282 */
+        double st[3][3] = {{0.0}};
+        for (int k = 0; k < s->ncount[i]; ++k) {
+            const int j = s->nlist[(size_t)i * MAXN + k];
+            double xij[3], r2;
+            orc_pair(s, i, j, xij, &r2);
+            if (s->rg * s->rg - r2 > 0) {   /* 1st term */
+                const double a = s->cofa[s->prop[i]] * (s->cofk) * (s->cofk);
+                const double ratio = s->c.interaction_ratio[s->prop[i]][s->prop[j]];
+                const double r = sqrt(r2);
+                const double w = ratio * k_wg(s, r, s->rg);
+                double fij[3];
+                for (int d = 0; d < 3; ++d)
+                    fij[d] = -a * (-s->gc[i][d]) * w / s->r2g * s->rg * (s->vol / s->dx);
+                for (int p = 0; p < 3; ++p)
+                    for (int q = 0; q < 3; ++q) st[p][q] += 1.0 * fij[p] * xij[q] / s->vol;
+            }
+            if (s->rg * s->rg - r2 > 0.0) {   /* 2nd term */
+                const double a = s->cofa[s->prop[i]] * (s->cofk) * (s->cofk);
+                const double ratio = s->c.interaction_ratio[s->prop[i]][s->prop[j]];
+                const double r = sqrt(r2);
+                const double dw = ratio * k_dwg(s, r, s->rg);
+                const double gradw[3] = {dw * xij[0] / r, dw * xij[1] / r, dw * xij[2] / r};
+                double gr = 0.0;
+                for (int d = 0; d < 3; ++d) gr += (-s->gc[i][d]) * xij[d];
+                double fij[3];
+                for (int d = 0; d < 3; ++d) fij[d] = -a * (gr) * gradw[d] / s->r2g * s->rg * (s->vol / s->dx);
+                for (int p = 0; p < 3; ++p)
+                    for (int q = 0; q < 3; ++q) st[p][q] += 1.0 * fij[p] * xij[q] / s->vol;
+            }
+        }
+        orc_virial_add(s, i, st);
+    }
+    for (int i = 0; i < s->n; ++i)   /* 3285-3294 */
+        s->vpres[i] = s->dim == 2 ? -1.0 / 2.0 * (s->virial[i][0][0] + s->virial[i][1][1])
+                                  : -1.0 / 3.0 * (s->virial[i][0][0] + s->virial[i][1][1] + s->virial[i][2][2]);
+}
+
 static void orc_one_step(OrcState* s)   /* main.cpp:597-686 without I/O */
 {
     orc_wall(s);
@@ -900,6 +1014,7 @@ OrcState* orc_create(const MphConfig* cfg, int n, const int* property, const dou
     ALLOC(s->vstrain, n); ALLOC(s->div_p, n); ALLOC(s->pres_p, n); ALLOC(s->lame_l, n);
     ALLOC(s->lame_m, n); ALLOC(s->normalizer, n); ALLOC(s->deform, n); ALLOC(s->strain, n);
     ALLOC(s->stress, n); ALLOC(s->ncount, n); ALLOC(s->sncount, n);
+    ALLOC(s->virial, n); ALLOC(s->vpres, n);
     s->nlist = (int*)malloc(sizeof(int) * (size_t)n * MAXN);
     s->snlist = (int*)malloc(sizeof(int) * (size_t)n * MAXN);
     memcpy(s->prop, property, sizeof(int) * n);
@@ -954,6 +1069,7 @@ int orc_call(OrcState* s, const char* name)
         {"calculateAcceleration", orc_kick}, {"calculateConvection", orc_convection},
         {"calculateElasticDeformationVector", orc_deformation}, {"calculateStress", orc_stress},
         {"calculateStressForce", orc_stress_force}, {"updateElasticPosition", orc_update_elastic},
+        {"calculateVirialStressAtParticle", orc_virial},
     };
     for (size_t k = 0; k < sizeof table / sizeof table[0]; ++k)
         if (strcmp(name, table[k].name) == 0) { table[k].fn(s); return 0; }
@@ -974,6 +1090,7 @@ int orc_get(OrcState* s, const char* name, void* out)
         {"Lambda", s->lambda, 1, 0}, {"Mu", s->mu, 1, 0}, {"LambdaLames", s->lame_l, 1, 0},
         {"MuLames", s->lame_m, 1, 0}, {"NeighborCount", s->ncount, 1, 1},
         {"InitialStructureNeighborCount", s->sncount, 1, 1}, {"Property", s->prop, 1, 1},
+        {"VirialStressAtParticle", s->virial, 9, 0}, {"VirialPressureAtParticle", s->vpres, 1, 0},
     };
     for (size_t k = 0; k < sizeof f / sizeof f[0]; ++k)
         if (strcmp(name, f[k].name) == 0) {
@@ -1021,7 +1138,7 @@ void orc_destroy(OrcState* s)
                     s->mu, s->young, s->dens_a, s->pres_a, s->vstrain, s->div_p, s->pres_p,
                     s->lame_l, s->lame_m, s->normalizer, s->deform, s->strain, s->stress,
                     s->ncount, s->nlist, s->sncount, s->snlist, s->cell_index, s->cell_particle,
-                    s->cell_begin, s->cell_end};
+                    s->cell_begin, s->cell_end, s->virial, s->vpres};
     for (size_t k = 0; k < sizeof ptrs / sizeof ptrs[0]; ++k) free(ptrs[k]);
     free(s);
 }

@@ -576,6 +576,21 @@ int mph_get(MphCtx* c, int field, void* out)
         for (int s = 0; s < ns; ++s)
             std::memcpy(o + (size_t)9 * c->S.orig[s], &c->S.normalizer[(size_t)9 * s], sizeof(double) * 9);
         return MPH_OK;
+    case MPH_FIELD_VIRIAL_STRESS:
+    case MPH_FIELD_VIRIAL_PRESSURE: {
+        const int w = field == MPH_FIELD_VIRIAL_STRESS ? 9 : 1;
+        std::memset(o, 0, sizeof(double) * w * (size_t)n);
+        if (!c->vir) return MPH_OK;   // never computed (the reference's array is uninitialised)
+        std::vector<double> h((size_t)w * c->n);
+        std::vector<int> id(c->n);
+        HIP_OK(c, hipMemcpyAsync(h.data(), w == 9 ? c->vir : c->vpres, sizeof(double) * w * c->n,
+                                 hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(c, hipMemcpyAsync(id.data(), c->A.id, sizeof(int) * c->n, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(c, hipStreamSynchronize(c->stream));
+        for (int i = 0; i < c->n; ++i)
+            if (id[i] >= 0) std::memcpy(o + (size_t)w * id[i], &h[(size_t)w * i], sizeof(double) * w);
+        return MPH_OK;
+    }
     case MPH_FIELD_LAMBDA_LAMES:
     case MPH_FIELD_MU_LAMES:
         std::memset(o, 0, sizeof(double) * n);
@@ -584,6 +599,23 @@ int mph_get(MphCtx* c, int field, void* out)
         return MPH_OK;
     default: return fail(c, MPH_ERR_ARG, "unknown field " + std::to_string(field));
     }
+}
+
+int mph_compute_virial(MphCtx* c)
+{
+    if (!c) return MPH_ERR_ARG;
+    if (c->dist) return fail(c, MPH_ERR_UNSUPPORTED, "mph_compute_virial: single-context mode only");
+    HIP_OK(c, hipSetDevice(c->device));
+    if (!c->vir) {
+        const size_t cap = (size_t)std::max(c->n, 1);
+        CK(dalloc(c, &c->vir, 9 * cap));
+        CK(dalloc(c, &c->vpres, cap));
+    }
+    // after a step the integrated state B is in A (list) order; before the first step A is current
+    launch_virial(c->L, c->stepped ? c->B : c->A, c->vir, c->vpres);
+    HIP_OK(c, hipGetLastError());
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    return MPH_OK;
 }
 
 int mph_set(MphCtx* c, int field, const void* in)

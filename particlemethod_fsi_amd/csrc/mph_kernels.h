@@ -82,6 +82,7 @@ void launch_neighbors(const Launch& L);
 void launch_pass_a(const Launch& L);
 void launch_pass_b(const Launch& L, int phase = 0);   // phase: 0 all, 1/2 slab inner/near-face
 void launch_structure(const Launch& L);
+void launch_virial(const Launch& L, const Soa& X, double* vir, double* vpres);   // X: state in A order
 
 // slab decomposition (mph_dist.hip)
 struct HaloFields {

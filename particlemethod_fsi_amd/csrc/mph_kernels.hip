@@ -1021,6 +1021,80 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
     B.id[i] = A.id[i];
 }
 
+// ------------------------------------------------------------------------ virial stress ----
+
+// calculateVirialStressAtParticle (main.cpp:3077-3318) for particle i of the current (post-step)
+// state: B holds the integrated positions and velocities in A order, the list and the pass-A
+// products (PressureP, PressureA, GravityCenter) are this step's.  The reference's four pair
+// loops (PressureP 3093-3125, PressureA 3127-3163, viscosity 3165-3206, diffuse interface
+// 3208-3282) are one sweep here; every term keeps its own radius test.  All particles, any type.
+template <int DIM>
+__global__ __launch_bounds__(256) void k_virial(DevParams P, const DevTables* __restrict__ T, Soa A, Soa B,
+                                                const double* __restrict__ pres, const double* __restrict__ pa,
+                                                const double* __restrict__ gx, const double* __restrict__ gy,
+                                                const double* __restrict__ gz, const int* __restrict__ nbr,
+                                                const int* __restrict__ ncount, double* __restrict__ vir,
+                                                double* __restrict__ vpres)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    const int ti = A.type[i];
+    const double xi = B.x[i], yi = B.y[i], zi = B.z[i];
+    const double vxi = B.vx[i], vyi = B.vy[i], vzi = B.vz[i];
+    const double pi = pres[i], pai = pa[i];
+    const double gi[3] = {gx[i], gy[i], gz[i]};
+    const double a = T->cofa[ti] * P.cofk * P.cofk;
+    const double dscale = P.rg / P.r2g * (P.vol / P.dx);
+    const double cvis = DIM == 2 ? 8.0 : 10.0;
+    double S[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
+    const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
+    const int* row = ell_row(nbr, i);
+    for (int k = 0; k < cnt; ++k) {
+        const int e = row[k * kTile];
+        const int j = e & kIndexMask, tj = e >> kTypeShift;
+        double q[3];
+        q[0] = image_exact<false>(B.x[j] - xi, P.dw[0], P.hw[0], P.w075[0]);
+        q[1] = image_exact<false>(B.y[j] - yi, P.dw[1], P.hw[1], P.w075[1]);
+        q[2] = image_exact<DIM == 2>(B.z[j] - zi, P.dw[2], P.hw[2], P.w075[2]);
+        const double r2 = r2_exact(q[0], q[1], q[2]);
+        if (!(r2 < P.rp2 || r2 < P.ra2 || r2 < P.rv2 || r2 < P.rg2)) continue;
+        const double r = sqrt(r2), ir = 1.0 / r;
+        const double ratio = T->ratio[ti * kTypes + tj];
+        // pair force f_ij = c q_ij + g1 (every term is along q_ij except the first
+        // diffuse-interface term); the virial adds f_ij (x) q_ij / V
+        double c = 0.0;
+        if (r2 < P.rp2) c += pi * (P.cdp * (1.0 - r * P.inv_rp)) * ir * P.vol;          // 3111-3120
+        if (r2 < P.ra2) {                                                                // 3147-3156
+            const double t = r * P.inv_ra;
+            c += pai * (ratio * (P.cda * (1.0 - t) * (1.0 - 3.0 * t))) * ir * P.vol;
+        }
+        if (r2 < P.rv2) {                                                                // 3183-3199 (x 0.5)
+            const double dv = (B.vx[j] - vxi) * q[0] + (B.vy[j] - vyi) * q[1] + (B.vz[j] - vzi) * q[2];
+            const double dwij = -(P.cdv * (1.0 - r * P.inv_rv));
+            c += 0.5 * (cvis * T->mu_ij[ti * kTypes + tj] * dv * dwij * (ir * ir * ir) * P.vol);
+        }
+        double g1[3] = {0.0, 0.0, 0.0};
+        if (r2 < P.rg2) {                                                                // 3225-3276
+            const double omt = 1.0 - r * P.inv_rg;
+            const double w = ratio * (P.cg * omt * omt);
+            const double dw = ratio * (P.cdg * omt);
+            const double gr = -(gi[0] * q[0] + gi[1] * q[1] + gi[2] * q[2]);
+            for (int d = 0; d < 3; ++d) g1[d] = a * gi[d] * w * dscale;                 // -a (-GC_i) w
+            c += -a * gr * dw * ir * dscale;
+        }
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+#pragma unroll
+            for (int v = 0; v < 3; ++v) S[u][v] += (c * q[u] + g1[u]) * q[v] / P.vol;
+    }
+    double* o = vir + (size_t)i * 9;
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+        for (int v = 0; v < 3; ++v) o[3 * u + v] = S[u][v];
+    vpres[i] = DIM == 2 ? -1.0 / 2.0 * (S[0][0] + S[1][1]) : -1.0 / 3.0 * (S[0][0] + S[1][1] + S[2][2]);
+}
+
 // ------------------------------------------------------------------------ elastic solid ----
 
 // Displacement u = Mod(x - x0 + W/2, W) - W/2 of calculateElasticDeformationVector (2700-2712),
@@ -1486,6 +1560,19 @@ void launch_pass_b(const Launch& L, int phase)
         if (P.dim == 3) MPH_PASS_B(false, 3); else MPH_PASS_B(false, 2);
     }
 #undef MPH_PASS_B
+}
+
+void launch_virial(const Launch& L, const Soa& X, double* vir, double* vpres)
+{
+    Profiler* prof = L.prof;
+    const DevParams& P = *L.P;
+    if (P.n == 0) return;
+    if (P.dim == 3)
+        MPH_LAUNCH("virial", L.stream, k_virial<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T, L.A, X,
+                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, vir, vpres);
+    else
+        MPH_LAUNCH("virial", L.stream, k_virial<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T, L.A, X,
+                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, vir, vpres);
 }
 
 void launch_structure(const Launch& L)

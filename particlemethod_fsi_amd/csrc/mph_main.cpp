@@ -126,6 +126,9 @@ int main(int argc, char** argv)
         steps_run += k;
         for (int s = 0; s < k; ++s) {
             if (vtk_after && s == k - 1) {
+                // main.cpp:672-673: the virial diagnostic runs before every VTK write
+                rc = mph_compute_virial(ctx);
+                if (rc) die(ctx, rc, "mph_compute_virial");
                 std::snprintf(name, sizeof(name), vtk.c_str(), istep);
                 rc = mph_write_vtk(ctx, name);
                 if (rc) die(ctx, rc, "writing a .vtk file");

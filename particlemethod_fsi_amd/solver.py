@@ -37,6 +37,7 @@ FIELDS = {
     "Strain": (19, 9, np.float64), "Stress": (20, 9, np.float64),
     "Normalizer": (21, 9, np.float64), "LambdaLames": (22, 1, np.float64),
     "MuLames": (23, 1, np.float64),
+    "VirialStressAtParticle": (24, 9, np.float64), "VirialPressureAtParticle": (25, 1, np.float64),
 }
 
 STATUS = {0: "MPH_OK", -1: "MPH_ERR_ARG", -2: "MPH_ERR_IO", -3: "MPH_ERR_NEIGHBOR_OVERFLOW",
@@ -51,7 +52,7 @@ EXPORTED_SYMBOLS = [
     "mph_write_vtk", "mph_last_error", "mph_destroy", "mph_profile_steps", "mph_neighbor_stats",
     "mph_dist_unique_id", "mph_create_dist", "mph_owned_count", "mph_derive_scalars",
     "mph_structure_init", "mph_create_dist_host", "mph_owned_ids", "mph_slab_bounds",
-    "mph_slab_owner", "mph_dist_selftest",
+    "mph_slab_owner", "mph_dist_selftest", "mph_compute_virial",
 ]
 
 # mph_host_exchange_fn (include/mph_gpu.h): (user, send_l, n, send_r, n, recv_l, n, recv_r, n)
@@ -121,6 +122,7 @@ def load_library() -> ctypes.CDLL:
         "mph_dist_selftest": (ip, [ip]),
         "mph_derive_scalars": (ip, [cfgp, vp]),
         "mph_structure_init": (ip, [cfgp, ip, vp, vp, vp, vp, vp, vp]),
+        "mph_compute_virial": (ip, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -304,6 +306,11 @@ class MphSolver:
         out = np.zeros(max(self.n, 1), np.int32)
         _check(self._L.mph_owned_ids(self._h, out.ctypes.data), self._h)
         return out[:k].copy()
+
+    def compute_virial(self):
+        """calculateVirialStressAtParticle (main.cpp:3077-3318) on the current state; read the result
+        with get("VirialStressAtParticle") / get("VirialPressureAtParticle")."""
+        _check(self._L.mph_compute_virial(self._h), self._h)
 
     def neighbor_stats(self):
         m = ctypes.c_double()

@@ -94,6 +94,11 @@ def run_case(name: str):
         if solid.any():
             names = names + SOLID
         snap("s%d" % s, names, True)
+        if k == 0:
+            # the VTK-step diagnostic (main.cpp:672-673) on the first stepped state; it writes
+            # only the two virial arrays, so the run continues unchanged
+            ref.call("calculateVirialStressAtParticle")
+            snap("s%d" % s, ["VirialStressAtParticle", "VirialPressureAtParticle"], True)
         if k == 0 and name == "dam2d":
             rows = [np.sort(ref.neighbors(i)) for i in range(ref.n)]
             out["s%d/nbr_offsets" % s] = np.cumsum([0] + [len(r) for r in rows]).astype(np.int32)

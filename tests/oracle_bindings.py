@@ -25,11 +25,13 @@ ORACLE_LIB = os.path.join(ORACLE_DIR, "_build", "libmph_oracle.so")
 REF_DIR = os.path.join(ORACLE_DIR, "_ref")
 
 VEC3 = {"Position", "InitialPosition", "Velocity", "Force", "Acceleration", "GravityCenter"}
-MAT3 = {"DeformGradient", "Strain", "Stress", "Normalizer"}
+MAT3 = {"DeformGradient", "Strain", "Stress", "Normalizer", "VirialStressAtParticle"}
 INTS = {"NeighborCount", "InitialStructureNeighborCount", "Property"}
 SCALARS = {"PressureP", "PressureA", "DensityA", "VolStrainP", "DivergenceP", "Mass", "Kappa",
-           "Lambda", "Mu", "LambdaLames", "MuLames"}
-ALL_FIELDS = sorted(VEC3 | MAT3 | INTS | SCALARS)
+           "Lambda", "Mu", "LambdaLames", "MuLames", "VirialPressureAtParticle"}
+# the virial diagnostic (main.cpp:3077-3318) is only defined after calculateVirialStressAtParticle
+VIRIAL = {"VirialStressAtParticle", "VirialPressureAtParticle"}
+ALL_FIELDS = sorted((VEC3 | MAT3 | INTS | SCALARS) - VIRIAL)
 
 
 def build_oracle() -> str:

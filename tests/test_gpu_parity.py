@@ -25,7 +25,8 @@ pytestmark = pytest.mark.gpu
 # (lambda + 2 mu) * 1e-15 ~ 1e-10 Pa until gravity loads the solid.
 FLOOR = {"PressureP": 1e-9, "PressureA": 1e-9, "Force": 1e-15, "Acceleration": 1e-12,
          "VolStrainP": 1e-13, "DivergenceP": 1e-12, "DensityA": 1e-13, "GravityCenter": 1e-16,
-         "DeformGradient": 1e-13, "Strain": 1e-13, "Stress": 1e-8}
+         "DeformGradient": 1e-13, "Strain": 1e-13, "Stress": 1e-8,
+         "VirialStressAtParticle": 1e-9, "VirialPressureAtParticle": 1e-9}
 
 
 def tol(field: str, step: int, ref: np.ndarray) -> float:
@@ -42,6 +43,8 @@ def tol(field: str, step: int, ref: np.ndarray) -> float:
 
 def compare(g: Golden, solver: MphSolver, step: int):
     report = {}
+    if g.has(step, "VirialStressAtParticle"):
+        solver.compute_virial()   # the reference's VTK-step diagnostic, main.cpp:672-673
     for f in g.fields(step):
         ref = g.get(step, f)
         mine = restrict(g, f, solver.get(f))
@@ -100,6 +103,13 @@ def test_gpu_matches_oracle_every_step(case, nsteps):
                 scale = float(np.max(np.abs(b))) if b.size else 0.0
                 t = {"Position": 1e-12, "Velocity": 1e-9}.get(f, rel * scale + FLOOR.get(f, 1e-12))
                 assert float(np.max(np.abs(a - b))) <= t, (k, f, float(np.max(np.abs(a - b))), t)
+            if k == nsteps - 1:
+                s.compute_virial()
+                o.call("calculateVirialStressAtParticle")
+                for f in ["VirialStressAtParticle", "VirialPressureAtParticle"]:
+                    a, b = s.get(f), o.get(f)
+                    t = rel * float(np.max(np.abs(b))) + FLOOR[f]
+                    assert float(np.max(np.abs(a - b))) <= t, (k, f, float(np.max(np.abs(a - b))), t)
             if solid.any():
                 for f in ["DeformGradient", "Stress", "Strain"]:
                     a, b = s.get(f)[solid], o.get(f)[solid]
