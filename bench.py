@@ -65,14 +65,14 @@ from oracle_bindings import RefSolver, OracleSolver, ref_available
 c = cases.get(%(case)r)
 cfg, p = c.build()
 threads = int(os.environ.get('OMP_NUM_THREADS', os.cpu_count() or 1))
-if ref_available(c.dim, c.module):
+if ref_available(c.dim, c.ref_variant):
     d = tempfile.mkdtemp(prefix='mphcpu_')
     dp, gp = os.path.join(d, 'c.data'), os.path.join(d, 'c.grid')
     open(dp, 'w').write(cases.data_text(c.data()))
     L = solver.load_library()
     L.mph_write_prof_arrays(gp.encode(), ctypes.byref(cfg), 0.0, p.n, p.property.ctypes.data,
                             p.position.ctypes.data, p.initial_position.ctypes.data, p.velocity.ctypes.data)
-    s = RefSolver(c.dim, c.module, dp, gp); kind = 'reference'
+    s = RefSolver(c.dim, c.ref_variant, dp, gp); kind = 'reference'
 else:
     s = OracleSolver(cfg, p); kind = 'port'
 s.init()

@@ -40,7 +40,7 @@ extern "C" {
 
 #define MPH_TYPE_COUNT 6            /* main.cpp:68 */
 #define MPH_MAX_NEIGHBOR_COUNT 512  /* main.cpp:100 (semantic limit; overflow is an error here) */
-#define MPH_ABI_VERSION 1
+#define MPH_ABI_VERSION 2
 
 /* Compile-time case modules of the reference (main.cpp:54-59) as a runtime switch.  The module
  * selects the clamp rule of updateElasticPosition (main.cpp:1918-2044).                        */
@@ -52,6 +52,15 @@ typedef enum MphModule {
     MPH_MODULE_HYDROELASTIC = 4, /* Hydroelastic: x0.x<0.01||>1.99, force zeroed     (2019-2044) */
     MPH_MODULE_NONE = 5          /* no clamp (only the unconditional drift of 2070-2079)          */
 } MphModule;
+
+/* calculateWall (main.cpp:2963-3072): the shipped rigid motion (the `#else` branch 3031-3071:
+ * rotation WallRotation + translation WallVelocity while Time < 0.2) or the compile-time
+ * `Rolling` branch (2974-3030: every step the walls turn about z through WallCenter by
+ * dtheta = MAX_ANGLE [sin(w t) - sin(w (t - Dt))], w = 2 pi / ROLLING_PERIOD, main.cpp:2959-2960). */
+typedef enum MphWallMotion {
+    MPH_WALL_RIGID = 0,
+    MPH_WALL_ROLLING = 1
+} MphWallMotion;
 
 typedef enum MphStatus {
     MPH_OK = 0,
@@ -99,7 +108,11 @@ typedef struct MphConfig {
     double particle_spacing;          /* .grid line 2 */
     double domain_min[3];
     double domain_max[3];
+    int    wall_motion;               /* MphWallMotion (compile-time `Rolling`, main.cpp:58) */
 } MphConfig;
+
+/* sizeof(MphConfig) as compiled into the library (FFI bindings check their mirror against it). */
+int mph_config_sizeof(void);
 
 /* Per-particle arrays readable with mph_get (original particle order). */
 typedef enum MphField {

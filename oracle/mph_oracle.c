@@ -624,6 +624,35 @@ static void orc_wall(OrcState* s)
 {
     for (int i = s->wall_b; i < s->wall_e; ++i)
         for (int d = 0; d < 3; ++d) s->f[i][d] = 0.0;
+    if (s->c.wall_motion == MPH_WALL_ROLLING) {   /* the `Rolling` branch, main.cpp:2974-3029 */
+        const double max_angle = (2.0 * M_PI / 180.0), period = 1.646;   /* 2959-2960 */
+        const double omega_t = 2.0 * M_PI / period;
+        const double theta = max_angle * sin(omega_t * s->time);
+        const double dtheta_dt = max_angle * omega_t * cos(omega_t * s->time);
+        const double theta_prev = max_angle * sin(omega_t * (s->time - s->dt));
+        const double delta_theta = theta - theta_prev;
+        const double cosD = cos(delta_theta), sinD = sin(delta_theta);
+        const double Rz[3][3] = {{cosD, -sinD, 0.0}, {sinD, cosD, 0.0}, {0.0, 0.0, 1.0}};
+        for (int i = s->wall_b; i < s->wall_e; ++i) {
+            const int t = s->prop[i];
+            const double* C = s->wall_c[t];
+            const double r[3] = {s->x[i][0] - C[0], s->x[i][1] - C[1], s->x[i][2] - C[2]};
+            double rr[3];
+            rr[0] = Rz[0][0] * r[0] + Rz[0][1] * r[1];
+            rr[1] = Rz[1][0] * r[0] + Rz[1][1] * r[1];
+            rr[2] = r[2];
+            const double w[3] = {0.0, 0.0, dtheta_dt};
+            s->v[i][0] = w[1] * rr[2] - w[2] * rr[1];
+            s->v[i][1] = w[2] * rr[0] - w[0] * rr[2];
+            s->v[i][2] = w[0] * rr[1] - w[1] * rr[0];
+            s->x[i][0] = rr[0] + C[0];
+            s->x[i][1] = rr[1] + C[1];
+            s->x[i][2] = rr[2] + C[2];
+        }
+        for (int t = 4; t < 6; ++t)
+            for (int d = 0; d < 3; ++d) s->wall_c[t][d] += s->c.wall_velocity[t][d] * s->dt;
+        return;
+    }
     for (int i = s->wall_b; i < s->wall_e; ++i) {
         if (!(s->time < 0.2)) continue;
         const int t = s->prop[i];

@@ -39,7 +39,10 @@ def data_text(values: dict) -> str:
     """A .data file in the reference's keyword format (main.cpp:743-767)."""
     lines = ["#######"]
     for k, v in values.items():
-        lines.append("%s\t%s" % (k, "\t".join(repr(float(x)) for x in v)))
+        if isinstance(v, str):   # e.g. "Wall6" -> "Center x y z Velocity ... Omega ..." (main.cpp:766)
+            lines.append("%s  %s" % (k, v))
+        else:
+            lines.append("%s\t%s" % (k, "\t".join(repr(float(x)) for x in v)))
     return "\n".join(lines) + "\n"
 
 
@@ -54,6 +57,12 @@ class Case:
     cuboids: list
     data_changes: dict = field(default_factory=dict)
     note: str = ""
+    wall_motion: int = 0   # MphWallMotion: 1 = the reference's compile-time `Rolling` (main.cpp:58)
+
+    @property
+    def ref_variant(self) -> str:
+        """Which oracle/_ref build holds the reference for this case (module + #defines)."""
+        return self.module + ("_rolling" if self.wall_motion else "")
 
     def describe(self) -> str:
         """One-line description for bench.py's config.workload."""
@@ -69,6 +78,7 @@ class Case:
         cfg = mphio.config_default(self.dim, self.module)
         _apply_data(cfg, self.data())
         parts = mphio.generate(self.cuboids)
+        cfg.wall_motion = self.wall_motion
         cfg.time = 0.0
         cfg.particle_spacing = mphio._e(self.spacing)
         for d in range(3):
@@ -193,6 +203,18 @@ _reg(Case("dam2d_st", 2, "bar", 0.001, CASES["dam2d"].lower, CASES["dam2d"].uppe
           CASES["dam2d"].cuboids, data_changes=_ST, note="dam2d with surface tension"))
 _reg(Case("box3d_st", 3, "dam", 0.001, CASES["box3d"].lower, CASES["box3d"].upper,
           CASES["box3d"].cuboids, data_changes=_ST, note="box3d with surface tension"))
+
+
+# the `Rolling` wall motion (calculateWall main.cpp:2974-3030): the tank walls turn about z
+# through WallCenter (Wall6 = type 4) by MAX_ANGLE sin(2 pi t / 1.646) while the fluid settles
+_ROLL = {"Wall6": "Center 0.1 0.1 0.0 Velocity 0.0 0.0 0.0 Omega 0.0 0.0 0.0"}
+_reg(Case("rolling2d", 2, "dam", 0.001, CASES["dam2d"].lower, CASES["dam2d"].upper,
+          CASES["dam2d"].cuboids, data_changes=_ROLL, wall_motion=1,
+          note="dam2d in a rolling tank (Rolling wall motion)"))
+_reg(Case("rolling3d", 3, "dam", 0.001, CASES["box3d"].lower, CASES["box3d"].upper,
+          CASES["box3d"].cuboids, data_changes={"Wall6": "Center 0.0125 0.0125 0.006 Velocity 0.0 0.0 0.0 "
+                                                         "Omega 0.0 0.0 0.0"}, wall_motion=1,
+          note="box3d in a rolling tank (Rolling wall motion)"))
 
 
 # elastic sub-stepping (main.cpp:653-663): ElasticDt = Dt/5 -> 5 substeps per step.  With the

@@ -14,6 +14,8 @@
 
 using namespace mph;
 
+extern "C" int mph_config_sizeof(void) { return (int)sizeof(MphConfig); }
+
 extern "C" int mph_config_default(MphConfig* cfg, int dim, int module)
 {
     if (!cfg || (dim != 2 && dim != 3) || module < 0 || module > MPH_MODULE_NONE) return MPH_ERR_ARG;
@@ -393,6 +395,7 @@ void make_dev_params(const MphConfig& c, const HostDerived& h, int n, int n_stru
     P.slab_axis = -1;
     P.dim = c.dim;
     P.module = c.module;
+    P.wall_motion = c.wall_motion;
     P.n_struct = n_struct;
     P.substeps = (int)(c.dt / c.elastic_dt + 0.5);
     for (int d = 0; d < 3; ++d) {

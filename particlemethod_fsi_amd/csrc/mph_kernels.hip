@@ -176,7 +176,29 @@ __device__ __forceinline__ void move_and_wrap(const DevParams& P, const DevState
 {
 #pragma clang fp contract(off)
     const int t = B.type[p];
-    if (dev_is_wall(t) && st->time < 0.2) {
+    if (dev_is_wall(t) && P.wall_motion == MPH_WALL_ROLLING) {
+        // the Rolling branch of calculateWall (main.cpp:2974-3022): rotate about z through
+        // WallCenter by the step's angle increment; the velocity is omega(t) x r_rot
+        const double max_angle = 2.0 * M_PI / 180.0, period = 1.646;   // main.cpp:2959-2960
+        const double omega_t = 2.0 * M_PI / period;
+        const double theta = max_angle * sin(omega_t * st->time);
+        const double dtheta_dt = max_angle * omega_t * cos(omega_t * st->time);
+        const double theta_prev = max_angle * sin(omega_t * (st->time - P.dt));
+        const double delta_theta = theta - theta_prev;
+        const double cosD = cos(delta_theta), sinD = sin(delta_theta);
+        const double* C = st->wall_c[t];
+        const double r0 = x - C[0], r1 = y - C[1], r2 = z - C[2];
+        const double a0 = cosD * r0 + -sinD * r1;
+        const double a1 = sinD * r0 + cosD * r1;
+        const double a2 = r2;
+        const double w0 = 0.0, w1 = 0.0, w2 = dtheta_dt;
+        B.vx[p] = w1 * a2 - w2 * a1;
+        B.vy[p] = w2 * a0 - w0 * a2;
+        B.vz[p] = w0 * a1 - w1 * a0;
+        x = a0 + C[0];
+        y = a1 + C[1];
+        z = a2 + C[2];
+    } else if (dev_is_wall(t) && st->time < 0.2) {
         const double* C = st->wall_c[t];
         const double* V = st->wall_vel[t];
         const double* w = st->wall_omega[t];

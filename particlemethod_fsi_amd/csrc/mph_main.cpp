@@ -65,6 +65,9 @@ int main(int argc, char** argv)
         for (int k = 0; k < 6; ++k)
             if (std::strcmp(m, names[k]) == 0) cfg.module = k;
     }
+    // the `Rolling` wall-motion #define of main.cpp:58 (calculateWall 2974-3030)
+    if (const char* w = std::getenv("MPH_WALL_MOTION"))
+        cfg.wall_motion = std::strcmp(w, "rolling") == 0 ? MPH_WALL_ROLLING : std::atoi(w);
     int rc = mph_read_data_file(data.c_str(), &cfg);
     if (rc) die(nullptr, rc, "reading the data file");
     int n = 0;

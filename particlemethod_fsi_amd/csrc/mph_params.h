@@ -29,7 +29,8 @@ struct DevParams {
     int n;             // particles held by this context
     int dim;           // 2 or 3
     int module;        // MphModule
-    int surface;       // any CofA != 0 -> surface-tension terms live (K12/K13)
+    int wall_motion;   // MphWallMotion
+    int surface;      // any CofA != 0 -> surface-tension terms live (K12/K13)
     int n_struct;      // structure particles (types 2,3)
     int gc[3];         // GPU linked-cell grid (gc[2] == 1 in 2-D)
     int ncell;         // gc[0]*gc[1]*gc[2]

@@ -56,6 +56,7 @@ class MphConfig(ctypes.Structure):
         ("particle_spacing", ctypes.c_double),
         ("domain_min", _D3),
         ("domain_max", _D3),
+        ("wall_motion", ctypes.c_int),
     ]
 
     def copy(self) -> "MphConfig":

@@ -53,6 +53,7 @@ EXPORTED_SYMBOLS = [
     "mph_dist_unique_id", "mph_create_dist", "mph_owned_count", "mph_derive_scalars",
     "mph_structure_init", "mph_create_dist_host", "mph_owned_ids", "mph_slab_bounds",
     "mph_slab_owner", "mph_dist_selftest", "mph_compute_virial",
+    "mph_config_sizeof",
 ]
 
 # mph_host_exchange_fn (include/mph_gpu.h): (user, send_l, n, send_r, n, recv_l, n, recv_r, n)
@@ -123,6 +124,7 @@ def load_library() -> ctypes.CDLL:
         "mph_derive_scalars": (ip, [cfgp, vp]),
         "mph_structure_init": (ip, [cfgp, ip, vp, vp, vp, vp, vp, vp]),
         "mph_compute_virial": (ip, [vp]),
+        "mph_config_sizeof": (ip, []),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

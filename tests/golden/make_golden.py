@@ -50,6 +50,8 @@ PLAN = {  # case -> steps (cumulative) to snapshot; the first is the full-field 
     "box3d_st": [1, 10],
     "gate2d_sub": [1, 10, 100],
     "gate3d_sub": [1, 10, 50],
+    "rolling2d": [1, 10, 100],
+    "rolling3d": [1, 10, 30],
 }
 
 
@@ -59,7 +61,7 @@ def run_case(name: str):
     c = cases.get(name)
     tmp = tempfile.mkdtemp(prefix="golden_")
     dp, gp = write_case_files(cases.data_text(c.data()), c.grid_text(), tmp)
-    ref = RefSolver(c.dim, c.module, dp, gp)
+    ref = RefSolver(c.dim, c.ref_variant, dp, gp)
     ref.init()
     prop = ref.get("Property")
     solid = (prop >= 2) & (prop < 4)

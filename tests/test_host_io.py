@@ -38,7 +38,8 @@ def test_config_struct_layout_matches_header():
     cfg = mphio.MphConfig()
     assert L.mph_config_default(ctypes.byref(cfg), 3, 1) == 0
     assert cfg.dim == 3 and cfg.module == 1 and cfg.dt == 1e100 and cfg.elastic_dt == 1e100
-    assert ctypes.sizeof(mphio.MphConfig) == 8 + 8 * (8 + 7 * 6 + 36 + 3 + 3 * 18 + 2 + 6)
+    assert ctypes.sizeof(mphio.MphConfig) == 8 + 8 * (8 + 7 * 6 + 36 + 3 + 3 * 18 + 2 + 6) + 8
+    assert ctypes.sizeof(mphio.MphConfig) == L.mph_config_sizeof()
 
 
 def _write_case(case, tmp):

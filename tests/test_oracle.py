@@ -85,7 +85,7 @@ from particlemethod_fsi_amd import cases
 c = cases.get(%(case)r)
 cfg, parts = c.build()
 dp, gp = write_case_files(cases.data_text(c.data()), c.grid_text())
-ref = RefSolver(c.dim, c.module, dp, gp); ref.init()
+ref = RefSolver(c.dim, c.ref_variant, dp, gp); ref.init()
 orc = OracleSolver(cfg, parts); orc.init()
 ref.step(3); orc.step(3)
 solid = (parts.property >= 2) & (parts.property < 4)
@@ -104,7 +104,7 @@ print("OK")
 @pytest.mark.parametrize("case", ["gate2d", "gate3d"])
 def test_oracle_per_kernel_against_live_reference(case):
     c = cases.get(case)
-    if not ref_available(c.dim, c.module):
+    if not ref_available(c.dim, c.ref_variant):
         pytest.skip("oracle/_ref not built (needs /root/reference)")
     import os
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
