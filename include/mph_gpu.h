@@ -199,6 +199,13 @@ double mph_time(const MphCtx* ctx);
 int mph_get_scalars(const MphCtx* ctx, double* out36);
 int mph_write_prof(MphCtx* ctx, const char* path);
 int mph_write_vtk(MphCtx* ctx, const char* path);
+/* writeVtkFile (main.cpp:984-1189) off the time loop's critical path: the fields are copied to
+ * host memory now (one D2H per field) and formatted and written by a background thread while
+ * the following steps run.  At most one file is in flight; mph_output_wait joins it and
+ * returns its status (also called by the next mph_write_vtk_async and by mph_destroy).
+ * The bytes are those of mph_write_vtk.                                                        */
+int mph_write_vtk_async(MphCtx* ctx, const char* path);
+int mph_output_wait(MphCtx* ctx);
 /* Message of the last failure on ctx; with ctx == NULL, of the last failed mph_create* on the
  * calling thread (the context is destroyed on failure).                                        */
 const char* mph_last_error(const MphCtx* ctx);

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mph_internal.h"
@@ -51,6 +52,8 @@ struct MphCtx {
     mph::DevParams P{};
     mph::DevTables T{};
     std::string err;
+    std::thread out_thread;      // mph_write_vtk_async: the file of the previous output step
+    int out_rc = 0;
     double time = 0.0;           // host mirror of Time (same additions as the device)
     bool stepped = false;
     hipStream_t stream = nullptr;

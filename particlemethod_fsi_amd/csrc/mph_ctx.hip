@@ -670,6 +670,50 @@ int mph_write_vtk(MphCtx* c, const char* path)
                                 acc.data(), force.data(), stress.data(), strain.data(), isnc.data(), nc.data());
 }
 
+int mph_output_wait(MphCtx* c)
+{
+    if (!c) return MPH_ERR_ARG;
+    if (c->out_thread.joinable()) c->out_thread.join();
+    const int rc = c->out_rc;
+    c->out_rc = MPH_OK;
+    if (rc) return fail(c, rc, "asynchronous .vtk write failed");
+    return MPH_OK;
+}
+
+int mph_write_vtk_async(MphCtx* c, const char* path)
+{
+    if (!c || !path) return MPH_ERR_ARG;
+    if (c->dist) return fail(c, MPH_ERR_UNSUPPORTED, "slab mode: gather the owned entries (mph_get) and use mph_write_vtk_arrays");
+    CK(mph_output_wait(c));   // at most one file in flight
+    struct Snap {
+        std::string path;
+        std::vector<double> pos, pos0, vel, acc, force, stress, strain;
+        std::vector<int> prop, isnc, nc;
+    };
+    const size_t n = (size_t)c->n_glob;
+    auto s = std::make_shared<Snap>();
+    s->path = path;
+    s->pos.resize(3 * n); s->vel.resize(3 * n); s->acc.resize(3 * n); s->force.resize(3 * n);
+    s->stress.resize(9 * n); s->strain.resize(9 * n); s->isnc.resize(n); s->nc.resize(n);
+    s->pos0 = c->pos0;
+    s->prop = c->prop;
+    CK(mph_get(c, MPH_FIELD_POSITION, s->pos.data()));
+    CK(mph_get(c, MPH_FIELD_VELOCITY, s->vel.data()));
+    CK(mph_get(c, MPH_FIELD_ACCELERATION, s->acc.data()));
+    CK(mph_get(c, MPH_FIELD_FORCE, s->force.data()));
+    CK(mph_get(c, MPH_FIELD_STRESS, s->stress.data()));
+    CK(mph_get(c, MPH_FIELD_STRAIN, s->strain.data()));
+    CK(mph_get(c, MPH_FIELD_INITIAL_STRUCTURE_NEIGHBOR_COUNT, s->isnc.data()));
+    CK(mph_get(c, MPH_FIELD_NEIGHBOR_COUNT, s->nc.data()));
+    const int nn = c->n_glob;
+    c->out_thread = std::thread([c, s, nn] {
+        c->out_rc = mph_write_vtk_arrays(s->path.c_str(), nn, s->prop.data(), s->pos.data(), s->pos0.data(),
+                                         s->vel.data(), s->acc.data(), s->force.data(), s->stress.data(),
+                                         s->strain.data(), s->isnc.data(), s->nc.data());
+    });
+    return MPH_OK;
+}
+
 int mph_profile_steps(MphCtx* c, int nsteps, double* avg_ms, int* launches, char* names32)
 {
     if (!c || nsteps <= 0 || !avg_ms || !launches || !names32) return MPH_ERR_ARG;
@@ -727,6 +771,7 @@ int mph_neighbor_stats(MphCtx* c, double* mean, int* mx)
 void mph_destroy(MphCtx* c)
 {
     if (!c) return;
+    if (c->out_thread.joinable()) c->out_thread.join();
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->graph1) (void)hipGraphExecDestroy(c->graph1);

@@ -133,7 +133,8 @@ int main(int argc, char** argv)
                 rc = mph_compute_virial(ctx);
                 if (rc) die(ctx, rc, "mph_compute_virial");
                 std::snprintf(name, sizeof(name), vtk.c_str(), istep);
-                rc = mph_write_vtk(ctx, name);
+                // formatted and written by a background thread while the next steps run
+                rc = mph_write_vtk_async(ctx, name);
                 if (rc) die(ctx, rc, "writing a .vtk file");
                 logf("@ Vtk Output Time : %e\n", time_now);
                 vtk_next += cfg.vtk_output_interval;
@@ -149,6 +150,8 @@ int main(int argc, char** argv)
         if (loop_s > 0)
             logf("throughput:              %e [particle-steps/sec]\n", (double)n * steps_run / loop_s);
     }
+    rc = mph_output_wait(ctx);
+    if (rc) die(ctx, rc, "writing a .vtk file");
     mph_destroy(ctx);
     if (g_log) std::fclose(g_log);
     return 0;

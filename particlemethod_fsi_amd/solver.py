@@ -53,7 +53,7 @@ EXPORTED_SYMBOLS = [
     "mph_dist_unique_id", "mph_create_dist", "mph_owned_count", "mph_derive_scalars",
     "mph_structure_init", "mph_create_dist_host", "mph_owned_ids", "mph_slab_bounds",
     "mph_slab_owner", "mph_dist_selftest", "mph_compute_virial",
-    "mph_config_sizeof",
+    "mph_config_sizeof", "mph_write_vtk_async", "mph_output_wait",
 ]
 
 # mph_host_exchange_fn (include/mph_gpu.h): (user, send_l, n, send_r, n, recv_l, n, recv_r, n)
@@ -125,6 +125,8 @@ def load_library() -> ctypes.CDLL:
         "mph_structure_init": (ip, [cfgp, ip, vp, vp, vp, vp, vp, vp]),
         "mph_compute_virial": (ip, [vp]),
         "mph_config_sizeof": (ip, []),
+        "mph_write_vtk_async": (ip, [vp, ctypes.c_char_p]),
+        "mph_output_wait": (ip, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -283,6 +285,13 @@ class MphSolver:
 
     def write_vtk(self, path: str):
         _check(self._L.mph_write_vtk(self._h, path.encode()), self._h)
+
+    def write_vtk_async(self, path: str):
+        """Snapshot now, format and write in the background (wait with output_wait())."""
+        _check(self._L.mph_write_vtk_async(self._h, path.encode()), self._h)
+
+    def output_wait(self):
+        _check(self._L.mph_output_wait(self._h), self._h)
 
     def write_prof(self, path: str):
         _check(self._L.mph_write_prof(self._h, path.encode()), self._h)

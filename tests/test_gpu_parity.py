@@ -182,3 +182,17 @@ def test_gpu_nonfinite_state_is_an_error_not_a_fault():
         with pytest.raises(MphError) as e:
             s.step(1)
         assert e.value.code == -9
+
+
+def test_gpu_vtk_async_equals_sync(tmp_path):
+    """mph_write_vtk_async snapshots the state when called: its file equals mph_write_vtk's of the
+    same step even though the solver has advanced while the background thread writes."""
+    cfg, parts = cases.get("gate2d").build()
+    with MphSolver(cfg, parts) as s:
+        s.step(3)
+        a, b = str(tmp_path / "sync.vtk"), str(tmp_path / "async.vtk")
+        s.write_vtk(a)
+        s.write_vtk_async(b)
+        s.step(5)
+        s.output_wait()
+        assert open(a, "rb").read() == open(b, "rb").read()

@@ -148,3 +148,53 @@ def test_structure_init_matches_reference(case):
     ref = g.get(0, "Normalizer")
     # neighbour sums in slot order instead of the reference's cell-scan order: reassociation only
     assert np.max(np.abs(N[g.solid] - ref)) <= 1e-12 * np.max(np.abs(ref))
+
+
+def _vtk_reference_format(n, prop, pos, pos0, vel, acc, force, stress, strain, isnc, nc):
+    """writeVtkFile's byte layout (main.cpp:984-1189) restated in Python (test-only), for sizes
+    where the library formats the sections in parallel."""
+    f32 = lambda a: a.astype(np.float32).astype(np.float64)
+    out = []
+    v3 = lambda a: "".join("%e %e %e\n" % tuple(r) for r in f32(a).reshape(n, 3).tolist())
+    out.append("# vtk DataFile Version 2.0\nUnstructured Grid Example\nASCII\nDATASET UNSTRUCTURED_GRID\n")
+    out.append("POINTS %d float\n" % n + v3(pos))
+    out.append("CELLS %d %d\n" % (n, 2 * n) + "".join("1 %d " % i for i in range(n)) + "\n")
+    out.append("CELL_TYPES %d\n" % n + "1 " * n + "\n\n")
+    out.append("POINT_DATA %d\nSCALARS label float 1\nLOOKUP_TABLE default\n" % n)
+    out.append("".join("%d\n" % t for t in prop.tolist()) + "\n\n")
+    out.append("VECTORS displacement float\n" + v3(pos - pos0))
+    for m, tag in ((stress, "stress"), (strain, "strain")):
+        mm = f32(m).reshape(n, 9)
+        for a in range(3):
+            for b in range(3):
+                out.append("\n SCALARS %s%d%d float \nLOOKUP_TABLE default\n" % (tag, a, b))
+                out.append("".join("%e\n" % x for x in mm[:, 3 * a + b].tolist()))
+    out.append("VECTORS velocity float\n" + v3(vel) + "\n")
+    out.append("VECTORS accel float\n" + v3(acc) + "\n")
+    out.append("SCALARS Initialneighbor float 1\nLOOKUP_TABLE default\n" + "".join("%d\n" % t for t in isnc.tolist()))
+    out.append("SCALARS neighbor float 1\nLOOKUP_TABLE default\n" + "".join("%d\n" % t for t in nc.tolist()))
+    out.append("VECTORS velocity float\n" + v3(vel) + "\n")
+    out.append("VECTORS force float\n" + v3(force) + "\n")
+    return "".join(out).encode()
+
+
+def test_vtk_writer_parallel_sections_byte_identical():
+    """Above 2 x 65536 particles mph_write_vtk_arrays formats each section on several threads; the
+    file must still be the reference's sequential byte stream."""
+    n = 150_000
+    rng = np.random.default_rng(7)
+    prop = rng.integers(0, 6, n).astype(np.int32)
+    arrs = [rng.normal(size=(n, 3)) * 10.0 ** rng.integers(-6, 3, (n, 1)) for _ in range(5)]
+    pos, pos0, vel, acc, force = arrs
+    stress, strain = rng.normal(size=(n, 3, 3)) * 1e4, rng.normal(size=(n, 3, 3)) * 1e-4
+    isnc = rng.integers(0, 40, n).astype(np.int32)
+    nc = rng.integers(0, 90, n).astype(np.int32)
+    L = solver.load_library()
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, "big.vtk")
+        rc = L.mph_write_vtk_arrays(path.encode(), n, prop.ctypes.data, pos.ctypes.data, pos0.ctypes.data,
+                                    vel.ctypes.data, acc.ctypes.data, force.ctypes.data, stress.ctypes.data,
+                                    strain.ctypes.data, isnc.ctypes.data, nc.ctypes.data)
+        assert rc == 0
+        raw = open(path, "rb").read()
+    assert raw == _vtk_reference_format(n, prop, pos, pos0, vel, acc, force, stress, strain, isnc, nc)
