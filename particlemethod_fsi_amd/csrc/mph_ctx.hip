@@ -358,8 +358,6 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         D.wo = wo;
         D.wi = wi;
         std::vector<int> eo_nb(ntile_s * wo * 64, 0), ei_nb(ntile_s * wi * 64, 0);
-        std::vector<double4> eo_pair(ntile_s * wo * 64, make_double4(0, 0, 0, 0));
-        std::vector<double4> ei_pair(ntile_s * wi * 64, make_double4(0, 0, 0, 0));
         std::vector<double4> wx0(ns);
         for (int s = 0; s < ns; ++s) {
             const size_t base_o = (size_t)(s >> 6) * wo * 64 + (s & 63);
@@ -368,26 +366,23 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
                 const size_t q = S.offset[s] + k;
                 const double* pr = &S.pair_out[4 * q];
                 eo_nb[base_o + (size_t)k * 64] = S.nbr[q];
-                eo_pair[base_o + (size_t)k * 64] = make_double4(pr[0], pr[1], pr[2], pr[3]);
                 for (int d = 0; d < 3; ++d) c[d] += pr[3] * pr[d];
             }
             wx0[s] = make_double4(c[0], c[1], c[2], 0.0);
             const size_t base_i = (size_t)(s >> 6) * wi * 64 + (s & 63);
             for (int k = 0; k < icnt[s]; ++k) {
                 const size_t q = S.in_offset[s] + k;
-                const double* pr = &S.pair_in[4 * q];
                 ei_nb[base_i + (size_t)k * 64] = S.in_nbr[q];
-                ei_pair[base_i + (size_t)k * 64] = make_double4(pr[0], pr[1], pr[2], pr[3]);
             }
         }
         const int sd = c->P.dim;
         CK(dalloc(c, &D.orig, ns)); CK(dalloc(c, &D.ocnt, ns)); CK(dalloc(c, &D.icnt, ns));
-        CK(dalloc(c, &D.eo_nb, eo_nb.size())); CK(dalloc(c, &D.eo_pair, eo_pair.size()));
-        CK(dalloc(c, &D.ei_nb, ei_nb.size())); CK(dalloc(c, &D.ei_pair, ei_pair.size()));
+        CK(dalloc(c, &D.eo_nb, eo_nb.size()));
+        CK(dalloc(c, &D.ei_nb, ei_nb.size()));
         CK(dalloc(c, &D.wx0, ns));
         CK(dalloc(c, &D.L, (size_t)ns * 9)); CK(dalloc(c, &D.lame, ns)); CK(dalloc(c, &D.inv_rho, ns));
         CK(dalloc(c, &D.clamp, ns)); CK(dalloc(c, &D.x0, ns)); CK(dalloc(c, &D.x, ns)); CK(dalloc(c, &D.v, ns));
-        CK(dalloc(c, &D.u, ns)); CK(dalloc(c, &D.P, (size_t)ns * sd)); CK(dalloc(c, &D.F, (size_t)ns * 9));
+        CK(dalloc(c, &D.u, ns)); CK(dalloc(c, &D.P, (size_t)ns * (sd == 2 ? 1 : 3))); CK(dalloc(c, &D.F, (size_t)ns * 9));
         CK(dalloc(c, &D.E, (size_t)ns * 9)); CK(dalloc(c, &D.S, (size_t)ns * 9));
         std::vector<double2> lame(ns);
         std::vector<double> irho(ns);
@@ -416,15 +411,15 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         };
         HIP_OK(c, hipMemcpyAsync(D.orig, S.orig.data(), sizeof(int) * ns, hipMemcpyHostToDevice, c->stream));
         HIP_OK(c, up(D.ocnt, ocnt)); HIP_OK(c, up(D.icnt, icnt));
-        HIP_OK(c, up(D.eo_nb, eo_nb)); HIP_OK(c, up(D.eo_pair, eo_pair));
-        HIP_OK(c, up(D.ei_nb, ei_nb)); HIP_OK(c, up(D.ei_pair, ei_pair));
+        HIP_OK(c, up(D.eo_nb, eo_nb));
+        HIP_OK(c, up(D.ei_nb, ei_nb));
         HIP_OK(c, up(D.wx0, wx0));
         HIP_OK(c, hipMemcpyAsync(D.L, S.normalizer.data(), sizeof(double) * 9 * ns, hipMemcpyHostToDevice, c->stream));
         HIP_OK(c, hipMemcpyAsync(D.lame, lame.data(), sizeof(double2) * ns, hipMemcpyHostToDevice, c->stream));
         HIP_OK(c, hipMemcpyAsync(D.inv_rho, irho.data(), sizeof(double) * ns, hipMemcpyHostToDevice, c->stream));
         HIP_OK(c, hipMemcpyAsync(D.clamp, clamp.data(), sizeof(int) * ns, hipMemcpyHostToDevice, c->stream));
         HIP_OK(c, hipMemcpyAsync(D.x0, x0.data(), sizeof(double4) * ns, hipMemcpyHostToDevice, c->stream));
-        HIP_OK(c, hipMemsetAsync(D.P, 0, sizeof(double4) * sd * ns, c->stream));
+        HIP_OK(c, hipMemsetAsync(D.P, 0, sizeof(double4) * (sd == 2 ? 1 : 3) * ns, c->stream));
         for (double* m : {D.F, D.E, D.S})
             HIP_OK(c, hipMemsetAsync(m, 0, sizeof(double) * 9 * ns, c->stream));
         HIP_OK(c, hipStreamSynchronize(c->stream));

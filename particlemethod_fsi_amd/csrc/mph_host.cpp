@@ -444,6 +444,10 @@ void make_dev_params(const MphConfig& c, const HostDerived& h, int n, int n_stru
     P.dim = c.dim;
     P.module = c.module;
     P.wall_motion = c.wall_motion;
+    {
+        const double rp = h.rp, hdp = c.dim == 2 ? rp * rp : rp * rp * rp;
+        P.cw_pair = (1.0 / h.swp) * (1.0 / hdp);   // as build_structure's per-pair weight
+    }
     P.n_struct = n_struct;
     P.substeps = (int)(c.dt / c.elastic_dt + 0.5);
     for (int d = 0; d < 3; ++d) {

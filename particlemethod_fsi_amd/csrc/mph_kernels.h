@@ -16,9 +16,7 @@ struct StructDev {
     int* ocnt = nullptr;          // InitialStructureNeighborCount per slot
     int* icnt = nullptr;          // in-degree (how many slots list s)
     int* eo_nb = nullptr;         // out-list neighbour slots, ELL [ntile * wo][64]
-    double4* eo_pair = nullptr;   // {x0_ij, w_ij}, ELL
     int* ei_nb = nullptr;         // in-list (senders i of the reference's scatter), ELL [ntile * wi][64]
-    double4* ei_pair = nullptr;   // {x0_is, w_is} of the sender i, ELL
     double4* wx0 = nullptr;       // sum_j w_sj x0_sj (the P_s half of StressForce, fixed)
     double* L = nullptr;          // Normalizer [ns][9]
     double2* lame = nullptr;      // (LambdaLames, MuLames)
@@ -28,7 +26,7 @@ struct StructDev {
     double4* x = nullptr;         // current position (valid during the substeps)
     double4* v = nullptr;
     double4* u = nullptr;         // displacement Mod(x - x0) (main.cpp:2700-2712), per substep
-    double4* P = nullptr;         // first Piola-Kirchhoff F S L, 3 rows of double4 (xyz, 0)
+    double4* P = nullptr;         // first Piola-Kirchhoff F S L: 2-D one double4 {P00,P01,P10,P11}, 3-D 3 rows
     double* F = nullptr;          // DeformGradient [ns][9]
     double* E = nullptr;          // Strain
     double* S = nullptr;          // Stress

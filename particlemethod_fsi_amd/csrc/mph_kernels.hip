@@ -1147,6 +1147,25 @@ __global__ __launch_bounds__(256) void k_struct_gather(DevParams P, int ns, cons
 #define MPH_US 4   // batch width of the elastic list loops
 #endif
 
+// x0_ij = Mod(x0_j - x0_i + W/2, W) - W/2 and weight(x0_ij, RadiusP) of the fixed Lagrangian
+// pair (main.cpp:2705-2716; weight() 268-295, norm over dim components): the same expressions as
+// the host's former per-pair table (mph_host.cpp build_structure), recomputed from the 32-byte
+// x0 records so that no per-pair table is streamed from HBM every substep.
+template <int DIM>
+__device__ __forceinline__ double4 struct_pair(const DevParams& P, double4 x0i, double4 x0j)
+{
+#pragma clang fp contract(off)
+    double q[3] = {0.0, 0.0, 0.0};
+    q[0] = image_exact<false>(x0j.x - x0i.x, P.dw[0], P.hw[0], P.w075[0]);
+    q[1] = image_exact<false>(x0j.y - x0i.y, P.dw[1], P.hw[1], P.w075[1]);
+    if (DIM == 3) q[2] = image_exact<false>(x0j.z - x0i.z, P.dw[2], P.hw[2], P.w075[2]);
+    double r2 = 0.0;
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) r2 += q[d] * q[d];
+    const double t = sqrt(r2) / P.rp;
+    return make_double4(q[0], q[1], q[2], P.cw_pair * ((1.0 - t) * (1.0 - t)));
+}
+
 // ELL entry k of slot s (tile width w)
 __device__ __forceinline__ size_t sell(int s, int w, int k)
 {
@@ -1158,9 +1177,9 @@ __device__ __forceinline__ size_t sell(int s, int w, int k)
 // slot; the fixed list is read ELL-tiled (coalesced) in batches of MPH_US, and per neighbour only
 // the 32-byte displacement record u_j is gathered.
 template <int DIM, int U = MPH_US>
-__global__ __launch_bounds__(256) void k_struct_stress(int ns, int wo, const int* __restrict__ ocnt,
+__global__ __launch_bounds__(256) void k_struct_stress(DevParams P, int ns, int wo, const int* __restrict__ ocnt,
                                                        const int* __restrict__ eo_nb,
-                                                       const double4* __restrict__ eo_pair,
+                                                       const double4* __restrict__ sx0,
                                                        const double4* __restrict__ su,
                                                        const double* __restrict__ L,
                                                        const double2* __restrict__ lame,
@@ -1170,6 +1189,7 @@ __global__ __launch_bounds__(256) void k_struct_stress(int ns, int wo, const int
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= ns) return;
     const double4 u4 = su[s];
+    const double4 x0s = sx0[s];
     const double ui[3] = {u4.x, u4.y, u4.z};
     double Fr[DIM][DIM];
 #pragma unroll
@@ -1179,15 +1199,16 @@ __global__ __launch_bounds__(256) void k_struct_stress(int ns, int wo, const int
     const int cnt = ocnt[s];
     for (int k0 = 0; k0 < cnt; k0 += U) {
         int t[U];
-        double4 pr[U], uj[U];
+        double4 pr[U], uj[U], xj[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) t[u] = eo_nb[sell(s, wo, k0 + u < cnt ? k0 + u : cnt - 1)];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const size_t e = sell(s, wo, k0 + u < cnt ? k0 + u : cnt - 1);
-            t[u] = eo_nb[e];
-            pr[u] = eo_pair[e];
+            uj[u] = su[t[u]];
+            xj[u] = sx0[t[u]];
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) uj[u] = su[t[u]];
+        for (int u = 0; u < U; ++u) pr[u] = struct_pair<DIM>(P, x0s, xj[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (k0 + u >= cnt) break;
@@ -1243,9 +1264,12 @@ __global__ __launch_bounds__(256) void k_struct_stress(int ns, int wo, const int
                 for (int l = 0; l < DIM; ++l) acc += F[a][k] * S[k][l] * Lm[l][b];
             PK[a][b] = acc;
         }
+    if (DIM == 2) {
+        sP[s] = make_double4(PK[0][0], PK[0][1], PK[1 % DIM][0], PK[1 % DIM][1 % DIM]);
+    } else {
 #pragma unroll
-    for (int a = 0; a < DIM; ++a)
-        sP[(size_t)s * DIM + a] = make_double4(PK[a][0], PK[a][1], DIM == 3 ? PK[a][DIM - 1] : 0.0, 0.0);
+        for (int a = 0; a < DIM; ++a) sP[(size_t)s * 3 + a] = make_double4(PK[a][0], PK[a][1], PK[a][DIM - 1], 0.0);
+    }
     double* oF = sF + (size_t)s * 9;
     double* oE = sE + (size_t)s * 9;
     double* oS = sS + (size_t)s * 9;
@@ -1265,11 +1289,27 @@ __global__ __launch_bounds__(256) void k_struct_stress(int ns, int wo, const int
 // fixed, wx0), followed by updateElasticPosition (1910-2082): module clamp, then the always-
 // compiled second drift of 2070-2079 (free particles drift twice per substep; structure
 // acceleration is zero).  Also refreshes the displacement u for the next substep.
+// first Piola-Kirchhoff rows of slot s (2-D: one packed double4, 3-D: three rows)
+template <int DIM>
+__device__ __forceinline__ void struct_P(const double4* sP, int s, double (&Pm)[DIM][3])
+{
+    if (DIM == 2) {
+        const double4 r = sP[s];
+        Pm[0][0] = r.x; Pm[0][1] = r.y; Pm[0][2] = 0.0;
+        Pm[1 % DIM][0] = r.z; Pm[1 % DIM][1] = r.w; Pm[1 % DIM][2] = 0.0;
+    } else {
+#pragma unroll
+        for (int a = 0; a < DIM; ++a) {
+            const double4 r = sP[(size_t)s * 3 + a];
+            Pm[a][0] = r.x; Pm[a][1] = r.y; Pm[a][2] = r.z;
+        }
+    }
+}
+
 template <int DIM, int U = MPH_US>
 __global__ __launch_bounds__(256) void k_struct_velocity(DevParams P, int ns, int wi,
                                                          const int* __restrict__ icnt,
                                                          const int* __restrict__ ei_nb,
-                                                         const double4* __restrict__ ei_pair,
                                                          const double4* __restrict__ wx0,
                                                          const double4* __restrict__ sP,
                                                          const double* __restrict__ inv_rho,
@@ -1284,41 +1324,41 @@ __global__ __launch_bounds__(256) void k_struct_velocity(DevParams P, int ns, in
     {
         const double4 c = wx0[s];
         const double cv[3] = {c.x, c.y, c.z};
+        double Ps[DIM][3];
+        struct_P<DIM>(sP, s, Ps);
 #pragma unroll
         for (int a = 0; a < DIM; ++a) {
-            const double4 r = sP[(size_t)s * DIM + a];
-            const double pr[3] = {r.x, r.y, r.z};
             double f = 0.0;
 #pragma unroll
-            for (int b = 0; b < DIM; ++b) f += pr[b] * cv[b];
+            for (int b = 0; b < DIM; ++b) f += Ps[a][b] * cv[b];
             dv[a] = f;
         }
     }
     const int cnt = icnt[s];
+    const double4 x0me = sx0[s];
     for (int k0 = 0; k0 < cnt; k0 += U) {
         int t[U];
-        double4 pr[U], Pi[U][DIM];
+        double4 xi0[U];
+        double Pi[U][DIM][3];
+#pragma unroll
+        for (int u = 0; u < U; ++u) t[u] = ei_nb[sell(s, wi, k0 + u < cnt ? k0 + u : cnt - 1)];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const size_t e = sell(s, wi, k0 + u < cnt ? k0 + u : cnt - 1);
-            t[u] = ei_nb[e];
-            pr[u] = ei_pair[e];
+            struct_P<DIM>(sP, t[u], Pi[u]);
+            xi0[u] = sx0[t[u]];
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int a = 0; a < DIM; ++a) Pi[u][a] = sP[(size_t)t[u] * DIM + a];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (k0 + u >= cnt) break;
-            const double x0[3] = {pr[u].x, pr[u].y, pr[u].z};
+            // the sender i's pair {x0_is, w_is} (main.cpp:2862-2880, from i's side)
+            const double4 pr = struct_pair<DIM>(P, xi0[u], x0me);
+            const double x0[3] = {pr.x, pr.y, pr.z};
 #pragma unroll
             for (int a = 0; a < DIM; ++a) {
-                const double row[3] = {Pi[u][a].x, Pi[u][a].y, Pi[u][a].z};
                 double f = 0.0;
 #pragma unroll
-                for (int b = 0; b < DIM; ++b) f += row[b] * x0[b];
-                dv[a] -= f * pr[u].w;
+                for (int b = 0; b < DIM; ++b) f += Pi[u][a][b] * x0[b];
+                dv[a] -= f * pr.w;
             }
         }
     }
@@ -1609,15 +1649,15 @@ void launch_structure(const Launch& L)
     for (int sub = 0; sub < P.substeps; ++sub) {
         if (P.dim == 3) {
             MPH_LAUNCH("struct_stress", L.stream, k_struct_stress<3>, dim3(blocks(ns, 256)), dim3(256), 0,
-                       L.stream, ns, S.wo, S.ocnt, S.eo_nb, S.eo_pair, S.u, S.L, S.lame, S.P, S.F, S.E, S.S);
+                       L.stream, P, ns, S.wo, S.ocnt, S.eo_nb, S.x0, S.u, S.L, S.lame, S.P, S.F, S.E, S.S);
             MPH_LAUNCH("struct_velocity", L.stream, k_struct_velocity<3>, dim3(blocks(ns, 256)), dim3(256), 0,
-                       L.stream, P, ns, S.wi, S.icnt, S.ei_nb, S.ei_pair, S.wx0, S.P, S.inv_rho, S.clamp, S.x0,
+                       L.stream, P, ns, S.wi, S.icnt, S.ei_nb, S.wx0, S.P, S.inv_rho, S.clamp, S.x0,
                        S.x, S.v, S.u);
         } else {
             MPH_LAUNCH("struct_stress", L.stream, k_struct_stress<2>, dim3(blocks(ns, 256)), dim3(256), 0,
-                       L.stream, ns, S.wo, S.ocnt, S.eo_nb, S.eo_pair, S.u, S.L, S.lame, S.P, S.F, S.E, S.S);
+                       L.stream, P, ns, S.wo, S.ocnt, S.eo_nb, S.x0, S.u, S.L, S.lame, S.P, S.F, S.E, S.S);
             MPH_LAUNCH("struct_velocity", L.stream, k_struct_velocity<2>, dim3(blocks(ns, 256)), dim3(256), 0,
-                       L.stream, P, ns, S.wi, S.icnt, S.ei_nb, S.ei_pair, S.wx0, S.P, S.inv_rho, S.clamp, S.x0,
+                       L.stream, P, ns, S.wi, S.icnt, S.ei_nb, S.wx0, S.P, S.inv_rho, S.clamp, S.x0,
                        S.x, S.v, S.u);
         }
     }

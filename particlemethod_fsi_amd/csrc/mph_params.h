@@ -55,6 +55,7 @@ struct DevParams {
     double ca, cda, cg, cdg, cp, cdp, cv, cdv;
     double cw;          // weight(): (1/Swp)/rp^dim (main.cpp:268-295)
     double n0a, n0p, r2g, cofk, dx, vol, dt, edt, cvis;
+    double cw_pair;    // (1/Swp)(1/RadiusP^dim) of weight() for the elastic pairs (main.cpp:268-295)
     double gravity[3];
     double ratio[kTypes][kTypes];   // InteractionRatio
     double mu_ij[kTypes][kTypes];   // 2 mu_i mu_j / (mu_i + mu_j) from ShearViscosity
