@@ -58,6 +58,9 @@
 #ifndef MPH_SEARCH_LDS
 #define MPH_SEARCH_LDS 1
 #endif
+#ifndef MPH_SEARCH_PREFETCH
+#define MPH_SEARCH_PREFETCH 1   // pipeline the per-column start[] loads of the LDS search
+#endif
 #ifndef MPH_LDS_CAP
 #define MPH_LDS_CAP 192   // candidates staged per wave and stencil column
 #endif
@@ -661,7 +664,8 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     const double uz = DIM == 3 ? grid_offset(zi, P.corg[2], P.dw[2]) : 0.0;
     const double ua = DIM == 3 ? uz : uy;
     const double ginva = DIM == 3 ? P.ginv[2] : P.ginv[1];
-    for (int col = 0; col < NCOL; ++col) {
+    // candidate range of this lane in stencil column col (cell ranges -> start[] loads)
+    auto col_range = [&](int col, int& jb, int& je) {
         int base;
         double d2;
         if (DIM == 3) {
@@ -675,7 +679,8 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             d2 = gx * gx;
             base = (cx + dxc) * P.gc[1];
         }
-        int jb = 0, je = 0;
+        jb = 0;
+        je = 0;
         if (act && d2 <= rcm2) {
             const double ra = sqrt(rcm2 - d2);
             const int lo = (int)fmax(floor((ua - ra) * ginva), (double)(cca - P.sa));
@@ -683,9 +688,18 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             jb = start[base + lo];
             je = start[base + hi + 1];
         }
+    };
+    // software pipeline: the start[] loads of column col + 1 are in flight while column col is
+    // staged and tested (the per-column chain start[] -> window -> staging loads is latency bound)
+    int nb_jb, nb_je;
+    col_range(0, nb_jb, nb_je);
+    for (int col = 0; col < NCOL; ++col) {
+        const int jb = nb_jb, je = nb_je;
+        if (MPH_SEARCH_PREFETCH && col + 1 < NCOL) col_range(col + 1, nb_jb, nb_je);
         const bool any = je > jb;
         const int mn = wave_min(any ? jb : 0x7fffffff);
         const int mx = wave_max(any ? je : -1);
+        if (!MPH_SEARCH_PREFETCH && col + 1 < NCOL) col_range(col + 1, nb_jb, nb_je);
         if (mx <= mn) continue;   // wave-uniform: no lane has candidates in this column
         const int span = mx - mn;
         if (MPH_DIAG_SEARCH & 2) { cnt += span & 1; continue; }
