@@ -153,11 +153,19 @@ typedef struct MphCtx MphCtx;
 int mph_config_default(MphConfig* cfg, int dim, int module);
 /* .data keyword file, main.cpp:729-786.  Unknown lines are ignored like the reference.      */
 int mph_read_data_file(const char* path, MphConfig* cfg);
-/* .grid / .prof header (Time; N dx xmin xmax ymin ymax zmin zmax), main.cpp:796-804.        */
+/* .grid / .prof header (Time; N dx xmin xmax ymin ymax zmin zmax), main.cpp:796-804.
+ * Both readers also accept the binary grid of mph_write_grid_binary (detected by its magic).  */
 int mph_read_grid_header(const char* path, MphConfig* cfg, int* n);
 /* .grid / .prof body: n lines "type x y z x0 y0 z0 vx vy vz", main.cpp:896-904.             */
 int mph_read_grid_particles(const char* path, int n, int* property, double* pos, double* pos0,
                             double* vel);
+/* Binary grid (the input-path variant of SURVEY 8f: the ASCII .grid of a 16M-particle case is
+ * 2 GB and takes the generator 33 s): magic "MPHGRIDB", int32 version 1, int32 n, double time,
+ * dx, domain_min[3], domain_max[3], then int32 property[n] (zero-padded to 8 bytes) and
+ * double position[n][3], initial_position[n][3], velocity[n][3], little endian.  The values
+ * are stored exactly (no %e rounding).                                                        */
+int mph_write_grid_binary(const char* path, const MphConfig* cfg, int n, const int* property,
+                          const double* pos, const double* pos0, const double* vel);
 /* .prof writer with the reference's exact format, main.cpp:957-982.                          */
 int mph_write_prof_arrays(const char* path, const MphConfig* cfg, double time, int n,
                           const int* property, const double* pos, const double* pos0,

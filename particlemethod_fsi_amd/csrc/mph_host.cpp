@@ -3,6 +3,7 @@
 // bit-identical to the reference's globals (checked by tests/test_host_io.py against
 // oracle/_ref ref_scalars).
 #include <cmath>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
@@ -86,10 +87,63 @@ extern "C" int mph_read_data_file(const char* path, MphConfig* c)
     return MPH_OK;
 }
 
+// ---- binary grid (mph_write_grid_binary) -------------------------------------------------------
+namespace {
+constexpr char kGridMagic[8] = {'M', 'P', 'H', 'G', 'R', 'I', 'D', 'B'};
+struct GridBinHeader {
+    char magic[8];
+    int32_t version, n;
+    double time, dx, dmin[3], dmax[3];
+};
+static_assert(sizeof(GridBinHeader) == 80, "binary grid header layout");
+
+bool is_grid_binary(const char* path, GridBinHeader* h)
+{
+    FILE* fp = std::fopen(path, "rb");
+    if (!fp) return false;
+    GridBinHeader t;
+    const bool ok = std::fread(&t, sizeof(t), 1, fp) == 1 && std::memcmp(t.magic, kGridMagic, 8) == 0 &&
+                    t.version == 1 && t.n >= 0;
+    std::fclose(fp);
+    if (ok && h) *h = t;
+    return ok;
+}
+}  // namespace
+
+extern "C" int mph_write_grid_binary(const char* path, const MphConfig* c, int n, const int* prop,
+                                     const double* pos, const double* pos0, const double* vel)
+{
+    if (!path || !c || n < 0 || (n > 0 && (!prop || !pos || !pos0 || !vel))) return MPH_ERR_ARG;
+    FILE* fp = std::fopen(path, "wb");
+    if (!fp) return MPH_ERR_IO;
+    GridBinHeader h{};
+    std::memcpy(h.magic, kGridMagic, 8);
+    h.version = 1;
+    h.n = n;
+    h.time = c->time;
+    h.dx = c->particle_spacing;
+    for (int d = 0; d < 3; ++d) { h.dmin[d] = c->domain_min[d]; h.dmax[d] = c->domain_max[d]; }
+    bool ok = std::fwrite(&h, sizeof(h), 1, fp) == 1;
+    ok = ok && std::fwrite(prop, sizeof(int), (size_t)n, fp) == (size_t)n;
+    const int32_t pad = 0;
+    if (n & 1) ok = ok && std::fwrite(&pad, sizeof(pad), 1, fp) == 1;
+    for (const double* a : {pos, pos0, vel}) ok = ok && std::fwrite(a, sizeof(double) * 3, (size_t)n, fp) == (size_t)n;
+    ok = std::fclose(fp) == 0 && ok;
+    return ok ? MPH_OK : MPH_ERR_IO;
+}
+
 // readGridFile header, main.cpp:796-804
 extern "C" int mph_read_grid_header(const char* path, MphConfig* c, int* n)
 {
     if (!path || !c || !n) return MPH_ERR_ARG;
+    GridBinHeader bh;
+    if (is_grid_binary(path, &bh)) {
+        c->time = bh.time;
+        c->particle_spacing = bh.dx;
+        for (int d = 0; d < 3; ++d) { c->domain_min[d] = bh.dmin[d]; c->domain_max[d] = bh.dmax[d]; }
+        *n = bh.n;
+        return MPH_OK;
+    }
     FILE* fp = std::fopen(path, "r");
     if (!fp) return MPH_ERR_IO;
     char buf[1024];
@@ -109,6 +163,19 @@ extern "C" int mph_read_grid_particles(const char* path, int n, int* prop, doubl
                                        double* vel)
 {
     if (!path || n < 0 || !prop || !pos || !pos0 || !vel) return MPH_ERR_ARG;
+    GridBinHeader bh;
+    if (is_grid_binary(path, &bh)) {
+        if (bh.n != n) return MPH_ERR_ARG;
+        FILE* fb = std::fopen(path, "rb");
+        if (!fb) return MPH_ERR_IO;
+        bool ok = std::fseek(fb, (long)sizeof(GridBinHeader), SEEK_SET) == 0;
+        ok = ok && std::fread(prop, sizeof(int), (size_t)n, fb) == (size_t)n;
+        int32_t pad;
+        if (n & 1) ok = ok && std::fread(&pad, sizeof(pad), 1, fb) == 1;
+        for (double* a : {pos, pos0, vel}) ok = ok && std::fread(a, sizeof(double) * 3, (size_t)n, fb) == (size_t)n;
+        std::fclose(fb);
+        return ok ? MPH_OK : MPH_ERR_IO;
+    }
     FILE* fp = std::fopen(path, "r");
     if (!fp) return MPH_ERR_IO;
     char buf[1024];

@@ -53,7 +53,7 @@ EXPORTED_SYMBOLS = [
     "mph_dist_unique_id", "mph_create_dist", "mph_owned_count", "mph_derive_scalars",
     "mph_structure_init", "mph_create_dist_host", "mph_owned_ids", "mph_slab_bounds",
     "mph_slab_owner", "mph_dist_selftest", "mph_compute_virial",
-    "mph_config_sizeof", "mph_write_vtk_async", "mph_output_wait",
+    "mph_config_sizeof", "mph_write_vtk_async", "mph_output_wait", "mph_write_grid_binary",
 ]
 
 # mph_host_exchange_fn (include/mph_gpu.h): (user, send_l, n, send_r, n, recv_l, n, recv_r, n)
@@ -125,6 +125,7 @@ def load_library() -> ctypes.CDLL:
         "mph_structure_init": (ip, [cfgp, ip, vp, vp, vp, vp, vp, vp]),
         "mph_compute_virial": (ip, [vp]),
         "mph_config_sizeof": (ip, []),
+        "mph_write_grid_binary": (ip, [ctypes.c_char_p, cfgp, ip, vp, vp, vp, vp]),
         "mph_write_vtk_async": (ip, [vp, ctypes.c_char_p]),
         "mph_output_wait": (ip, [vp]),
     }
@@ -151,6 +152,14 @@ def read_case_files(data_path: str, grid_path: str, dim: int, module: str | int 
     _check(L.mph_read_grid_particles(grid_path.encode(), N, prop.ctypes.data, pos.ctypes.data,
                                      pos0.ctypes.data, vel.ctypes.data))
     return cfg, mphio.Particles(prop, pos, pos0, vel)
+
+
+def write_grid_binary(path: str, cfg: mphio.MphConfig, parts: "mphio.Particles"):
+    """Binary grid (include/mph_gpu.h mph_write_grid_binary); read_case_files reads it back."""
+    p = [np.ascontiguousarray(a, np.float64) for a in (parts.position, parts.initial_position, parts.velocity)]
+    prop = np.ascontiguousarray(parts.property, np.int32)
+    _check(load_library().mph_write_grid_binary(path.encode(), ctypes.byref(cfg), parts.n, prop.ctypes.data,
+                                                p[0].ctypes.data, p[1].ctypes.data, p[2].ctypes.data))
 
 
 def derive_scalars(cfg: mphio.MphConfig) -> np.ndarray:

@@ -198,3 +198,20 @@ def test_vtk_writer_parallel_sections_byte_identical():
         assert rc == 0
         raw = open(path, "rb").read()
     assert raw == _vtk_reference_format(n, prop, pos, pos0, vel, acc, force, stress, strain, isnc, nc)
+
+
+@pytest.mark.parametrize("case", ["dam2d", "gate3d", "bar2d"])
+def test_binary_grid_roundtrip(case):
+    """mph_write_grid_binary -> mph_read_grid_header/_particles (magic-detected) returns exactly
+    what the ASCII .grid gave, so a binary grid is a drop-in for the reference's input file."""
+    with tempfile.TemporaryDirectory() as tmp:
+        c, dp, gp = _write_case(case, tmp)
+        cfg_t, p_t = solver.read_case_files(dp, gp, c.dim, c.module)
+        gb = os.path.join(tmp, "c.gridb")
+        solver.write_grid_binary(gb, cfg_t, p_t)
+        cfg_b, p_b = solver.read_case_files(dp, gb, c.dim, c.module)
+        assert bytes(cfg_b) == bytes(cfg_t)
+        for a, b in ((p_t.property, p_b.property), (p_t.position, p_b.position),
+                     (p_t.initial_position, p_b.initial_position), (p_t.velocity, p_b.velocity)):
+            assert np.array_equal(a, b)
+        assert os.path.getsize(gb) == 80 + 4 * (p_t.n + (p_t.n & 1)) + 72 * p_t.n
