@@ -163,6 +163,19 @@ __device__ __forceinline__ int xcd_block(int b, int nb)
 
 __device__ __forceinline__ int nbr_entry(int j, int type) { return j | (type << kTypeShift); }
 
+// The ELL list is written once per step and read once per pass.  MPH_LIST_NT=1 makes the pass
+// reads non-temporal (D1M: pass A -1 %, within noise); non-temporal list *stores* in the search
+// lose the write combining of the scattered 4-byte entries (search 0.41 -> 0.77 ms), so the
+// stores stay plain.
+#ifndef MPH_LIST_NT
+#define MPH_LIST_NT 0
+#endif
+__device__ __forceinline__ int list_load(const int* p)
+{
+    return MPH_LIST_NT ? __builtin_nontemporal_load(p) : *p;
+}
+__device__ __forceinline__ void list_store(int* p, int v) { *p = v; }
+
 __device__ __forceinline__ const int* ell_row(const int* nbr, int i)
 {
     return nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
@@ -612,7 +625,7 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
                         a = r2_exact(q0, q1, q2) <= P.rc2;
                     }
                     if (a && j < je && j != i) {
-                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) out[cnt * kTile] = nbr_entry(j, A.type[j]);
+                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) list_store(out + cnt * kTile, nbr_entry(j, A.type[j]));
                         ++cnt;
                     }
                 }
@@ -726,7 +739,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                 for (int u = 0; u < SB; ++u) {
                     const int j = j0 + u;
                     if (accept_interior(P, xs[u] - xi, ys[u] - yi, zs[u] - zi, lo2, hi2) && j < je && j != i) {
-                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) out[cnt * kTile] = nbr_entry(j, st[k0 + u]);
+                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) list_store(out + cnt * kTile, nbr_entry(j, st[k0 + u]));
                         ++cnt;
                     }
                 }
@@ -746,7 +759,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                 for (int u = 0; u < SB; ++u) {
                     const int j = j0 + u;
                     if (accept_interior(P, xs[u] - xi, ys[u] - yi, zs[u] - zi, lo2, hi2) && j < je && j != i) {
-                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) out[cnt * kTile] = nbr_entry(j, A.type[j]);
+                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) list_store(out + cnt * kTile, nbr_entry(j, A.type[j]));
                         ++cnt;
                     }
                 }
@@ -810,7 +823,7 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
         int TT[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int e = row[(k0 + u < cnt ? k0 + u : cnt - 1) * kTile];
+            const int e = list_load(row + (k0 + u < cnt ? k0 + u : cnt - 1) * kTile);
             jj[u] = e & kIndexMask;
             TT[u] = e >> kTypeShift;
             if (MPH_DIAG_GATHER == 1) jj[u] = min((int)(blockIdx.x * blockDim.x + threadIdx.x) ^ 1, P.n - 1);
@@ -903,7 +916,7 @@ __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_
         int TT[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int e = row[(k0 + u < cnt ? k0 + u : cnt - 1) * kTile];
+            const int e = list_load(row + (k0 + u < cnt ? k0 + u : cnt - 1) * kTile);
             jj[u] = e & kIndexMask;
             TT[u] = e >> kTypeShift;
             if (MPH_DIAG_GATHER == 1) jj[u] = min((int)(blockIdx.x * blockDim.x + threadIdx.x) ^ 1, P.n - 1);
