@@ -410,6 +410,12 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
             return hipMemcpyAsync(d, v.data(), v.size() * sizeof(v[0]), hipMemcpyHostToDevice, c->stream);
         };
         HIP_OK(c, hipMemcpyAsync(D.orig, S.orig.data(), sizeof(int) * ns, hipMemcpyHostToDevice, c->stream));
+        {
+            std::vector<int> slot_of((size_t)c->n_glob, -1);
+            for (int s = 0; s < ns; ++s) slot_of[S.orig[s]] = s;
+            CK(dalloc(c, &D.slot_of, slot_of.size()));
+            HIP_OK(c, hipMemcpy(D.slot_of, slot_of.data(), sizeof(int) * slot_of.size(), hipMemcpyHostToDevice));
+        }
         HIP_OK(c, up(D.ocnt, ocnt)); HIP_OK(c, up(D.icnt, icnt));
         HIP_OK(c, up(D.eo_nb, eo_nb));
         HIP_OK(c, up(D.ei_nb, ei_nb));

@@ -12,6 +12,7 @@ namespace mph {
 // [(s >> 6) * W + k][s & 63], so the 64 lanes of a wavefront read entry k with one coalesced load.
 struct StructDev {
     int* orig = nullptr;          // slot -> original particle index
+    int* slot_of = nullptr;       // original particle index -> slot (-1: not structure)
     int wo = 0, wi = 0;           // ELL widths (max out / in count)
     int* ocnt = nullptr;          // InitialStructureNeighborCount per slot
     int* icnt = nullptr;          // in-degree (how many slots list s)
@@ -51,6 +52,14 @@ struct Soa {
     // (profiles/r01: TA ~64 % busy in pass A); the type of j travels in the list entry instead
     // (kTypeShift), so a neighbour costs 48 gathered bytes instead of 64.
     double2* p6 = nullptr;
+};
+
+// Pass B hands the integrated structure particles straight to the slot-ordered elastic arrays
+// (null slot_of: no structure particles, or slab mode).
+struct StructHook {
+    const int* slot_of;
+    double4 *sx, *sv, *su;
+    const double4* sx0;
 };
 
 // Everything one launch sequence needs.

@@ -16,7 +16,8 @@
 //                    ViscosityV (2478), InterfaceForce (2427), Gravity (2917), Acceleration (2938),
 //                    Convection (1892)
 //   k_struct_*       elastic substeps: DeformationVector (2673) + Stress (2756) -> PK1 stress;
-//                    StressForce (2812) in gather form + updateElasticPosition (1910)
+//                    StressForce (2812) in gather form + updateElasticPosition (1910); pass B
+//                    hands the structure particles to them and the last substep writes back
 //
 // All arithmetic is FP64.  Neighbour membership and every per-kernel radius test reproduce the
 // reference's FP64 expressions bit for bit (no contraction, IEEE division), so NeighborCount is
@@ -890,6 +891,15 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
     pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
 }
 
+// Displacement u = Mod(x - x0 + W/2, W) - W/2 of calculateElasticDeformationVector (2700-2712),
+// computed once per slot and substep instead of once per pair (same expression, same bits).
+__device__ __forceinline__ double4 struct_disp(const DevParams& P, double4 x, double4 x0)
+{
+    return make_double4(image_exact<false>(x.x - x0.x, P.dw[0], P.hw[0], P.w075[0]),
+                        image_exact<false>(x.y - x0.y, P.dw[1], P.hw[1], P.w075[1]),
+                        image_exact<false>(x.z - x0.z, P.dw[2], P.hw[2], P.w075[2]), 0.0);
+}
+
 // ---------------------------------------------------------------------------- pass B -------
 
 // Pass B needs, per neighbour, only what pass A could not know: P_j (and, with surface tension,
@@ -1002,7 +1012,7 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
                                                 const int* __restrict__ nbr,
                                                 const int* __restrict__ ncount,
                                                 double4* __restrict__ force, double4* __restrict__ acc,
-                                                Soa B, int phase)
+                                                Soa B, int phase, StructHook H)
 {
     __shared__ double s_ratio[kTypes * kTypes];
     if (SURF) {
@@ -1068,6 +1078,14 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
     B.vz[i] = vo2;
     B.type[i] = ti;
     B.id[i] = A.id[i];
+    if (solid && H.slot_of) {
+        // the elastic substeps' slot-ordered state (structure particles do not drift here)
+        const int s = H.slot_of[A.id[i]];
+        const double4 x4 = make_double4(xo0, xo1, xo2, (double)ti);
+        H.sx[s] = x4;
+        H.sv[s] = make_double4(vo0, vo1, vo2, 0.0);
+        H.su[s] = struct_disp(P, x4, H.sx0[s]);
+    }
 }
 
 // ------------------------------------------------------------------------ virial stress ----
@@ -1145,30 +1163,6 @@ __global__ __launch_bounds__(256) void k_virial(DevParams P, const DevTables* __
 }
 
 // ------------------------------------------------------------------------ elastic solid ----
-
-// Displacement u = Mod(x - x0 + W/2, W) - W/2 of calculateElasticDeformationVector (2700-2712),
-// computed once per slot and substep instead of once per pair (same expression, same bits).
-__device__ __forceinline__ double4 struct_disp(const DevParams& P, double4 x, double4 x0)
-{
-    return make_double4(image_exact<false>(x.x - x0.x, P.dw[0], P.hw[0], P.w075[0]),
-                        image_exact<false>(x.y - x0.y, P.dw[1], P.hw[1], P.w075[1]),
-                        image_exact<false>(x.z - x0.z, P.dw[2], P.hw[2], P.w075[2]), 0.0);
-}
-
-__global__ __launch_bounds__(256) void k_struct_gather(DevParams P, int ns, const int* __restrict__ sorig,
-                                                       const int* __restrict__ rank_of, Soa B,
-                                                       const double4* __restrict__ sx0,
-                                                       double4* __restrict__ sx, double4* __restrict__ sv,
-                                                       double4* __restrict__ su)
-{
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= ns) return;
-    const int r = rank_of[sorig[s]];
-    const double4 x = make_double4(B.x[r], B.y[r], B.z[r], (double)B.type[r]);
-    sx[s] = x;
-    sv[s] = make_double4(B.vx[r], B.vy[r], B.vz[r], 0.0);
-    su[s] = struct_disp(P, x, sx0[s]);
-}
 
 #ifndef MPH_US
 #define MPH_US 4   // batch width of the elastic list loops
@@ -1343,7 +1337,10 @@ __global__ __launch_bounds__(256) void k_struct_velocity(DevParams P, int ns, in
                                                          const int* __restrict__ clamp,
                                                          const double4* __restrict__ sx0,
                                                          double4* __restrict__ sx, double4* __restrict__ sv,
-                                                         double4* __restrict__ su)
+                                                         double4* __restrict__ su, int last,
+                                                         const int* __restrict__ sorig,
+                                                         const int* __restrict__ rank_of, Soa B,
+                                                         double4* __restrict__ force)
 {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= ns) return;
@@ -1405,26 +1402,18 @@ __global__ __launch_bounds__(256) void k_struct_velocity(DevParams P, int ns, in
         for (int d = 0; d < 3; ++d) xx[d] += vv[d] * P.edt;
     }
     for (int d = 0; d < 3; ++d) xx[d] += vv[d] * P.edt;
+    if (last) {
+        // back into the integrated state (A order) for the next step's sort
+        const int r = rank_of[sorig[s]];
+        B.x[r] = xx[0]; B.y[r] = xx[1]; B.z[r] = xx[2];
+        B.vx[r] = vv[0]; B.vy[r] = vv[1]; B.vz[r] = vv[2];
+        if (cl == 1) force[r] = make_double4(0.0, 0.0, 0.0, 0.0);
+        return;
+    }
     sv[s] = make_double4(vv[0], vv[1], vv[2], 0.0);
     const double4 xn = make_double4(xx[0], xx[1], xx[2], xo.w);
     sx[s] = xn;
     su[s] = struct_disp(P, xn, x0s);
-}
-
-__global__ __launch_bounds__(256) void k_struct_scatter(int ns, const int* __restrict__ sorig,
-                                                        const int* __restrict__ rank_of,
-                                                        const int* __restrict__ clamp,
-                                                        const double4* __restrict__ sx,
-                                                        const double4* __restrict__ sv, Soa B,
-                                                        double4* __restrict__ force)
-{
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= ns) return;
-    const int r = rank_of[sorig[s]];
-    const double4 x = sx[s], v = sv[s];
-    B.x[r] = x.x; B.y[r] = x.y; B.z[r] = x.z;
-    B.vx[r] = v.x; B.vy[r] = v.y; B.vz[r] = v.z;
-    if (clamp[s] == 1) force[r] = make_double4(0.0, 0.0, 0.0, 0.0);
 }
 
 // ------------------------------------------------------------------ slab decomposition -----
@@ -1635,6 +1624,19 @@ void launch_pass_a(const Launch& L)
                    L.A, L.nbr, L.ncount, po);
 }
 
+static StructHook struct_hook(const Launch& L)
+{
+    StructHook h{};
+    if (L.P->n_struct > 0 && L.S && L.S->slot_of) {
+        h.slot_of = L.S->slot_of;
+        h.sx = L.S->x;
+        h.sv = L.S->v;
+        h.su = L.S->u;
+        h.sx0 = L.S->x0;
+    }
+    return h;
+}
+
 void launch_pass_b(const Launch& L, int phase)
 {
     Profiler* prof = L.prof;
@@ -1642,7 +1644,8 @@ void launch_pass_b(const Launch& L, int phase)
     if (P.n == 0) return;
 #define MPH_PASS_B(S, D)                                                                            \
     MPH_LAUNCH("pass_b", L.stream, (k_pass_b<S, D>), dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, \
-               L.T, L.A, L.rec, L.fpart, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, L.force, L.acc, L.B, phase)
+               L.T, L.A, L.rec, L.fpart, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, L.force, L.acc, L.B, phase, \
+               struct_hook(L))
     if (P.surface) {
         if (P.dim == 3) MPH_PASS_B(true, 3); else MPH_PASS_B(true, 2);
     } else {
@@ -1671,25 +1674,21 @@ void launch_structure(const Launch& L)
     const int ns = P.n_struct;
     if (ns == 0) return;
     const StructDev& S = *L.S;
-    MPH_LAUNCH("struct_gather", L.stream, k_struct_gather, dim3(blocks(ns, 256)), dim3(256), 0, L.stream, P, ns,
-               S.orig, L.rank_of, L.B, S.x0, S.x, S.v, S.u);
     for (int sub = 0; sub < P.substeps; ++sub) {
         if (P.dim == 3) {
             MPH_LAUNCH("struct_stress", L.stream, k_struct_stress<3>, dim3(blocks(ns, 256)), dim3(256), 0,
                        L.stream, P, ns, S.wo, S.ocnt, S.eo_nb, S.x0, S.u, S.L, S.lame, S.P, S.F, S.E, S.S);
             MPH_LAUNCH("struct_velocity", L.stream, k_struct_velocity<3>, dim3(blocks(ns, 256)), dim3(256), 0,
                        L.stream, P, ns, S.wi, S.icnt, S.ei_nb, S.wx0, S.P, S.inv_rho, S.clamp, S.x0,
-                       S.x, S.v, S.u);
+                       S.x, S.v, S.u, sub == P.substeps - 1, S.orig, L.rank_of, L.B, L.force);
         } else {
             MPH_LAUNCH("struct_stress", L.stream, k_struct_stress<2>, dim3(blocks(ns, 256)), dim3(256), 0,
                        L.stream, P, ns, S.wo, S.ocnt, S.eo_nb, S.x0, S.u, S.L, S.lame, S.P, S.F, S.E, S.S);
             MPH_LAUNCH("struct_velocity", L.stream, k_struct_velocity<2>, dim3(blocks(ns, 256)), dim3(256), 0,
                        L.stream, P, ns, S.wi, S.icnt, S.ei_nb, S.wx0, S.P, S.inv_rho, S.clamp, S.x0,
-                       S.x, S.v, S.u);
+                       S.x, S.v, S.u, sub == P.substeps - 1, S.orig, L.rank_of, L.B, L.force);
         }
     }
-    MPH_LAUNCH("struct_scatter", L.stream, k_struct_scatter, dim3(blocks(ns, 256)), dim3(256), 0, L.stream,
-               ns, S.orig, L.rank_of, S.clamp, S.x, S.v, L.B, L.force);
 }
 
 void launch_scan(int* cnt, int ncell, int* bsum, int* start, int total, hipStream_t stream, Profiler* prof)
