@@ -62,6 +62,9 @@
 #ifndef MPH_SEARCH_PREFETCH
 #define MPH_SEARCH_PREFETCH 1   // pipeline the per-column start[] loads of the LDS search
 #endif
+#ifndef MPH_PREP_RUNS
+#define MPH_PREP_RUNS 1   // k_prep: one cell-histogram atomic per run of equal keys in a wave
+#endif
 #ifndef MPH_LDS_CAP
 #define MPH_LDS_CAP 192   // candidates staged per wave and stencil column
 #endif
@@ -244,6 +247,33 @@ __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __res
                                               int* __restrict__ cnt, int mode)
 {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (MPH_PREP_RUNS) {
+        // The particles arrive in the previous cell order, so consecutive lanes often share a
+        // cell: one histogram atomic per run of equal keys (slot = run base + rank in the run).
+        // Every lane of the wave takes part in the shuffles; lanes past n form runs of their own.
+        const bool live = p < P.n;
+        int k = -1 - (int)(threadIdx.x & 63);
+        if (live) {
+            double x = B.x[p], y = B.y[p], z = B.z[p];
+            if (mode == 1) move_and_wrap(P, st, B, p, x, y, z);
+            if (!isfinite(x + y + z)) atomicOr(const_cast<int*>(&st->overflow), 4);   // MPH_ERR_NONFINITE
+            k = cell_id(P, x, y, z);
+            key[p] = k;
+        }
+        const int lane = threadIdx.x & 63;
+        const int kprev = __shfl_up(k, 1, 64);
+        const bool head = lane == 0 || kprev != k;
+        const unsigned long long heads = __ballot(head);
+        const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+        const int hl = 63 - __clzll(heads & upto);
+        const unsigned long long above = heads & ~upto;
+        const int next = above ? __ffsll((long long)above) - 1 : 64;
+        int base = 0;
+        if (live && head) base = atomicAdd(&cnt[k], next - lane);
+        base = __shfl(base, hl, 64);
+        if (live) slot[p] = base + (lane - hl);
+        return;
+    }
     if (p >= P.n) return;
     double x = B.x[p], y = B.y[p], z = B.z[p];
     if (mode == 1) move_and_wrap(P, st, B, p, x, y, z);
