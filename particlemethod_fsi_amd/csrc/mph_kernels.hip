@@ -769,8 +769,14 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
 #pragma unroll
                 for (int u = 0; u < SB; ++u) {
                     const int j = j0 + u;
-                    if (accept_interior(P, xs[u] - xi, ys[u] - yi, zs[u] - zi, lo2, hi2) && j < je && j != i) {
-                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) list_store(out + cnt * kTile, nbr_entry(j, st[k0 + u]));
+                    // non-short-circuit conditions (one exec mask), and no branch on the list
+                    // capacity: past kMaxNeighbor the last slot is overwritten and the overflow
+                    // flag ends the run (MPH_ERR_NEIGHBOR_OVERFLOW)
+                    const bool a = accept_interior(P, xs[u] - xi, ys[u] - yi, zs[u] - zi, lo2, hi2) &
+                                   (j < je) & (j != i);
+                    if (a) {
+                        if (!MPH_DIAG_NOSTORE)
+                            list_store(out + min(cnt, kMaxNeighbor - 1) * kTile, nbr_entry(j, st[k0 + u]));
                         ++cnt;
                     }
                 }
