@@ -575,6 +575,26 @@ static inline double image_ref(double a, double b, double w)
     return mod_ref(a - b + 0.5 * w, w) - 0.5 * w;
 }
 
+// f(b, e) over [0, n) in contiguous chunks on the host's cores (the per-slot work of
+// build_structure is independent, so results do not depend on the thread count).
+template <class F>
+static void parallel_ranges(int n, F f)
+{
+    const int hw = (int)std::thread::hardware_concurrency();
+    const int nt = std::max(1, std::min({hw > 0 ? hw : 1, 32, n / 2048}));
+    if (nt <= 1) {
+        f(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const int chunk = (n + nt - 1) / nt;
+    for (int t = 0; t < nt; ++t) {
+        const int b = t * chunk, e = std::min(n, b + chunk);
+        if (b < e) th.emplace_back([&f, b, e] { f(b, e); });
+    }
+    for (auto& x : th) x.join();
+}
+
 int build_structure(const MphConfig& c, const HostDerived& h, int n, const int* prop,
                     const double* pos0, StructureInit& S, std::string& err)
 {
@@ -613,7 +633,9 @@ int build_structure(const MphConfig& c, const HostDerived& h, int n, const int* 
         head[k] = s;
     }
     std::vector<std::vector<int>> rows(ns);
-    for (int s = 0; s < ns; ++s) {
+    std::vector<int> too_many(ns, 0);
+    parallel_ranges(ns, [&](int sb, int se) {
+    for (int s = sb; s < se; ++s) {
         const int i = S.orig[s];
         const double* xi = pos0 + 3 * i;
         const int c0 = cell_of(xi, 0), c1 = cell_of(xi, 1), c2 = cell_of(xi, 2);
@@ -647,11 +669,14 @@ int build_structure(const MphConfig& c, const HostDerived& h, int n, const int* 
                     }
                 }
         std::sort(row.begin(), row.end());
-        if ((int)row.size() >= kMaxNeighbor) {
-            err = "structure particle " + std::to_string(i) + " has >= 512 initial neighbours";
+        too_many[s] = (int)row.size() >= kMaxNeighbor;
+    }
+    });
+    for (int s = 0; s < ns; ++s)
+        if (too_many[s]) {
+            err = "structure particle " + std::to_string(S.orig[s]) + " has >= 512 initial neighbours";
             return MPH_ERR_NEIGHBOR_OVERFLOW;
         }
-    }
     for (int s = 0; s < ns; ++s) {
         S.count[s] = (int)rows[s].size();
         S.offset[s + 1] = S.offset[s] + S.count[s];
@@ -679,7 +704,8 @@ int build_structure(const MphConfig& c, const HostDerived& h, int n, const int* 
     // 2x2 inverse with identity fallback (2-D) or cofactor inverse without fallback (3-D)
     const double rp = h.rp;
     const double hd = dim == 2 ? rp * rp : rp * rp * rp;
-    for (int s = 0; s < ns; ++s) {
+    parallel_ranges(ns, [&](int sb, int se) {
+    for (int s = sb; s < se; ++s) {
         const int i = S.orig[s];
         double N[3][3] = {{0.0}};
         for (int k = S.offset[s]; k < S.offset[s + 1]; ++k) {
@@ -723,6 +749,7 @@ int build_structure(const MphConfig& c, const HostDerived& h, int n, const int* 
         for (int a = 0; a < 3; ++a)
             for (int b = 0; b < 3; ++b) S.normalizer[(size_t)s * 9 + 3 * a + b] = N[a][b];
     }
+    });
     // per-pair constants of the fixed Lagrangian neighbourhood: x0_ij and weight(x0_ij)
     auto pair = [&](int s, int t, double* out4) {
         const int i = S.orig[s], j = S.orig[t];
@@ -735,12 +762,10 @@ int build_structure(const MphConfig& c, const HostDerived& h, int n, const int* 
         out4[3] = (1.0 / h.swp) * (1.0 / hd) * ((1.0 - q) * (1.0 - q));
     };
     S.pair_out.resize((size_t)S.nbr.size() * 4);
-    for (int s = 0; s < ns; ++s)
-        for (int k = S.offset[s]; k < S.offset[s + 1]; ++k) pair(s, S.nbr[k], &S.pair_out[(size_t)k * 4]);
-    S.pair_in.resize((size_t)S.in_nbr.size() * 4);
-    for (int s = 0; s < ns; ++s)
-        for (int k = S.in_offset[s]; k < S.in_offset[s + 1]; ++k)
-            pair(S.in_nbr[k], s, &S.pair_in[(size_t)k * 4]);   // x0_{i s} from the sender i
+    parallel_ranges(ns, [&](int sb, int se) {
+        for (int s = sb; s < se; ++s)
+            for (int k = S.offset[s]; k < S.offset[s + 1]; ++k) pair(s, S.nbr[k], &S.pair_out[(size_t)k * 4]);
+    });
     return MPH_OK;
 }
 

@@ -15,7 +15,7 @@ struct StructureInit {
     std::vector<int> count;         // InitialStructureNeighborCount per slot
     std::vector<int> offset, nbr;   // CSR of neighbour slots (ascending)
     std::vector<int> in_offset, in_nbr;      // transpose: who lists me (senders of the scatter)
-    std::vector<double> pair_out, pair_in;   // per pair {x0_ij[3], weight(x0_ij)}
+    std::vector<double> pair_out;            // per pair {x0_ij[3], weight(x0_ij)} (host: sum w x0)
     std::vector<double> normalizer;          // [ns][3][3]
     std::vector<double> lame_l, lame_m;
 };
