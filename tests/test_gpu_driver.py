@@ -1,0 +1,124 @@
+"""End to end: the drop-in executable (particlemethod_fsi_amd/lib/mph_explicit) against the
+reference executable itself (oracle/_ref/mph_reference_2d_bar, built from the reference's own
+src/main.cpp by oracle/Makefile) on the same .data/.grid files, same command line
+(main.cpp:494-508).
+
+Both write output.vtk, the .prof files at OutputInterval and the .vtk files at VtkOutputInterval
+(main.cpp:572-683).  Compared:
+  * the same file names;
+  * output.vtk byte for byte (written before the first step);
+  * every later .prof / .vtk section by section: integers (types, neighbour counts) exactly,
+    numbers printed with %e to within one unit of their 7th significant digit (2e-6 relative)
+    plus 1e-9 of the section's largest magnitude for entries that are pure roundoff in both runs
+    (e.g. the horizontal acceleration of fluid at rest, ~1e-11).
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from particlemethod_fsi_amd import cases
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_EXE = os.path.join(ROOT, "oracle", "_ref", "mph_reference_2d_bar")
+DRIVER = os.path.join(ROOT, "particlemethod_fsi_amd", "lib", "mph_explicit")
+# 31 steps of the results/Dam case with .prof every 10 steps and .vtk every 10 steps
+RUN = {"EndTime": [0.003], "OutputInterval": [0.001], "VtkOutputInterval": [0.001]}
+
+
+def write_case(d):
+    c = cases.get("dam2d")
+    values = c.data()
+    values.update(RUN)
+    with open(os.path.join(d, "dam.data"), "w") as fh:
+        fh.write(cases.data_text(values))
+    with open(os.path.join(d, "dam.grid"), "w") as fh:
+        fh.write(c.grid_text())
+
+
+def run(exe, d, env=None):
+    cmd = [exe, "dam.data", "dam.grid", "dam%03d.prof", "dam%03d.vtk", "dam.log", "4"]
+    r = subprocess.run(cmd, cwd=d, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (exe, r.stdout[-1000:], r.stderr[-2000:])
+    return sorted(f for f in os.listdir(d) if f.endswith((".vtk", ".prof")))
+
+
+def sections(path):
+    """-> list of (header, [token rows]): a .vtk splits at its keyword lines, a .prof into its two
+    header lines and one section per column of the particle rows."""
+    with open(path) as fh:
+        lines = [ln.split() for ln in fh.read().splitlines()]
+    if path.endswith(".prof"):
+        rows = lines[2:]
+        cols = [("prof col %d" % k, [[r[k]] for r in rows]) for k in range(len(rows[0]))] if rows else []
+        return [("prof header", lines[:2])] + cols
+    out = []
+    for ln in lines:
+        if ln and not _number(ln[0]):
+            out.append((" ".join(ln), []))
+        elif ln:
+            if not out:
+                out.append(("", []))
+            out[-1][1].append(ln)
+    return out
+
+
+def _number(t):
+    try:
+        float(t)
+        return True
+    except ValueError:
+        return False
+
+
+def compare_numeric(a_path, b_path):
+    """Integers exactly; %e numbers to one unit of the 7th digit (2e-6 relative) plus a roundoff
+    floor of 1e-9 of the section's largest magnitude (the parity tests' relative floors)."""
+    sa, sb = sections(a_path), sections(b_path)
+    assert [h for h, _ in sa] == [h for h, _ in sb], a_path
+    for (h, ra), (_, rb) in zip(sa, sb):
+        ta = [t for r in ra for t in r]
+        tb = [t for r in rb for t in r]
+        assert len(ta) == len(tb), (a_path, h)
+        ints = [x.lstrip("-").isdigit() and y.lstrip("-").isdigit() for x, y in zip(ta, tb)]
+        assert all(x == y for x, y, i in zip(ta, tb, ints) if i), (a_path, h)
+        a = np.array([float(x) for x, i in zip(ta, ints) if not i])
+        b = np.array([float(y) for y, i in zip(tb, ints) if not i])
+        if not a.size:
+            continue
+        tol = 2e-6 * np.abs(b) + 1e-9 * float(np.max(np.abs(b))) + 1e-30
+        bad = np.abs(a - b) > tol
+        assert not bad.any(), (a_path, h, a[bad][:3], b[bad][:3])
+
+
+def test_reference_executable_runs(tmp_path):
+    """CPU half of the comparison (also checks the harness builds of oracle/_ref are sane)."""
+    if not os.path.exists(REF_EXE):
+        pytest.skip("oracle/_ref/mph_reference_2d_bar not built (needs /root/reference)")
+    d = str(tmp_path / "ref")
+    os.makedirs(d)
+    write_case(d)
+    files = run(REF_EXE, d)
+    assert "output.vtk" in files and "dam000.prof" in files and len(files) >= 6, files
+
+
+@pytest.mark.gpu
+def test_driver_matches_reference_executable(tmp_path):
+    if not os.path.exists(REF_EXE):
+        pytest.skip("oracle/_ref/mph_reference_2d_bar not built (needs /root/reference)")
+    assert os.path.exists(DRIVER), "mph_explicit not built"
+    dr, dg = str(tmp_path / "ref"), str(tmp_path / "gpu")
+    os.makedirs(dr)
+    os.makedirs(dg)
+    write_case(dr)
+    write_case(dg)
+    files_ref = run(REF_EXE, dr)
+    env = dict(os.environ, MPH_DIM="2", MPH_MODULE="bar")
+    files_gpu = run(DRIVER, dg, env)
+    assert files_gpu == files_ref
+    with open(os.path.join(dr, "output.vtk"), "rb") as a, open(os.path.join(dg, "output.vtk"), "rb") as b:
+        assert a.read() == b.read()
+    for f in files_ref:
+        if f != "output.vtk":
+            compare_numeric(os.path.join(dg, f), os.path.join(dr, f))
