@@ -9,8 +9,9 @@ Both write output.vtk, the .prof files at OutputInterval and the .vtk files at V
   * output.vtk byte for byte (written before the first step);
   * every later .prof / .vtk section by section: integers (types, neighbour counts) exactly,
     numbers printed with %e to within one unit of their 7th significant digit (2e-6 relative)
-    plus 1e-9 of the section's largest magnitude for entries that are pure roundoff in both runs
-    (e.g. the horizontal acceleration of fluid at rest, ~1e-11).
+    plus 1e-9 of the section's largest magnitude, plus the parity tests' absolute tolerances
+    for the quantity (FLOORS), since many entries are pure roundoff in both runs (e.g. the
+    horizontal velocity of fluid at rest, ~1e-13 m/s).
 """
 import os
 import subprocess
@@ -21,14 +22,19 @@ import pytest
 from particlemethod_fsi_amd import cases
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-REF_EXE = os.path.join(ROOT, "oracle", "_ref", "mph_reference_2d_bar")
+REF_DIR = os.path.join(ROOT, "oracle", "_ref")
+REF_EXE = os.path.join(REF_DIR, "mph_reference_2d_bar")
+# case -> (reference build, MPH_DIM, MPH_MODULE of the drop-in driver)
+VARIANTS = {"dam2d": ("mph_reference_2d_bar", "2", "bar"),
+            # the sub-stepped gate: with ElasticDt = Dt the reference solid is unstable
+            "gate3d_sub": ("mph_reference_3d_dam", "3", "dam")}
 DRIVER = os.path.join(ROOT, "particlemethod_fsi_amd", "lib", "mph_explicit")
 # 31 steps of the results/Dam case with .prof every 10 steps and .vtk every 10 steps
 RUN = {"EndTime": [0.003], "OutputInterval": [0.001], "VtkOutputInterval": [0.001]}
 
 
-def write_case(d):
-    c = cases.get("dam2d")
+def write_case(d, case="dam2d"):
+    c = cases.get(case)
     values = c.data()
     values.update(RUN)
     with open(os.path.join(d, "dam.data"), "w") as fh:
@@ -56,7 +62,10 @@ def sections(path):
     out = []
     for ln in lines:
         if ln and not _number(ln[0]):
-            out.append((" ".join(ln), []))
+            if out and not out[-1][1]:   # consecutive keyword lines: one header
+                out[-1] = (out[-1][0] + " | " + " ".join(ln), [])
+            else:
+                out.append((" ".join(ln), []))
         elif ln:
             if not out:
                 out.append(("", []))
@@ -70,6 +79,15 @@ def _number(t):
         return True
     except ValueError:
         return False
+
+
+# absolute floors = the parity tests' tolerances for the same quantities (test_gpu_parity.py):
+# positions 1e-12 m, velocities 1e-9 m/s, accelerations ~1e-9 of O(1) m/s^2, elastic tensors at
+# rest (stress 1e-8 Pa, strain 1e-13); .prof columns: 1-6 positions, 7-9 velocities
+FLOORS = {"POINTS": 1e-12, "displacement": 1e-12, "velocity": 1e-9, "accel": 1e-9, "stress": 1e-8,
+          "strain": 1e-13, "prof col 1": 1e-12, "prof col 2": 1e-12, "prof col 3": 1e-12,
+          "prof col 4": 1e-12, "prof col 5": 1e-12, "prof col 6": 1e-12, "prof col 7": 1e-9,
+          "prof col 8": 1e-9, "prof col 9": 1e-9}
 
 
 def compare_numeric(a_path, b_path):
@@ -87,7 +105,8 @@ def compare_numeric(a_path, b_path):
         b = np.array([float(y) for y, i in zip(tb, ints) if not i])
         if not a.size:
             continue
-        tol = 2e-6 * np.abs(b) + 1e-9 * float(np.max(np.abs(b))) + 1e-30
+        floor = FLOORS.get(next((k for k in FLOORS if k in h), ""), 1e-30)
+        tol = 2e-6 * np.abs(b) + 1e-9 * float(np.max(np.abs(b))) + floor
         bad = np.abs(a - b) > tol
         assert not bad.any(), (a_path, h, a[bad][:3], b[bad][:3])
 
@@ -104,17 +123,20 @@ def test_reference_executable_runs(tmp_path):
 
 
 @pytest.mark.gpu
-def test_driver_matches_reference_executable(tmp_path):
-    if not os.path.exists(REF_EXE):
-        pytest.skip("oracle/_ref/mph_reference_2d_bar not built (needs /root/reference)")
+@pytest.mark.parametrize("case", sorted(VARIANTS))
+def test_driver_matches_reference_executable(tmp_path, case):
+    exe, dim, module = VARIANTS[case]
+    exe = os.path.join(REF_DIR, exe)
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref reference executable not built (needs /root/reference)")
     assert os.path.exists(DRIVER), "mph_explicit not built"
     dr, dg = str(tmp_path / "ref"), str(tmp_path / "gpu")
     os.makedirs(dr)
     os.makedirs(dg)
-    write_case(dr)
-    write_case(dg)
-    files_ref = run(REF_EXE, dr)
-    env = dict(os.environ, MPH_DIM="2", MPH_MODULE="bar")
+    write_case(dr, case)
+    write_case(dg, case)
+    files_ref = run(exe, dr)
+    env = dict(os.environ, MPH_DIM=dim, MPH_MODULE=module)
     files_gpu = run(DRIVER, dg, env)
     assert files_gpu == files_ref
     with open(os.path.join(dr, "output.vtk"), "rb") as a, open(os.path.join(dg, "output.vtk"), "rb") as b:
