@@ -29,6 +29,7 @@
 // 32-byte records); SoA makes consecutive lanes gather consecutive doubles.
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cstdlib>
 
 #include "mph_kernels.h"
@@ -666,8 +667,31 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
     return cnt;
 }
 
+#ifndef MPH_DPP_REDUCE
+#define MPH_DPP_REDUCE 1   // wave min/max by DPP row shifts + row broadcasts (else ds_bpermute)
+#endif
+
+// Wave-wide min / max (result in every lane).  DPP form: shifts within 16-lane rows, then
+// row_bcast:15 / :31 carry the partial results across rows (gfx9 family), lane 63 holds the
+// total; 7 dependent VALU steps instead of 6 dependent LDS permutes.
+template <bool MAX>
+__device__ __forceinline__ int wave_reduce_dpp(int v)
+{
+    const int id = MAX ? INT_MIN : INT_MAX;
+    auto op = [](int a, int b) { return MAX ? max(a, b) : min(a, b); };
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x111, 0xf, 0xf, false));   // row_shr:1
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x112, 0xf, 0xf, false));   // row_shr:2
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x113, 0xf, 0xf, false));   // row_shr:3
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x114, 0xf, 0xe, false));   // row_shr:4
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x118, 0xf, 0xc, false));   // row_shr:8
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x143, 0xc, 0xf, false));   // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
 __device__ __forceinline__ int wave_min(int v)
 {
+    if (MPH_DPP_REDUCE) return wave_reduce_dpp<false>(v);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
     return v;
@@ -675,6 +699,7 @@ __device__ __forceinline__ int wave_min(int v)
 
 __device__ __forceinline__ int wave_max(int v)
 {
+    if (MPH_DPP_REDUCE) return wave_reduce_dpp<true>(v);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
     return v;
