@@ -94,15 +94,17 @@ print(json.dumps({'value': p.n * k / (t3 - t2), 'unit': 'particle-steps/s', 'cor
         return {"error": repr(e)}
 
 
-def load_pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if present."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def load_pmc(name: str, case: str, kernel: str, key: str):
+    """`key` of `kernel` from a committed rocprofv3 PMC summary (profiles/<name>.json, written by
+    tools/pmc_traffic.py / tools/pmc_fp64.py), if it was measured on this case."""
     try:
-        with open(path) as fh:
+        with open(os.path.join(ROOT, "profiles", name + ".json")) as fh:
             d = json.load(fh)
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
+    if d.get("case") != case:
+        return None
+    return d.get(kernel, {}).get(key)
 
 
 def main():
@@ -187,7 +189,12 @@ def main():
     step_ms = sum(v["avg_ms"] * v["launches"] for v in prof.values()) / args.profile_steps
     alg_bytes = alg_bytes_of(dom)
     achieved = alg_bytes / (prof[dom]["avg_ms"] * 1e-3) / 1e9
-    traffic = load_pmc_traffic(dom)
+    traffic = load_pmc("pmc_traffic", case_name, dom, "hbm_bytes_per_launch")
+    # FP64 utilisation: PMC lane FLOPs per launch over the same live launch time
+    flops = {k: load_pmc("pmc_fp64", case_name, k, "lane_flops_per_launch") for k in prof}
+    fp64 = {k: {"tflops": f / (prof[k]["avg_ms"] * 1e-3) / 1e12,
+                "frac": f / (prof[k]["avg_ms"] * 1e-3) / 1e12 / FP64_PEAK_TFLOPS}
+            for k, f in flops.items() if f}
     out = {
         "metric": "particle-steps/sec + achieved HBM GB/s, dam-break, 1/2/4/8 MI355X",
         "value": value,
@@ -212,6 +219,10 @@ def main():
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
                      "avg_launch_ms": prof[dom]["avg_ms"]},
+        "fp64": ({"peak_tflops": FP64_PEAK_TFLOPS, "source": "profiles/pmc_fp64.json (64 x "
+                  "SQ_INSTS_VALU_FLOPS_FP64 per launch, masked lanes included)",
+                  "kernels": {k: {a: round(b, 4) for a, b in v.items()} for k, v in fp64.items()}}
+                 if fp64 else None),
         "kernels_ms": {k: round(v["avg_ms"], 5) for k, v in prof.items()},
         "profiled_step_ms": step_ms,
     }

@@ -11,6 +11,7 @@ import collections
 import csv
 import glob
 import json
+import os
 import sys
 
 
@@ -34,7 +35,8 @@ def main():
              "k_rank_scatter": "rank_scatter", "k_scan_down": "scan_down", "k_scan_reduce": "scan_reduce",
              "k_place": "place"}
     out = {"_note": "HBM bytes per launch = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE "
-                    "correction, MI355X_MICROARCH.md); averaged over launches; " + tag}
+                    "correction, MI355X_MICROARCH.md); averaged over launches; " + tag,
+           "case": os.environ.get("MPH_PMC_CASE", "d1m")}
     for k, short in names.items():
         if k in fetch or k in write:
             f, w = fetch.get(k, 0.0), write.get(k, 0.0)
