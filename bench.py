@@ -13,6 +13,9 @@ neighbour search, density/pressure sums, pressure/surface/viscous forces, gravit
 For N > 1 (torchrun, one rank per GPU) the ranks run the slab decomposition (z slabs, RCCL
 halo exchange; csrc/mph_dist.hip) of the D1M tank extended N-fold along z, so the per-GPU work
 stays about one D1M (weak scaling); `value` counts every particle of the whole job per step.
+Other cases (`--case bar2d_400k`, `fsi3d`, ...) split the same problem over the N ranks (strong
+scaling; 2-D cases in x slabs, 3-D in z slabs; elastic particles stay with the slab of their
+InitialPosition).
 MPH_SLAB_TRANSPORT=host switches the halo transport to host staging over gloo (diagnostics).
 
 Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel's algorithmic HBM bytes per
@@ -44,7 +47,7 @@ ALG_BYTES = {"pass_a": 92.0, "neighbors_pass_a": 92.0, "pass_b": 140.0, "sort": 
 #   struct_velocity read P (72), v, x (48), out- and in-lists (8 n_s); write v, x (48)
 STRUCT_BYTES = {"struct_stress": (208.0, 4.0), "struct_velocity": (168.0, 8.0)}
 B_ALG_STEP = 372.0          # grid build 140 + pass 1 92 + pass 2 140
-SLAB_AXIS = 2               # z slabs for the dam workloads
+SLAB_AXIS = {2: 0, 3: 2}    # by dimension: z slabs for the 3-D dam workloads, x in 2-D
 
 
 def dist_env():
@@ -141,7 +144,7 @@ def main():
     if dist is not None:
         from particlemethod_fsi_amd.dist import gloo_slab, rccl_slab
         mk = gloo_slab if os.environ.get("MPH_SLAB_TRANSPORT") == "host" else rccl_slab
-        solver = MphSolver(cfg, parts, device=device, slab=mk(rank, world, SLAB_AXIS))
+        solver = MphSolver(cfg, parts, device=device, slab=mk(rank, world, SLAB_AXIS[case.dim]))
         n_local = len(solver.owned_ids())
     else:
         solver = MphSolver(cfg, parts, device=device)
@@ -204,15 +207,15 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if world == 1 or case_name != args.case else "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (reference generator algorithm + results/Dam/dam.data parameters)",
         "config": {"workload": "%s: %s, %d particles, ~%d per GPU"
                                % (case_name, case.describe(), n_total, n_total // world),
                    "particles": n_total, "dim": case.dim, "module": case.module, "dt": cfg.dt,
-                   "parallelism": "single" if world == 1 else "slab%d-z (%s halo exchange)" % (
-                       world, "host-staged" if os.environ.get("MPH_SLAB_TRANSPORT") == "host" else "RCCL")},
+                   "parallelism": "single" if world == 1 else "slab%d-%s (%s halo exchange)" % (
+                       world, "xyz"[SLAB_AXIS[case.dim]], "host-staged" if os.environ.get("MPH_SLAB_TRANSPORT") == "host" else "RCCL")},
         "achieved_hbm_gbps_alg": B_ALG_STEP * value / 1e9,
         "neighbors": {"mean": mean_nb, "max": max_nb},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS,

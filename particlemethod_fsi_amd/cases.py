@@ -161,6 +161,11 @@ _reg(Case("bar2d_400k", 2, "bar", 0.0001, (-0.001, -0.05, 0.0), (0.25, 0.05, 0.0
 ], data_changes={"Dt": [1e-5], "ElasticDt": [1e-5]},
    note="2-D elastic cantilever, total-Lagrangian solid (SURVEY 8d Bar, BASELINE configs[2])"))
 
+# small 3-D cantilever (Bar_Module): the 3-D elastic path across slab faces (slab tests)
+_reg(Case("bar3d", 3, "bar", 0.001, (-0.01, -0.03, -0.03), (0.08, 0.03, 0.03), [
+    Cuboid(2, (0.0, -0.005, -0.005), (0.06, 0.005, 0.005), 0.001),
+], note="3-D elastic cantilever, 6,000 structure particles (slab tests)"))
+
 # 2-D dam break onto an elastic gate (DAM_Module), 7,035 particles = 4,850 + 400 + 1,785
 _reg(Case("gate2d", 2, "dam", 0.001, (-0.01, 0.0, 0.0), (0.21, 0.40, 0.001), [
     Cuboid(1, (0.0, 0.003, 0.0), (0.05, 0.10, 0.001), 0.001),

@@ -41,6 +41,9 @@ struct MphDist {
     void* host_user = nullptr;
     char* host_stage = nullptr;   // pinned staging for the host transport (4 messages)
     int* hcnt = nullptr;          // pinned count messages (send 4, recv 4)
+    // elastic ghost slots (static): local slot indices sent to / received from each neighbour
+    int *ss_l = nullptr, *ss_r = nullptr, *sr_l = nullptr, *sr_r = nullptr;
+    int nss_l = 0, nss_r = 0, nsr_l = 0, nsr_r = 0;
 };
 
 struct MphCtx {
@@ -62,6 +65,7 @@ struct MphCtx {
     std::vector<int> prop;
     std::vector<double> pos0;
     mph::StructureInit S;
+    std::vector<int> sl_orig;    // local structure slot -> original particle index
     // device
     mph::DevTables* dT = nullptr;
     mph::DevState* dst = nullptr;
@@ -108,6 +112,9 @@ int ctx_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, c
 
 // slab mode (mph_dist.hip)
 int dist_setup(MphCtx* c, const double* pos, std::vector<int>& owned);   // geometry + owned set
+// elastic slots of this rank: lsl = [owned | ghosts from the left | ghosts from the right] (global
+// slot ids), n_own owned; records the per-substep ghost exchange lists
+int dist_struct_setup(MphCtx* c, std::vector<int>& lsl, int& n_own);
 int dist_alloc(MphCtx* c);                                               // exchange buffers
 int dist_init(MphCtx* c);                                                // first exchange + init sums
 int dist_step(MphCtx* c, int nsteps, Profiler* prof = nullptr);

@@ -175,13 +175,13 @@ int download_w(MphCtx* c, const double4* d, const int* ids, double* out)
 
 int download_struct_m33(MphCtx* c, const double* d, double* out)
 {
-    const int ns = (int)c->S.orig.size();
+    const int ns = c->Sd.n_own;   // slots computed here (slab mode: owned)
     std::memset(out, 0, sizeof(double) * 9 * (size_t)c->n_glob);
     if (ns == 0) return MPH_OK;
     std::vector<double> h((size_t)ns * 9);
     HIP_OK(c, hipMemcpyAsync(h.data(), d, sizeof(double) * 9 * ns, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipStreamSynchronize(c->stream));
-    for (int s = 0; s < ns; ++s) std::memcpy(out + (size_t)9 * c->S.orig[s], &h[(size_t)9 * s], sizeof(double) * 9);
+    for (int s = 0; s < ns; ++s) std::memcpy(out + (size_t)9 * c->sl_orig[s], &h[(size_t)9 * s], sizeof(double) * 9);
     return MPH_OK;
 }
 
@@ -235,13 +235,9 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     c->prop.assign(property, property + n);
     c->pos0.assign(pos0, pos0 + 3 * (size_t)n);
     std::string err;
-    if (c->dist) {
-        for (int i = 0; i < n; ++i)
-            if (is_struct(property[i]))
-                return fail(c, MPH_ERR_UNSUPPORTED, "slab mode does not support elastic-solid particles");
-    } else {
-        CK(fail(c, build_structure(c->cfg, c->h, n, property, pos0, c->S, err), err));
-    }
+    // the fixed Lagrangian structure lists (every rank builds all of them in slab mode and keeps
+    // its owned slots plus their ghost neighbours, dist_struct_setup)
+    CK(fail(c, build_structure(c->cfg, c->h, n, property, pos0, c->S, err), err));
     const int ns = (int)c->S.orig.size();
     make_dev_params(c->cfg, c->h, n, ns, c->P);
     const double rc = std::sqrt(c->P.rc2);
@@ -339,17 +335,32 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         HIP_OK(c, hipMemcpy(c->B.type, types.data(), sizeof(int) * m, hipMemcpyHostToDevice));
         HIP_OK(c, hipMemcpy(c->B.id, ids.data(), sizeof(int) * m, hipMemcpyHostToDevice));
     }
-    // elastic solid
+    // elastic solid: local slots = [computed here | ghosts] (single GPU: every slot, no ghosts)
     if (ns > 0) {
         StructDev& D = c->Sd;
         const StructureInit& S = c->S;
-        // ELL tiles of the fixed out-list and of its transpose (StructDev)
-        const size_t ntile_s = ((size_t)ns + 63) / 64;
-        std::vector<int> ocnt(ns), icnt(ns);
+        std::vector<int> lsl;   // local slot -> global slot
+        int no = ns;
+        if (c->dist) {
+            CK(dist_struct_setup(c, lsl, no));
+        } else {
+            lsl.resize(ns);
+            for (int s = 0; s < ns; ++s) lsl[s] = s;
+        }
+        const int nl = (int)lsl.size();
+        std::vector<int> loc(ns, -1);
+        for (int k = 0; k < nl; ++k) loc[lsl[k]] = k;
+        D.n_own = no;
+        c->sl_orig.resize(nl);
+        for (int k = 0; k < nl; ++k) c->sl_orig[k] = S.orig[lsl[k]];
+        // ELL tiles of the fixed out-list and of its transpose (StructDev), computed slots only
+        const size_t ntile_s = ((size_t)std::max(no, 1) + 63) / 64;
+        std::vector<int> ocnt(std::max(no, 1), 0), icnt(std::max(no, 1), 0);
         int wo = 0, wi = 0;
-        for (int s = 0; s < ns; ++s) {
-            ocnt[s] = S.offset[s + 1] - S.offset[s];
-            icnt[s] = S.in_offset[s + 1] - S.in_offset[s];
+        for (int s = 0; s < no; ++s) {
+            const int g = lsl[s];
+            ocnt[s] = S.offset[g + 1] - S.offset[g];
+            icnt[s] = S.in_offset[g + 1] - S.in_offset[g];
             wo = std::max(wo, ocnt[s]);
             wi = std::max(wi, icnt[s]);
         }
@@ -358,40 +369,46 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         D.wo = wo;
         D.wi = wi;
         std::vector<int> eo_nb(ntile_s * wo * 64, 0), ei_nb(ntile_s * wi * 64, 0);
-        std::vector<double4> wx0(ns);
-        for (int s = 0; s < ns; ++s) {
+        std::vector<double4> wx0(nl, make_double4(0.0, 0.0, 0.0, 0.0));
+        for (int s = 0; s < no; ++s) {
+            const int g = lsl[s];
             const size_t base_o = (size_t)(s >> 6) * wo * 64 + (s & 63);
-            double c[3] = {0.0, 0.0, 0.0};
+            double c3[3] = {0.0, 0.0, 0.0};
             for (int k = 0; k < ocnt[s]; ++k) {
-                const size_t q = S.offset[s] + k;
+                const size_t q = S.offset[g] + k;
                 const double* pr = &S.pair_out[4 * q];
-                eo_nb[base_o + (size_t)k * 64] = S.nbr[q];
-                for (int d = 0; d < 3; ++d) c[d] += pr[3] * pr[d];
+                eo_nb[base_o + (size_t)k * 64] = loc[S.nbr[q]];
+                for (int d = 0; d < 3; ++d) c3[d] += pr[3] * pr[d];
             }
-            wx0[s] = make_double4(c[0], c[1], c[2], 0.0);
+            wx0[s] = make_double4(c3[0], c3[1], c3[2], 0.0);
             const size_t base_i = (size_t)(s >> 6) * wi * 64 + (s & 63);
             for (int k = 0; k < icnt[s]; ++k) {
-                const size_t q = S.in_offset[s] + k;
-                ei_nb[base_i + (size_t)k * 64] = S.in_nbr[q];
+                const size_t q = S.in_offset[g] + k;
+                ei_nb[base_i + (size_t)k * 64] = loc[S.in_nbr[q]];
             }
         }
+        for (int e : eo_nb) if (e < 0) return fail(c, MPH_ERR_DOMAIN, "structure list leaves the ghost slots");
+        for (int e : ei_nb) if (e < 0) return fail(c, MPH_ERR_DOMAIN, "structure list leaves the ghost slots");
         const int sd = c->P.dim;
-        CK(dalloc(c, &D.orig, ns)); CK(dalloc(c, &D.ocnt, ns)); CK(dalloc(c, &D.icnt, ns));
+        CK(dalloc(c, &D.orig, nl)); CK(dalloc(c, &D.ocnt, ocnt.size())); CK(dalloc(c, &D.icnt, icnt.size()));
+        CK(dalloc(c, &D.bidx, nl));
         CK(dalloc(c, &D.eo_nb, eo_nb.size()));
         CK(dalloc(c, &D.ei_nb, ei_nb.size()));
-        CK(dalloc(c, &D.wx0, ns));
-        CK(dalloc(c, &D.L, (size_t)ns * 9)); CK(dalloc(c, &D.lame, ns)); CK(dalloc(c, &D.inv_rho, ns));
-        CK(dalloc(c, &D.clamp, ns)); CK(dalloc(c, &D.x0, ns)); CK(dalloc(c, &D.x, ns)); CK(dalloc(c, &D.v, ns));
-        CK(dalloc(c, &D.u, ns)); CK(dalloc(c, &D.P, (size_t)ns * (sd == 2 ? 1 : 3))); CK(dalloc(c, &D.F, (size_t)ns * 9));
-        CK(dalloc(c, &D.E, (size_t)ns * 9)); CK(dalloc(c, &D.S, (size_t)ns * 9));
-        std::vector<double2> lame(ns);
-        std::vector<double> irho(ns);
-        std::vector<int> clamp(ns);
-        std::vector<double4> x0(ns);
-        for (int s = 0; s < ns; ++s) {
-            const int i = S.orig[s];
+        CK(dalloc(c, &D.wx0, nl));
+        CK(dalloc(c, &D.L, (size_t)nl * 9)); CK(dalloc(c, &D.lame, nl)); CK(dalloc(c, &D.inv_rho, nl));
+        CK(dalloc(c, &D.clamp, nl)); CK(dalloc(c, &D.x0, nl)); CK(dalloc(c, &D.x, nl)); CK(dalloc(c, &D.v, nl));
+        CK(dalloc(c, &D.u, nl)); CK(dalloc(c, &D.P, (size_t)nl * (sd == 2 ? 1 : 3))); CK(dalloc(c, &D.F, (size_t)nl * 9));
+        CK(dalloc(c, &D.E, (size_t)nl * 9)); CK(dalloc(c, &D.S, (size_t)nl * 9));
+        std::vector<double2> lame(nl);
+        std::vector<double> irho(nl), Lm((size_t)nl * 9);
+        std::vector<int> clamp(nl);
+        std::vector<double4> x0(nl);
+        for (int s = 0; s < nl; ++s) {
+            const int g = lsl[s];
+            const int i = S.orig[g];
             const int t = property[i];
-            lame[s] = make_double2(S.lame_l[s], S.lame_m[s]);
+            std::memcpy(&Lm[(size_t)9 * s], &S.normalizer[(size_t)9 * g], sizeof(double) * 9);
+            lame[s] = make_double2(S.lame_l[g], S.lame_m[g]);
             irho[s] = 1.0 / cfg->density[t];
             const double* p0 = pos0 + 3 * i;
             int cl = 0;   // updateElasticPosition module clamps (main.cpp:1918-2044)
@@ -409,10 +426,10 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         auto up = [&](auto* d, const auto& v) {
             return hipMemcpyAsync(d, v.data(), v.size() * sizeof(v[0]), hipMemcpyHostToDevice, c->stream);
         };
-        HIP_OK(c, hipMemcpyAsync(D.orig, S.orig.data(), sizeof(int) * ns, hipMemcpyHostToDevice, c->stream));
+        HIP_OK(c, hipMemcpyAsync(D.orig, c->sl_orig.data(), sizeof(int) * nl, hipMemcpyHostToDevice, c->stream));
         {
             std::vector<int> slot_of((size_t)c->n_glob, -1);
-            for (int s = 0; s < ns; ++s) slot_of[S.orig[s]] = s;
+            for (int s = 0; s < no; ++s) slot_of[c->sl_orig[s]] = s;
             CK(dalloc(c, &D.slot_of, slot_of.size()));
             HIP_OK(c, hipMemcpy(D.slot_of, slot_of.data(), sizeof(int) * slot_of.size(), hipMemcpyHostToDevice));
         }
@@ -420,14 +437,16 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         HIP_OK(c, up(D.eo_nb, eo_nb));
         HIP_OK(c, up(D.ei_nb, ei_nb));
         HIP_OK(c, up(D.wx0, wx0));
-        HIP_OK(c, hipMemcpyAsync(D.L, S.normalizer.data(), sizeof(double) * 9 * ns, hipMemcpyHostToDevice, c->stream));
-        HIP_OK(c, hipMemcpyAsync(D.lame, lame.data(), sizeof(double2) * ns, hipMemcpyHostToDevice, c->stream));
-        HIP_OK(c, hipMemcpyAsync(D.inv_rho, irho.data(), sizeof(double) * ns, hipMemcpyHostToDevice, c->stream));
-        HIP_OK(c, hipMemcpyAsync(D.clamp, clamp.data(), sizeof(int) * ns, hipMemcpyHostToDevice, c->stream));
-        HIP_OK(c, hipMemcpyAsync(D.x0, x0.data(), sizeof(double4) * ns, hipMemcpyHostToDevice, c->stream));
-        HIP_OK(c, hipMemsetAsync(D.P, 0, sizeof(double4) * (sd == 2 ? 1 : 3) * ns, c->stream));
+        HIP_OK(c, up(D.L, Lm));
+        HIP_OK(c, up(D.lame, lame));
+        HIP_OK(c, up(D.inv_rho, irho));
+        HIP_OK(c, up(D.clamp, clamp));
+        HIP_OK(c, up(D.x0, x0));
+        HIP_OK(c, hipMemsetAsync(D.P, 0, sizeof(double4) * (sd == 2 ? 1 : 3) * nl, c->stream));
+        HIP_OK(c, hipMemsetAsync(D.u, 0, sizeof(double4) * nl, c->stream));
+        HIP_OK(c, hipMemsetAsync(D.bidx, 0, sizeof(int) * nl, c->stream));
         for (double* m : {D.F, D.E, D.S})
-            HIP_OK(c, hipMemsetAsync(m, 0, sizeof(double) * 9 * ns, c->stream));
+            HIP_OK(c, hipMemsetAsync(m, 0, sizeof(double) * 9 * nl, c->stream));
         HIP_OK(c, hipStreamSynchronize(c->stream));
     }
     fill_launch(c);

@@ -28,6 +28,15 @@
 // Owned particles see every neighbour (band width h >= rc), run the same FP64 expressions as
 // the single-GPU path, and get bit-identical neighbour sets; sums may be ordered differently
 // (local cell grid), so values agree with the single-GPU run to reassociation roundoff.
+//
+// Elastic-solid particles (types 2, 3) are owned by the slab of their InitialPosition for good:
+// their fixed Lagrangian lists (calculateInitialNeighbor, main.cpp:1497-1658) then map to a static
+// set of ghost slots owned by the two neighbours (dist_struct_setup).  They never migrate; they
+// are mirrored as fluid-pass ghosts like any particle near a face, and may sit up to kStructMargin
+// beyond their slab's face (the band width grows by that much).  Each elastic substep
+// (main.cpp:653-660) becomes
+//   7. ghost displacements u -> k_struct_stress on the owned slots -> ghost stresses P ->
+//      k_struct_velocity on the owned slots (the last substep writes the owned B entries).
 // Transport: RCCL ncclSend/ncclRecv (xGMI) or a host callback (tests, mph_create_dist_host).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -45,6 +54,7 @@ using namespace mph;
 namespace {
 
 constexpr size_t kMsgBytes = 56;   // per particle, k_dist_pack layout
+constexpr double kStructMargin = 4.0;   // x ParticleSpacing: elastic particle displacement across a face
 
 #define RCCL_OK(ctx, expr)                                                                     \
     do {                                                                                       \
@@ -65,6 +75,7 @@ SlabGeom make_geom(const HostDerived& h, int axis, int rank, int nranks, double 
 {
     SlabGeom g{};
     g.axis = axis;
+    g.w = h.dw[axis];
     const int l = (rank + nranks - 1) % nranks, r = (rank + 1) % nranks;
     slab_of(h, axis, rank, nranks, g.lo, g.hi);
     slab_of(h, axis, l, nranks, g.llo, g.lhi);
@@ -85,6 +96,28 @@ double wrap_coord(const HostDerived& h, int axis, double x)
 }
 
 double halo_width(const DevParams& P) { return std::sqrt(P.rc2) * (1.0 + 1e-6); }
+
+int owner_rank(const HostDerived& h, int axis, int nranks, double x)
+{
+    const double a = wrap_coord(h, axis, x);
+    for (int r = 0; r < nranks; ++r) {
+        double lo, hi;
+        slab_of(h, axis, r, nranks, lo, hi);
+        if (slab_owns(a, lo, hi, r == 0, r == nranks - 1)) return r;
+    }
+    return nranks - 1;
+}
+
+// signed periodic offset of x from the centre of rank r's slab
+double slab_offset(const HostDerived& h, int axis, int r, int nranks, double x)
+{
+    double lo, hi;
+    slab_of(h, axis, r, nranks, lo, hi);
+    const double W = h.dw[axis];
+    double off = x - 0.5 * (lo + hi);
+    off -= W * std::floor(off / W + 0.5);
+    return off;
+}
 
 int check_geometry(const MphConfig& cfg, int nranks, int axis, std::string& err)
 {
@@ -238,6 +271,42 @@ int halo_exchange(MphCtx* c, Profiler* prof, hipStream_t stream)
     return MPH_OK;
 }
 
+// One static ghost exchange of per-slot double4 records (w rows per slot) of the elastic arrays.
+int struct_exchange(MphCtx* c, double4* a, int w, Profiler* prof)
+{
+    MphDist& D = *c->dist;
+    Launch L = c->L;
+    L.prof = prof;
+    double4* sl = (double4*)D.send_l;
+    double4* sr = (double4*)D.send_r;
+    double4* rl = (double4*)D.recv_l;
+    double4* rr = (double4*)D.recv_r;
+    launch_struct_pack(L, a, w, D.ss_l, D.nss_l, sl);
+    launch_struct_pack(L, a, w, D.ss_r, D.nss_r, sr);
+    const size_t b = sizeof(double4) * w;
+    MPH_CK(exchange(c, c->stream, sl, b * D.nss_l, sr, b * D.nss_r, rl, b * D.nsr_l, rr, b * D.nsr_r));
+    launch_struct_unpack(L, rl, w, D.sr_l, D.nsr_l, a);
+    launch_struct_unpack(L, rr, w, D.sr_r, D.nsr_r, a);
+    return MPH_OK;
+}
+
+// Step 7: the elastic substeps on the owned slots, ghosts refreshed before each half.
+int struct_substeps(MphCtx* c, Profiler* prof)
+{
+    if (c->P.n_struct == 0) return MPH_OK;
+    Launch L = c->L;
+    L.prof = prof;
+    StructDev& S = c->Sd;
+    const int wP = c->P.dim == 2 ? 1 : 3;
+    for (int sub = 0; sub < c->P.substeps; ++sub) {
+        MPH_CK(struct_exchange(c, S.u, 1, prof));
+        launch_struct_stress(L);
+        MPH_CK(struct_exchange(c, S.P, wP, prof));
+        launch_struct_velocity(L, sub == c->P.substeps - 1);
+    }
+    return MPH_OK;
+}
+
 int check_state(MphCtx* c)
 {
     DevState hs;
@@ -259,8 +328,12 @@ int dist_setup(MphCtx* c, const double* pos, std::vector<int>& owned)
     MPH_CK(ctx_fail(c, check_geometry(c->cfg, D.nranks, axis, err), err));
     D.left = (D.rank + D.nranks - 1) % D.nranks;
     D.right = (D.rank + 1) % D.nranks;
-    const double halo = halo_width(c->P);
+    // elastic particles may be displaced up to kStructMargin dx beyond their static slab
+    const bool has_struct = !c->S.orig.empty();
+    const double smargin = has_struct ? kStructMargin * h.dx : 0.0;
+    const double halo = halo_width(c->P) + smargin;
     D.g = make_geom(h, axis, D.rank, D.nranks, halo);
+    D.g.smargin = smargin;
     const double W = h.dw[axis];
     const double cw = W / c->P.gc[axis];
     // slabs must be wider than two halos plus a migration margin, so that a band particle is
@@ -287,6 +360,12 @@ int dist_setup(MphCtx* c, const double* pos, std::vector<int>& owned)
     size_t near = 0;
     for (int i = 0; i < c->n_glob; ++i) {
         const double a = wrap_coord(h, axis, pos[3 * (size_t)i + axis]);
+        if (is_struct(c->prop[i])) {
+            // static owner: the slab of the InitialPosition
+            if (owner_rank(h, axis, D.nranks, c->pos0[3 * (size_t)i + axis]) == D.rank) owned.push_back(i);
+            else ++near;
+            continue;
+        }
         if (slab_owns(a, D.g.lo, D.g.hi, D.g.first, D.g.last)) {
             owned.push_back(i);
         } else {
@@ -301,6 +380,72 @@ int dist_setup(MphCtx* c, const double* pos, std::vector<int>& owned)
     D.cap = (int)std::min<size_t>(want, (size_t)c->n_glob);
     D.msg_cap = D.cap;
     D.n_own = (int)owned.size();
+    return MPH_OK;
+}
+
+int dist_struct_setup(MphCtx* c, std::vector<int>& lsl, int& n_own)
+{
+    MphDist& D = *c->dist;
+    const HostDerived& h = c->h;
+    const StructureInit& S = c->S;
+    const int axis = D.g.axis, R = D.nranks;
+    const int ns = (int)S.orig.size();
+    std::vector<int> owner(ns);
+    for (int s = 0; s < ns; ++s) owner[s] = owner_rank(h, axis, R, c->pos0[3 * (size_t)S.orig[s] + axis]);
+    // ghost slots of rank r: the list neighbours (out- and in-lists) of its owned slots that other
+    // ranks own, split by side (periodic offset of x0 from r's slab centre), ascending slot id
+    std::string err;
+    auto ghosts = [&](int r, std::vector<int>& gl, std::vector<int>& gr) {
+        std::vector<char> seen(ns, 0);
+        gl.clear();
+        gr.clear();
+        const int left = (r + R - 1) % R, right = (r + 1) % R;
+        auto visit = [&](int j) {
+            if (owner[j] == r || seen[j]) return;
+            seen[j] = 1;
+            const bool lside = slab_offset(h, axis, r, R, c->pos0[3 * (size_t)S.orig[j] + axis]) < 0.0;
+            if (owner[j] != (lside ? left : right)) err = "structure list spans more than one slab";
+            (lside ? gl : gr).push_back(j);
+        };
+        for (int s = 0; s < ns; ++s) {
+            if (owner[s] != r) continue;
+            for (int q = S.offset[s]; q < S.offset[s + 1]; ++q) visit(S.nbr[q]);
+            for (int q = S.in_offset[s]; q < S.in_offset[s + 1]; ++q) visit(S.in_nbr[q]);
+        }
+        std::sort(gl.begin(), gl.end());
+        std::sort(gr.begin(), gr.end());
+    };
+    std::vector<int> gl, gr, lgl, lgr, rgl, rgr;
+    ghosts(D.rank, gl, gr);
+    ghosts(D.left, lgl, lgr);
+    ghosts(D.right, rgl, rgr);
+    if (!err.empty()) return ctx_fail(c, MPH_ERR_DOMAIN, "slab mode: " + err);
+    lsl.clear();
+    for (int s = 0; s < ns; ++s)
+        if (owner[s] == D.rank) lsl.push_back(s);
+    n_own = (int)lsl.size();
+    std::vector<int> loc(ns, -1);
+    for (int k = 0; k < n_own; ++k) loc[lsl[k]] = k;
+    std::vector<int> rl, rr, sl, sr;
+    for (int j : gl) { rl.push_back((int)lsl.size()); loc[j] = (int)lsl.size(); lsl.push_back(j); }
+    for (int j : gr) { rr.push_back((int)lsl.size()); loc[j] = (int)lsl.size(); lsl.push_back(j); }
+    // to the left: the left rank's from-right ghosts (ours); to the right: its from-left ghosts
+    for (int j : lgr) sl.push_back(loc[j]);
+    for (int j : rgl) sr.push_back(loc[j]);
+    for (int k : sl) if (k < 0 || k >= n_own) return ctx_fail(c, MPH_ERR_DOMAIN, "slab mode: elastic ghost routing");
+    for (int k : sr) if (k < 0 || k >= n_own) return ctx_fail(c, MPH_ERR_DOMAIN, "slab mode: elastic ghost routing");
+    const size_t most = std::max({sl.size(), sr.size(), rl.size(), rr.size()});
+    if (most * 3 * sizeof(double4) > (size_t)D.msg_cap * kMsgBytes)
+        return ctx_fail(c, MPH_ERR_CAPACITY, "slab mode: elastic ghost message exceeds the exchange buffers");
+    D.nss_l = (int)sl.size(); D.nss_r = (int)sr.size();
+    D.nsr_l = (int)rl.size(); D.nsr_r = (int)rr.size();
+    MPH_CK(ctx_dalloc(c, &D.ss_l, sl.size())); MPH_CK(ctx_dalloc(c, &D.ss_r, sr.size()));
+    MPH_CK(ctx_dalloc(c, &D.sr_l, rl.size())); MPH_CK(ctx_dalloc(c, &D.sr_r, rr.size()));
+    auto up = [&](int* d, const std::vector<int>& v) {
+        return v.empty() ? hipSuccess : hipMemcpy(d, v.data(), sizeof(int) * v.size(), hipMemcpyHostToDevice);
+    };
+    MPH_HIP_OK(c, up(D.ss_l, sl)); MPH_HIP_OK(c, up(D.ss_r, sr));
+    MPH_HIP_OK(c, up(D.sr_l, rl)); MPH_HIP_OK(c, up(D.sr_r, rr));
     return MPH_OK;
 }
 
@@ -375,6 +520,7 @@ int dist_step(MphCtx* c, int nsteps, Profiler* prof)
         MPH_HIP_OK(c, hipEventRecord(D.ev_h, D.stream2));
         MPH_HIP_OK(c, hipStreamWaitEvent(c->stream, D.ev_h, 0));
         launch_pass_b(L, 2);
+        MPH_CK(struct_substeps(c, prof));
         MPH_HIP_OK(c, hipGetLastError());
         c->time += c->cfg.dt;
         c->stepped = true;

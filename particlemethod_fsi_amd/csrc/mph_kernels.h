@@ -12,7 +12,9 @@ namespace mph {
 // [(s >> 6) * W + k][s & 63], so the 64 lanes of a wavefront read entry k with one coalesced load.
 struct StructDev {
     int* orig = nullptr;          // slot -> original particle index
-    int* slot_of = nullptr;       // original particle index -> slot (-1: not structure)
+    int* slot_of = nullptr;       // original particle index -> slot (-1: not structure / not owned)
+    int* bidx = nullptr;          // slot -> index of its B entry this step (written by pass B)
+    int n_own = 0;                // slots computed here (slab mode: owned, then ghost slots)
     int wo = 0, wi = 0;           // ELL widths (max out / in count)
     int* ocnt = nullptr;          // InitialStructureNeighborCount per slot
     int* icnt = nullptr;          // in-degree (how many slots list s)
@@ -55,11 +57,13 @@ struct Soa {
 };
 
 // Pass B hands the integrated structure particles straight to the slot-ordered elastic arrays
-// (null slot_of: no structure particles, or slab mode).
+// (null slot_of: no structure particles) and records where each slot's B entry lives (bidx), so
+// the last substep can write the result back.
 struct StructHook {
     const int* slot_of;
     double4 *sx, *sv, *su;
     const double4* sx0;
+    int* bidx;
 };
 
 // Everything one launch sequence needs.
@@ -89,6 +93,11 @@ void launch_neighbors(const Launch& L);
 void launch_pass_a(const Launch& L);
 void launch_pass_b(const Launch& L, int phase = 0);   // phase: 0 all, 1/2 slab inner/near-face
 void launch_structure(const Launch& L);
+void launch_struct_stress(const Launch& L);
+void launch_struct_velocity(const Launch& L, bool last);
+// slab mode: rows of per-slot double4 records (w per slot) gathered into / scattered from a message
+void launch_struct_pack(const Launch& L, const double4* src, int w, const int* idx, int m, double4* buf);
+void launch_struct_unpack(const Launch& L, const double4* buf, int w, const int* idx, int m, double4* dst);
 void launch_virial(const Launch& L, const Soa& X, double* vir, double* vpres);   // X: state in A order
 
 // slab decomposition (mph_dist.hip)

@@ -1139,13 +1139,18 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
     B.vz[i] = vo2;
     B.type[i] = ti;
     B.id[i] = A.id[i];
-    if (solid && H.slot_of) {
-        // the elastic substeps' slot-ordered state (structure particles do not drift here)
-        const int s = H.slot_of[A.id[i]];
-        const double4 x4 = make_double4(xo0, xo1, xo2, (double)ti);
-        H.sx[s] = x4;
-        H.sv[s] = make_double4(vo0, vo1, vo2, 0.0);
-        H.su[s] = struct_disp(P, x4, H.sx0[s]);
+    const int id = A.id[i];
+    if (solid && H.slot_of && id >= 0) {
+        // the elastic substeps' slot-ordered state (structure particles do not drift here);
+        // slab mode: slots of owned particles only (ghost ids are negative)
+        const int s = H.slot_of[id];
+        if (s >= 0) {
+            const double4 x4 = make_double4(xo0, xo1, xo2, (double)ti);
+            H.sx[s] = x4;
+            H.sv[s] = make_double4(vo0, vo1, vo2, 0.0);
+            H.su[s] = struct_disp(P, x4, H.sx0[s]);
+            H.bidx[s] = i;
+        }
     }
 }
 
@@ -1399,8 +1404,7 @@ __global__ __launch_bounds__(256) void k_struct_velocity(DevParams P, int ns, in
                                                          const double4* __restrict__ sx0,
                                                          double4* __restrict__ sx, double4* __restrict__ sv,
                                                          double4* __restrict__ su, int last,
-                                                         const int* __restrict__ sorig,
-                                                         const int* __restrict__ rank_of, Soa B,
+                                                         const int* __restrict__ bidx, Soa B,
                                                          double4* __restrict__ force)
 {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1464,8 +1468,8 @@ __global__ __launch_bounds__(256) void k_struct_velocity(DevParams P, int ns, in
     }
     for (int d = 0; d < 3; ++d) xx[d] += vv[d] * P.edt;
     if (last) {
-        // back into the integrated state (A order) for the next step's sort
-        const int r = rank_of[sorig[s]];
+        // back into the integrated state (A order) at the entry pass B took it from
+        const int r = bidx[s];
         B.x[r] = xx[0]; B.y[r] = xx[1]; B.z[r] = xx[2];
         B.vx[r] = vv[0]; B.vy[r] = vv[1]; B.vz[r] = vv[2];
         if (cl == 1) force[r] = make_double4(0.0, 0.0, 0.0, 0.0);
@@ -1499,7 +1503,7 @@ __global__ __launch_bounds__(256) void k_dist_classify(DevParams P, DevState* __
             double x = B.x[p], y = B.y[p], z = B.z[p];
             if (move) move_and_wrap(P, st, B, p, x, y, z);
             const double a = g.axis == 0 ? x : (g.axis == 1 ? y : z);
-            c = slab_class(g, a);
+            c = dev_is_struct(B.type[p]) ? slab_class_static(g, a) : slab_class(g, a);
             if (c == kSlabLost) {
                 atomicOr(&st->overflow, 2);
                 c = kInner;
@@ -1585,6 +1589,27 @@ __global__ __launch_bounds__(256) void k_dist_unpack(const char* __restrict__ bu
     C.vx[s] = d[3 * m + k]; C.vy[s] = d[4 * m + k]; C.vz[s] = d[5 * m + k];
     C.type[s] = q[k];
     C.id[s] = -1 - q[m + k];
+}
+
+// Elastic ghost slots (slab mode): w double4 rows per slot, slot k of the message = idx[k].
+__global__ __launch_bounds__(256) void k_struct_pack(const double4* __restrict__ src, int w,
+                                                     const int* __restrict__ idx, int m,
+                                                     double4* __restrict__ buf)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= m * w) return;
+    const int k = t / w, r = t - k * w;
+    buf[t] = src[(size_t)idx[k] * w + r];
+}
+
+__global__ __launch_bounds__(256) void k_struct_unpack(const double4* __restrict__ buf, int w,
+                                                       const int* __restrict__ idx, int m,
+                                                       double4* __restrict__ dst)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= m * w) return;
+    const int k = t / w, r = t - k * w;
+    dst[(size_t)idx[k] * w + r] = buf[t];
 }
 
 // pass-A values of two C-index ranges, read at their sorted position dst_of[c]
@@ -1694,6 +1719,7 @@ static StructHook struct_hook(const Launch& L)
         h.sv = L.S->v;
         h.su = L.S->u;
         h.sx0 = L.S->x0;
+        h.bidx = L.S->bidx;
     }
     return h;
 }
@@ -1728,28 +1754,61 @@ void launch_virial(const Launch& L, const Soa& X, double* vir, double* vpres)
                    L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, vir, vpres);
 }
 
-void launch_structure(const Launch& L)
+void launch_struct_stress(const Launch& L)
 {
     Profiler* prof = L.prof;
     const DevParams& P = *L.P;
-    const int ns = P.n_struct;
-    if (ns == 0) return;
     const StructDev& S = *L.S;
-    for (int sub = 0; sub < P.substeps; ++sub) {
-        if (P.dim == 3) {
-            MPH_LAUNCH("struct_stress", L.stream, k_struct_stress<3>, dim3(blocks(ns, 256)), dim3(256), 0,
-                       L.stream, P, ns, S.wo, S.ocnt, S.eo_nb, S.x0, S.u, S.L, S.lame, S.P, S.F, S.E, S.S);
-            MPH_LAUNCH("struct_velocity", L.stream, k_struct_velocity<3>, dim3(blocks(ns, 256)), dim3(256), 0,
-                       L.stream, P, ns, S.wi, S.icnt, S.ei_nb, S.wx0, S.P, S.inv_rho, S.clamp, S.x0,
-                       S.x, S.v, S.u, sub == P.substeps - 1, S.orig, L.rank_of, L.B, L.force);
-        } else {
-            MPH_LAUNCH("struct_stress", L.stream, k_struct_stress<2>, dim3(blocks(ns, 256)), dim3(256), 0,
-                       L.stream, P, ns, S.wo, S.ocnt, S.eo_nb, S.x0, S.u, S.L, S.lame, S.P, S.F, S.E, S.S);
-            MPH_LAUNCH("struct_velocity", L.stream, k_struct_velocity<2>, dim3(blocks(ns, 256)), dim3(256), 0,
-                       L.stream, P, ns, S.wi, S.icnt, S.ei_nb, S.wx0, S.P, S.inv_rho, S.clamp, S.x0,
-                       S.x, S.v, S.u, sub == P.substeps - 1, S.orig, L.rank_of, L.B, L.force);
-        }
+    const int ns = S.n_own;
+    if (ns <= 0) return;
+    if (P.dim == 3)
+        MPH_LAUNCH("struct_stress", L.stream, k_struct_stress<3>, dim3(blocks(ns, 256)), dim3(256), 0, L.stream,
+                   P, ns, S.wo, S.ocnt, S.eo_nb, S.x0, S.u, S.L, S.lame, S.P, S.F, S.E, S.S);
+    else
+        MPH_LAUNCH("struct_stress", L.stream, k_struct_stress<2>, dim3(blocks(ns, 256)), dim3(256), 0, L.stream,
+                   P, ns, S.wo, S.ocnt, S.eo_nb, S.x0, S.u, S.L, S.lame, S.P, S.F, S.E, S.S);
+}
+
+void launch_struct_velocity(const Launch& L, bool last)
+{
+    Profiler* prof = L.prof;
+    const DevParams& P = *L.P;
+    const StructDev& S = *L.S;
+    const int ns = S.n_own;
+    if (ns <= 0) return;
+    if (P.dim == 3)
+        MPH_LAUNCH("struct_velocity", L.stream, k_struct_velocity<3>, dim3(blocks(ns, 256)), dim3(256), 0,
+                   L.stream, P, ns, S.wi, S.icnt, S.ei_nb, S.wx0, S.P, S.inv_rho, S.clamp, S.x0, S.x, S.v, S.u,
+                   last ? 1 : 0, S.bidx, L.B, L.force);
+    else
+        MPH_LAUNCH("struct_velocity", L.stream, k_struct_velocity<2>, dim3(blocks(ns, 256)), dim3(256), 0,
+                   L.stream, P, ns, S.wi, S.icnt, S.ei_nb, S.wx0, S.P, S.inv_rho, S.clamp, S.x0, S.x, S.v, S.u,
+                   last ? 1 : 0, S.bidx, L.B, L.force);
+}
+
+void launch_structure(const Launch& L)
+{
+    if (L.P->n_struct == 0) return;
+    for (int sub = 0; sub < L.P->substeps; ++sub) {
+        launch_struct_stress(L);
+        launch_struct_velocity(L, sub == L.P->substeps - 1);
     }
+}
+
+void launch_struct_pack(const Launch& L, const double4* src, int w, const int* idx, int m, double4* buf)
+{
+    Profiler* prof = L.prof;
+    if (m <= 0) return;
+    MPH_LAUNCH("struct_pack", L.stream, k_struct_pack, dim3(blocks(m * w, 256)), dim3(256), 0, L.stream, src, w,
+               idx, m, buf);
+}
+
+void launch_struct_unpack(const Launch& L, const double4* buf, int w, const int* idx, int m, double4* dst)
+{
+    Profiler* prof = L.prof;
+    if (m <= 0) return;
+    MPH_LAUNCH("struct_unpack", L.stream, k_struct_unpack, dim3(blocks(m * w, 256)), dim3(256), 0, L.stream, buf,
+               w, idx, m, dst);
 }
 
 void launch_scan(int* cnt, int ncell, int* bsum, int* start, int total, hipStream_t stream, Profiler* prof)

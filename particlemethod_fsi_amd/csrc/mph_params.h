@@ -93,6 +93,10 @@ struct SlabGeom {
     int first, last, lfirst, llast, rfirst, rlast;   // first/last-rank flags: me, left, right
     double lo, hi, llo, lhi, rlo, rhi;               // slabs of me and my periodic neighbours
     double h;
+    // elastic-solid particles are owned by the slab of their InitialPosition for good (their
+    // fixed Lagrangian lists then never change rank); w = domain width along the axis, smargin =
+    // how far beyond a face such a particle may be displaced (h includes it)
+    double w, smargin;
 };
 
 // Particle classes of one step's redistribution, in the order of their segment in the local
@@ -116,6 +120,20 @@ MPH_HD inline int slab_class(const SlabGeom& g, double c)
     if (slab_owns(c, g.llo, g.lhi, g.lfirst, g.llast)) return kMigL;
     if (slab_owns(c, g.rlo, g.rhi, g.rfirst, g.rlast)) return kMigR;
     return kSlabLost;
+}
+
+// Elastic-solid particle of this rank (never migrates): band by its periodic distance from the
+// faces, lost if displaced more than smargin beyond one.
+MPH_HD inline int slab_class_static(const SlabGeom& g, double c)
+{
+    const double half = 0.5 * (g.hi - g.lo);
+    double off = c - (g.lo + half);
+    off -= g.w * __builtin_floor(off / g.w + 0.5);
+    const double dl = off + half, dr = half - off;
+    if (dl < -g.smargin || dr < -g.smargin) return kSlabLost;
+    if (dl < g.h) return kBandL;
+    if (dr <= g.h) return kBandR;
+    return kInner;
 }
 
 // Per-type tables read with per-lane type indices (device memory; staged through LDS where hot).

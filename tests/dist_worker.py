@@ -15,7 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
-SLAB_AXIS = {"channel3d": 2, "channel3d_st": 2, "channel2d": 0, "dam2d": 0, "box3d": 0}
+SLAB_AXIS = {"channel3d": 2, "channel3d_st": 2, "channel2d": 0, "dam2d": 0, "box3d": 0,
+             "bar2d": 0, "bar3d": 0, "gate2d_sub": 0}
 
 
 def _init(rank, world, port):

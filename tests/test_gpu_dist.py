@@ -25,7 +25,10 @@ pytestmark = pytest.mark.gpu
 FIELDS = ["Position", "Velocity", "PressureP", "NeighborCount", "Force", "VolStrainP", "DivergenceP",
           "DensityA", "GravityCenter", "PressureA", "Acceleration"]
 FLOOR = {"PressureP": 1e-9, "PressureA": 1e-9, "Force": 1e-15, "Acceleration": 1e-12,
-         "VolStrainP": 1e-13, "DivergenceP": 1e-12, "DensityA": 1e-13, "GravityCenter": 1e-16}
+         "VolStrainP": 1e-13, "DivergenceP": 1e-12, "DensityA": 1e-13, "GravityCenter": 1e-16,
+         "DeformGradient": 1e-13, "Strain": 1e-13, "Stress": 1e-8}
+# elastic-solid cases: the per-slot tensors of the owned structure particles as well
+STRUCT_FIELDS = FIELDS + ["DeformGradient", "Strain", "Stress"]
 
 
 def _free_port():
@@ -34,10 +37,10 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def run_slab(case, world, checkpoints, out):
+def run_slab(case, world, checkpoints, out, fields=FIELDS):
     ctx = mp.get_context("spawn")
     port = _free_port()
-    ps = [ctx.Process(target=dist_worker.gpu_worker, args=(r, world, port, case, checkpoints, FIELDS, out))
+    ps = [ctx.Process(target=dist_worker.gpu_worker, args=(r, world, port, case, checkpoints, fields, out))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -50,7 +53,7 @@ def run_slab(case, world, checkpoints, out):
     return np.load(out)
 
 
-def close(f, a, b):
+def close(f, a, b, rel=1e-8):
     if f == "NeighborCount":
         return np.array_equal(a, b), int((a != b).sum())
     err = float(np.max(np.abs(a - b))) if a.size else 0.0
@@ -59,8 +62,15 @@ def close(f, a, b):
     elif f == "Velocity":
         t = 1e-9
     else:
-        t = 1e-8 * float(np.max(np.abs(b))) + FLOOR.get(f, 1e-12)
+        t = rel * float(np.max(np.abs(b))) + FLOOR.get(f, 1e-12)
     return err <= t, (err, t)
+
+
+# Elastic cases run near the solid's stability limit (dt c/dx ~ 0.95), where reassociation
+# roundoff grows ~10x per 10 steps: test_gpu_parity's solid bound (1e-7 relative), and for
+# DivergenceP -- a difference of nearly equal sums -- 1e-6, the growth one GPU context itself shows
+# against the oracle on bar3d (tools/slab_diag.py: 8.9e-9 / 9.7e-8 / 7.4e-7 at steps 10 / 20 / 30).
+STRUCT_REL = {"DivergenceP": 1e-6}
 
 
 @pytest.mark.parametrize("case,world", [("channel3d", 2), ("channel3d", 3), ("channel2d", 4),
@@ -87,6 +97,30 @@ def test_slab_ranks_match_oracle(tmp_path, case, world):
             assert ok, (case, world, k, f, info)
     if case.startswith("channel"):
         assert moved, "no particle migrated between slabs"
+
+
+@pytest.mark.parametrize("case,world", [("bar2d", 2), ("bar2d", 3), ("bar3d", 2), ("gate2d_sub", 2)])
+def test_slab_structure_ranks_match_oracle(tmp_path, case, world):
+    """Elastic-solid particles across slab faces: static owners by InitialPosition, ghost slots of
+    the fixed Lagrangian lists exchanged before every stress / velocity half-substep."""
+    from oracle_bindings import OracleSolver
+    checkpoints = [1, 10, 30]
+    r = run_slab(case, world, checkpoints, str(tmp_path / "slab.npz"), STRUCT_FIELDS)
+    cfg, parts = cases.get(case).build()
+    o = OracleSolver(cfg, parts)
+    o.init()
+    done = 0
+    for k in checkpoints:
+        o.step(k - done)
+        done = k
+        assert (r["s%d/owner" % k] >= 0).all()
+        for f in STRUCT_FIELDS:
+            ok, info = close(f, r["s%d/%s" % (k, f)], o.get(f), STRUCT_REL.get(f, 1e-7))
+            assert ok, (case, world, k, f, info)
+    # the structure straddles a slab face (elastic ghosts in use) except in the gate case
+    prop = parts.property
+    sown = r["owner0"][(prop == 2) | (prop == 3)]
+    assert case.startswith("gate") or len(set(sown.tolist())) > 1
 
 
 def test_slab_matches_single_gpu(tmp_path):

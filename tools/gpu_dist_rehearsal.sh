@@ -8,5 +8,5 @@ mkdir -p gpurun_out
 for N in ${RANKS:-2 4}; do
   MPH_SLAB_TRANSPORT=host MPH_BENCH_DEVICE=0 timeout -k 10 600 python -m torch.distributed.run \
     --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 --master-port $((29500 + N)) \
-    bench.py --gpus $N --steps ${STEPS:-10} --warmup 2 > gpurun_out/rehearsal_n$N.log 2>&1 || exit 20
+    bench.py --gpus $N --steps ${STEPS:-10} --warmup 2 --case ${CASE:-d1m} > gpurun_out/rehearsal_${CASE:-d1m}_n$N.log 2>&1 || exit 20
 done
