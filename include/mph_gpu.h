@@ -176,6 +176,14 @@ int mph_write_vtk_arrays(const char* path, int n, const int* property, const dou
                          const double* force, const double* stress, const double* strain,
                          const int* initial_structure_neighbor_count, const int* neighbor_count);
 
+/* Binary VTK XML (.vtu) alternative to the ASCII writer: the same point fields as
+ * mph_write_vtk_arrays, Float32/Int32 in raw appended data (UInt64 headers), stress and strain as
+ * 9-component tensors, one VTK_VERTEX cell per particle.                                       */
+int mph_write_vtu_arrays(const char* path, int n, const int* property, const double* pos,
+                         const double* pos0, const double* vel, const double* accel,
+                         const double* force, const double* stress, const double* strain,
+                         const int* initial_structure_neighbor_count, const int* neighbor_count);
+
 /* Every constant the reference derives before its time loop (initializeWeight/Fluid/Wall/Domain,
  * main.cpp:1191-1469), without a device: 36 doubles in the slot order of mph_get_scalars.      */
 int mph_derive_scalars(const MphConfig* cfg, double* out36);
@@ -207,6 +215,7 @@ double mph_time(const MphCtx* ctx);
 int mph_get_scalars(const MphCtx* ctx, double* out36);
 int mph_write_prof(MphCtx* ctx, const char* path);
 int mph_write_vtk(MphCtx* ctx, const char* path);
+int mph_write_vtu(MphCtx* ctx, const char* path);   /* mph_write_vtu_arrays of the current state */
 /* writeVtkFile (main.cpp:984-1189) off the time loop's critical path: the fields are copied to
  * host memory now (one D2H per field) and formatted and written by a background thread while
  * the following steps run.  At most one file is in flight; mph_output_wait joins it and

@@ -671,7 +671,7 @@ int mph_write_prof(MphCtx* c, const char* path)
                                  vel.data());
 }
 
-int mph_write_vtk(MphCtx* c, const char* path)
+static int write_vtk_any(MphCtx* c, const char* path, bool xml)
 {
     if (!c || !path) return MPH_ERR_ARG;
     if (c->dist) return fail(c, MPH_ERR_UNSUPPORTED, "slab mode: gather the owned entries (mph_get) and use mph_write_vtk_arrays");
@@ -686,9 +686,14 @@ int mph_write_vtk(MphCtx* c, const char* path)
     CK(mph_get(c, MPH_FIELD_STRAIN, strain.data()));
     CK(mph_get(c, MPH_FIELD_INITIAL_STRUCTURE_NEIGHBOR_COUNT, isnc.data()));
     CK(mph_get(c, MPH_FIELD_NEIGHBOR_COUNT, nc.data()));
-    return mph_write_vtk_arrays(path, c->n_glob, c->prop.data(), pos.data(), c->pos0.data(), vel.data(),
-                                acc.data(), force.data(), stress.data(), strain.data(), isnc.data(), nc.data());
+    auto writer = xml ? mph_write_vtu_arrays : mph_write_vtk_arrays;
+    return writer(path, c->n_glob, c->prop.data(), pos.data(), c->pos0.data(), vel.data(), acc.data(), force.data(),
+                  stress.data(), strain.data(), isnc.data(), nc.data());
 }
+
+int mph_write_vtk(MphCtx* c, const char* path) { return write_vtk_any(c, path, false); }
+
+int mph_write_vtu(MphCtx* c, const char* path) { return write_vtk_any(c, path, true); }
 
 int mph_output_wait(MphCtx* c)
 {

@@ -6,7 +6,8 @@
 // loop while Time < EndTime + 1e-5*Dt writing the .prof before a step (583-589) and the .vtk
 // after a step (672-683).  Differences: the physics runs on one MI355X through libmph_gpu.so;
 // the .prof holds the current state (the OpenACC build writes stale host arrays);
-// the timing report is wall time of the step loop, not clock() CPU time.
+// the timing report is wall time of the step loop, not clock() CPU time.  A <vtk pattern> ending
+// in ".vtu" writes binary VTK XML files instead (mph_write_vtu).
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
@@ -100,6 +101,7 @@ int main(int argc, char** argv)
     const double dt = cfg.dt;
     int istep = (int)(time_now / dt);
     double out_next = 0.0, vtk_next = 0.0;
+    const bool vtu = vtk.size() > 4 && vtk.compare(vtk.size() - 4, 4, ".vtu") == 0;
     long long steps_run = 0;
     double loop_s = 0.0;
     char name[1024];
@@ -134,7 +136,7 @@ int main(int argc, char** argv)
                 if (rc) die(ctx, rc, "mph_compute_virial");
                 std::snprintf(name, sizeof(name), vtk.c_str(), istep);
                 // formatted and written by a background thread while the next steps run
-                rc = mph_write_vtk_async(ctx, name);
+                rc = vtu ? mph_write_vtu(ctx, name) : mph_write_vtk_async(ctx, name);
                 if (rc) die(ctx, rc, "writing a .vtk file");
                 logf("@ Vtk Output Time : %e\n", time_now);
                 vtk_next += cfg.vtk_output_interval;

@@ -54,6 +54,7 @@ EXPORTED_SYMBOLS = [
     "mph_structure_init", "mph_create_dist_host", "mph_owned_ids", "mph_slab_bounds",
     "mph_slab_owner", "mph_dist_selftest", "mph_compute_virial",
     "mph_config_sizeof", "mph_write_vtk_async", "mph_output_wait", "mph_write_grid_binary",
+    "mph_write_vtu_arrays", "mph_write_vtu",
 ]
 
 # mph_host_exchange_fn (include/mph_gpu.h): (user, send_l, n, send_r, n, recv_l, n, recv_r, n)
@@ -127,6 +128,8 @@ def load_library() -> ctypes.CDLL:
         "mph_config_sizeof": (ip, []),
         "mph_write_grid_binary": (ip, [ctypes.c_char_p, cfgp, ip, vp, vp, vp, vp]),
         "mph_write_vtk_async": (ip, [vp, ctypes.c_char_p]),
+        "mph_write_vtu_arrays": (ip, [ctypes.c_char_p, ip] + [vp] * 10),
+        "mph_write_vtu": (ip, [vp, ctypes.c_char_p]),
         "mph_output_wait": (ip, [vp]),
     }
     for name, (res, args) in sig.items():
@@ -160,6 +163,25 @@ def write_grid_binary(path: str, cfg: mphio.MphConfig, parts: "mphio.Particles")
     prop = np.ascontiguousarray(parts.property, np.int32)
     _check(load_library().mph_write_grid_binary(path.encode(), ctypes.byref(cfg), parts.n, prop.ctypes.data,
                                                 p[0].ctypes.data, p[1].ctypes.data, p[2].ctypes.data))
+
+
+def read_vtu(path: str) -> dict:
+    """Arrays of a .vtu written by mph_write_vtu(_arrays): {name: ndarray}, 'Points' for the
+    coordinates (raw appended data, UInt64 block headers)."""
+    import re
+    raw = open(path, "rb").read()
+    head, _, data = raw.partition(b'<AppendedData encoding="raw">')
+    data = data[data.index(b"_") + 1:]
+    dt = {"Float32": np.float32, "Int32": np.int32, "UInt8": np.uint8}
+    out = {}
+    for m in re.finditer(rb"<DataArray ([^>]*)/>", head):
+        attrs = dict(re.findall(rb'(\w+)="([^"]*)"', m.group(1)))
+        off = int(attrs[b"offset"])
+        nb = int(np.frombuffer(data[off:off + 8], np.uint64)[0])
+        a = np.frombuffer(data[off + 8:off + 8 + nb], dt[attrs[b"type"].decode()])
+        k = int(attrs.get(b"NumberOfComponents", b"1"))
+        out[attrs.get(b"Name", b"Points").decode()] = a.reshape(-1, k) if k > 1 else a
+    return out
 
 
 def derive_scalars(cfg: mphio.MphConfig) -> np.ndarray:
@@ -294,6 +316,10 @@ class MphSolver:
 
     def write_vtk(self, path: str):
         _check(self._L.mph_write_vtk(self._h, path.encode()), self._h)
+
+    def write_vtu(self, path: str):
+        """Binary VTK XML (.vtu) of the same fields as write_vtk (Float32, appended raw data)."""
+        _check(self._L.mph_write_vtu(self._h, path.encode()), self._h)
 
     def write_vtk_async(self, path: str):
         """Snapshot now, format and write in the background (wait with output_wait())."""

@@ -215,3 +215,39 @@ def test_binary_grid_roundtrip(case):
                      (p_t.initial_position, p_b.initial_position), (p_t.velocity, p_b.velocity)):
             assert np.array_equal(a, b)
         assert os.path.getsize(gb) == 80 + 4 * (p_t.n + (p_t.n & 1)) + 72 * p_t.n
+
+
+def test_vtu_writer_roundtrip():
+    """mph_write_vtu_arrays (binary VTK XML): every field of the ASCII writer,
+    read back with solver.read_vtu, equals its float32 / int32 value exactly; the XML header
+    declares one VTK_VERTEX cell per particle."""
+    n = 1000
+    rng = np.random.default_rng(3)
+    prop = rng.integers(0, 6, n).astype(np.int32)
+    pos, pos0, vel, acc, force = [rng.normal(size=(n, 3)) for _ in range(5)]
+    stress, strain = rng.normal(size=(n, 3, 3)) * 1e4, rng.normal(size=(n, 3, 3)) * 1e-4
+    isnc = rng.integers(0, 40, n).astype(np.int32)
+    nc = rng.integers(0, 90, n).astype(np.int32)
+    L = solver.load_library()
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, "out.vtu")
+        rc = L.mph_write_vtu_arrays(path.encode(), n, prop.ctypes.data, pos.ctypes.data, pos0.ctypes.data,
+                                    vel.ctypes.data, acc.ctypes.data, force.ctypes.data, stress.ctypes.data,
+                                    strain.ctypes.data, isnc.ctypes.data, nc.ctypes.data)
+        assert rc == 0
+        d = solver.read_vtu(path)
+        head = open(path, "rb").read(2048)
+    assert b'NumberOfPoints="1000" NumberOfCells="1000"' in head
+    f32 = lambda a: a.astype(np.float32)  # noqa: E731
+    np.testing.assert_array_equal(d["Points"], f32(pos))
+    np.testing.assert_array_equal(d["displacement"], f32(pos - pos0))
+    np.testing.assert_array_equal(d["stress"], f32(stress.reshape(n, 9)))
+    np.testing.assert_array_equal(d["strain"], f32(strain.reshape(n, 9)))
+    for k, a in (("velocity", vel), ("accel", acc), ("force", force)):
+        np.testing.assert_array_equal(d[k], f32(a))
+    np.testing.assert_array_equal(d["label"], prop)
+    np.testing.assert_array_equal(d["Initialneighbor"], isnc)
+    np.testing.assert_array_equal(d["neighbor"], nc)
+    np.testing.assert_array_equal(d["connectivity"], np.arange(n))
+    np.testing.assert_array_equal(d["offsets"], np.arange(1, n + 1))
+    assert (d["types"] == 1).all()
