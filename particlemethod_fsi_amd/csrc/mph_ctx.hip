@@ -63,7 +63,9 @@ void ctx_fill_launch(MphCtx* c)
     L.st = c->dst;
     L.stream = c->stream;
     L.prof = nullptr;
-    L.A = c->A; L.B = c->B; L.rank_of = c->rank_of; L.dst_of = nullptr;
+    // rank_of (original id -> sorted index) has no reader on the single-GPU path (fields are
+    // returned through A.id), so k_rank_scatter skips that scatter; slab mode uses dst_of.
+    L.A = c->A; L.B = c->B; L.rank_of = nullptr; L.dst_of = nullptr;
     L.key = c->key; L.slot = c->slot; L.tmp = c->tmp; L.cnt = c->cnt; L.start = c->start; L.bsum = c->bsum;
     L.nbr = c->nbr; L.ncount = c->ncount;
     L.pres = c->pres; L.gx = c->gx; L.gy = c->gy; L.gz = c->gz; L.pa = c->pa;

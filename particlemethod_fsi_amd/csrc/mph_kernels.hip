@@ -389,14 +389,16 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_down(int* __restrict__ cn
 #pragma unroll
         for (int k = 0; k < kScanItems / 4; ++k) {
             st[k] = make_int4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
-            ct[k] = make_int4(0, 0, 0, 0);   // histogram ready for the next step
+            // histogram ready for the next step; all-zero runs of 16 cells (most of the D1M tank is
+            // empty, ~7 cells per particle) are left alone, so their lines are not written
+            if (s != 0) ct[k] = make_int4(0, 0, 0, 0);
         }
     } else {
 #pragma unroll
         for (int k = 0; k < kScanItems; ++k)
             if (base + k < ncell) {
                 start[base + k] = o[k];
-                cnt[base + k] = 0;
+                if (v[k] != 0) cnt[base + k] = 0;
             }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) start[ncell] = n;
@@ -452,7 +454,7 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
         q[2] = make_double2(B.vy[p], B.vz[p]);
     }
     if (dst_of) dst_of[p] = dst;   // slab mode: ids are global (ghosts negative)
-    else rank_of[id] = dst;
+    else if (rank_of) rank_of[id] = dst;
 }
 
 // ----------------------------------------------------------------------------- pass A sums --
