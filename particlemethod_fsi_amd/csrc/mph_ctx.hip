@@ -91,12 +91,22 @@ int dalloc(MphCtx* c, T** p, size_t count)
 
 void fill_launch(MphCtx* c) { ctx_fill_launch(c); }
 
-void enqueue_step(const Launch& L)
+// Force and Acceleration (main.cpp:2085-2096, 2892-2956) are outputs only: no kernel reads them,
+// and every step overwrites all of them.  So only the last step of a replayed batch stores them
+// (pass B -6 % at D1M); mph_get after any mph_step sees the last step's values as before.
+void enqueue_step(const Launch& L, bool last)
 {
     launch_sort(L, 1);
     launch_neighbors(L);
     launch_pass_a(L);
-    launch_pass_b(L);
+    if (last) {
+        launch_pass_b(L);
+    } else {
+        Launch Lb = L;
+        Lb.force = nullptr;
+        Lb.acc = nullptr;
+        launch_pass_b(Lb);
+    }
     launch_structure(L);
 }
 
@@ -104,7 +114,7 @@ int capture(MphCtx* c, int steps, hipGraphExec_t* out)
 {
     hipGraph_t g = nullptr;
     HIP_OK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    for (int k = 0; k < steps; ++k) enqueue_step(c->L);
+    for (int k = 0; k < steps; ++k) enqueue_step(c->L, k == steps - 1);
     HIP_OK(c, hipStreamEndCapture(c->stream, &g));
     HIP_OK(c, hipGraphInstantiate(out, g, nullptr, nullptr, 0));
     HIP_OK(c, hipGraphDestroy(g));
@@ -751,7 +761,7 @@ int mph_profile_steps(MphCtx* c, int nsteps, double* avg_ms, int* launches, char
     } else {
         Launch L = c->L;
         L.prof = &prof;
-        for (int k = 0; k < nsteps; ++k) enqueue_step(L);
+        for (int k = 0; k < nsteps; ++k) enqueue_step(L, k == nsteps - 1);
         HIP_OK(c, hipGetLastError());
         HIP_OK(c, hipStreamSynchronize(c->stream));
         for (int k = 0; k < nsteps; ++k) c->time += c->cfg.dt;

@@ -1131,8 +1131,10 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
             xo2 += vo2 * P.dt;
         }
     }
-    force[i] = make_double4(f0, f1, f2, 0.0);
-    acc[i] = ao;
+    if (force) {   // null on all but the last step of a replayed batch (enqueue_step)
+        force[i] = make_double4(f0, f1, f2, 0.0);
+        acc[i] = ao;
+    }
     B.x[i] = xo0;
     B.y[i] = xo1;
     B.z[i] = xo2;
