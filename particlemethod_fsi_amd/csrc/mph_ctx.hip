@@ -93,12 +93,21 @@ void fill_launch(MphCtx* c) { ctx_fill_launch(c); }
 
 // Force and Acceleration (main.cpp:2085-2096, 2892-2956) are outputs only: no kernel reads them,
 // and every step overwrites all of them.  So only the last step of a replayed batch stores them
-// (pass B -6 % at D1M); mph_get after any mph_step sees the last step's values as before.
+// (pass B -6 % at D1M); mph_get after any mph_step sees the last step's values as before.  The
+// same holds in pass A for DensityA, VolStrainP, DivergenceP and, without surface tension (pass B
+// then reads neither), GravityCenter and PressureA.  The virial (k_virial) runs after a batch.
 void enqueue_step(const Launch& L, bool last)
 {
     launch_sort(L, 1);
     launch_neighbors(L);
-    launch_pass_a(L);
+    if (last) {
+        launch_pass_a(L);
+    } else {
+        Launch La = L;
+        La.dens_a = La.vstrain = La.divp = nullptr;
+        if (!L.P->surface) La.gx = La.gy = La.gz = La.pa = nullptr;
+        launch_pass_a(La);
+    }
     if (last) {
         launch_pass_b(L);
     } else {

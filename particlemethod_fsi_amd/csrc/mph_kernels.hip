@@ -533,13 +533,19 @@ __device__ __forceinline__ void pass_a_finish(const DevParams& P, const DevTable
     double pa = T->cofa[ti] * (o.da - P.n0a) / P.dx;
     if (P.n0a <= o.da) pa = 0.0;
     out.pres[i] = p;
-    out.gx[i] = o.g0;
-    out.gy[i] = o.g1;
-    out.gz[i] = o.g2;
-    out.pa[i] = pa;
-    out.dens_a[i] = o.da;
-    out.vstrain[i] = vstr;
-    out.divp[i] = o.dv;
+    // null on the non-last steps of a replayed batch when nothing downstream reads them
+    // (enqueue_step): GravityCenter/PressureA without surface tension, the three diagnostics
+    if (out.gx) {
+        out.gx[i] = o.g0;
+        out.gy[i] = o.g1;
+        out.gz[i] = o.g2;
+        out.pa[i] = pa;
+    }
+    if (out.dens_a) {
+        out.dens_a[i] = o.da;
+        out.vstrain[i] = vstr;
+        out.divp[i] = o.dv;
+    }
     if (out.fpart) {
         out.fpart[i] = make_double4(p * o.s0 + o.v0, p * o.s1 + o.v1, p * o.s2 + o.v2, 0.0);
         out.rec[i] = make_double4(xi, yi, zi, p);
