@@ -184,6 +184,16 @@ int mph_write_vtu_arrays(const char* path, int n, const int* property, const dou
                          const double* force, const double* stress, const double* strain,
                          const int* initial_structure_neighbor_count, const int* neighbor_count);
 
+/* setInitialVelocityProfile (main.cpp:395-441) on host arrays (original order; vel is updated in
+ * place).  Bar_Module: the beam's first bending mode on the structure particles, v = (0,
+ * 0.01 c0 f(x0)/f(L), 0) with c0 = sqrt(3.25e6/Density) and f of main.cpp:387-392 (the
+ * reference's only call, main.cpp:571, is commented out: an explicit option).  Turek_Hron: the
+ * parabolic inlet on fluid particles with x <= 0.01 and, while time < 0.7, x > 1.5 -- the
+ * reference calls it every step before calculateWall (main.cpp:592-594), which mph_step does on
+ * the device by itself for MPH_MODULE_TUREK_HRON.  Other modules: no change.                   */
+int mph_velocity_profile_arrays(const MphConfig* cfg, double time, int n, const int* property,
+                                const double* pos, const double* pos0, double* vel);
+
 /* Every constant the reference derives before its time loop (initializeWeight/Fluid/Wall/Domain,
  * main.cpp:1191-1469), without a device: 36 doubles in the slot order of mph_get_scalars.      */
 int mph_derive_scalars(const MphConfig* cfg, double* out36);
@@ -209,6 +219,10 @@ int mph_synchronize(MphCtx* ctx);
 int mph_get(MphCtx* ctx, int field, void* host_out);
 /* Overwrite Position or Velocity (original order) -- the reference's `acc update device`.    */
 int mph_set(MphCtx* ctx, int field, const void* host_in);
+/* setInitialVelocityProfile() (main.cpp:395-441) applied once to the current state, as the
+ * reference's commented call after the initialisation sums would (main.cpp:571); see
+ * mph_velocity_profile_arrays.                                                                */
+int mph_set_initial_velocity_profile(MphCtx* ctx);
 int mph_particle_count(const MphCtx* ctx);
 double mph_time(const MphCtx* ctx);
 /* Derived scalar constants, same slots as oracle/ref_harness.inc ref_scalars (36 doubles).  */
@@ -255,7 +269,9 @@ int mph_neighbor_stats(MphCtx* ctx, double* mean, int* max);
  * a face to the neighbour at the start of the next step.  Per step: one exchange of
  * (x, v, type, id) for migrants + ghosts before the cell sort, one of the pass-A values
  * (PressureP [, GravityCenter, PressureA]) of the ghosts before the force pass.
- * Elastic-solid particles (types 2, 3) are not supported in slab mode (MPH_ERR_UNSUPPORTED).
+ * Elastic-solid particles (types 2, 3) are owned for good by the slab of their InitialPosition;
+ * their fixed Lagrangian lists reach into static ghost slots of the two neighbours, refreshed
+ * before each half of every elastic substep (displacements, then first Piola-Kirchhoff stress).
  *
  * mph_get in slab mode fills only the entries of the particles this rank owns (indexed by the
  * original particle index, arrays of mph_particle_count() = the global count); the other

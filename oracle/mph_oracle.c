@@ -992,8 +992,56 @@ static void orc_virial(OrcState* s)
                                   : -1.0 / 3.0 * (s->virial[i][0][0] + s->virial[i][1][1] + s->virial[i][2][2]);
 }
 
+/* setInitialVelocityProfile, main.cpp:395-441 (constants 374-384).  Bar_Module: the beam's first
+ * bending mode on the structure particles (its only call, main.cpp:571, is commented out, so it
+ * is an explicit option here).  Turek_Hron: the parabolic inlet (x <= 0.01) and, while
+ * Time < 0.7, the outlet band (x > 1.5) on the fluid particles -- called every step before
+ * calculateWall (main.cpp:592-594).  Other modules: no body.                                  */
+static double orc_beam_mode(double x)   /* compute_fx, main.cpp:387-392 */
+{
+    const double kL = 1.875, L = 0.20, k = kL / L;
+    const double kx = k * x;
+    const double term1 = (cos(kL) + cosh(kL)) * (cosh(kx) - cos(kx));
+    const double term2 = (sin(kL) - sinh(kL)) * (sinh(kx) - sin(kx));
+    return term1 + term2;
+}
+
+static void orc_velocity_profile(OrcState* s)
+{
+    if (s->c.module == MPH_MODULE_BAR) {
+        const double K = 3.25e6, L = 0.20;
+        for (int i = s->struct_b; i < s->struct_e; ++i) {
+            const double rho = s->c.density[s->prop[i]];
+            const double c0 = sqrt(K / rho);
+            const double fx = orc_beam_mode(s->x0[i][0]);
+            const double fL = orc_beam_mode(L);
+            s->v[i][0] = 0.0;
+            s->v[i][1] = 0.01 * c0 * fx / fL;
+            s->v[i][2] = 0.0;
+        }
+    } else if (s->c.module == MPH_MODULE_TUREK_HRON) {
+        const double YMIN = 0.0, YMAX = 0.41, UMAX = 1.0, H = YMAX - YMIN;
+        for (int i = s->fluid_b; i < s->fluid_e; ++i) {
+            const double x = s->x[i][0], y = s->x[i][1];
+            if (x <= 0.01) {
+                const double uy = y - YMIN;
+                s->v[i][0] = (1.5 * 4.0 * UMAX / (H * H)) * uy * (H - uy);
+                s->v[i][1] = 0.0;
+                s->v[i][2] = 0.0;
+            }
+            if (x > 1.5 && s->time < 0.7) {
+                const double uy = y - YMIN;
+                s->v[i][0] = (4.0 * UMAX / (H * H)) * uy * (H - uy);
+                s->v[i][1] = 0.0;
+                s->v[i][2] = 0.0;
+            }
+        }
+    }
+}
+
 static void orc_one_step(OrcState* s)   /* main.cpp:597-686 without I/O */
 {
+    if (s->c.module == MPH_MODULE_TUREK_HRON) orc_velocity_profile(s);   /* main.cpp:592-594 */
     orc_wall(s);
     orc_periodic(s);
     orc_reset_force(s);
@@ -1099,6 +1147,7 @@ int orc_call(OrcState* s, const char* name)
         {"calculateElasticDeformationVector", orc_deformation}, {"calculateStress", orc_stress},
         {"calculateStressForce", orc_stress_force}, {"updateElasticPosition", orc_update_elastic},
         {"calculateVirialStressAtParticle", orc_virial},
+        {"setInitialVelocityProfile", orc_velocity_profile},
     };
     for (size_t k = 0; k < sizeof table / sizeof table[0]; ++k)
         if (strcmp(name, table[k].name) == 0) { table[k].fn(s); return 0; }

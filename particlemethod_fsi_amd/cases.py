@@ -58,6 +58,10 @@ class Case:
     data_changes: dict = field(default_factory=dict)
     note: str = ""
     wall_motion: int = 0   # MphWallMotion: 1 = the reference's compile-time `Rolling` (main.cpp:58)
+    time0: float = 0.0     # the .grid Time line (a restart time, main.cpp:797); "%f" text
+    # reference functions run once after the initialisation sums, e.g. the commented
+    # setInitialVelocityProfile() call of main.cpp:571
+    init_calls: tuple = ()
 
     @property
     def ref_variant(self) -> str:
@@ -79,7 +83,7 @@ class Case:
         _apply_data(cfg, self.data())
         parts = mphio.generate(self.cuboids)
         cfg.wall_motion = self.wall_motion
-        cfg.time = 0.0
+        cfg.time = float("%f" % self.time0)
         cfg.particle_spacing = mphio._e(self.spacing)
         for d in range(3):
             cfg.domain_min[d] = mphio._e(self.lower[d])
@@ -87,7 +91,8 @@ class Case:
         return cfg, parts
 
     def grid_text(self) -> str:
-        return mphio.format_grid(mphio.generate(self.cuboids), self.spacing, self.lower, self.upper)
+        return mphio.format_grid(mphio.generate(self.cuboids), self.spacing, self.lower, self.upper,
+                                 self.time0)
 
 
 def _apply_data(cfg, values):
@@ -220,6 +225,50 @@ _reg(Case("rolling3d", 3, "dam", 0.001, CASES["box3d"].lower, CASES["box3d"].upp
           CASES["box3d"].cuboids, data_changes={"Wall6": "Center 0.0125 0.0125 0.006 Velocity 0.0 0.0 0.0 "
                                                          "Omega 0.0 0.0 0.0"}, wall_motion=1,
           note="box3d in a rolling tank (Rolling wall motion)"))
+
+
+# the shipped rigid wall motion of calculateWall (main.cpp:3031-3071): Wall6/Wall7 (types 4/5)
+# translate with Velocity and turn by the quaternion of Omega*Dt (initializeWall 1371-1410) while
+# Time < 0.2, after which only WallCenter keeps advancing.  The .grid Time line starts the run at
+# 0.1995 (a restart), so both sides of the switch are inside the checked steps.
+_MOVE2 = {"Wall6": "Center 0.1 0.1 0.0 Velocity 0.02 0.01 0.0 Omega 0.0 0.0 0.3",
+          "Wall7": "Center 0.2 0.1 0.0 Velocity -0.01 0.0 0.0 Omega 0.0 0.0 -0.2"}
+_reg(Case("movwall2d", 2, "dam", 0.001, CASES["dam2d"].lower, CASES["dam2d"].upper, [
+    Cuboid(1, (0.0, 0.003, 0.0), (0.05, 0.10, 0.001), 0.001),
+    Cuboid(4, (0.0, 0.0, 0.0), (0.2, 0.003, 0.001), 0.001),
+    Cuboid(5, (0.2, 0.0, 0.0), (0.203, 0.20, 0.001), 0.001),
+    Cuboid(4, (-0.003, 0.0, 0.0), (0.0, 0.20, 0.001), 0.001),
+], data_changes=_MOVE2, time0=0.1995, note="dam2d with moving walls (restart at Time 0.1995)"))
+_reg(Case("movwall3d", 3, "dam", 0.001, CASES["box3d"].lower, CASES["box3d"].upper,
+          CASES["box3d"].cuboids,
+          data_changes={"Wall6": "Center 0.0125 0.0125 0.006 Velocity 0.01 0.0 -0.02 Omega 0.2 -0.1 0.3"},
+          time0=0.1995, note="box3d with a translating + rotating wall (restart at Time 0.1995)"))
+
+# the other case modules of main.cpp:54-59 (Turek_Hron, Rolling1, Hydroelastic):
+# updateElasticPosition's clamps (1944-2044) and, for Turek_Hron, the per-step inlet profile
+# (setInitialVelocityProfile 419-441, called at 592-594).
+# Turek-Hron-like channel, dx 1 cm: fluid over x in (0, 1.6) (inlet x <= 0.01, outlet band
+# x > 1.5), walls above and below, a small elastic plate around x0 = 0.205 (the clamp line).
+_reg(Case("turek2d", 2, "turek_hron", 0.01, (0.0, -0.05, 0.0), (1.6, 0.46, 0.01), [
+    Cuboid(1, (0.0, 0.0, 0.0), (0.19, 0.41, 0.01), 0.01),
+    Cuboid(1, (0.19, 0.0, 0.0), (0.25, 0.19, 0.01), 0.01),
+    Cuboid(1, (0.19, 0.22, 0.0), (0.25, 0.41, 0.01), 0.01),
+    Cuboid(1, (0.25, 0.0, 0.0), (1.6, 0.41, 0.01), 0.01),
+    Cuboid(2, (0.19, 0.19, 0.0), (0.25, 0.22, 0.01), 0.01),
+    Cuboid(4, (0.0, -0.03, 0.0), (1.6, 0.0, 0.01), 0.01),
+    Cuboid(4, (0.0, 0.41, 0.0), (1.6, 0.44, 0.01), 0.01),
+], note="2-D Turek-Hron channel with inlet profile (Turek_Hron module)"))
+_reg(Case("gate2d_rolling1", 2, "rolling1", 0.001, CASES["gate2d"].lower, CASES["gate2d"].upper,
+          CASES["gate2d"].cuboids, note="gate2d under the Rolling1 clamp (x0.y < 0.003)"))
+# Hydroelastic: a 2 m plate clamped at both ends (x0 < 0.01 or x0 > 1.99) loaded by a fluid block
+_reg(Case("hydro2d", 2, "hydroelastic", 0.005, (-0.05, -0.05, 0.0), (2.05, 0.2, 0.005), [
+    Cuboid(1, (0.5, 0.01, 0.0), (1.5, 0.06, 0.005), 0.005),
+    Cuboid(2, (0.0, 0.0, 0.0), (2.0, 0.01, 0.005), 0.005),
+], note="clamped elastic plate under a fluid block (Hydroelastic module)"))
+# Bar_Module with the (commented-out, main.cpp:571) initial velocity profile of the beam
+_reg(Case("bar2d_ivp", 2, "bar", CASES["bar2d"].spacing, CASES["bar2d"].lower, CASES["bar2d"].upper,
+          CASES["bar2d"].cuboids, init_calls=("setInitialVelocityProfile",),
+          note="bar2d started in its first bending mode (setInitialVelocityProfile)"))
 
 
 # elastic sub-stepping (main.cpp:653-663): ElasticDt = Dt/5 -> 5 substeps per step.  With the

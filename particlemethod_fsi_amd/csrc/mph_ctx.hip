@@ -680,6 +680,20 @@ int mph_set(MphCtx* c, int field, const void* in)
     return MPH_OK;
 }
 
+int mph_set_initial_velocity_profile(MphCtx* c)
+{
+    if (!c) return MPH_ERR_ARG;
+    HIP_OK(c, hipSetDevice(c->device));
+    const size_t n = (size_t)c->n_glob;
+    // slab mode: mph_get fills the owned entries and mph_set writes only those back
+    std::vector<double> pos(3 * n, 0.0), vel(3 * n, 0.0);
+    CK(mph_get(c, MPH_FIELD_POSITION, pos.data()));
+    CK(mph_get(c, MPH_FIELD_VELOCITY, vel.data()));
+    CK(mph_velocity_profile_arrays(&c->cfg, c->time, c->n_glob, c->prop.data(), pos.data(), c->pos0.data(),
+                                   vel.data()));
+    return mph_set(c, MPH_FIELD_VELOCITY, vel.data());
+}
+
 int mph_write_prof(MphCtx* c, const char* path)
 {
     if (!c || !path) return MPH_ERR_ARG;

@@ -463,6 +463,60 @@ extern "C" int mph_structure_init(const MphConfig* cfg, int n, const int* prop, 
     return MPH_OK;
 }
 
+// setInitialVelocityProfile (main.cpp:395-441, case constants 374-392) on host arrays in the
+// reference's layout.  Bar_Module: first bending mode of the L = 0.2 m beam on the structure
+// particles, v_y = 0.01 c0 f(x0)/f(L), c0 = sqrt(K/rho).  Turek_Hron: the parabolic inlet profile
+// on the fluid particles (x <= 0.01, and x > 1.5 while time < 0.7).  Other modules: no change.
+namespace {
+double beam_mode(double x)   // compute_fx, main.cpp:387-392
+{
+    const double kL = 1.875, L = 0.20, k = kL / L;
+    const double kx = k * x;
+    const double term1 = (std::cos(kL) + std::cosh(kL)) * (std::cosh(kx) - std::cos(kx));
+    const double term2 = (std::sin(kL) - std::sinh(kL)) * (std::sinh(kx) - std::sin(kx));
+    return term1 + term2;
+}
+}  // namespace
+
+extern "C" int mph_velocity_profile_arrays(const MphConfig* c, double time, int n, const int* prop,
+                                           const double* pos, const double* pos0, double* vel)
+{
+    if (!c || n < 0 || (n > 0 && (!prop || !pos || !pos0 || !vel))) return MPH_ERR_ARG;
+    if (c->module == MPH_MODULE_BAR) {
+        const double K = 3.25e6, L = 0.20;
+        for (int i = 0; i < n; ++i) {
+            if (!mph::is_struct(prop[i])) continue;
+            const double rho = c->density[prop[i]];
+            const double c0 = std::sqrt(K / rho);
+            const double fx = beam_mode(pos0[3 * (size_t)i]);
+            const double fL = beam_mode(L);
+            vel[3 * (size_t)i] = 0.0;
+            vel[3 * (size_t)i + 1] = 0.01 * c0 * fx / fL;
+            vel[3 * (size_t)i + 2] = 0.0;
+        }
+    } else if (c->module == MPH_MODULE_TUREK_HRON) {
+        const double ymin = 0.0, ymax = 0.41, umax = 1.0, h = ymax - ymin;
+        for (int i = 0; i < n; ++i) {
+            if (!mph::is_fluid(prop[i])) continue;
+            const double x = pos[3 * (size_t)i], y = pos[3 * (size_t)i + 1];
+            double* v = vel + 3 * (size_t)i;
+            if (x <= 0.01) {
+                const double uy = y - ymin;
+                v[0] = (1.5 * 4.0 * umax / (h * h)) * uy * (h - uy);
+                v[1] = 0.0;
+                v[2] = 0.0;
+            }
+            if (x > 1.5 && time < 0.7) {
+                const double uy = y - ymin;
+                v[0] = (4.0 * umax / (h * h)) * uy * (h - uy);
+                v[1] = 0.0;
+                v[2] = 0.0;
+            }
+        }
+    }
+    return MPH_OK;
+}
+
 namespace mph {
 
 // ---- derived constants: initializeWeight/Fluid/Wall/Domain (main.cpp:1191-1469) ------------

@@ -197,6 +197,24 @@ __device__ __forceinline__ void move_and_wrap(const DevParams& P, const DevState
 {
 #pragma clang fp contract(off)
     const int t = B.type[p];
+    if (P.module == MPH_MODULE_TUREK_HRON && dev_is_fluid(t)) {
+        // Turek_Hron: setInitialVelocityProfile (main.cpp:419-441) runs every step before
+        // calculateWall (592-594): parabolic inlet for x <= 0.01 and, while Time < 0.7, the same
+        // profile (without the 1.5 factor) for x > 1.5; YMIN/YMAX/UMAX from main.cpp:374-377
+        const double ymin = 0.0, ymax = 0.41, umax = 1.0, h = ymax - ymin;
+        if (x <= 0.01) {
+            const double uy = y - ymin;
+            B.vx[p] = (1.5 * 4.0 * umax / (h * h)) * uy * (h - uy);
+            B.vy[p] = 0.0;
+            B.vz[p] = 0.0;
+        }
+        if (x > 1.5 && st->time < 0.7) {
+            const double uy = y - ymin;
+            B.vx[p] = (4.0 * umax / (h * h)) * uy * (h - uy);
+            B.vy[p] = 0.0;
+            B.vz[p] = 0.0;
+        }
+    }
     if (dev_is_wall(t) && P.wall_motion == MPH_WALL_ROLLING) {
         // the Rolling branch of calculateWall (main.cpp:2974-3022): rotate about z through
         // WallCenter by the step's angle increment; the velocity is omega(t) x r_rot

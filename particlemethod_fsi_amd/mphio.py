@@ -251,9 +251,10 @@ def generate(cuboids: list[Cuboid]) -> Particles:
                      velocity=np.ascontiguousarray(np.concatenate(vel)) if vel else np.zeros((0, 3)))
 
 
-def format_grid(p: Particles, spacing: float, lower, upper) -> str:
-    """Text of the generator's ``writefile`` (generator.cpp:839-862)."""
-    out = ["%f\n" % 0.0,
+def format_grid(p: Particles, spacing: float, lower, upper, time: float = 0.0) -> str:
+    """Text of the generator's ``writefile`` (generator.cpp:839-862); ``time`` is the first line
+    (0 from the generator; a .prof restart carries its Time, main.cpp:797, 961)."""
+    out = ["%f\n" % time,
            "%d %e  %e %e %e  %e %e %e\n" % (p.n, spacing, lower[0], upper[0], lower[1], upper[1],
                                              lower[2], upper[2])]
     for i in range(p.n):

@@ -54,7 +54,8 @@ EXPORTED_SYMBOLS = [
     "mph_structure_init", "mph_create_dist_host", "mph_owned_ids", "mph_slab_bounds",
     "mph_slab_owner", "mph_dist_selftest", "mph_compute_virial",
     "mph_config_sizeof", "mph_write_vtk_async", "mph_output_wait", "mph_write_grid_binary",
-    "mph_write_vtu_arrays", "mph_write_vtu",
+    "mph_write_vtu_arrays", "mph_write_vtu", "mph_velocity_profile_arrays",
+    "mph_set_initial_velocity_profile",
 ]
 
 # mph_host_exchange_fn (include/mph_gpu.h): (user, send_l, n, send_r, n, recv_l, n, recv_r, n)
@@ -131,6 +132,8 @@ def load_library() -> ctypes.CDLL:
         "mph_write_vtu_arrays": (ip, [ctypes.c_char_p, ip] + [vp] * 10),
         "mph_write_vtu": (ip, [vp, ctypes.c_char_p]),
         "mph_output_wait": (ip, [vp]),
+        "mph_velocity_profile_arrays": (ip, [cfgp, dp, ip, vp, vp, vp, vp]),
+        "mph_set_initial_velocity_profile": (ip, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -308,6 +311,11 @@ class MphSolver:
         fid, _, _ = FIELDS[name]
         arr = np.ascontiguousarray(values, np.float64)
         _check(self._L.mph_set(self._h, fid, arr.ctypes.data), self._h)
+
+    def set_initial_velocity_profile(self):
+        """setInitialVelocityProfile (main.cpp:395-441) once on the current state: Bar beam mode or
+        Turek_Hron inlet, by the configured module (the Turek inlet also runs every step)."""
+        _check(self._L.mph_set_initial_velocity_profile(self._h), self._h)
 
     def scalars(self) -> np.ndarray:
         out = np.zeros(36)

@@ -52,6 +52,12 @@ PLAN = {  # case -> steps (cumulative) to snapshot; the first is the full-field 
     "gate3d_sub": [1, 10, 50],
     "rolling2d": [1, 10, 100],
     "rolling3d": [1, 10, 30],
+    "movwall2d": [1, 10, 100],
+    "movwall3d": [1, 10, 30],
+    "turek2d": [1, 10, 100],
+    "gate2d_rolling1": [1, 10, 100],
+    "hydro2d": [1, 10, 100],
+    "bar2d_ivp": [1, 10, 100],
 }
 
 
@@ -63,6 +69,8 @@ def run_case(name: str):
     dp, gp = write_case_files(cases.data_text(c.data()), c.grid_text(), tmp)
     ref = RefSolver(c.dim, c.ref_variant, dp, gp)
     ref.init()
+    for fn in c.init_calls:   # e.g. the commented setInitialVelocityProfile() of main.cpp:571
+        ref.call(fn)
     prop = ref.get("Property")
     solid = (prop >= 2) & (prop < 4)
     out = {"scalars": ref.scalars(), "Property": prop}
@@ -107,7 +115,8 @@ def run_case(name: str):
             out["s%d/nbr_ids" % s] = np.concatenate(rows).astype(np.int32)
     meta = {"case": name, "n": int(ref.n), "dim": c.dim, "module": c.module, "steps": PLAN[name],
             "time": ref.time, "generator": "tests/golden/make_golden.py",
-            "reference": "oracle/_ref/libmphref_%dd_%s.so" % (c.dim, c.module)}
+            "init_calls": list(c.init_calls),
+            "reference": "oracle/_ref/libmphref_%dd_%s.so" % (c.dim, c.ref_variant)}
     out["meta"] = np.frombuffer(json.dumps(meta).encode(), np.uint8)
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
     print(name, "n=%d" % ref.n, "->", os.path.getsize(os.path.join(HERE, name + ".npz")), "bytes")

@@ -65,6 +65,9 @@ def test_gpu_matches_reference_golden(case):
     g = Golden(case)
     cfg, parts = cases.get(case).build()
     with MphSolver(cfg, parts) as s:
+        for fn in cases.get(case).init_calls:
+            assert fn == "setInitialVelocityProfile", fn
+            s.set_initial_velocity_profile()
         assert np.array_equal(s.scalars(), g.z["scalars"])
         compare(g, s, 0)
         done = 0
@@ -76,7 +79,8 @@ def test_gpu_matches_reference_golden(case):
 
 
 @pytest.mark.parametrize("case,nsteps", [("dam2d", 20), ("gate3d", 12), ("gate3d_sub", 20),
-                                          ("box3d_st", 20), ("rolling2d", 20), ("rolling3d", 20)])
+                                          ("box3d_st", 20), ("rolling2d", 20), ("rolling3d", 20),
+                                          ("turek2d", 20), ("movwall3d", 10), ("hydro2d", 20)])
 def test_gpu_matches_oracle_every_step(case, nsteps):
     """Step-by-step against the oracle: all fields, including the ones the golden files do not
     store at every step (Force, DensityA, GravityCenter, VolStrainP, ...).  gate3d (ElasticDt =
@@ -157,15 +161,28 @@ def test_gpu_vtk_byte_identical_at_step0(tmp_path):
         assert hashlib.sha256(open(q, "rb").read()).digest() == bytes(g.z["sha256/dam000.prof"])
 
 
-def test_gpu_graph_chunking_equivalence():
-    """mph_step(8) (one 8-step graph) == 8 x mph_step(1) bitwise."""
-    cfg, parts = cases.get("box3d").build()
+CHUNK_FIELDS = ["Position", "Velocity", "Force", "Acceleration", "GravityCenter", "PressureP",
+                "PressureA", "DensityA", "VolStrainP", "DivergenceP", "NeighborCount", "Kappa",
+                "DeformGradient", "Strain", "Stress"]
+
+
+@pytest.mark.parametrize("case", ["box3d", "box3d_st", "gate2d", "bar2d"])
+def test_gpu_graph_chunking_equivalence(case):
+    """mph_step(8) (one 8-step graph, whose first 7 steps skip the output-only stores of pass A
+    and pass B) == 8 x mph_step(1) (every step stores), bitwise, for every field mph_get returns
+    and the virial diagnostic: without surface tension (box3d), with it (box3d_st) and with the
+    elastic clamp that zeroes Force after pass B (gate2d, bar2d)."""
+    cfg, parts = cases.get(case).build()
     with MphSolver(cfg, parts) as a, MphSolver(cfg, parts) as b:
         a.step(8)
         for _ in range(8):
             b.step(1)
-        assert np.array_equal(a.get("Position"), b.get("Position"))
-        assert np.array_equal(a.get("Velocity"), b.get("Velocity"))
+        for f in CHUNK_FIELDS:
+            assert np.array_equal(a.get(f), b.get(f), equal_nan=True), (case, f)
+        a.compute_virial()
+        b.compute_virial()
+        for f in ["VirialStressAtParticle", "VirialPressureAtParticle"]:
+            assert np.array_equal(a.get(f), b.get(f), equal_nan=True), (case, f)
 
 
 def test_gpu_nonfinite_state_is_an_error_not_a_fault():
