@@ -127,3 +127,25 @@ def band_worker(rank, world, port, case, out_path):
         np.save(out_path, np.array(res))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def gpu_rank_worker(rank, world, port, case, axis, nsteps, fields, out_dir, transport="host"):
+    """One slab rank of a large case on cuda:0 (several ranks share the GPU): run `nsteps`, then
+    save this rank's owned particle ids and their `fields` to out_dir/rank<r>.npz (no gather
+    through the process group, so it scales to the 16M-particle configuration)."""
+    dist = _init(rank, world, port)
+    from particlemethod_fsi_amd import MphSolver, cases
+    from particlemethod_fsi_amd.dist import gloo_slab, rccl_slab
+    c = cases.get(case)
+    cfg, parts = c.build()
+    mk = gloo_slab if transport == "host" else rccl_slab
+    with MphSolver(cfg, parts, device=0, slab=mk(rank, world, axis)) as s:
+        del parts
+        s.step(nsteps)
+        ids = s.owned_ids()
+        res = {"ids": ids, "time": np.array([s.time])}
+        for f in fields:
+            res[f] = s.get(f)[ids]
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), **res)
+    dist.barrier()
+    dist.destroy_process_group()

@@ -1,0 +1,96 @@
+"""GPU: BASELINE configs[4] -- the 3-D dam break with 16,205,500 particles.
+
+The oracle needs minutes per D16M step (and the reference ~100 GB for its three int[N][512]
+tables), so this configuration is checked through size-independent properties and against the
+single-context run, which the smaller parity tests pin to the oracle:
+
+1. one context (~37 GB of HBM): a rerun is bitwise identical, Time advances by exactly Dt per step,
+   no neighbour overflow and NeighborCount within the lattice bound (<= 80 at rc = 2.6 dx);
+2. the 8-way z-slab decomposition that the driver's 8-GPU job runs (8 ranks sharing the one test
+   GPU, host-staged transport) against the single context after 3 steps: ownership is a partition
+   of all particles, NeighborCount exact, positions 1e-12 m, velocities 1e-9 m/s, PressureP
+   1e-8 relative + 1e-9 Pa (the slabs' local cell grids order neighbour sums differently).
+"""
+import multiprocessing as mp
+import socket
+
+import numpy as np
+import pytest
+
+from particlemethod_fsi_amd import MphSolver, cases
+
+import dist_worker
+
+pytestmark = pytest.mark.gpu
+
+STEPS = 3
+FIELDS = ["Position", "Velocity", "PressureP", "NeighborCount", "VolStrainP", "DivergenceP"]
+FLOOR = {"PressureP": 1e-9, "VolStrainP": 1e-13, "DivergenceP": 1e-12}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _single(nsteps):
+    cfg, parts = cases.get("d16m").build()
+    n = parts.n
+    with MphSolver(cfg, parts) as s:
+        del parts
+        s.step(nsteps)
+        out = {f: s.get(f) for f in FIELDS}
+        out["time"] = s.time
+        out["mean_max"] = s.neighbor_stats()
+    return cfg, n, out
+
+
+def test_d16m_single_context_rerun_time_and_counts():
+    cfg, n, a = _single(10)   # one 8-step graph + two 1-step graphs
+    assert n == 16205500
+    _, _, b = _single(10)
+    for f in ("Position", "Velocity", "PressureP", "NeighborCount"):
+        assert np.array_equal(a[f], b[f]), f
+    t = 0.0
+    for _ in range(10):
+        t += cfg.dt
+    assert a["time"] == t
+    nc = a["NeighborCount"]
+    assert nc.max() <= 80 and nc.min() >= 1, (int(nc.min()), int(nc.max()))
+    assert np.isfinite(a["Position"]).all() and np.isfinite(a["PressureP"]).all()
+
+
+def test_d16m_slab8_matches_single_context(tmp_path):
+    world = 8
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    ps = [ctx.Process(target=dist_worker.gpu_rank_worker,
+                      args=(r, world, port, "d16m", 2, STEPS, FIELDS, str(tmp_path)))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(900)
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    cfg, n, ref = _single(STEPS)
+    seen = np.zeros(n, np.int32)
+    for r in range(world):
+        z = np.load(str(tmp_path / ("rank%d.npz" % r)))
+        ids = z["ids"]
+        assert float(z["time"][0]) == ref["time"]
+        seen[ids] += 1
+        for f in FIELDS:
+            a, b = z[f], ref[f][ids]
+            if f == "NeighborCount":
+                assert np.array_equal(a, b), (r, f, int((a != b).sum()))
+                continue
+            err = float(np.max(np.abs(a - b))) if len(ids) else 0.0
+            t = {"Position": 1e-12, "Velocity": 1e-9}.get(
+                f, 1e-8 * float(np.max(np.abs(ref[f]))) + FLOOR.get(f, 1e-12))
+            assert err <= t, (r, f, err, t)
+    assert (seen == 1).all(), "ownership is not a partition: %d missing, %d duplicated" % (
+        int((seen == 0).sum()), int((seen > 1).sum()))
