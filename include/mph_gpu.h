@@ -281,7 +281,10 @@ int mph_neighbor_stats(MphCtx* ctx, double* mean, int* max);
 int mph_dist_unique_id(char* out128);
 /* Same as mph_create, but this rank owns only the particles whose slab (along `axis`) is
  * `rank` of `nranks`; all ranks pass the full particle set.  Transport: RCCL (ncclSend/Recv
- * with the two periodic neighbours, on the context's stream).                                */
+ * with the two periodic neighbours, on the context's stream).  Every size of a step is kept on
+ * the device and messages travel with fixed capacities (grown between mph_step batches when a
+ * count passes 80 %), so the steps are replayed from captured hipGraphs with no host round trip
+ * (MPH_SLAB_GRAPHS=0: direct launches).                                                       */
 int mph_create_dist(MphCtx** ctx, const MphConfig* cfg, int n, const int* property,
                     const double* pos, const double* pos0, const double* vel, int device,
                     int rank, int nranks, const char* unique_id128, int axis);
@@ -300,6 +303,11 @@ int mph_create_dist_host(MphCtx** ctx, const MphConfig* cfg, int n, const int* p
  * exchange delivers each message to the right buffer (the per-peer ordering nranks == 2 relies
  * on) without a second GPU.  Returns 0 on success.                                            */
 int mph_dist_selftest(int device);
+/* Slab-mode facts for reports: out8 = {ranks in the communicator (ncclCommCount; 1 without
+ * slabs), rank, RCCL transport (1) or host-staged (0), steps replayed from captured graphs,
+ * local array capacity, largest send / receive message capacity (particles), particles held
+ * (owned + ghosts)}.                                                                          */
+int mph_dist_info(const MphCtx* ctx, int* out8);
 /* Particles currently owned by this rank (after the last migration); their original indices.  */
 int mph_owned_count(const MphCtx* ctx);
 int mph_owned_ids(MphCtx* ctx, int* out_ids);

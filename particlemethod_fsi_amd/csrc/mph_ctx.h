@@ -17,30 +17,31 @@ struct MphDist {
     int rank = 0, nranks = 1, left = 0, right = 0;
     mph::SlabGeom g{};
     int cap = 0;                  // capacity of every local per-particle array
-    int msg_cap = 0;              // capacity (particles) of one exchange message
-    int n_own = 0;                // owned particles after the last redistribution
-    // segment sizes of the last redistribution (kMigR..kMigL) and of the two received messages
-    int seg[mph::kSlabClasses] = {0};
-    int from_l_mig = 0, from_l_band = 0, from_r_band = 0, from_r_mig = 0;
+    int n_own = 0;                // owned particles after the last redistribution (host mirror)
+    // Every size of a step lives on the device (DistLayout), so a step has no host round trip and
+    // the RCCL transport replays whole steps from captured graphs.  Messages travel with fixed
+    // capacities (particles) per direction; a pair of neighbours derives the same capacity for
+    // its shared direction from the same counts (send of one = receive of the other).
+    mph::DistLayout* lay = nullptr;    // device
+    mph::DistLayout* hlay = nullptr;   // pinned host mirror (read after a step batch)
+    int cap_sl = 0, cap_sr = 0, cap_rl = 0, cap_rr = 0;
+    size_t region = 0;            // bytes of each of the four message buffers
     mph::Soa C;                   // redistributed state (pre-sort order)
     int* cls = nullptr;           // class of every B entry
     int* bcnt = nullptr;          // per (class, block) counts -> offsets
     int* boff = nullptr;
     int* bsum = nullptr;
-    int* dseg = nullptr;          // device copy of the class segment starts (7 ints)
-    int* hseg = nullptr;          // pinned host mirror
-    char *send_l = nullptr, *send_r = nullptr, *recv_l = nullptr, *recv_r = nullptr;  // device
-    int *cnt_send = nullptr, *cnt_recv = nullptr;    // device count messages (4 ints each way)
+    char *send_l = nullptr, *send_r = nullptr, *recv_l = nullptr, *recv_r = nullptr;  // device, resizable
     hipStream_t stream2 = nullptr;                   // halo exchange beside the inner pass B
     hipEvent_t ev_a = nullptr, ev_h = nullptr;       // pass A done / halo landed
     // transport: RCCL communicator, or a host callback (tests / hosts without RCCL)
     bool rccl = false;
+    bool graphs = false;          // steps replayed from captured graphs (RCCL transport)
     char uid[128] = {0};          // ncclUniqueId
     void* comm = nullptr;         // ncclComm_t
     mph_host_exchange_fn host_fn = nullptr;
     void* host_user = nullptr;
     char* host_stage = nullptr;   // pinned staging for the host transport (4 messages)
-    int* hcnt = nullptr;          // pinned count messages (send 4, recv 4)
     // elastic ghost slots (static): local slot indices sent to / received from each neighbour
     int *ss_l = nullptr, *ss_r = nullptr, *sr_l = nullptr, *sr_r = nullptr;
     int nss_l = 0, nss_r = 0, nsr_l = 0, nsr_r = 0;
@@ -118,6 +119,7 @@ int dist_struct_setup(MphCtx* c, std::vector<int>& lsl, int& n_own);
 int dist_alloc(MphCtx* c);                                               // exchange buffers
 int dist_init(MphCtx* c);                                                // first exchange + init sums
 int dist_step(MphCtx* c, int nsteps, Profiler* prof = nullptr);
+int dist_sync(MphCtx* c);                // host mirror of the layout + error flags after a batch
 void dist_free(MphCtx* c);
 
 }  // namespace mph

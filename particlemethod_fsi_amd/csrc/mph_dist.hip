@@ -43,6 +43,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstddef>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -157,7 +159,9 @@ int exchange(MphCtx* c, hipStream_t stream, const void* send_l, size_t bsl, cons
         RCCL_OK(c, ncclGroupEnd());
         return MPH_OK;
     }
-    const size_t region = (size_t)D.msg_cap * kMsgBytes;
+    const size_t region = D.region;
+    if (bsl > region || bsr > region || brl > region || brr > region)
+        return ctx_fail(c, MPH_ERR_CAPACITY, "slab mode: message larger than the staging buffers");
     char* hs_l = D.host_stage;
     char* hs_r = D.host_stage + region;
     char* hr_l = D.host_stage + 2 * region;
@@ -172,47 +176,73 @@ int exchange(MphCtx* c, hipStream_t stream, const void* send_l, size_t bsl, cons
     return MPH_OK;
 }
 
+template <typename T>
+T* lay_field(DistLayout* lay, size_t off) { return reinterpret_cast<T*>(reinterpret_cast<char*>(lay) + off); }
+
+// Message capacity (particles) of a direction whose live count is c: room to grow by half before
+// the next capacity check (between step batches, dist_sync).
+int msg_capacity(int c) { return c + c / 2 + 4096; }
+
+// (Re)allocate the four message buffers for the current capacities: redistribution (56 B per
+// particle), pass-A halo (up to 40 B per particle of both directions' capacities), elastic ghosts.
+int msg_alloc(MphCtx* c)
+{
+    MphDist& D = *c->dist;
+    const size_t most = std::max({D.cap_sl, D.cap_sr, D.cap_rl, D.cap_rr});
+    size_t region = kMsgBytes * most;
+    region = std::max(region, sizeof(double) * 5 * (size_t)std::max(D.cap_sl + D.cap_rl, D.cap_sr + D.cap_rr));
+    const size_t smost = std::max({D.nss_l, D.nss_r, D.nsr_l, D.nsr_r});
+    region = std::max(region, 3 * sizeof(double4) * smost);
+    region = (region + 255) & ~(size_t)255;
+    if (region <= D.region && D.send_l) return MPH_OK;
+    for (char** b : {&D.send_l, &D.send_r, &D.recv_l, &D.recv_r}) {
+        if (*b) (void)hipFree(*b);
+        *b = nullptr;
+        MPH_HIP_OK(c, hipMalloc((void**)b, region));
+    }
+    if (!D.rccl) {
+        if (D.host_stage) (void)hipHostFree(D.host_stage);
+        D.host_stage = nullptr;
+        MPH_HIP_OK(c, hipHostMalloc((void**)&D.host_stage, 4 * region, hipHostMallocDefault));
+    }
+    D.region = region;
+    return MPH_OK;
+}
+
 // Steps 1-3 of the protocol: classify, partition, exchange migrants + ghosts.  Leaves the new
-// local set (n entries, owned and ghosts) in D.C.
-int redistribute(MphCtx* c, bool move, Profiler* prof)
+// local set (owned and ghosts) in D.C and its sizes in D.lay -- on the device: nothing here reads
+// a size on the host, so the step can be captured.  init: first redistribution of mph_create,
+// which reads the counts once to size the message buffers.
+int redistribute(MphCtx* c, bool move, bool init, Profiler* prof)
 {
     MphDist& D = *c->dist;
     Launch L = c->L;
     L.prof = prof;
-    const int n_prev = c->n;
-    const int nb = dist_blocks(n_prev);
-    launch_dist_classify(L, D.g, n_prev, move ? 1 : 0, D.cls, D.bcnt);
-    launch_scan(D.bcnt, kSlabClasses * nb, D.bsum, D.boff, n_prev, c->stream, prof);
-    launch_dist_scatter(L, n_prev, D.cls, D.boff, D.C, D.dseg);
-    // count messages straight from the device segment table; one host sync for both the local
-    // segment sizes and the neighbours' counts
-    launch_dist_counts(L, D.dseg, D.cnt_send);
-    MPH_CK(exchange(c, c->stream, D.cnt_send, 2 * sizeof(int), D.cnt_send + 2, 2 * sizeof(int), D.cnt_recv,
-                    2 * sizeof(int), D.cnt_recv + 2, 2 * sizeof(int)));
-    int* hc = D.hcnt;
-    MPH_HIP_OK(c, hipMemcpyAsync(D.hseg, D.dseg, sizeof(int) * (kSlabClasses + 1), hipMemcpyDeviceToHost,
-                                 c->stream));
-    MPH_HIP_OK(c, hipMemcpyAsync(hc + 4, D.cnt_recv, sizeof(int) * 4, hipMemcpyDeviceToHost, c->stream));
-    MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
-    for (int k = 0; k < kSlabClasses; ++k) D.seg[k] = D.hseg[k + 1] - D.hseg[k];
-    const int mR = D.seg[kMigR], bR = D.seg[kBandR], bL = D.seg[kBandL], mL = D.seg[kMigL];
-    const int nc = D.hseg[kSlabDrop];                 // kept entries (classes 0..4)
-    D.from_l_mig = hc[4]; D.from_l_band = hc[5];     // their {migR, bandR}
-    D.from_r_band = hc[6]; D.from_r_mig = hc[7];     // their {bandL, migL}
-    const int fl = D.from_l_mig + D.from_l_band, fr = D.from_r_band + D.from_r_mig;
-    const int n_new = nc + fl + fr;
-    if (n_new > D.cap || fl > D.msg_cap || fr > D.msg_cap)
-        return ctx_fail(c, MPH_ERR_CAPACITY, "slab mode: local particle capacity " + std::to_string(D.cap) +
-                                                 " exceeded (" + std::to_string(n_new) + ")");
-    launch_dist_pack(L, D.C, D.hseg[kBandL], bL + mL, D.send_l);
-    launch_dist_pack(L, D.C, 0, mR + bR, D.send_r);
-    MPH_CK(exchange(c, c->stream, D.send_l, kMsgBytes * (bL + mL), D.send_r, kMsgBytes * (mR + bR), D.recv_l,
-                    kMsgBytes * fl, D.recv_r, kMsgBytes * fr));
-    launch_dist_unpack(L, D.recv_l, fl, D.C, nc);
-    launch_dist_unpack(L, D.recv_r, fr, D.C, nc + fl);
-    c->n = n_new;
-    c->P.n = n_new;
-    D.n_own = bR + D.seg[kInner] + bL + D.from_l_mig + D.from_r_mig;
+    const int nb = dist_blocks(D.cap);
+    launch_dist_classify(L, D.g, D.cap, D.lay, move ? 1 : 0, D.cls, D.bcnt);
+    launch_scan(D.bcnt, kSlabClasses * nb, D.bsum, D.boff, 0, c->stream, prof);
+    launch_dist_scatter(L, D.cap, D.lay, D.cls, D.boff, D.C, lay_field<int>(D.lay, offsetof(DistLayout, seg)));
+    launch_dist_counts(L, D.lay);
+    int* snd = lay_field<int>(D.lay, offsetof(DistLayout, send));
+    int* rcv = lay_field<int>(D.lay, offsetof(DistLayout, recv));
+    MPH_CK(exchange(c, c->stream, snd, 2 * sizeof(int), snd + 2, 2 * sizeof(int), rcv, 2 * sizeof(int), rcv + 2,
+                    2 * sizeof(int)));
+    if (init) {
+        MPH_HIP_OK(c, hipMemcpyAsync(D.hlay, D.lay, sizeof(DistLayout), hipMemcpyDeviceToHost, c->stream));
+        MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
+        const DistLayout& h = *D.hlay;
+        D.cap_sl = msg_capacity(h.send[0] + h.send[1]);
+        D.cap_sr = msg_capacity(h.send[2] + h.send[3]);
+        D.cap_rl = msg_capacity(h.recv[0] + h.recv[1]);
+        D.cap_rr = msg_capacity(h.recv[2] + h.recv[3]);
+        MPH_CK(msg_alloc(c));
+    }
+    launch_dist_pack(L, D.C, D.lay, 0, D.cap_sl, D.send_l);
+    launch_dist_pack(L, D.C, D.lay, 1, D.cap_sr, D.send_r);
+    MPH_CK(exchange(c, c->stream, D.send_l, kMsgBytes * D.cap_sl, D.send_r, kMsgBytes * D.cap_sr, D.recv_l,
+                    kMsgBytes * D.cap_rl, D.recv_r, kMsgBytes * D.cap_rr));
+    launch_dist_unpack(L, D.recv_l, D.lay, 0, D.cap_rl, D.cap, D.C);
+    launch_dist_unpack(L, D.recv_r, D.lay, 1, D.cap_rr, D.cap, D.C);
     return MPH_OK;
 }
 
@@ -239,7 +269,8 @@ HaloFields halo_fields(MphCtx* c)
     return F;
 }
 
-// Step 5: the pass-A values of every neighbour's ghosts.
+// Step 5: the pass-A values of every neighbour's ghosts (ranges from the device layout, fixed
+// message capacities: to/from the left cap_sl + cap_rl particles, to/from the right cap_sr + cap_rr).
 int halo_exchange(MphCtx* c, Profiler* prof, hipStream_t stream)
 {
     MphDist& D = *c->dist;
@@ -247,27 +278,17 @@ int halo_exchange(MphCtx* c, Profiler* prof, hipStream_t stream)
     L.prof = prof;
     L.stream = stream;
     const HaloFields F = halo_fields(c);
-    const int nc = D.hseg[kSlabDrop];
-    const int fl = D.from_l_mig + D.from_l_band;
-    // to left: the left neighbour's migrants we now own, then our band-left particles
-    const int l1 = nc, ln1 = D.from_l_mig, l2 = D.hseg[kBandL], ln2 = D.seg[kBandL];
-    // to right: the right neighbour's migrants we now own, then our band-right particles
-    const int r1 = nc + fl + D.from_r_band, rn1 = D.from_r_mig, r2 = D.hseg[kBandR], rn2 = D.seg[kBandR];
-    // from left: values of our migL ghosts, then of the left neighbour's bandR ghosts
-    const int fl1 = D.hseg[kMigL], fln1 = D.seg[kMigL], fl2 = nc + D.from_l_mig, fln2 = D.from_l_band;
-    // from right: values of our migR ghosts, then of the right neighbour's bandL ghosts
-    const int fr1 = D.hseg[kMigR], frn1 = D.seg[kMigR], fr2 = nc + fl, frn2 = D.from_r_band;
+    const int capl = D.cap_sl + D.cap_rl, capr = D.cap_sr + D.cap_rr;
     double* sl = (double*)D.send_l;
     double* sr = (double*)D.send_r;
     double* rl = (double*)D.recv_l;
     double* rr = (double*)D.recv_r;
-    launch_halo_pack(L, c->rank_of, l1, ln1, l2, ln2, F, sl);
-    launch_halo_pack(L, c->rank_of, r1, rn1, r2, rn2, F, sr);
+    launch_halo_pack(L, c->rank_of, D.lay, 0, capl, F, sl);
+    launch_halo_pack(L, c->rank_of, D.lay, 1, capr, F, sr);
     const size_t b = sizeof(double) * F.nf;
-    MPH_CK(exchange(c, stream, sl, b * (ln1 + ln2), sr, b * (rn1 + rn2), rl, b * (fln1 + fln2), rr,
-                    b * (frn1 + frn2)));
-    launch_halo_unpack(L, rl, c->rank_of, fl1, fln1, fl2, fln2, F);
-    launch_halo_unpack(L, rr, c->rank_of, fr1, frn1, fr2, frn2, F);
+    MPH_CK(exchange(c, stream, sl, b * capl, sr, b * capr, rl, b * capl, rr, b * capr));
+    launch_halo_unpack(L, rl, c->rank_of, D.lay, 2, capl, F);
+    launch_halo_unpack(L, rr, c->rank_of, D.lay, 3, capr, F);
     return MPH_OK;
 }
 
@@ -307,13 +328,6 @@ int struct_substeps(MphCtx* c, Profiler* prof)
     return MPH_OK;
 }
 
-int check_state(MphCtx* c)
-{
-    DevState hs;
-    MPH_HIP_OK(c, hipMemcpyAsync(&hs, c->dst, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
-    MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
-    return ctx_state_status(c, hs);
-}
 
 }  // namespace
 
@@ -378,7 +392,6 @@ int dist_setup(MphCtx* c, const double* pos, std::vector<int>& owned)
     }
     const size_t want = (size_t)((owned.size() + near) * 1.25) + 65536;
     D.cap = (int)std::min<size_t>(want, (size_t)c->n_glob);
-    D.msg_cap = D.cap;
     D.n_own = (int)owned.size();
     return MPH_OK;
 }
@@ -434,9 +447,6 @@ int dist_struct_setup(MphCtx* c, std::vector<int>& lsl, int& n_own)
     for (int j : rgl) sr.push_back(loc[j]);
     for (int k : sl) if (k < 0 || k >= n_own) return ctx_fail(c, MPH_ERR_DOMAIN, "slab mode: elastic ghost routing");
     for (int k : sr) if (k < 0 || k >= n_own) return ctx_fail(c, MPH_ERR_DOMAIN, "slab mode: elastic ghost routing");
-    const size_t most = std::max({sl.size(), sr.size(), rl.size(), rr.size()});
-    if (most * 3 * sizeof(double4) > (size_t)D.msg_cap * kMsgBytes)
-        return ctx_fail(c, MPH_ERR_CAPACITY, "slab mode: elastic ghost message exceeds the exchange buffers");
     D.nss_l = (int)sl.size(); D.nss_r = (int)sr.size();
     D.nsr_l = (int)rl.size(); D.nsr_r = (int)rr.size();
     MPH_CK(ctx_dalloc(c, &D.ss_l, sl.size())); MPH_CK(ctx_dalloc(c, &D.ss_r, sr.size()));
@@ -462,25 +472,64 @@ int dist_alloc(MphCtx* c)
     MPH_CK(ctx_dalloc(c, &D.bcnt, nslots + 1));
     MPH_CK(ctx_dalloc(c, &D.boff, nslots + 1));
     MPH_CK(ctx_dalloc(c, &D.bsum, nslots / 4096 + 2));
-    MPH_CK(ctx_dalloc(c, &D.dseg, kSlabClasses + 2));
-    MPH_CK(ctx_dalloc(c, &D.cnt_send, 4));
-    MPH_CK(ctx_dalloc(c, &D.cnt_recv, 4));
-    const size_t region = (size_t)D.msg_cap * kMsgBytes;
-    MPH_CK(ctx_dalloc(c, &D.send_l, region)); MPH_CK(ctx_dalloc(c, &D.send_r, region));
-    MPH_CK(ctx_dalloc(c, &D.recv_l, region)); MPH_CK(ctx_dalloc(c, &D.recv_r, region));
+    MPH_CK(ctx_dalloc(c, &D.lay, 1));
+    MPH_HIP_OK(c, hipHostMalloc((void**)&D.hlay, sizeof(DistLayout), hipHostMallocDefault));
+    std::memset(D.hlay, 0, sizeof(DistLayout));
+    D.hlay->n = c->n;   // the uploaded owned set, classified by the first redistribution
+    MPH_HIP_OK(c, hipMemcpyAsync(D.lay, D.hlay, sizeof(DistLayout), hipMemcpyHostToDevice, c->stream));
+    // every kernel of a slab step reads the live particle count from the layout; P.n is the
+    // capacity the launch grids are sized for
+    c->P.n = cap;
+    c->P.n_dev = lay_field<int>(D.lay, offsetof(DistLayout, n));
+    // first message buffers (the count exchange of the first redistribution uses them); their
+    // capacities follow from the first counts (redistribute, init)
+    D.cap_sl = D.cap_sr = D.cap_rl = D.cap_rr = msg_capacity(0);
+    MPH_CK(msg_alloc(c));
     MPH_HIP_OK(c, hipStreamCreateWithFlags(&D.stream2, hipStreamNonBlocking));
     MPH_HIP_OK(c, hipEventCreateWithFlags(&D.ev_a, hipEventDisableTiming));
     MPH_HIP_OK(c, hipEventCreateWithFlags(&D.ev_h, hipEventDisableTiming));
-    MPH_HIP_OK(c, hipHostMalloc((void**)&D.hseg, sizeof(int) * (kSlabClasses + 2), hipHostMallocDefault));
-    MPH_HIP_OK(c, hipHostMalloc((void**)&D.hcnt, sizeof(int) * 8, hipHostMallocDefault));
     if (D.rccl) {
         ncclUniqueId id;
         std::memcpy(&id, D.uid, sizeof(id));
         ncclComm_t comm = nullptr;
         RCCL_OK(c, ncclCommInitRank(&comm, D.nranks, id, D.rank));
         D.comm = comm;
-    } else {
-        MPH_HIP_OK(c, hipHostMalloc((void**)&D.host_stage, 4 * region, hipHostMallocDefault));
+    }
+    return MPH_OK;
+}
+
+int dist_sync(MphCtx* c)
+{
+    MphDist& D = *c->dist;
+    DevState hs;
+    MPH_HIP_OK(c, hipMemcpyAsync(&hs, c->dst, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
+    MPH_HIP_OK(c, hipMemcpyAsync(D.hlay, D.lay, sizeof(DistLayout), hipMemcpyDeviceToHost, c->stream));
+    MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
+    if (hs.overflow & 8)
+        return ctx_fail(c, MPH_ERR_CAPACITY, "slab mode: a redistribution exceeded the message or local capacity");
+    MPH_CK(ctx_state_status(c, hs));
+    const DistLayout& h = *D.hlay;
+    c->n = h.n;
+    D.n_own = h.n_own;
+    if (h.hw[4] > D.cap)
+        return ctx_fail(c, MPH_ERR_CAPACITY, "slab mode: local particle capacity " + std::to_string(D.cap) +
+                                                 " exceeded (" + std::to_string(h.hw[4]) + ")");
+    // capacity check between batches: a direction above 80 % of its message capacity grows (both
+    // ranks of the pair see the same counts, so they grow the shared direction alike); the
+    // captured graphs hold the old sizes and are re-captured by the next step
+    int* caps[4] = {&D.cap_sl, &D.cap_sr, &D.cap_rl, &D.cap_rr};
+    bool grow = false;
+    for (int k = 0; k < 4; ++k)
+        if (h.hw[k] * 5 > *caps[k] * 4) {
+            *caps[k] = msg_capacity(h.hw[k]);
+            grow = true;
+        }
+    if (grow) {
+        MPH_CK(msg_alloc(c));
+        if (c->graph1) { (void)hipGraphExecDestroy(c->graph1); c->graph1 = nullptr; }
+        if (c->graph8) { (void)hipGraphExecDestroy(c->graph8); c->graph8 = nullptr; }
+        MPH_HIP_OK(c, hipMemsetAsync(lay_field<int>(D.lay, offsetof(DistLayout, hw)), 0, 4 * sizeof(int),
+                                     c->stream));
     }
     return MPH_OK;
 }
@@ -489,43 +538,77 @@ int dist_init(MphCtx* c)
 {
     // calculateNeighbor, DensityA, GravityCenter, DensityP of the initialisation (main.cpp:565-568)
     // on owned + ghosts (no motion, no time advance)
-    MPH_CK(redistribute(c, false, nullptr));
+    MPH_CK(redistribute(c, false, true, nullptr));
     sort_local(c, 0, nullptr);
     launch_neighbors(c->L);
     launch_pass_a(c->L);
+    MPH_CK(dist_sync(c));
     // the integrated-state set B starts as the sorted local set (owned + ghosts, ids signed)
     MPH_CK(copy_soa(c, c->B, c->A, c->n));
     MPH_HIP_OK(c, hipGetLastError());
-    return check_state(c);
+    return dist_sync(c);
+}
+
+// One slab step on the context's stream (no host synchronisation inside: RCCL transport steps
+// are captured into graphs by dist_step; the host transport stages each message through host
+// memory and so synchronises in exchange()).
+int dist_enqueue_step(MphCtx* c, Profiler* prof)
+{
+    Launch L = c->L;
+    L.prof = prof;
+    MphDist& D = *c->dist;
+    MPH_CK(redistribute(c, true, false, prof));
+    sort_local(c, 2, prof);
+    launch_neighbors(L);
+    launch_pass_a(L);
+    // the pass-A halo travels on stream2 while pass B runs the particles that have no ghost
+    // neighbours; the near-face particles follow once the halo has landed (inner pass B is
+    // enqueued first, so that a host-staged exchange, which blocks the host, also overlaps with it)
+    MPH_HIP_OK(c, hipEventRecord(D.ev_a, c->stream));
+    launch_pass_b(L, 1);
+    MPH_HIP_OK(c, hipStreamWaitEvent(D.stream2, D.ev_a, 0));
+    MPH_CK(halo_exchange(c, prof, D.stream2));
+    MPH_HIP_OK(c, hipEventRecord(D.ev_h, D.stream2));
+    MPH_HIP_OK(c, hipStreamWaitEvent(c->stream, D.ev_h, 0));
+    launch_pass_b(L, 2);
+    MPH_CK(struct_substeps(c, prof));
+    return MPH_OK;
+}
+
+int dist_capture(MphCtx* c, int steps, hipGraphExec_t* out)
+{
+    hipGraph_t g = nullptr;
+    MPH_HIP_OK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    int rc = MPH_OK;
+    for (int k = 0; k < steps && rc == MPH_OK; ++k) rc = dist_enqueue_step(c, nullptr);
+    const hipError_t e = hipStreamEndCapture(c->stream, &g);
+    if (rc != MPH_OK) {
+        if (g) (void)hipGraphDestroy(g);
+        return rc;
+    }
+    MPH_HIP_OK(c, e);
+    const hipError_t ei = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    MPH_HIP_OK(c, ei);
+    return MPH_OK;
 }
 
 int dist_step(MphCtx* c, int nsteps, Profiler* prof)
 {
-    Launch L = c->L;
-    L.prof = prof;
-    for (int k = 0; k < nsteps; ++k) {
-        MPH_CK(redistribute(c, true, prof));
-        sort_local(c, 2, prof);
-        launch_neighbors(L);
-        launch_pass_a(L);
-        // the pass-A halo travels on stream2 while pass B runs the particles that have no
-        // ghost neighbours; the near-face particles follow once the halo has landed
-        // (inner pass B is enqueued first, so that a host-staged exchange, which blocks the host,
-        // also overlaps with it)
-        MphDist& D = *c->dist;
-        MPH_HIP_OK(c, hipEventRecord(D.ev_a, c->stream));
-        launch_pass_b(L, 1);
-        MPH_HIP_OK(c, hipStreamWaitEvent(D.stream2, D.ev_a, 0));
-        MPH_CK(halo_exchange(c, prof, D.stream2));
-        MPH_HIP_OK(c, hipEventRecord(D.ev_h, D.stream2));
-        MPH_HIP_OK(c, hipStreamWaitEvent(c->stream, D.ev_h, 0));
-        launch_pass_b(L, 2);
-        MPH_CK(struct_substeps(c, prof));
-        MPH_HIP_OK(c, hipGetLastError());
-        c->time += c->cfg.dt;
-        c->stepped = true;
+    MphDist& D = *c->dist;
+    int left = nsteps;
+    if (D.graphs && !prof) {
+        if (!c->graph1) MPH_CK(dist_capture(c, 1, &c->graph1));
+        if (!c->graph8 && nsteps >= 8) MPH_CK(dist_capture(c, 8, &c->graph8));
+        while (left >= 8) { MPH_HIP_OK(c, hipGraphLaunch(c->graph8, c->stream)); left -= 8; }
+        while (left > 0) { MPH_HIP_OK(c, hipGraphLaunch(c->graph1, c->stream)); left -= 1; }
+    } else {
+        for (; left > 0; --left) MPH_CK(dist_enqueue_step(c, prof));
     }
-    return check_state(c);
+    MPH_HIP_OK(c, hipGetLastError());
+    for (int k = 0; k < nsteps; ++k) c->time += c->cfg.dt;
+    c->stepped = true;
+    return dist_sync(c);
 }
 
 void dist_free(MphCtx* c)
@@ -537,8 +620,9 @@ void dist_free(MphCtx* c)
     if (D->ev_a) (void)hipEventDestroy(D->ev_a);
     if (D->ev_h) (void)hipEventDestroy(D->ev_h);
     if (D->stream2) (void)hipStreamDestroy(D->stream2);
-    if (D->hseg) (void)hipHostFree(D->hseg);
-    if (D->hcnt) (void)hipHostFree(D->hcnt);
+    if (D->hlay) (void)hipHostFree(D->hlay);
+    for (char* b : {D->send_l, D->send_r, D->recv_l, D->recv_r})
+        if (b) (void)hipFree(b);
     if (D->host_stage) (void)hipHostFree(D->host_stage);
     delete D;
     c->dist = nullptr;
@@ -568,6 +652,7 @@ int mph_create_dist(MphCtx** ctx, const MphConfig* cfg, int n, const int* proper
     D->nranks = nranks;
     D->g.axis = axis;
     D->rccl = true;
+    D->graphs = std::getenv("MPH_SLAB_GRAPHS") == nullptr || std::string(std::getenv("MPH_SLAB_GRAPHS")) != "0";
     std::memcpy(D->uid, unique_id128, sizeof(D->uid));
     return ctx_create(ctx, cfg, n, property, pos, pos0, vel, device, D);
 }
@@ -622,6 +707,26 @@ int mph_dist_selftest(int device)
         MPH_HIP_OK(&c, hipMemcpy(gl.data(), rl, nr, hipMemcpyDeviceToHost));
         MPH_HIP_OK(&c, hipMemcpy(gr.data(), rr, nl, hipMemcpyDeviceToHost));
         if (gl != hr || gr != hl) return ctx_fail(&c, MPH_ERR_RCCL, "RCCL self-exchange delivered wrong bytes");
+        // the same exchange captured into a hipGraph and replayed (slab steps replay RCCL calls
+        // from captured graphs)
+        MPH_HIP_OK(&c, hipMemset(rl, 0, nr));
+        MPH_HIP_OK(&c, hipMemset(rr, 0, nl));
+        hipGraph_t g = nullptr;
+        hipGraphExec_t ge = nullptr;
+        MPH_HIP_OK(&c, hipStreamBeginCapture(c.stream, hipStreamCaptureModeThreadLocal));
+        const int rc = exchange(&c, c.stream, sl, nl, sr, nr, rl, nr, rr, nl);
+        const hipError_t e = hipStreamEndCapture(c.stream, &g);
+        MPH_CK(rc);
+        MPH_HIP_OK(&c, e);
+        const hipError_t ei = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        MPH_HIP_OK(&c, ei);
+        for (int rep = 0; rep < 2; ++rep) MPH_HIP_OK(&c, hipGraphLaunch(ge, c.stream));
+        MPH_HIP_OK(&c, hipStreamSynchronize(c.stream));
+        (void)hipGraphExecDestroy(ge);
+        MPH_HIP_OK(&c, hipMemcpy(gl.data(), rl, nr, hipMemcpyDeviceToHost));
+        MPH_HIP_OK(&c, hipMemcpy(gr.data(), rr, nl, hipMemcpyDeviceToHost));
+        if (gl != hr || gr != hl) return ctx_fail(&c, MPH_ERR_RCCL, "graph-replayed RCCL exchange delivered wrong bytes");
         return MPH_OK;
     };
     status = run();
@@ -631,6 +736,28 @@ int mph_dist_selftest(int device)
     for (void* p : c.allocs) (void)hipFree(p);
     if (c.stream) (void)hipStreamDestroy(c.stream);
     return status;
+}
+
+int mph_dist_info(const MphCtx* c, int* out8)
+{
+    if (!c || !out8) return MPH_ERR_ARG;
+    std::memset(out8, 0, 8 * sizeof(int));
+    if (!c->dist) {
+        out8[0] = 1;
+        return MPH_OK;
+    }
+    const MphDist& D = *c->dist;
+    int count = D.nranks;
+    if (D.rccl && D.comm && ncclCommCount((ncclComm_t)D.comm, &count) != ncclSuccess) count = -1;
+    out8[0] = count;
+    out8[1] = D.rank;
+    out8[2] = D.rccl ? 1 : 0;
+    out8[3] = D.graphs ? 1 : 0;
+    out8[4] = D.cap;
+    out8[5] = std::max(D.cap_sl, D.cap_sr);
+    out8[6] = std::max(D.cap_rl, D.cap_rr);
+    out8[7] = c->n;
+    return MPH_OK;
 }
 
 int mph_owned_count(const MphCtx* c)

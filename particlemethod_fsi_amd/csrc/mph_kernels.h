@@ -108,14 +108,19 @@ struct HaloFields {
 };
 void launch_scan(int* cnt, int ncell, int* bsum, int* start, int total, hipStream_t stream, Profiler* prof);
 int dist_blocks(int n);
-void launch_dist_classify(const Launch& L, const SlabGeom& g, int n, int move, int* cls, int* bcnt);
-void launch_dist_scatter(const Launch& L, int n, const int* cls, const int* boff, const Soa& C, int* dseg);
-void launch_dist_counts(const Launch& L, const int* dseg, int* cnt_send);
-void launch_dist_pack(const Launch& L, const Soa& C, int off, int m, char* buf);
-void launch_dist_unpack(const Launch& L, const char* buf, int m, const Soa& C, int off);
-void launch_halo_pack(const Launch& L, const int* dst_of, int o1, int n1, int o2, int n2, const HaloFields& F,
-                      double* buf);
-void launch_halo_unpack(const Launch& L, const double* buf, const int* dst_of, int o1, int n1, int o2, int n2,
-                        const HaloFields& F);
+// slab redistribution; every size is read from the device layout (graph-capturable).  cap = local
+// array capacity, cap_msg = capacity (particles) of the message of that side.
+void launch_dist_classify(const Launch& L, const SlabGeom& g, int cap, const DistLayout* lay, int move, int* cls,
+                          int* bcnt);
+void launch_dist_scatter(const Launch& L, int cap, const DistLayout* lay, const int* cls, const int* boff,
+                         const Soa& C, int* dseg);
+void launch_dist_counts(const Launch& L, DistLayout* lay);
+void launch_dist_pack(const Launch& L, const Soa& C, DistLayout* lay, int side, int cap_msg, char* buf);
+void launch_dist_unpack(const Launch& L, const char* buf, DistLayout* lay, int side, int cap_msg, int cap,
+                        const Soa& C);
+void launch_halo_pack(const Launch& L, const int* dst_of, const DistLayout* lay, int dir, int cap,
+                      const HaloFields& F, double* buf);
+void launch_halo_unpack(const Launch& L, const double* buf, const int* dst_of, const DistLayout* lay, int dir,
+                        int cap, const HaloFields& F);
 
 }  // namespace mph

@@ -166,6 +166,14 @@ __device__ __forceinline__ int xcd_block(int b, int nb)
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
 }
 
+// Particles held by this context: exact on a single GPU; in slab mode the device-resident count
+// of the last redistribution (P.n is then only the capacity the grids are sized for).
+__device__ __forceinline__ int dev_n(const DevParams& P) { return P.n_dev ? *P.n_dev : P.n; }
+
+// Blocks of 256 that hold live particles; the rest of a capacity-sized grid exits at once.  The
+// XCD remap runs over the live blocks only, so the work stays spread over all 8 XCDs.
+__device__ __forceinline__ int live_blocks(int n) { return (n + 255) >> 8; }
+
 __device__ __forceinline__ int nbr_entry(int j, int type) { return j | (type << kTypeShift); }
 
 // The ELL list is written once per step and read once per pass.  MPH_LIST_NT=1 makes the pass
@@ -266,11 +274,12 @@ __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __res
                                               int* __restrict__ cnt, int mode)
 {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int n = dev_n(P);
     if (MPH_PREP_RUNS) {
         // The particles arrive in the previous cell order, so consecutive lanes often share a
         // cell: one histogram atomic per run of equal keys (slot = run base + rank in the run).
         // Every lane of the wave takes part in the shuffles; lanes past n form runs of their own.
-        const bool live = p < P.n;
+        const bool live = p < n;
         int k = -1 - (int)(threadIdx.x & 63);
         if (live) {
             double x = B.x[p], y = B.y[p], z = B.z[p];
@@ -293,7 +302,7 @@ __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __res
         if (live) slot[p] = base + (lane - hl);
         return;
     }
-    if (p >= P.n) return;
+    if (p >= n) return;
     double x = B.x[p], y = B.y[p], z = B.z[p];
     if (mode == 1) move_and_wrap(P, st, B, p, x, y, z);
     if (!isfinite(x + y + z)) atomicOr(const_cast<int*>(&st->overflow), 4);   // MPH_ERR_NONFINITE
@@ -384,7 +393,8 @@ __global__ __launch_bounds__(1024) void k_scan_top(int* __restrict__ bsum, int n
 
 __global__ __launch_bounds__(kScanThreads) void k_scan_down(int* __restrict__ cnt, int ncell,
                                                             const int* __restrict__ bsum,
-                                                            int* __restrict__ start, int n)
+                                                            int* __restrict__ start, int n,
+                                                            const int* __restrict__ n_dev)
 {
     __shared__ int lds[kScanThreads / 64];
     const int base = blockIdx.x * kScanBlock + threadIdx.x * kScanItems;
@@ -419,7 +429,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_down(int* __restrict__ cn
                 if (v[k] != 0) cnt[base + k] = 0;
             }
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) start[ncell] = n;
+    if (blockIdx.x == 0 && threadIdx.x == 0) start[ncell] = n_dev ? *n_dev : n;
 }
 
 // Unordered placement; block 0 also advances Time and WallCenter (main.cpp:685, 3066-3070)
@@ -438,7 +448,7 @@ __global__ __launch_bounds__(256) void k_place(DevParams P, DevState* __restrict
             st->time += P.dt;
         }
     }
-    if (p >= P.n) return;
+    if (p >= dev_n(P)) return;
     tmp[start[key[p]] + slot[p]] = p;
 }
 
@@ -450,7 +460,7 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
                                                       int* __restrict__ rank_of, int* __restrict__ dst_of)
 {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= P.n) return;
+    if (p >= dev_n(P)) return;
     const int k = key[p];
     const int s = start[k], e = start[k + 1];
     int r = 0;
@@ -862,9 +872,11 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int
                                                    int* __restrict__ nbr, int* __restrict__ ncount,
                                                    DevState* __restrict__ st)
 {
-    const int i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    const bool live = i < P.n;
-    const int ii = live ? i : P.n - 1;
+    const int n = dev_n(P);
+    if ((int)blockIdx.x >= live_blocks(n)) return;
+    const int i = xcd_block(blockIdx.x, live_blocks(n)) * blockDim.x + threadIdx.x;
+    const bool live = i < n;
+    const int ii = live ? i : n - 1;
     const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
     const bool fast = wave_interior(P, live, xi, yi, zi);
     int cnt = 0;
@@ -914,7 +926,7 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
             const int e = list_load(row + (k0 + u < cnt ? k0 + u : cnt - 1) * kTile);
             jj[u] = e & kIndexMask;
             TT[u] = e >> kTypeShift;
-            if (MPH_DIAG_GATHER == 1) jj[u] = min((int)(blockIdx.x * blockDim.x + threadIdx.x) ^ 1, P.n - 1);
+            if (MPH_DIAG_GATHER == 1) jj[u] = min((int)(blockIdx.x * blockDim.x + threadIdx.x) ^ 1, dev_n(P) - 1);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -954,6 +966,8 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
                                                 const int* __restrict__ nbr,
                                                 const int* __restrict__ ncount, PassAOut pout)
 {
+    const int n = dev_n(P);
+    if ((int)blockIdx.x >= live_blocks(n)) return;
     __shared__ double s_ratio[kTypes * kTypes];
     __shared__ double s_mu[kTypes * kTypes];
     if (threadIdx.x < kTypes * kTypes) {
@@ -961,9 +975,9 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
         s_mu[threadIdx.x] = T->mu_ij[threadIdx.x];
     }
     __syncthreads();
-    const int i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    const bool live = i < P.n;
-    const int ii = live ? i : P.n - 1;
+    const int i = xcd_block(blockIdx.x, live_blocks(n)) * blockDim.x + threadIdx.x;
+    const bool live = i < n;
+    const int ii = live ? i : n - 1;
     const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
     const bool fast = wave_interior(P, live, xi, yi, zi);
     if (!live) return;
@@ -1016,7 +1030,7 @@ __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_
             const int e = list_load(row + (k0 + u < cnt ? k0 + u : cnt - 1) * kTile);
             jj[u] = e & kIndexMask;
             TT[u] = e >> kTypeShift;
-            if (MPH_DIAG_GATHER == 1) jj[u] = min((int)(blockIdx.x * blockDim.x + threadIdx.x) ^ 1, P.n - 1);
+            if (MPH_DIAG_GATHER == 1) jj[u] = min((int)(blockIdx.x * blockDim.x + threadIdx.x) ^ 1, dev_n(P) - 1);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1101,15 +1115,17 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
                                                 double4* __restrict__ force, double4* __restrict__ acc,
                                                 Soa B, int phase, StructHook H)
 {
+    const int n = dev_n(P);
+    if ((int)blockIdx.x >= live_blocks(n)) return;
     __shared__ double s_ratio[kTypes * kTypes];
     if (SURF) {
         if (threadIdx.x < kTypes * kTypes) s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
         __syncthreads();
     }
-    const int i = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    const int ii = i < P.n ? i : P.n - 1;
+    const int i = xcd_block(blockIdx.x, live_blocks(n)) * blockDim.x + threadIdx.x;
+    const int ii = i < n ? i : n - 1;
     const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
-    bool live = i < P.n;
+    bool live = i < n;
     if (phase) {
         // slab mode: phase 1 = particles whose neighbours are all owned (run while the halo of
         // pass-A values is in flight), phase 2 = the rest (after the halo arrived)
@@ -1518,11 +1534,12 @@ __global__ __launch_bounds__(256) void k_struct_velocity(DevParams P, int ns, in
 __device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << (threadIdx.x & 63)) - 1ull; }
 
 __global__ __launch_bounds__(256) void k_dist_classify(DevParams P, DevState* __restrict__ st, SlabGeom g,
-                                                       Soa B, int n, int move, int* __restrict__ cls,
-                                                       int* __restrict__ bcnt, int nb)
+                                                       Soa B, const DistLayout* __restrict__ lay, int move,
+                                                       int* __restrict__ cls, int* __restrict__ bcnt, int nb)
 {
     __shared__ int wc[4][kSlabClasses];
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int n = lay->n;   // entries of B: the previous redistribution's count
     int c = -1;
     if (p < n) {
         if (B.id[p] < 0) {
@@ -1553,12 +1570,14 @@ __global__ __launch_bounds__(256) void k_dist_classify(DevParams P, DevState* __
     }
 }
 
-__global__ __launch_bounds__(256) void k_dist_scatter(Soa B, int n, const int* __restrict__ cls,
+__global__ __launch_bounds__(256) void k_dist_scatter(Soa B, const DistLayout* __restrict__ lay,
+                                                      const int* __restrict__ cls,
                                                       const int* __restrict__ boff, int nb, Soa C,
                                                       int* __restrict__ dseg)
 {
     __shared__ int wc[4][kSlabClasses];
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int n = lay->n;
     const int c = p < n ? cls[p] : -1;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int rank = 0;
@@ -1581,19 +1600,46 @@ __global__ __launch_bounds__(256) void k_dist_scatter(Soa B, int n, const int* _
 }
 
 // count messages from the segment starts: left-going {bandL, migL}, right-going {migR, bandR}
-__global__ void k_dist_counts(const int* __restrict__ dseg, int* __restrict__ cnt_send)
+__global__ void k_dist_counts(DistLayout* __restrict__ lay)
 {
     if (threadIdx.x != 0) return;
-    cnt_send[0] = dseg[kBandL + 1] - dseg[kBandL];
-    cnt_send[1] = dseg[kMigL + 1] - dseg[kMigL];
-    cnt_send[2] = dseg[kMigR + 1] - dseg[kMigR];
-    cnt_send[3] = dseg[kBandR + 1] - dseg[kBandR];
+    const int* seg = lay->seg;
+    lay->send[0] = seg[kBandL + 1] - seg[kBandL];
+    lay->send[1] = seg[kMigL + 1] - seg[kMigL];
+    lay->send[2] = seg[kMigR + 1] - seg[kMigR];
+    lay->send[3] = seg[kBandR + 1] - seg[kBandR];
+}
+
+// Messages of a redistribution travel with a fixed capacity (so the exchange has host-known
+// sizes and can sit inside a captured graph); the live counts are the 2-int count messages.
+// side 0: [bandL | migL] to the left, side 1: [migR | bandR] to the right.
+__device__ __forceinline__ void dist_send_range(const DistLayout* lay, int side, int& off, int& m)
+{
+    off = side == 0 ? lay->seg[kBandL] : lay->seg[kMigR];
+    m = side == 0 ? lay->send[0] + lay->send[1] : lay->send[2] + lay->send[3];
+}
+
+// side 0: from the left (their {migR, bandR}) appended at nc, side 1: from the right after it
+__device__ __forceinline__ void dist_recv_range(const DistLayout* lay, int side, int& off, int& m)
+{
+    const int nc = lay->seg[kSlabDrop];
+    const int fl = lay->recv[0] + lay->recv[1];
+    off = side == 0 ? nc : nc + fl;
+    m = side == 0 ? fl : lay->recv[2] + lay->recv[3];
 }
 
 // message layout: x[m] y[m] z[m] vx[m] vy[m] vz[m] (double) type[m] id[m] (int) = 56 B/particle
-__global__ __launch_bounds__(256) void k_dist_pack(Soa C, int off, int m, char* __restrict__ buf)
+__global__ __launch_bounds__(256) void k_dist_pack(Soa C, DistLayout* __restrict__ lay, int side, int cap,
+                                                   DevState* __restrict__ st, char* __restrict__ buf)
 {
+    int off, m;
+    dist_send_range(lay, side, off, m);
+    if (m > cap) {   // more than the message capacity: an error (MPH_ERR_CAPACITY), never a fault
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&st->overflow, 8);
+        m = cap;
+    }
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicMax(&lay->hw[side], m);
     if (k >= m) return;
     double* d = (double*)buf;
     int* q = (int*)(d + 6 * (size_t)m);
@@ -1605,18 +1651,40 @@ __global__ __launch_bounds__(256) void k_dist_pack(Soa C, int off, int m, char* 
 }
 
 // received message -> C[off, off+m); ownership flips (their migrants are ours, their band
-// particles are our ghosts): id -> -1-id for every entry.
-__global__ __launch_bounds__(256) void k_dist_unpack(const char* __restrict__ buf, int m, Soa C, int off)
+// particles are our ghosts): id -> -1-id for every entry.  The right-hand message completes the
+// layout: n = kept + received, n_own = the kept owned classes + the received migrants.
+__global__ __launch_bounds__(256) void k_dist_unpack(const char* __restrict__ buf, DistLayout* __restrict__ lay,
+                                                     int side, int cap_msg, int cap, DevState* __restrict__ st,
+                                                     Soa C)
 {
+    int off, m;
+    dist_recv_range(lay, side, off, m);
+    const int mm = m;   // the sender's count = the stride of its message
+    const bool first = blockIdx.x == 0 && threadIdx.x == 0;
+    if (mm > cap_msg || off + m > cap) {   // the sender flagged it too; read nothing out of range
+        if (first) atomicOr(&st->overflow, 8);
+        m = mm > cap_msg ? 0 : max(0, min(m, cap - off));
+    }
+    if (first) {
+        atomicMax(&lay->hw[2 + side], mm);
+        if (side == 1) {
+            const int* seg = lay->seg;
+            const int n = min(off + m, cap);
+            lay->n = n;
+            lay->n_own = (seg[kBandR + 1] - seg[kBandR]) + (seg[kInner + 1] - seg[kInner]) +
+                         (seg[kBandL + 1] - seg[kBandL]) + lay->recv[0] + lay->recv[3];
+            atomicMax(&lay->hw[4], off + (lay->recv[2] + lay->recv[3]));
+        }
+    }
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= m) return;
     const double* d = (const double*)buf;
-    const int* q = (const int*)(d + 6 * (size_t)m);
+    const int* q = (const int*)(d + 6 * (size_t)mm);
     const int s = off + k;
-    C.x[s] = d[k]; C.y[s] = d[m + k]; C.z[s] = d[2 * m + k];
-    C.vx[s] = d[3 * m + k]; C.vy[s] = d[4 * m + k]; C.vz[s] = d[5 * m + k];
+    C.x[s] = d[k]; C.y[s] = d[mm + k]; C.z[s] = d[2 * mm + k];
+    C.vx[s] = d[3 * mm + k]; C.vy[s] = d[4 * mm + k]; C.vz[s] = d[5 * mm + k];
     C.type[s] = q[k];
-    C.id[s] = -1 - q[m + k];
+    C.id[s] = -1 - q[mm + k];
 }
 
 // Elastic ghost slots (slab mode): w double4 rows per slot, slot k of the message = idx[k].
@@ -1640,22 +1708,43 @@ __global__ __launch_bounds__(256) void k_struct_unpack(const double4* __restrict
     dst[(size_t)idx[k] * w + r] = buf[t];
 }
 
-// pass-A values of two C-index ranges, read at their sorted position dst_of[c]
-__global__ __launch_bounds__(256) void k_halo_pack(const int* __restrict__ dst_of, int o1, int n1, int o2,
-                                                   int n2, HaloFields F, double* __restrict__ buf)
+// C-index ranges of the pass-A halo (mph_dist.hip step 5), from the device layout: dir 0 = to the
+// left [the left neighbour's migrants we now own | our band-left], 1 = to the right [the right
+// neighbour's migrants we now own | our band-right], 2 = from the left [our migrants that went
+// left | the left neighbour's band-right ghosts], 3 = from the right (mirror image).
+__device__ __forceinline__ void halo_ranges(const DistLayout* L, int dir, int& o1, int& n1, int& o2, int& n2)
 {
+    const int* seg = L->seg;
+    const int nc = seg[kSlabDrop];
+    const int fl = L->recv[0] + L->recv[1];
+    if (dir == 0) { o1 = nc; n1 = L->recv[0]; o2 = seg[kBandL]; n2 = seg[kBandL + 1] - seg[kBandL]; }
+    else if (dir == 1) { o1 = nc + fl + L->recv[2]; n1 = L->recv[3]; o2 = seg[kBandR]; n2 = seg[kBandR + 1] - seg[kBandR]; }
+    else if (dir == 2) { o1 = seg[kMigL]; n1 = seg[kMigL + 1] - seg[kMigL]; o2 = nc + L->recv[0]; n2 = L->recv[1]; }
+    else { o1 = seg[kMigR]; n1 = seg[kMigR + 1] - seg[kMigR]; o2 = nc + fl; n2 = L->recv[2]; }
+}
+
+// pass-A values of two C-index ranges, read at their sorted position dst_of[c]; cap bounds the
+// message (the counts are within it once the redistribution's capacity checks passed)
+__global__ __launch_bounds__(256) void k_halo_pack(const int* __restrict__ dst_of, const DistLayout* __restrict__ lay,
+                                                   int dir, int cap, HaloFields F, double* __restrict__ buf)
+{
+    int o1, n1, o2, n2;
+    halo_ranges(lay, dir, o1, n1, o2, n2);
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    const int m = n1 + n2;
+    const int m = min(n1 + n2, cap);
     if (k >= m) return;
     const int a = dst_of[k < n1 ? o1 + k : o2 + (k - n1)];
     for (int f = 0; f < F.nf; ++f) buf[(size_t)f * m + k] = F.f[f][a];
 }
 
 __global__ __launch_bounds__(256) void k_halo_unpack(const double* __restrict__ buf, const int* __restrict__ dst_of,
-                                                     int o1, int n1, int o2, int n2, HaloFields F)
+                                                     const DistLayout* __restrict__ lay, int dir, int cap,
+                                                     HaloFields F)
 {
+    int o1, n1, o2, n2;
+    halo_ranges(lay, dir, o1, n1, o2, n2);
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    const int m = n1 + n2;
+    const int m = min(n1 + n2, cap);
     if (k >= m) return;
     const int a = dst_of[k < n1 ? o1 + k : o2 + (k - n1)];
     for (int f = 0; f < F.nf; ++f) F.f[f][a] = buf[(size_t)f * m + k];
@@ -1699,7 +1788,7 @@ void launch_sort(const Launch& L, int mode)
                P.ncell, L.bsum);
     MPH_LAUNCH("scan_top", L.stream, k_scan_top, dim3(1), dim3(1024), 0, L.stream, L.bsum, nb);
     MPH_LAUNCH("scan_down", L.stream, k_scan_down, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt,
-               P.ncell, L.bsum, L.start, n);
+               P.ncell, L.bsum, L.start, n, P.n_dev);
     MPH_LAUNCH("place", L.stream, k_place, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.key,
                L.slot, L.start, L.tmp, mode);
     MPH_LAUNCH("rank_scatter", L.stream, k_rank_scatter, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P,
@@ -1845,64 +1934,64 @@ void launch_scan(int* cnt, int ncell, int* bsum, int* start, int total, hipStrea
     MPH_LAUNCH("scan_reduce", stream, k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, stream, cnt, ncell, bsum);
     MPH_LAUNCH("scan_top", stream, k_scan_top, dim3(1), dim3(1024), 0, stream, bsum, nb);
     MPH_LAUNCH("scan_down", stream, k_scan_down, dim3(nb), dim3(kScanThreads), 0, stream, cnt, ncell, bsum,
-               start, total);
+               start, total, (const int*)nullptr);
 }
 
 int dist_blocks(int n) { return blocks(n > 0 ? n : 1, 256); }
 
-void launch_dist_classify(const Launch& L, const SlabGeom& g, int n, int move, int* cls, int* bcnt)
+void launch_dist_classify(const Launch& L, const SlabGeom& g, int cap, const DistLayout* lay, int move, int* cls,
+                          int* bcnt)
 {
     Profiler* prof = L.prof;
-    const int nb = dist_blocks(n);
+    const int nb = dist_blocks(cap);
     MPH_LAUNCH("dist_classify", L.stream, k_dist_classify, dim3(nb), dim3(256), 0, L.stream, *L.P, L.st, g,
-               L.B, n, move, cls, bcnt, nb);
+               L.B, lay, move, cls, bcnt, nb);
 }
 
-void launch_dist_scatter(const Launch& L, int n, const int* cls, const int* boff, const Soa& C, int* dseg)
+void launch_dist_scatter(const Launch& L, int cap, const DistLayout* lay, const int* cls, const int* boff,
+                         const Soa& C, int* dseg)
 {
     Profiler* prof = L.prof;
-    const int nb = dist_blocks(n);
-    MPH_LAUNCH("dist_scatter", L.stream, k_dist_scatter, dim3(nb), dim3(256), 0, L.stream, L.B, n, cls, boff,
+    const int nb = dist_blocks(cap);
+    MPH_LAUNCH("dist_scatter", L.stream, k_dist_scatter, dim3(nb), dim3(256), 0, L.stream, L.B, lay, cls, boff,
                nb, C, dseg);
 }
 
-void launch_dist_counts(const Launch& L, const int* dseg, int* cnt_send)
+void launch_dist_counts(const Launch& L, DistLayout* lay)
 {
     Profiler* prof = L.prof;
-    MPH_LAUNCH("dist_counts", L.stream, k_dist_counts, dim3(1), dim3(64), 0, L.stream, dseg, cnt_send);
+    MPH_LAUNCH("dist_counts", L.stream, k_dist_counts, dim3(1), dim3(64), 0, L.stream, lay);
 }
 
-void launch_dist_pack(const Launch& L, const Soa& C, int off, int m, char* buf)
+void launch_dist_pack(const Launch& L, const Soa& C, DistLayout* lay, int side, int cap_msg, char* buf)
 {
     Profiler* prof = L.prof;
-    if (m <= 0) return;
-    MPH_LAUNCH("dist_pack", L.stream, k_dist_pack, dim3(blocks(m, 256)), dim3(256), 0, L.stream, C, off, m, buf);
+    MPH_LAUNCH("dist_pack", L.stream, k_dist_pack, dim3(dist_blocks(cap_msg)), dim3(256), 0, L.stream, C, lay,
+               side, cap_msg, L.st, buf);
 }
 
-void launch_dist_unpack(const Launch& L, const char* buf, int m, const Soa& C, int off)
+void launch_dist_unpack(const Launch& L, const char* buf, DistLayout* lay, int side, int cap_msg, int cap,
+                        const Soa& C)
 {
     Profiler* prof = L.prof;
-    if (m <= 0) return;
-    MPH_LAUNCH("dist_unpack", L.stream, k_dist_unpack, dim3(blocks(m, 256)), dim3(256), 0, L.stream, buf, m, C,
-               off);
+    MPH_LAUNCH("dist_unpack", L.stream, k_dist_unpack, dim3(dist_blocks(cap_msg)), dim3(256), 0, L.stream, buf,
+               lay, side, cap_msg, cap, L.st, C);
 }
 
-void launch_halo_pack(const Launch& L, const int* dst_of, int o1, int n1, int o2, int n2, const HaloFields& F,
-                      double* buf)
+void launch_halo_pack(const Launch& L, const int* dst_of, const DistLayout* lay, int dir, int cap,
+                      const HaloFields& F, double* buf)
 {
     Profiler* prof = L.prof;
-    if (n1 + n2 <= 0) return;
-    MPH_LAUNCH("halo_pack", L.stream, k_halo_pack, dim3(blocks(n1 + n2, 256)), dim3(256), 0, L.stream, dst_of,
-               o1, n1, o2, n2, F, buf);
+    MPH_LAUNCH("halo_pack", L.stream, k_halo_pack, dim3(dist_blocks(cap)), dim3(256), 0, L.stream, dst_of, lay,
+               dir, cap, F, buf);
 }
 
-void launch_halo_unpack(const Launch& L, const double* buf, const int* dst_of, int o1, int n1, int o2, int n2,
-                        const HaloFields& F)
+void launch_halo_unpack(const Launch& L, const double* buf, const int* dst_of, const DistLayout* lay, int dir,
+                        int cap, const HaloFields& F)
 {
     Profiler* prof = L.prof;
-    if (n1 + n2 <= 0) return;
-    MPH_LAUNCH("halo_unpack", L.stream, k_halo_unpack, dim3(blocks(n1 + n2, 256)), dim3(256), 0, L.stream, buf,
-               dst_of, o1, n1, o2, n2, F);
+    MPH_LAUNCH("halo_unpack", L.stream, k_halo_unpack, dim3(dist_blocks(cap)), dim3(256), 0, L.stream, buf,
+               dst_of, lay, dir, cap, F);
 }
 
 }  // namespace mph

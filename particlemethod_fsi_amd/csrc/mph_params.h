@@ -26,7 +26,10 @@ inline bool is_wall(int t) { return t >= 4 && t < 6; }    // main.cpp:73-74
 // (main.cpp:1191-1469), in the reference's own arithmetic, plus what the GPU path precomputes.
 // Passed by value as a kernel argument (kernarg segment -> scalar loads).
 struct DevParams {
-    int n;             // particles held by this context
+    int n;             // particles held by this context (slab mode: the array capacity, a bound)
+    // slab mode: the device-resident particle count (DistLayout.n), which the kernels read so
+    // that a step needs no host round trip for sizes; null on a single GPU (n is exact)
+    const int* n_dev;
     int dim;           // 2 or 3
     int module;        // MphModule
     int wall_motion;   // MphWallMotion
@@ -135,6 +138,20 @@ MPH_HD inline int slab_class_static(const SlabGeom& g, double c)
     if (dr <= g.h) return kBandR;
     return kInner;
 }
+
+// Device-resident sizes of one slab redistribution (mph_dist.hip), written by the kernels of the
+// step itself, so that a whole step -- RCCL calls included -- can be captured into a hipGraph.
+// send/recv double as the count messages of the exchange (2 ints to each neighbour).
+struct DistLayout {
+    int n;                        // local particles (owned + ghosts) after the last redistribution
+    int n_own;
+    int seg[kSlabClasses + 1];    // class segment starts in C (k_dist_scatter)
+    int send[4];                  // to the left {bandL, migL}, to the right {migR, bandR}
+    int recv[4];                  // from the left their {migR, bandR}, from the right their {bandL, migL}
+    int hw[5];                    // high-water marks since the last reset: send_l, send_r, recv_l,
+                                  // recv_r, n (capacity tuning between step batches)
+    int pad;
+};
 
 // Per-type tables read with per-lane type indices (device memory; staged through LDS where hot).
 struct DevTables {

@@ -55,7 +55,7 @@ EXPORTED_SYMBOLS = [
     "mph_slab_owner", "mph_dist_selftest", "mph_compute_virial",
     "mph_config_sizeof", "mph_write_vtk_async", "mph_output_wait", "mph_write_grid_binary",
     "mph_write_vtu_arrays", "mph_write_vtu", "mph_velocity_profile_arrays",
-    "mph_set_initial_velocity_profile",
+    "mph_set_initial_velocity_profile", "mph_dist_info",
 ]
 
 # mph_host_exchange_fn (include/mph_gpu.h): (user, send_l, n, send_r, n, recv_l, n, recv_r, n)
@@ -134,6 +134,7 @@ def load_library() -> ctypes.CDLL:
         "mph_output_wait": (ip, [vp]),
         "mph_velocity_profile_arrays": (ip, [cfgp, dp, ip, vp, vp, vp, vp]),
         "mph_set_initial_velocity_profile": (ip, [vp]),
+        "mph_dist_info": (ip, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -360,6 +361,13 @@ class MphSolver:
         out = np.zeros(max(self.n, 1), np.int32)
         _check(self._L.mph_owned_ids(self._h, out.ctypes.data), self._h)
         return out[:k].copy()
+
+    def dist_info(self) -> dict:
+        """Slab-mode facts (mph_dist_info): communicator size, transport, graph replay, capacities."""
+        a = np.zeros(8, np.int32)
+        _check(self._L.mph_dist_info(self._h, a.ctypes.data), self._h)
+        keys = ["nranks", "rank", "rccl", "graphs", "cap", "cap_send", "cap_recv", "held"]
+        return {k: int(v) for k, v in zip(keys, a)}
 
     def compute_virial(self):
         """calculateVirialStressAtParticle (main.cpp:3077-3318) on the current state; read the result
