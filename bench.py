@@ -10,12 +10,15 @@ neighbour search, density/pressure sums, pressure/surface/viscous forces, gravit
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--case d1m] [--no-cpu-baseline]
 
-For N > 1 (torchrun, one rank per GPU) the ranks run the slab decomposition (z slabs, RCCL
-halo exchange; csrc/mph_dist.hip) of the D1M tank extended N-fold along z, so the per-GPU work
-stays about one D1M (weak scaling); `value` counts every particle of the whole job per step.
-Other cases (`--case bar2d_400k`, `fsi3d`, ...) split the same problem over the N ranks (strong
-scaling; 2-D cases in x slabs, 3-D in z slabs; elastic particles stay with the slab of their
-InitialPosition).
+For N > 1 (torchrun, one rank per GPU) the ranks run BASELINE configs[4]: the 16,205,500-particle
+dam break cut into N z slabs (csrc/mph_dist.hip: RCCL ncclSend/Recv with the two
+slab neighbours, steps replayed from captured hipGraphs), strong scaling; `value` counts every
+particle of the whole job per step.  Each rank generates only its own window of the problem
+(slab-local creation).  Other cases (`--case bar2d_400k`, `fsi3d`, `d1m_x8` ...) split the same
+way (2-D cases in x slabs, 3-D in z slabs; elastic particles stay with the slab of their
+InitialPosition).  After the timed steps the ranks check that ownership is a partition of all
+particles and that the NeighborCount total matches the single-GPU run's at the same step
+(profiles/d16m_ncount_sum.json), so a scaling run is also a correctness run.
 MPH_SLAB_TRANSPORT=host switches the halo transport to host staging over gloo (diagnostics).
 
 Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel's algorithmic HBM bytes per
@@ -110,6 +113,54 @@ def load_pmc(name: str, case: str, kernel: str, key: str):
     return d.get(kernel, {}).get(key)
 
 
+def _id_hash(ids):
+    """xor of a 64-bit mix of every id (order-free fingerprint of an id set)."""
+    import numpy as np
+    x = ids.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+    x ^= x >> np.uint64(29)
+    x *= np.uint64(0xBF58476D1CE4E5B9)
+    x ^= x >> np.uint64(32)
+    return int(np.bitwise_xor.reduce(x)) if len(x) else 0
+
+
+def slab_checks(solver, dist, n_total, case_name, steps_done):
+    """After a multi-rank run: RCCL communicator size, graph replay, ownership a partition of all
+    particles (count, id sum, id-set fingerprint), and the NeighborCount total over the owned
+    particles against the single-GPU run's at the same step (bit-exact neighbour sets)."""
+    import numpy as np
+    import torch
+    info = solver.dist_info()
+    ids = solver.owned_ids()
+    nc = solver.get("NeighborCount")[ids]
+    loc = torch.tensor([len(ids), int(ids.astype(np.int64).sum()), int(nc.astype(np.int64).sum()),
+                        int(nc.max()) if len(nc) else 0], dtype=torch.int64)
+    tot = loc.clone()
+    dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    mx = loc[3:4].clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    hashes = [None] * dist.get_world_size()
+    dist.all_gather_object(hashes, _id_hash(ids))
+    h = 0
+    for v in hashes:
+        h ^= v
+    partition = (int(tot[0]) == n_total and int(tot[1]) == n_total * (n_total - 1) // 2
+                 and h == _id_hash(np.arange(n_total)))
+    expected = None
+    try:
+        with open(os.path.join(ROOT, "profiles", "%s_ncount_sum.json" % case_name)) as fh:
+            table = json.load(fh)["sum_after_steps"]
+        if steps_done < len(table):
+            expected = int(table[steps_done])
+    except (OSError, ValueError, KeyError):
+        pass
+    return {"rccl_nranks": info["nranks"], "transport": "rccl" if info["rccl"] else "host-staged",
+            "graphs": bool(info["graphs"]), "partition_ok": bool(partition), "owned_total": int(tot[0]),
+            "steps_done": steps_done, "neighbor_count_sum": int(tot[2]),
+            "neighbor_count_sum_single_gpu": expected,
+            "neighbor_count_ok": (expected == int(tot[2])) if expected is not None else None,
+            "neighbor_count_max": int(mx[0])}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -128,25 +179,28 @@ def main():
     case_name = args.case
     if world > 1:
         # one process per GPU; torch.distributed (gloo) is only the control plane (rendezvous,
-        # RCCL unique id, timing reduction).  Particle data moves over the library's own RCCL
-        # communicator (ncclSend/Recv with the two slab neighbours, csrc/mph_dist.hip).
+        # RCCL unique id, timing reduction, the post-run checks).  Particle data moves over the
+        # library's own RCCL communicator (ncclSend/Recv with the two slab neighbours).
         import torch
         import torch.distributed as tdist
         torch.cuda.set_device(device)
         tdist.init_process_group("gloo")
         dist = tdist
         if case_name == "d1m":
-            case_name = "d1m_x%d" % world
+            case_name = "d16m"   # BASELINE configs[4]: 16M particles, N MI355X, z slabs
 
     case = cases.get(case_name)
-    cfg, parts = case.build()
-    n_total = parts.n
     if dist is not None:
-        from particlemethod_fsi_amd.dist import gloo_slab, rccl_slab
+        from particlemethod_fsi_amd.dist import build_local, gloo_slab, rccl_slab
+        axis = SLAB_AXIS[case.dim]
+        cfg, parts, ids, n_total = build_local(case, rank, world, axis)
         mk = gloo_slab if os.environ.get("MPH_SLAB_TRANSPORT") == "host" else rccl_slab
-        solver = MphSolver(cfg, parts, device=device, slab=mk(rank, world, SLAB_AXIS[case.dim]))
+        solver = MphSolver(cfg, parts, device=device, slab=mk(rank, world, axis, ids=ids, n_glob=n_total))
+        del parts, ids
         n_local = len(solver.owned_ids())
     else:
+        cfg, parts = case.build()
+        n_total = parts.n
         solver = MphSolver(cfg, parts, device=device)
         n_local = n_total
 
@@ -172,6 +226,9 @@ def main():
 
     mean_nb, max_nb = solver.neighbor_stats()
     prof = solver.profile(args.profile_steps)
+    checks = None
+    if dist is not None:
+        checks = slab_checks(solver, dist, n_total, case_name, args.warmup + args.steps + args.profile_steps)
     ns, mean_ns = 0, 0.0
     if any(k in prof for k in STRUCT_BYTES):
         isnc = solver.get("InitialStructureNeighborCount")
@@ -207,7 +264,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "weak" if world == 1 or case_name != args.case else "strong",
+        "scaling": "weak" if world == 1 else "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (reference generator algorithm + results/Dam/dam.data parameters)",
@@ -229,6 +286,8 @@ def main():
         "kernels_ms": {k: round(v["avg_ms"], 5) for k, v in prof.items()},
         "profiled_step_ms": step_ms,
     }
+    if checks is not None:
+        out["slab"] = checks
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.case)
     solver.close()

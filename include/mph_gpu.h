@@ -299,6 +299,26 @@ typedef int (*mph_host_exchange_fn)(void* user, const void* send_l, size_t bytes
 int mph_create_dist_host(MphCtx** ctx, const MphConfig* cfg, int n, const int* property,
                          const double* pos, const double* pos0, const double* vel, int device,
                          int rank, int nranks, int axis, mph_host_exchange_fn fn, void* user);
+/* General slab-mode constructor: the transport (RCCL unique id, or a host exchange callback) and,
+ * with n_glob > 0, slab-local creation -- the arrays hold only the n particles this rank needs,
+ * with their original indices ids[n] (ascending) among n_glob: every particle whose coordinate
+ * along the axis (Position; InitialPosition for elastic particles) lies within the window of
+ * mph_slab_window.  Others are not needed (ghosts arrive from the neighbours).  In slab-local mode
+ * mph_get returns the static inputs (Property, InitialPosition, Mass, ...) for the particles this
+ * rank was created with, and the state for the particles it owns.                             */
+typedef struct MphSlabOptions {
+    int rank, nranks, axis;
+    const char* unique_id128;          /* RCCL transport, or NULL and host_fn:                  */
+    mph_host_exchange_fn host_fn;      /* host-staged transport                                  */
+    void* host_user;
+    int n_glob;                        /* 0: the arrays hold every particle (n == n_glob)       */
+    const int* ids;
+} MphSlabOptions;
+int mph_create_slab(MphCtx** ctx, const MphConfig* cfg, int n, const int* property, const double* pos,
+                    const double* pos0, const double* vel, int device, const MphSlabOptions* opt);
+/* Host-only: the periodic window [lo, hi) (out2) along `axis` that rank `rank` of `nranks` needs
+ * at slab-local creation: its slab widened by two halo widths on each side.                   */
+int mph_slab_window(const MphConfig* cfg, int rank, int nranks, int axis, double* out2);
 /* One-rank RCCL communicator on `device` whose two neighbours are itself: checks that the
  * exchange delivers each message to the right buffer (the per-peer ordering nranks == 2 relies
  * on) without a second GPU.  Returns 0 on success.                                            */

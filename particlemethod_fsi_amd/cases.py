@@ -79,16 +79,28 @@ class Case:
 
     def build(self):
         """-> (MphConfig, Particles), exactly what the reference reads from data + grid files."""
+        cfg, _ = self._config()
+        return cfg, mphio.generate(self.cuboids)
+
+    def build_window(self, axis: int, lo: float, hi: float):
+        """-> (MphConfig, Particles, ids, n_glob): only the particles whose coordinate along `axis`
+        lies in the periodic window [lo, hi) (a slab rank's share, mph_slab_window), generated
+        without the rest of the problem; ids are their indices in build()'s order."""
+        cfg, _ = self._config()
+        W = cfg.domain_max[axis] - cfg.domain_min[axis]
+        parts, ids, n_glob = mphio.generate_window(self.cuboids, axis, lo, hi, cfg.domain_min[axis], W)
+        return cfg, parts, ids, n_glob
+
+    def _config(self):
         cfg = mphio.config_default(self.dim, self.module)
         _apply_data(cfg, self.data())
-        parts = mphio.generate(self.cuboids)
         cfg.wall_motion = self.wall_motion
         cfg.time = float("%f" % self.time0)
         cfg.particle_spacing = mphio._e(self.spacing)
         for d in range(3):
             cfg.domain_min[d] = mphio._e(self.lower[d])
             cfg.domain_max[d] = mphio._e(self.upper[d])
-        return cfg, parts
+        return cfg, None
 
     def grid_text(self) -> str:
         return mphio.format_grid(mphio.generate(self.cuboids), self.spacing, self.lower, self.upper,

@@ -62,11 +62,14 @@ struct MphCtx {
     bool stepped = false;
     hipStream_t stream = nullptr;
     hipGraphExec_t graph1 = nullptr, graph8 = nullptr;
-    // host copies (original order)
+    // host copies of the static inputs: original order, or -- slab-local creation -- the
+    // particles this rank was created with, whose original indices are gid (ascending)
     std::vector<int> prop;
     std::vector<double> pos0;
+    std::vector<int> gid;
     mph::StructureInit S;
     std::vector<int> sl_orig;    // local structure slot -> original particle index
+    std::vector<int> sl_s;       // local structure slot -> index into S (the lists built here)
     // device
     mph::DevTables* dT = nullptr;
     mph::DevState* dst = nullptr;
@@ -108,8 +111,12 @@ inline int stencil_margin(const DevParams& P, int d)
 int ctx_state_status(MphCtx* c, const DevState& hs);   // kernel error flags -> MphStatus
 
 void ctx_set_global_error(const std::string& msg);   // mph_last_error(NULL)
+// ids/n_glob: slab-local creation (the arrays hold n of n_glob particles, original indices ids)
 int ctx_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, const double* pos,
-               const double* pos0, const double* vel, int device, MphDist* dist);
+               const double* pos0, const double* vel, int device, MphDist* dist, const int* ids = nullptr,
+               int n_glob = 0);
+// original index of host input k (identity unless created slab-local)
+inline int glob_id(const MphCtx* c, int k) { return c->gid.empty() ? k : c->gid[k]; }
 
 // slab mode (mph_dist.hip)
 int dist_setup(MphCtx* c, const double* pos, std::vector<int>& owned);   // geometry + owned set

@@ -238,7 +238,7 @@ namespace mph {
 static thread_local std::string g_create_error;   // mph_last_error(NULL) after a failed create
 
 static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property, const double* pos,
-                    const double* pos0, const double* vel, int device)
+                    const double* pos0, const double* vel, int device, const int* ids, int n_glob)
 {
     if (cfg->dim != 2 && cfg->dim != 3) return MPH_ERR_ARG;
     if (cfg->module < 0 || cfg->module > MPH_MODULE_NONE) return MPH_ERR_ARG;
@@ -248,6 +248,14 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     c->cfg = *cfg;
     c->n = n;
     c->n_glob = n;
+    if (ids) {
+        if (!c->dist || n_glob < n) return MPH_ERR_ARG;
+        for (int i = 0; i < n; ++i)
+            if (ids[i] < 0 || ids[i] >= n_glob || (i > 0 && ids[i] <= ids[i - 1]))
+                return fail(c, MPH_ERR_ARG, "slab-local creation: ids must be ascending original indices below n_glob");
+        c->gid.assign(ids, ids + n);
+        c->n_glob = n_glob;
+    }
     c->device = device;
     c->time = cfg->time;
     HIP_OK(c, hipSetDevice(device));
@@ -345,16 +353,16 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         std::vector<int> sel(m);
         for (int i = 0; i < m; ++i) sel[i] = c->dist ? owned[i] : i;
         std::vector<double> comp(m);
-        std::vector<int> ids(m), types(m);
+        std::vector<int> gids(m), types(m);
         double* dstc[6] = {c->B.x, c->B.y, c->B.z, c->B.vx, c->B.vy, c->B.vz};
         for (int k = 0; k < 6; ++k) {
             const double* src = k < 3 ? pos : vel;
             for (int i = 0; i < m; ++i) comp[i] = src[3 * (size_t)sel[i] + (k % 3)];
             HIP_OK(c, hipMemcpy(dstc[k], comp.data(), sizeof(double) * m, hipMemcpyHostToDevice));
         }
-        for (int i = 0; i < m; ++i) { ids[i] = sel[i]; types[i] = property[sel[i]]; }
+        for (int i = 0; i < m; ++i) { gids[i] = glob_id(c, sel[i]); types[i] = property[sel[i]]; }
         HIP_OK(c, hipMemcpy(c->B.type, types.data(), sizeof(int) * m, hipMemcpyHostToDevice));
-        HIP_OK(c, hipMemcpy(c->B.id, ids.data(), sizeof(int) * m, hipMemcpyHostToDevice));
+        HIP_OK(c, hipMemcpy(c->B.id, gids.data(), sizeof(int) * m, hipMemcpyHostToDevice));
     }
     // elastic solid: local slots = [computed here | ghosts] (single GPU: every slot, no ghosts)
     if (ns > 0) {
@@ -373,7 +381,8 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         for (int k = 0; k < nl; ++k) loc[lsl[k]] = k;
         D.n_own = no;
         c->sl_orig.resize(nl);
-        for (int k = 0; k < nl; ++k) c->sl_orig[k] = S.orig[lsl[k]];
+        for (int k = 0; k < nl; ++k) c->sl_orig[k] = glob_id(c, S.orig[lsl[k]]);
+        c->sl_s.assign(lsl.begin(), lsl.begin() + no);
         // ELL tiles of the fixed out-list and of its transpose (StructDev), computed slots only
         const size_t ntile_s = ((size_t)std::max(no, 1) + 63) / 64;
         std::vector<int> ocnt(std::max(no, 1), 0), icnt(std::max(no, 1), 0);
@@ -494,7 +503,7 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
 void ctx_set_global_error(const std::string& msg) { g_create_error = msg; }
 
 int ctx_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, const double* pos,
-               const double* pos0, const double* vel, int device, MphDist* dist)
+               const double* pos0, const double* vel, int device, MphDist* dist, const int* ids, int n_glob)
 {
     g_create_error.clear();
     if (!out || !cfg || n < 0 || (n > 0 && (!property || !pos || !pos0 || !vel))) {
@@ -505,7 +514,7 @@ int ctx_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, c
     *out = nullptr;
     MphCtx* c = new MphCtx();
     c->dist = dist;
-    const int r = ctx_init(c, cfg, n, property, pos, pos0, vel, device);
+    const int r = ctx_init(c, cfg, n, property, pos, pos0, vel, device, ids, n_glob);
     if (r != MPH_OK) {
         g_create_error = c->err.empty() ? "mph_create failed with status " + std::to_string(r) : c->err;
         mph_destroy(c);
@@ -570,14 +579,20 @@ int mph_get(MphCtx* c, int field, void* out)
 {
     if (!c || !out) return MPH_ERR_ARG;
     HIP_OK(c, hipSetDevice(c->device));
-    const int n = c->n_glob;
     double* o = (double*)out;
     int* oi = (int*)out;
-    const int ns = (int)c->S.orig.size();
+    // structure rows: every list built here (single context), or the slots this rank computes
+    // (slab mode: its owned elastic particles; the lists of ghost slots are partial)
+    const int ns = c->dist ? (int)c->sl_s.size() : (int)c->S.orig.size();
+    auto sidx = [c](int k) { return c->dist ? c->sl_s[k] : k; };
+    // static inputs: every particle, or (slab-local creation) the ones this rank was created with
+    const int nin = (int)c->prop.size();
     switch (field) {
     case MPH_FIELD_POSITION: return download_soa3(c, c->B.x, c->B.y, c->B.z, c->B.id, o);
     case MPH_FIELD_VELOCITY: return download_soa3(c, c->B.vx, c->B.vy, c->B.vz, c->B.id, o);
-    case MPH_FIELD_INITIAL_POSITION: std::memcpy(o, c->pos0.data(), sizeof(double) * 3 * n); return MPH_OK;
+    case MPH_FIELD_INITIAL_POSITION:
+        for (int k = 0; k < nin; ++k) std::memcpy(o + 3 * (size_t)glob_id(c, k), &c->pos0[3 * (size_t)k], 3 * sizeof(double));
+        return MPH_OK;
     case MPH_FIELD_FORCE: return download_vec(c, c->force, c->A.id, o, 3);
     case MPH_FIELD_ACCELERATION: return download_vec(c, c->acc, c->A.id, o, 3);
     case MPH_FIELD_GRAVITY_CENTER: return download_soa3(c, c->gx, c->gy, c->gz, c->A.id, o);
@@ -588,39 +603,44 @@ int mph_get(MphCtx* c, int field, void* out)
     case MPH_FIELD_DIVERGENCE_P: return download_scalar(c, c->divp, c->A.id, o);
     case MPH_FIELD_NEIGHBOR_COUNT: return download_scalar(c, c->ncount, c->A.id, oi);
     case MPH_FIELD_MASS:
-        for (int i = 0; i < n; ++i) o[i] = c->cfg.density[c->prop[i]] * c->h.vol;
+        for (int k = 0; k < nin; ++k) o[glob_id(c, k)] = c->cfg.density[c->prop[k]] * c->h.vol;
         return MPH_OK;
     case MPH_FIELD_KAPPA: {
         // initializeFluid (1317-1319) before the first step, calculatePhysicalCoefficients after
-        std::vector<double> vs(n, 0.0);
+        std::vector<double> vs(c->stepped ? (size_t)c->n_glob : 0, 0.0);
         if (c->stepped) CK(download_scalar(c, c->vstrain, c->A.id, vs.data()));
-        for (int i = 0; i < n; ++i)
-            o[i] = (c->stepped && vs[i] < 0.0) ? 0.0 : c->cfg.bulk_modulus[c->prop[i]];
+        for (int k = 0; k < nin; ++k) {
+            const int i = glob_id(c, k);
+            o[i] = (c->stepped && vs[i] < 0.0) ? 0.0 : c->cfg.bulk_modulus[c->prop[k]];
+        }
         return MPH_OK;
     }
     case MPH_FIELD_LAMBDA:
-        for (int i = 0; i < n; ++i) o[i] = c->cfg.bulk_viscosity[c->prop[i]];
+        for (int k = 0; k < nin; ++k) o[glob_id(c, k)] = c->cfg.bulk_viscosity[c->prop[k]];
         return MPH_OK;
     case MPH_FIELD_MU:
-        for (int i = 0; i < n; ++i) o[i] = c->cfg.shear_viscosity[c->prop[i]];
+        for (int k = 0; k < nin; ++k) o[glob_id(c, k)] = c->cfg.shear_viscosity[c->prop[k]];
         return MPH_OK;
-    case MPH_FIELD_PROPERTY: std::memcpy(oi, c->prop.data(), sizeof(int) * n); return MPH_OK;
+    case MPH_FIELD_PROPERTY:
+        for (int k = 0; k < nin; ++k) oi[glob_id(c, k)] = c->prop[k];
+        return MPH_OK;
     case MPH_FIELD_INITIAL_STRUCTURE_NEIGHBOR_COUNT:
-        std::memset(oi, 0, sizeof(int) * n);
-        for (int s = 0; s < ns; ++s) oi[c->S.orig[s]] = c->S.count[s];
+        for (int k = 0; k < nin; ++k) oi[glob_id(c, k)] = 0;
+        for (int k = 0; k < ns; ++k) oi[glob_id(c, c->S.orig[sidx(k)])] = c->S.count[sidx(k)];
         return MPH_OK;
     case MPH_FIELD_DEFORM_GRADIENT: return download_struct_m33(c, c->Sd.F, o);
     case MPH_FIELD_STRAIN: return download_struct_m33(c, c->Sd.E, o);
     case MPH_FIELD_STRESS: return download_struct_m33(c, c->Sd.S, o);
     case MPH_FIELD_NORMALIZER:
-        std::memset(o, 0, sizeof(double) * 9 * (size_t)n);
-        for (int s = 0; s < ns; ++s)
-            std::memcpy(o + (size_t)9 * c->S.orig[s], &c->S.normalizer[(size_t)9 * s], sizeof(double) * 9);
+        for (int k = 0; k < nin; ++k) std::memset(o + (size_t)9 * glob_id(c, k), 0, sizeof(double) * 9);
+        for (int k = 0; k < ns; ++k)
+            std::memcpy(o + (size_t)9 * glob_id(c, c->S.orig[sidx(k)]), &c->S.normalizer[(size_t)9 * sidx(k)],
+                        sizeof(double) * 9);
         return MPH_OK;
     case MPH_FIELD_VIRIAL_STRESS:
     case MPH_FIELD_VIRIAL_PRESSURE: {
         const int w = field == MPH_FIELD_VIRIAL_STRESS ? 9 : 1;
-        std::memset(o, 0, sizeof(double) * w * (size_t)n);
+        std::memset(o, 0, sizeof(double) * w * (size_t)c->n_glob);
         if (!c->vir) return MPH_OK;   // never computed (the reference's array is uninitialised)
         std::vector<double> h((size_t)w * c->n);
         std::vector<int> id(c->n);
@@ -634,9 +654,10 @@ int mph_get(MphCtx* c, int field, void* out)
     }
     case MPH_FIELD_LAMBDA_LAMES:
     case MPH_FIELD_MU_LAMES:
-        std::memset(o, 0, sizeof(double) * n);
-        for (int s = 0; s < ns; ++s)
-            o[c->S.orig[s]] = field == MPH_FIELD_LAMBDA_LAMES ? c->S.lame_l[s] : c->S.lame_m[s];
+        for (int k = 0; k < nin; ++k) o[glob_id(c, k)] = 0.0;
+        for (int k = 0; k < ns; ++k)
+            o[glob_id(c, c->S.orig[sidx(k)])] =
+                field == MPH_FIELD_LAMBDA_LAMES ? c->S.lame_l[sidx(k)] : c->S.lame_m[sidx(k)];
         return MPH_OK;
     default: return fail(c, MPH_ERR_ARG, "unknown field " + std::to_string(field));
     }
@@ -689,8 +710,17 @@ int mph_set_initial_velocity_profile(MphCtx* c)
     std::vector<double> pos(3 * n, 0.0), vel(3 * n, 0.0);
     CK(mph_get(c, MPH_FIELD_POSITION, pos.data()));
     CK(mph_get(c, MPH_FIELD_VELOCITY, vel.data()));
-    CK(mph_velocity_profile_arrays(&c->cfg, c->time, c->n_glob, c->prop.data(), pos.data(), c->pos0.data(),
-                                   vel.data()));
+    // the static inputs this context holds, with the current state of the same particles
+    const int nin = (int)c->prop.size();
+    std::vector<double> p(3 * (size_t)nin), v(3 * (size_t)nin);
+    for (int k = 0; k < nin; ++k)
+        for (int d = 0; d < 3; ++d) {
+            p[3 * (size_t)k + d] = pos[3 * (size_t)glob_id(c, k) + d];
+            v[3 * (size_t)k + d] = vel[3 * (size_t)glob_id(c, k) + d];
+        }
+    CK(mph_velocity_profile_arrays(&c->cfg, c->time, nin, c->prop.data(), p.data(), c->pos0.data(), v.data()));
+    for (int k = 0; k < nin; ++k)
+        for (int d = 0; d < 3; ++d) vel[3 * (size_t)glob_id(c, k) + d] = v[3 * (size_t)k + d];
     return mph_set(c, MPH_FIELD_VELOCITY, vel.data());
 }
 

@@ -372,7 +372,8 @@ int dist_setup(MphCtx* c, const double* pos, std::vector<int>& owned)
     // initial owned set and a capacity for owned + ghosts (+ headroom for migration imbalance)
     owned.clear();
     size_t near = 0;
-    for (int i = 0; i < c->n_glob; ++i) {
+    const int nin = (int)c->prop.size();   // the particles passed in (all, or this rank's window)
+    for (int i = 0; i < nin; ++i) {
         const double a = wrap_coord(h, axis, pos[3 * (size_t)i + axis]);
         if (is_struct(c->prop[i])) {
             // static owner: the slab of the InitialPosition
@@ -657,6 +658,28 @@ int mph_create_dist(MphCtx** ctx, const MphConfig* cfg, int n, const int* proper
     return ctx_create(ctx, cfg, n, property, pos, pos0, vel, device, D);
 }
 
+int mph_create_slab(MphCtx** ctx, const MphConfig* cfg, int n, const int* property, const double* pos,
+                    const double* pos0, const double* vel, int device, const MphSlabOptions* opt)
+{
+    if (!opt || opt->rank < 0 || opt->rank >= opt->nranks) return MPH_ERR_ARG;
+    if ((opt->unique_id128 == nullptr) == (opt->host_fn == nullptr)) return MPH_ERR_ARG;
+    if (opt->n_glob > 0 && !opt->ids) return MPH_ERR_ARG;
+    MphDist* D = new MphDist();
+    D->rank = opt->rank;
+    D->nranks = opt->nranks;
+    D->g.axis = opt->axis;
+    if (opt->unique_id128) {
+        D->rccl = true;
+        D->graphs = std::getenv("MPH_SLAB_GRAPHS") == nullptr || std::string(std::getenv("MPH_SLAB_GRAPHS")) != "0";
+        std::memcpy(D->uid, opt->unique_id128, sizeof(D->uid));
+    } else {
+        D->host_fn = opt->host_fn;
+        D->host_user = opt->host_user;
+    }
+    return ctx_create(ctx, cfg, n, property, pos, pos0, vel, device, D, opt->n_glob > 0 ? opt->ids : nullptr,
+                      opt->n_glob);
+}
+
 int mph_create_dist_host(MphCtx** ctx, const MphConfig* cfg, int n, const int* property, const double* pos,
                          const double* pos0, const double* vel, int device, int rank, int nranks, int axis,
                          mph_host_exchange_fn fn, void* user)
@@ -796,6 +819,21 @@ int mph_slab_bounds(const MphConfig* cfg, int rank, int nranks, int axis, double
     make_dev_params(*cfg, h, 0, 0, P);
     slab_of(h, axis, rank, nranks, out3[0], out3[1]);
     out3[2] = halo_width(P);
+    return MPH_OK;
+}
+
+int mph_slab_window(const MphConfig* cfg, int rank, int nranks, int axis, double* out2)
+{
+    double b[3];
+    const int rc = mph_slab_bounds(cfg, rank, nranks, axis, b);
+    if (rc != MPH_OK) return rc;
+    if (!out2) return MPH_ERR_ARG;
+    // two halo widths, each including the elastic particles' displacement margin, so that the
+    // first redistribution's capacity estimate (dist_setup) and the structure lists of the owned
+    // elastic particles (calculateInitialNeighbor reach) see every particle they need
+    const double m = 2.0 * (b[2] + kStructMargin * cfg->particle_spacing);
+    out2[0] = b[0] - m;
+    out2[1] = b[1] + m;
     return MPH_OK;
 }
 

@@ -54,17 +54,25 @@ class GlooExchange:
             np.frombuffer(mv, dtype=np.uint8)[:] = b.numpy()
 
 
-def rccl_slab(rank: int, nranks: int, axis: int, group=None) -> solver.Slab:
+def rccl_slab(rank: int, nranks: int, axis: int, group=None, ids=None, n_glob: int = 0) -> solver.Slab:
     """Slab options with an RCCL communicator: rank 0 makes the unique id, everyone receives it
     through torch.distributed (any backend)."""
     import torch.distributed as dist
     obj = [solver.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0, group=group)
-    return solver.Slab(rank, nranks, axis, uid=obj[0])
+    return solver.Slab(rank, nranks, axis, uid=obj[0], ids=ids, n_glob=n_glob)
 
 
-def gloo_slab(rank: int, nranks: int, axis: int, group=None) -> solver.Slab:
-    return solver.Slab(rank, nranks, axis, exchange=GlooExchange(rank, nranks, group))
+def gloo_slab(rank: int, nranks: int, axis: int, group=None, ids=None, n_glob: int = 0) -> solver.Slab:
+    return solver.Slab(rank, nranks, axis, exchange=GlooExchange(rank, nranks, group), ids=ids, n_glob=n_glob)
+
+
+def build_local(case, rank: int, nranks: int, axis: int):
+    """This rank's share of a registered case for slab-local creation: (cfg, particles of its
+    window, their original indices, total count) -- generated without the rest of the problem."""
+    cfg, _ = case._config()
+    lo, hi = solver.slab_window(cfg, rank, nranks, axis)
+    return case.build_window(axis, lo, hi)
 
 
 def gather_field(s: solver.MphSolver, name: str, group=None) -> np.ndarray:

@@ -251,6 +251,43 @@ def generate(cuboids: list[Cuboid]) -> Particles:
                      velocity=np.ascontiguousarray(np.concatenate(vel)) if vel else np.zeros((0, 3)))
 
 
+def generate_window(cuboids: list[Cuboid], axis: int, lo: float, hi: float, dmin: float, width: float):
+    """The particles of ``generate(cuboids)`` whose coordinate along ``axis`` lies in the periodic
+    window [lo, hi) of a domain starting at ``dmin`` with ``width``, without building the others
+    (slab-local creation, include/mph_gpu.h mph_create_slab).  Returns (Particles, ids, n_glob):
+    the original indices of the kept particles (ascending) and the total count.  Cuboid lattices
+    are separable, so the window only filters the value list of one axis."""
+    span = hi - lo
+    props, pos, vel, ids = [], [], [], []
+    base = 0
+    for cub in cuboids:
+        ax = [np.array([_e(v) for v in _axis_values(cub.lower[d], cub.upper[d], cub.space)])
+              for d in range(3)]
+        cnt = [len(a) for a in ax]
+        keep = [np.arange(c) for c in cnt]
+        if span < width:
+            a = ax[axis]
+            u = a - dmin
+            u = u - width * np.floor(u / width) + dmin    # periodic wrap into [dmin, dmin + width)
+            off = (u - lo) - width * np.floor((u - lo) / width)
+            keep[axis] = np.nonzero(off < span)[0]
+        if all(len(k) for k in keep):
+            I, J, K = np.meshgrid(keep[0], keep[1], keep[2], indexing="ij")
+            ids.append(base + ((I * cnt[1] + J) * cnt[2] + K).ravel())
+            X, Y, Z = np.meshgrid(ax[0][keep[0]], ax[1][keep[1]], ax[2][keep[2]], indexing="ij")
+            p = np.stack([X.ravel(), Y.ravel(), Z.ravel()], axis=1)
+            pos.append(p)
+            props.append(np.full(p.shape[0], cub.type, dtype=np.int32))
+            vel.append(np.tile(np.array([_e(v) for v in cub.velocity]), (p.shape[0], 1)))
+        base += cnt[0] * cnt[1] * cnt[2]
+    P = np.concatenate(pos) if pos else np.zeros((0, 3))
+    parts = Particles(property=np.concatenate(props) if props else np.zeros(0, np.int32),
+                      position=np.ascontiguousarray(P), initial_position=P.copy(),
+                      velocity=np.ascontiguousarray(np.concatenate(vel)) if vel else np.zeros((0, 3)))
+    idx = np.concatenate(ids).astype(np.int32) if ids else np.zeros(0, np.int32)
+    return parts, idx, base
+
+
 def format_grid(p: Particles, spacing: float, lower, upper, time: float = 0.0) -> str:
     """Text of the generator's ``writefile`` (generator.cpp:839-862); ``time`` is the first line
     (0 from the generator; a .prof restart carries its Time, main.cpp:797, 961)."""

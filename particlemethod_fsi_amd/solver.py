@@ -55,13 +55,20 @@ EXPORTED_SYMBOLS = [
     "mph_slab_owner", "mph_dist_selftest", "mph_compute_virial",
     "mph_config_sizeof", "mph_write_vtk_async", "mph_output_wait", "mph_write_grid_binary",
     "mph_write_vtu_arrays", "mph_write_vtu", "mph_velocity_profile_arrays",
-    "mph_set_initial_velocity_profile", "mph_dist_info",
+    "mph_set_initial_velocity_profile", "mph_dist_info", "mph_create_slab", "mph_slab_window",
 ]
 
 # mph_host_exchange_fn (include/mph_gpu.h): (user, send_l, n, send_r, n, recv_l, n, recv_r, n)
 HOST_EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                     ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
                                     ctypes.c_void_p, ctypes.c_size_t)
+
+
+class MphSlabOptions(ctypes.Structure):
+    """include/mph_gpu.h MphSlabOptions."""
+    _fields_ = [("rank", ctypes.c_int), ("nranks", ctypes.c_int), ("axis", ctypes.c_int),
+                ("unique_id128", ctypes.c_char_p), ("host_fn", HOST_EXCHANGE_FN),
+                ("host_user", ctypes.c_void_p), ("n_glob", ctypes.c_int), ("ids", ctypes.c_void_p)]
 
 
 class MphError(RuntimeError):
@@ -135,6 +142,8 @@ def load_library() -> ctypes.CDLL:
         "mph_velocity_profile_arrays": (ip, [cfgp, dp, ip, vp, vp, vp, vp]),
         "mph_set_initial_velocity_profile": (ip, [vp]),
         "mph_dist_info": (ip, [vp, vp]),
+        "mph_create_slab": (ip, [ctypes.POINTER(vp), cfgp, ip, vp, vp, vp, vp, ip, ctypes.POINTER(MphSlabOptions)]),
+        "mph_slab_window": (ip, [cfgp, ip, ip, ip, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -211,6 +220,13 @@ def slab_bounds(cfg: mphio.MphConfig, rank: int, nranks: int, axis: int):
     return float(out[0]), float(out[1]), float(out[2])
 
 
+def slab_window(cfg: mphio.MphConfig, rank: int, nranks: int, axis: int):
+    """(lo, hi): the periodic window of particles a rank needs for slab-local creation."""
+    out = np.zeros(2)
+    _check(load_library().mph_slab_window(ctypes.byref(cfg), rank, nranks, axis, out.ctypes.data))
+    return float(out[0]), float(out[1])
+
+
 def slab_owner(cfg: mphio.MphConfig, nranks: int, axis: int, x: float) -> int:
     return _check(load_library().mph_slab_owner(ctypes.byref(cfg), nranks, axis, float(x)))
 
@@ -220,10 +236,15 @@ class Slab:
     Transport: RCCL with the 128-byte unique id `uid` (mph_create_dist), or a host callback
     `exchange(send_l, send_r, recv_l, recv_r)` over memoryviews (mph_create_dist_host)."""
 
-    def __init__(self, rank: int, nranks: int, axis: int, uid: bytes | None = None, exchange=None):
+    def __init__(self, rank: int, nranks: int, axis: int, uid: bytes | None = None, exchange=None,
+                 ids: np.ndarray | None = None, n_glob: int = 0):
+        """ids/n_glob: slab-local creation -- the particles handed to MphSolver are only this
+        rank's window (slab_window), with their original indices ids among n_glob."""
         if (uid is None) == (exchange is None):
             raise ValueError("Slab needs exactly one of uid (RCCL) or exchange (host transport)")
         self.rank, self.nranks, self.axis, self.uid, self.exchange = rank, nranks, axis, uid, exchange
+        self.ids = None if ids is None else np.ascontiguousarray(ids, np.int32)
+        self.n_glob = int(n_glob) if ids is not None else 0
 
 
 def unique_id() -> bytes:
@@ -253,14 +274,24 @@ class MphSolver:
         ptrs = [a.ctypes.data for a in self._arrays]
         if slab is None:
             rc = L.mph_create(ctypes.byref(h), ctypes.byref(self.cfg), self.n, *ptrs, int(device))
-        elif slab.uid is not None:
-            uid = ctypes.create_string_buffer(bytes(slab.uid), 128)
-            rc = L.mph_create_dist(ctypes.byref(h), ctypes.byref(self.cfg), self.n, *ptrs, int(device),
-                                   slab.rank, slab.nranks, uid, slab.axis)
         else:
-            self._cb = HOST_EXCHANGE_FN(_host_exchange_adapter(slab.exchange))
-            rc = L.mph_create_dist_host(ctypes.byref(h), ctypes.byref(self.cfg), self.n, *ptrs,
-                                        int(device), slab.rank, slab.nranks, slab.axis, self._cb, None)
+            opt = MphSlabOptions()
+            opt.rank, opt.nranks, opt.axis = slab.rank, slab.nranks, slab.axis
+            if slab.uid is not None:
+                self._uid = ctypes.create_string_buffer(bytes(slab.uid), 128)
+                opt.unique_id128 = ctypes.cast(self._uid, ctypes.c_char_p)
+            else:
+                self._cb = HOST_EXCHANGE_FN(_host_exchange_adapter(slab.exchange))
+                opt.host_fn = self._cb
+            if slab.ids is not None:
+                if len(slab.ids) != parts.n:
+                    raise ValueError("Slab.ids must index the particles passed in")
+                opt.n_glob = slab.n_glob
+                opt.ids = slab.ids.ctypes.data
+                self._keep_ids = slab.ids
+                self.n = slab.n_glob
+            rc = L.mph_create_slab(ctypes.byref(h), ctypes.byref(self.cfg), parts.n, *ptrs, int(device),
+                                   ctypes.byref(opt))
         if rc < 0:
             msg = (L.mph_last_error(None) or b"").decode()
             raise MphError(rc, msg or "mph_create failed")

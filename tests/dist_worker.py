@@ -27,16 +27,23 @@ def _init(rank, world, port):
     return dist
 
 
-def gpu_worker(rank, world, port, case, checkpoints, fields, out_path):
+def gpu_worker(rank, world, port, case, checkpoints, fields, out_path, local=False):
     """Run `case` as rank `rank` of `world` on cuda:0; at every checkpoint (cumulative step
-    count) gather `fields` over the ranks; rank 0 saves them to out_path (.npz)."""
+    count) gather `fields` over the ranks; rank 0 saves them to out_path (.npz).  local: the rank
+    is created from its own window of the case only (slab-local creation)."""
     dist = _init(rank, world, port)
     from particlemethod_fsi_amd import MphSolver, cases
-    from particlemethod_fsi_amd.dist import gather_field, gloo_slab
+    from particlemethod_fsi_amd.dist import build_local, gather_field, gloo_slab
     c = cases.get(case)
-    cfg, parts = c.build()
+    axis = SLAB_AXIS[case]
+    if local:
+        cfg, parts, ids, n_glob = build_local(c, rank, world, axis)
+        slab = gloo_slab(rank, world, axis, ids=ids, n_glob=n_glob)
+    else:
+        cfg, parts = c.build()
+        slab = gloo_slab(rank, world, axis)
     res = {}
-    with MphSolver(cfg, parts, device=0, slab=gloo_slab(rank, world, SLAB_AXIS[case])) as s:
+    with MphSolver(cfg, parts, device=0, slab=slab) as s:
         def owner_map():
             parts_ = [None] * world
             dist.all_gather_object(parts_, s.owned_ids())
@@ -130,16 +137,17 @@ def band_worker(rank, world, port, case, out_path):
 
 
 def gpu_rank_worker(rank, world, port, case, axis, nsteps, fields, out_dir, transport="host"):
-    """One slab rank of a large case on cuda:0 (several ranks share the GPU): run `nsteps`, then
-    save this rank's owned particle ids and their `fields` to out_dir/rank<r>.npz (no gather
-    through the process group, so it scales to the 16M-particle configuration)."""
+    """One slab rank of a large case on cuda:0 (several ranks share the GPU), created from its own
+    window of the case only (slab-local creation): run `nsteps`, then save this rank's owned
+    particle ids and their `fields` to out_dir/rank<r>.npz (no gather through the process group,
+    so it scales to the 16M-particle configuration)."""
     dist = _init(rank, world, port)
     from particlemethod_fsi_amd import MphSolver, cases
-    from particlemethod_fsi_amd.dist import gloo_slab, rccl_slab
+    from particlemethod_fsi_amd.dist import build_local, gloo_slab, rccl_slab
     c = cases.get(case)
-    cfg, parts = c.build()
+    cfg, parts, ids, n_glob = build_local(c, rank, world, axis)
     mk = gloo_slab if transport == "host" else rccl_slab
-    with MphSolver(cfg, parts, device=0, slab=mk(rank, world, axis)) as s:
+    with MphSolver(cfg, parts, device=0, slab=mk(rank, world, axis, ids=ids, n_glob=n_glob)) as s:
         del parts
         s.step(nsteps)
         ids = s.owned_ids()

@@ -37,10 +37,10 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def run_slab(case, world, checkpoints, out, fields=FIELDS):
+def run_slab(case, world, checkpoints, out, fields=FIELDS, local=False):
     ctx = mp.get_context("spawn")
     port = _free_port()
-    ps = [ctx.Process(target=dist_worker.gpu_worker, args=(r, world, port, case, checkpoints, fields, out))
+    ps = [ctx.Process(target=dist_worker.gpu_worker, args=(r, world, port, case, checkpoints, fields, out, local))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -73,12 +73,15 @@ def close(f, a, b, rel=1e-8):
 STRUCT_REL = {"DivergenceP": 1e-6}
 
 
-@pytest.mark.parametrize("case,world", [("channel3d", 2), ("channel3d", 3), ("channel2d", 4),
-                                        ("channel3d_st", 2), ("dam2d", 2)])
-def test_slab_ranks_match_oracle(tmp_path, case, world):
+@pytest.mark.parametrize("case,world,local", [("channel3d", 2, False), ("channel3d", 3, False),
+                                              ("channel2d", 4, False), ("channel3d_st", 2, False),
+                                              ("dam2d", 2, False), ("channel3d", 3, True),
+                                              ("channel2d", 4, True)])
+def test_slab_ranks_match_oracle(tmp_path, case, world, local):
+    """local: every rank is created from its own window of the case (slab-local creation)."""
     from oracle_bindings import OracleSolver
     checkpoints = [1, 5, 20]
-    r = run_slab(case, world, checkpoints, str(tmp_path / "slab.npz"))
+    r = run_slab(case, world, checkpoints, str(tmp_path / "slab.npz"), local=local)
     cfg, parts = cases.get(case).build()
     assert (r["owner0"] >= 0).all()
     o = OracleSolver(cfg, parts)
@@ -99,13 +102,16 @@ def test_slab_ranks_match_oracle(tmp_path, case, world):
         assert moved, "no particle migrated between slabs"
 
 
-@pytest.mark.parametrize("case,world", [("bar2d", 2), ("bar2d", 3), ("bar3d", 2), ("gate2d_sub", 2)])
-def test_slab_structure_ranks_match_oracle(tmp_path, case, world):
+@pytest.mark.parametrize("case,world,local", [("bar2d", 2, False), ("bar2d", 3, False), ("bar3d", 2, False),
+                                              ("gate2d_sub", 2, False), ("bar2d", 3, True),
+                                              ("gate2d_sub", 2, True)])
+def test_slab_structure_ranks_match_oracle(tmp_path, case, world, local):
     """Elastic-solid particles across slab faces: static owners by InitialPosition, ghost slots of
-    the fixed Lagrangian lists exchanged before every stress / velocity half-substep."""
+    the fixed Lagrangian lists exchanged before every stress / velocity half-substep.  local: the
+    structure lists are built from each rank's window only."""
     from oracle_bindings import OracleSolver
     checkpoints = [1, 10, 30]
-    r = run_slab(case, world, checkpoints, str(tmp_path / "slab.npz"), STRUCT_FIELDS)
+    r = run_slab(case, world, checkpoints, str(tmp_path / "slab.npz"), STRUCT_FIELDS, local=local)
     cfg, parts = cases.get(case).build()
     o = OracleSolver(cfg, parts)
     o.init()
