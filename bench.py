@@ -50,6 +50,10 @@ ALG_BYTES = {"pass_a": 92.0, "neighbors_pass_a": 92.0, "pass_b": 140.0, "sort": 
 #   struct_velocity read P (72), v, x (48), out- and in-lists (8 n_s); write v, x (48)
 STRUCT_BYTES = {"struct_stress": (208.0, 4.0), "struct_velocity": (168.0, 8.0)}
 B_ALG_STEP = 372.0          # grid build 140 + pass 1 92 + pass 2 140
+# the reference-literal gather bytes per particle-step (3-D): neighbour fields of its 8
+# neighbour loops, the 343-cell search, the list reset/write and the bitonic passes -- what the
+# north star's "50 % of HBM at 1e8" is consistent with; a label, never a measured figure
+B_GATHER_3D = 42.7e3
 SLAB_AXIS = {2: 0, 3: 2}    # by dimension: z slabs for the 3-D dam workloads, x in 2-D
 
 
@@ -250,6 +254,17 @@ def main():
     alg_bytes = alg_bytes_of(dom)
     achieved = alg_bytes / (prof[dom]["avg_ms"] * 1e-3) / 1e9
     traffic = load_pmc("pmc_traffic", case_name, dom, "hbm_bytes_per_launch")
+    # measured HBM traffic of a whole step: rocprofv3 FETCH_SIZE/WRITE_SIZE per kernel in the timed
+    # region's store pattern (tools/profile.sh + tools/pmc_traffic.py, calibration
+    # profiles/pmc_calib.json), over this run's own step time
+    step_bytes = None
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as fh:
+            d = json.load(fh)
+        if d.get("case") == case_name and world == 1:
+            step_bytes = d.get("hbm_bytes_per_step")
+    except (OSError, ValueError):
+        pass
     # FP64 utilisation: PMC lane FLOPs per launch over the same live launch time
     flops = {k: load_pmc("pmc_fp64", case_name, k, "lane_flops_per_launch") for k in prof}
     fp64 = {k: {"tflops": f / (prof[k]["avg_ms"] * 1e-3) / 1e12,
@@ -274,6 +289,15 @@ def main():
                    "parallelism": "single" if world == 1 else "slab%d-%s (%s halo exchange)" % (
                        world, "xyz"[SLAB_AXIS[case.dim]], "host-staged" if os.environ.get("MPH_SLAB_TRANSPORT") == "host" else "RCCL")},
         "achieved_hbm_gbps_alg": B_ALG_STEP * value / 1e9,
+        "achieved_hbm_gbps_measured": (step_bytes / (elapsed / args.steps) / 1e9) if step_bytes else None,
+        "hbm_measured": ({"bytes_per_step": step_bytes, "bytes_per_particle_step": step_bytes / n_total,
+                          "source": "profiles/pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE per kernel, "
+                                    "8-step store pattern (calibrated: profiles/pmc_calib.json)"}
+                         if step_bytes else None),
+        "gather_literal_gbps": {"value": (B_GATHER_3D if case.dim == 3 else 12e3) * value / 1e9,
+                                "note": "reference-literal gather bytes (SURVEY 8d B_gather, %.1f kB per "
+                                        "particle-step) x rate: a label for the north-star target, not "
+                                        "HBM traffic" % ((B_GATHER_3D if case.dim == 3 else 12e3) / 1e3)},
         "neighbors": {"mean": mean_nb, "max": max_nb},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,

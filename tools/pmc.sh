@@ -1,5 +1,6 @@
 #!/bin/bash
-# Diagnostic PMC passes (one rocprofv3 --pmc run per counter group) on a short bench.
+# Diagnostic PMC passes (one rocprofv3 --pmc run per counter group) on a short bench, in the
+# timed region's store pattern (8-step batches; tools/pmc_fp64.py drops the init launch).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -11,5 +12,5 @@ i=0
 for grp in "$@"; do
   i=$((i+1))
   timeout -k 10 600 rocprofv3 --pmc $grp --output-format csv -d $OUT/g$i -o g$i -- \
-      python3 bench.py --case $CASE --steps 3 --warmup 1 --no-cpu-baseline --profile-steps 1 > $OUT/g$i.log 2>&1 || exit 30
+      python3 bench.py --case $CASE --steps 8 --warmup 8 --no-cpu-baseline --profile-steps 8 > $OUT/g$i.log 2>&1 || exit 30
 done

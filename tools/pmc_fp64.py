@@ -25,14 +25,17 @@ def main():
     for path in glob.glob(src + "/g*/*counter_collection.csv"):
         for r in csv.DictReader(open(path)):
             name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("mph::", "").split("<")[0]
-            acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            acc[name][r["Counter_Name"]].append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
     out = {"_note": "lane FP64 FLOPs per launch = 64 x SQ_INSTS_VALU_FLOPS_FP64, averaged over "
                     "launches (upper bound: masked lanes count); " + tag,
            "case": os.environ.get("MPH_PMC_CASE", "d1m")}
     for name, d in sorted(acc.items()):
-        if not sum(d.get("SQ_INSTS_VALU_FLOPS_FP64", [0.0])):
+        vals = [v for _, v in sorted(d.get("SQ_INSTS_VALU_FLOPS_FP64", []))]
+        if len(vals) % 8 == 1 and len(vals) > 1:
+            vals = vals[1:]   # mph_create's initialisation launch (runs step in batches of 8)
+        if not sum(vals):
             continue
-        f = sum(d["SQ_INSTS_VALU_FLOPS_FP64"]) / len(d["SQ_INSTS_VALU_FLOPS_FP64"])
+        f = sum(vals) / len(vals)
         out[name.replace("k_", "", 1)] = {"wave_flops": f, "lane_flops_per_launch": 64.0 * f}
     with open(dst, "w") as fh:
         json.dump(out, fh, indent=1)

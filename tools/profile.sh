@@ -1,6 +1,9 @@
 #!/bin/bash
 # rocprofv3 evidence for profiles/: one kernel-trace + stats pass, then one PMC pass per TCC
 # counter (FETCH_SIZE and WRITE_SIZE do not fit one pass on gfx950; MI355X_MICROARCH.md PMC slots).
+# The PMC passes replay the same store pattern as the timed region: 8-step graphs (the first 7
+# steps skip the output-only stores) and an 8-step profiled batch; tools/pmc_traffic.py drops each
+# kernel's first launch (the initialisation sums of mph_create).
 # Every GPU step is time-limited; the chain stops at the first failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -8,10 +11,11 @@ export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
 CASE=${CASE:-d1m}
-ARGS="--case $CASE --steps ${STEPS:-20} --warmup 4 --no-cpu-baseline"
+ARGS="--case $CASE --steps ${STEPS:-24} --warmup 8 --no-cpu-baseline"
+PMC_ARGS="--case $CASE --steps 8 --warmup 8 --profile-steps 8 --no-cpu-baseline"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- \
     python3 bench.py $ARGS > $OUT/bench_under_kt.log 2>&1 || exit 21
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- \
-    python3 bench.py --case $CASE --steps 4 --warmup 2 --no-cpu-baseline --profile-steps 1 > $OUT/fetch.log 2>&1 || exit 22
+    python3 bench.py $PMC_ARGS > $OUT/fetch.log 2>&1 || exit 22
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- \
-    python3 bench.py --case $CASE --steps 4 --warmup 2 --no-cpu-baseline --profile-steps 1 > $OUT/write.log 2>&1 || exit 23
+    python3 bench.py $PMC_ARGS > $OUT/write.log 2>&1 || exit 23
