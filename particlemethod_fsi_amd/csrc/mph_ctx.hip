@@ -6,6 +6,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -264,9 +265,13 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     c->prop.assign(property, property + n);
     c->pos0.assign(pos0, pos0 + 3 * (size_t)n);
     std::string err;
-    // the fixed Lagrangian structure lists (every rank builds all of them in slab mode and keeps
-    // its owned slots plus their ghost neighbours, dist_struct_setup)
-    CK(fail(c, build_structure(c->cfg, c->h, n, property, pos0, c->S, err), err));
+    // the fixed Lagrangian structure lists: on the device for a single context (calculate-
+    // InitialNeighbor + calculateNormalizer as kernels, launch_struct_init); in slab mode on the
+    // host over the particles this rank was given, which also routes the static ghost slots
+    // (dist_struct_setup).  MPH_STRUCT_INIT=host selects the host build everywhere.
+    const char* sie = std::getenv("MPH_STRUCT_INIT");
+    const bool gpu_init = !c->dist && !(sie && std::string(sie) == "host");
+    CK(fail(c, build_structure(c->cfg, c->h, n, property, pos0, c->S, err, !gpu_init), err));
     const int ns = (int)c->S.orig.size();
     make_dev_params(c->cfg, c->h, n, ns, c->P);
     const double rc = std::sqrt(c->P.rc2);
@@ -367,7 +372,7 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     // elastic solid: local slots = [computed here | ghosts] (single GPU: every slot, no ghosts)
     if (ns > 0) {
         StructDev& D = c->Sd;
-        const StructureInit& S = c->S;
+        StructureInit& S = c->S;
         std::vector<int> lsl;   // local slot -> global slot
         int no = ns;
         if (c->dist) {
@@ -383,64 +388,25 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         c->sl_orig.resize(nl);
         for (int k = 0; k < nl; ++k) c->sl_orig[k] = glob_id(c, S.orig[lsl[k]]);
         c->sl_s.assign(lsl.begin(), lsl.begin() + no);
-        // ELL tiles of the fixed out-list and of its transpose (StructDev), computed slots only
-        const size_t ntile_s = ((size_t)std::max(no, 1) + 63) / 64;
-        std::vector<int> ocnt(std::max(no, 1), 0), icnt(std::max(no, 1), 0);
-        int wo = 0, wi = 0;
-        for (int s = 0; s < no; ++s) {
-            const int g = lsl[s];
-            ocnt[s] = S.offset[g + 1] - S.offset[g];
-            icnt[s] = S.in_offset[g + 1] - S.in_offset[g];
-            wo = std::max(wo, ocnt[s]);
-            wi = std::max(wi, icnt[s]);
-        }
-        wo = std::max(wo, 1);
-        wi = std::max(wi, 1);
-        D.wo = wo;
-        D.wi = wi;
-        std::vector<int> eo_nb(ntile_s * wo * 64, 0), ei_nb(ntile_s * wi * 64, 0);
-        std::vector<double4> wx0(nl, make_double4(0.0, 0.0, 0.0, 0.0));
-        for (int s = 0; s < no; ++s) {
-            const int g = lsl[s];
-            const size_t base_o = (size_t)(s >> 6) * wo * 64 + (s & 63);
-            double c3[3] = {0.0, 0.0, 0.0};
-            for (int k = 0; k < ocnt[s]; ++k) {
-                const size_t q = S.offset[g] + k;
-                const double* pr = &S.pair_out[4 * q];
-                eo_nb[base_o + (size_t)k * 64] = loc[S.nbr[q]];
-                for (int d = 0; d < 3; ++d) c3[d] += pr[3] * pr[d];
-            }
-            wx0[s] = make_double4(c3[0], c3[1], c3[2], 0.0);
-            const size_t base_i = (size_t)(s >> 6) * wi * 64 + (s & 63);
-            for (int k = 0; k < icnt[s]; ++k) {
-                const size_t q = S.in_offset[g] + k;
-                ei_nb[base_i + (size_t)k * 64] = loc[S.in_nbr[q]];
-            }
-        }
-        for (int e : eo_nb) if (e < 0) return fail(c, MPH_ERR_DOMAIN, "structure list leaves the ghost slots");
-        for (int e : ei_nb) if (e < 0) return fail(c, MPH_ERR_DOMAIN, "structure list leaves the ghost slots");
         const int sd = c->P.dim;
-        CK(dalloc(c, &D.orig, nl)); CK(dalloc(c, &D.ocnt, ocnt.size())); CK(dalloc(c, &D.icnt, icnt.size()));
+        CK(dalloc(c, &D.orig, nl)); CK(dalloc(c, &D.ocnt, std::max(no, 1))); CK(dalloc(c, &D.icnt, std::max(no, 1)));
         CK(dalloc(c, &D.bidx, nl));
-        CK(dalloc(c, &D.eo_nb, eo_nb.size()));
-        CK(dalloc(c, &D.ei_nb, ei_nb.size()));
         CK(dalloc(c, &D.wx0, nl));
         CK(dalloc(c, &D.L, (size_t)nl * 9)); CK(dalloc(c, &D.lame, nl)); CK(dalloc(c, &D.inv_rho, nl));
         CK(dalloc(c, &D.clamp, nl)); CK(dalloc(c, &D.x0, nl)); CK(dalloc(c, &D.x, nl)); CK(dalloc(c, &D.v, nl));
         CK(dalloc(c, &D.u, nl)); CK(dalloc(c, &D.P, (size_t)nl * (sd == 2 ? 1 : 3))); CK(dalloc(c, &D.F, (size_t)nl * 9));
         CK(dalloc(c, &D.E, (size_t)nl * 9)); CK(dalloc(c, &D.S, (size_t)nl * 9));
         std::vector<double2> lame(nl);
-        std::vector<double> irho(nl), Lm((size_t)nl * 9);
+        std::vector<double> irho(nl);
         std::vector<int> clamp(nl);
         std::vector<double4> x0(nl);
         for (int s = 0; s < nl; ++s) {
             const int g = lsl[s];
             const int i = S.orig[g];
             const int t = property[i];
-            std::memcpy(&Lm[(size_t)9 * s], &S.normalizer[(size_t)9 * g], sizeof(double) * 9);
             lame[s] = make_double2(S.lame_l[g], S.lame_m[g]);
             irho[s] = 1.0 / cfg->density[t];
-            const double* p0 = pos0 + 3 * i;
+            const double* p0 = pos0 + 3 * (size_t)i;
             int cl = 0;   // updateElasticPosition module clamps (main.cpp:1918-2044)
             switch (cfg->module) {
             case MPH_MODULE_BAR: cl = p0[0] < 0.001 ? 1 : 0; break;
@@ -456,6 +422,75 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         auto up = [&](auto* d, const auto& v) {
             return hipMemcpyAsync(d, v.data(), v.size() * sizeof(v[0]), hipMemcpyHostToDevice, c->stream);
         };
+        HIP_OK(c, up(D.x0, x0));
+        if (gpu_init) {
+            // calculateInitialNeighbor + calculateNormalizer on the device (single context: the
+            // local slots are all slots, in file order); the host keeps counts and normalizers
+            // for mph_get
+            fill_launch(c);
+            auto alloc = [](void* ctx, size_t bytes) -> void* {
+                int st = MPH_OK;
+                return ctx_alloc((MphCtx*)ctx, bytes, &st);
+            };
+            const int r = launch_struct_init(c->L, ns, D.x0, c->key, c->slot, c->tmp, c->rank_of, D.ocnt, D.icnt,
+                                             &D.eo_nb, &D.wo, &D.ei_nb, &D.wi, D.L, D.wx0, alloc, c);
+            if (r == -2) return fail(c, MPH_ERR_NEIGHBOR_OVERFLOW, "a structure particle has >= 512 initial neighbours");
+            if (r == -3) return fail(c, MPH_ERR_DEVICE_OOM, "structure list allocation failed");
+            if (r != 0) return fail(c, MPH_ERR_HIP, "structure initialisation kernels failed");
+            S.count.resize(ns);
+            S.normalizer.resize((size_t)ns * 9);
+            HIP_OK(c, hipMemcpyAsync(S.count.data(), D.ocnt, sizeof(int) * ns, hipMemcpyDeviceToHost, c->stream));
+            HIP_OK(c, hipMemcpyAsync(S.normalizer.data(), D.L, sizeof(double) * 9 * ns, hipMemcpyDeviceToHost,
+                                     c->stream));
+            HIP_OK(c, hipStreamSynchronize(c->stream));
+        } else {
+            // ELL tiles of the host-built fixed out-list and of its transpose (StructDev), computed slots only
+            const size_t ntile_s = ((size_t)std::max(no, 1) + 63) / 64;
+            std::vector<int> ocnt(std::max(no, 1), 0), icnt(std::max(no, 1), 0);
+            int wo = 0, wi = 0;
+            for (int s = 0; s < no; ++s) {
+                const int g = lsl[s];
+                ocnt[s] = S.offset[g + 1] - S.offset[g];
+                icnt[s] = S.in_offset[g + 1] - S.in_offset[g];
+                wo = std::max(wo, ocnt[s]);
+                wi = std::max(wi, icnt[s]);
+            }
+            wo = std::max(wo, 1);
+            wi = std::max(wi, 1);
+            D.wo = wo;
+            D.wi = wi;
+            std::vector<int> eo_nb(ntile_s * wo * 64, 0), ei_nb(ntile_s * wi * 64, 0);
+            std::vector<double4> wx0(nl, make_double4(0.0, 0.0, 0.0, 0.0));
+            for (int s = 0; s < no; ++s) {
+                const int g = lsl[s];
+                const size_t base_o = (size_t)(s >> 6) * wo * 64 + (s & 63);
+                double c3[3] = {0.0, 0.0, 0.0};
+                for (int k = 0; k < ocnt[s]; ++k) {
+                    const size_t q = S.offset[g] + k;
+                    const double* pr = &S.pair_out[4 * q];
+                    eo_nb[base_o + (size_t)k * 64] = loc[S.nbr[q]];
+                    for (int d = 0; d < 3; ++d) c3[d] += pr[3] * pr[d];
+                }
+                wx0[s] = make_double4(c3[0], c3[1], c3[2], 0.0);
+                const size_t base_i = (size_t)(s >> 6) * wi * 64 + (s & 63);
+                for (int k = 0; k < icnt[s]; ++k) {
+                    const size_t q = S.in_offset[g] + k;
+                    ei_nb[base_i + (size_t)k * 64] = loc[S.in_nbr[q]];
+                }
+            }
+            for (int e : eo_nb) if (e < 0) return fail(c, MPH_ERR_DOMAIN, "structure list leaves the ghost slots");
+            for (int e : ei_nb) if (e < 0) return fail(c, MPH_ERR_DOMAIN, "structure list leaves the ghost slots");
+            std::vector<double> Lm((size_t)nl * 9);
+            for (int s = 0; s < nl; ++s)
+                std::memcpy(&Lm[(size_t)9 * s], &S.normalizer[(size_t)9 * lsl[s]], sizeof(double) * 9);
+            CK(dalloc(c, &D.eo_nb, eo_nb.size()));
+            CK(dalloc(c, &D.ei_nb, ei_nb.size()));
+            HIP_OK(c, up(D.ocnt, ocnt)); HIP_OK(c, up(D.icnt, icnt));
+            HIP_OK(c, up(D.eo_nb, eo_nb));
+            HIP_OK(c, up(D.ei_nb, ei_nb));
+            HIP_OK(c, up(D.wx0, wx0));
+            HIP_OK(c, up(D.L, Lm));
+        }
         HIP_OK(c, hipMemcpyAsync(D.orig, c->sl_orig.data(), sizeof(int) * nl, hipMemcpyHostToDevice, c->stream));
         {
             std::vector<int> slot_of((size_t)c->n_glob, -1);
@@ -463,15 +498,9 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
             CK(dalloc(c, &D.slot_of, slot_of.size()));
             HIP_OK(c, hipMemcpy(D.slot_of, slot_of.data(), sizeof(int) * slot_of.size(), hipMemcpyHostToDevice));
         }
-        HIP_OK(c, up(D.ocnt, ocnt)); HIP_OK(c, up(D.icnt, icnt));
-        HIP_OK(c, up(D.eo_nb, eo_nb));
-        HIP_OK(c, up(D.ei_nb, ei_nb));
-        HIP_OK(c, up(D.wx0, wx0));
-        HIP_OK(c, up(D.L, Lm));
         HIP_OK(c, up(D.lame, lame));
         HIP_OK(c, up(D.inv_rho, irho));
         HIP_OK(c, up(D.clamp, clamp));
-        HIP_OK(c, up(D.x0, x0));
         HIP_OK(c, hipMemsetAsync(D.P, 0, sizeof(double4) * (sd == 2 ? 1 : 3) * nl, c->stream));
         HIP_OK(c, hipMemsetAsync(D.u, 0, sizeof(double4) * nl, c->stream));
         HIP_OK(c, hipMemsetAsync(D.bidx, 0, sizeof(int) * nl, c->stream));

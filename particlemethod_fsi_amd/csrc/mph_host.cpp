@@ -740,7 +740,7 @@ static void parallel_ranges(int n, F f)
 }
 
 int build_structure(const MphConfig& c, const HostDerived& h, int n, const int* prop,
-                    const double* pos0, StructureInit& S, std::string& err)
+                    const double* pos0, StructureInit& S, std::string& err, bool lists)
 {
     S.orig.clear();
     for (int i = 0; i < n; ++i)
@@ -753,6 +753,19 @@ int build_structure(const MphConfig& c, const HostDerived& h, int n, const int* 
     S.lame_l.assign(ns, 0.0);
     S.lame_m.assign(ns, 0.0);
     if (ns == 0) return MPH_OK;
+    if (!lists) {
+        S.offset.clear();
+        S.in_offset.clear();
+        S.in_nbr.clear();
+        S.pair_out.clear();
+        for (int s = 0; s < ns; ++s) {   // Lame constants, main.cpp:2533-2539
+            const int t = prop[S.orig[s]];
+            const double E = c.young_modulus[t], v = c.poisson_ratio[t];
+            S.lame_l[s] = (E * v) / ((1.0 + v) * (1.0 - 2.0 * v));
+            S.lame_m[s] = E / (2.0 * (1.0 + v));
+        }
+        return MPH_OK;
+    }
     const int dim = c.dim;
     const double rc = h.max_radius + (0.1 * h.dx);
     const double rc2 = rc * rc;

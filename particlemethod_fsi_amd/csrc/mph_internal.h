@@ -24,7 +24,9 @@ void derive_constants(const MphConfig& c, HostDerived& h);
 void fill_scalars(const HostDerived& h, const MphConfig& c, double* out36);
 int choose_grid(const HostDerived& h, int dim, double rc, int sub, int gc[3], double ginv[3], std::string& err);
 void make_dev_params(const MphConfig& c, const HostDerived& h, int n, int n_struct, DevParams& P);
+// lists = false: only the slots (orig), zero counts and the Lame constants (the device builds the
+// lists and normalizers, launch_struct_init)
 int build_structure(const MphConfig& c, const HostDerived& h, int n, const int* prop,
-                    const double* pos0, StructureInit& S, std::string& err);
+                    const double* pos0, StructureInit& S, std::string& err, bool lists = true);
 
 }  // namespace mph

@@ -93,6 +93,14 @@ void launch_neighbors(const Launch& L);
 void launch_pass_a(const Launch& L);
 void launch_pass_b(const Launch& L, int phase = 0);   // phase: 0 all, 1/2 slab inner/near-face
 void launch_structure(const Launch& L);
+// calculateInitialNeighbor + calculateNormalizer of the ns structure slots (x0 in slot order) on
+// the device: counts (ocnt), ELL out-rows (*eo, width *wo) and their transpose (*ei, *wi), both
+// sorted ascending, Normalizer (Lm [ns][9]) and sum_j w_sj x0_sj (wx0).  The ELL arrays are
+// allocated through alloc(actx, bytes) once their widths are known.  key/slot/tmp/sorted: ns
+// ints of scratch each.  Returns 0, -1 (HIP error), -2 (a slot reached 512 neighbours), -3 (OOM).
+int launch_struct_init(const Launch& L, int ns, const double4* x0, int* key, int* slot, int* tmp, int* sorted,
+                       int* ocnt, int* icnt, int** eo, int* wo, int** ei, int* wi, double* Lm, double4* wx0,
+                       void* (*alloc)(void*, size_t), void* actx);
 void launch_struct_stress(const Launch& L);
 void launch_struct_velocity(const Launch& L, bool last);
 // slab mode: rows of per-slot double4 records (w per slot) gathered into / scattered from a message

@@ -31,6 +31,7 @@
 
 #include <climits>
 #include <cstdlib>
+#include <vector>
 
 #include "mph_kernels.h"
 #include "mph_params.h"
@@ -1525,6 +1526,188 @@ __global__ __launch_bounds__(256) void k_struct_velocity(DevParams P, int ns, in
     su[s] = struct_disp(P, xn, x0s);
 }
 
+// --------------------------------------------------------- elastic-solid initialisation ----
+// calculateInitialNeighbor (main.cpp:1497-1658), calculateNormalizer (2544-2653) on the device.
+// The structure slots (x0 in slot = file order) are binned on the GPU cell grid of the fluid
+// search (cells >= rc/2, the contiguous axis halved); each slot scans the 5x5(x9) stencil of
+// slot cells with the reference's exact test  q0^2+q1^2+q2^2 <= (MaxRadius+MARGIN)^2  on the
+// Mod image of InitialPosition (2-D: q2 = 0, main.cpp:1605), structure j only (the binned set).
+// Rows are then sorted ascending, the transpose (the senders of calculateStressForce's scatter)
+// is built with atomics and sorted, and the normalizer sums run over the sorted rows in the
+// host's order -- so lists, counts, Normalizer and the fixed sum w x0 equal the host build.
+
+__global__ __launch_bounds__(256) void k_sinit_bin(DevParams P, int ns, const double4* __restrict__ x0,
+                                                   int* __restrict__ key, int* __restrict__ cnt,
+                                                   int* __restrict__ slot)
+{
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ns) return;
+    const double4 p = x0[s];
+    const int k = cell_id(P, p.x, p.y, p.z);
+    key[s] = k;
+    slot[s] = atomicAdd(&cnt[k], 1);
+}
+
+// cell order, slot-ascending inside a cell (deterministic)
+__global__ __launch_bounds__(256) void k_sinit_place(int ns, const int* __restrict__ key,
+                                                     const int* __restrict__ slot,
+                                                     const int* __restrict__ start, int* __restrict__ tmp,
+                                                     int* __restrict__ sorted, int phase)
+{
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ns) return;
+    const int k = key[s];
+    if (phase == 0) {
+        tmp[start[k] + slot[s]] = s;
+        return;
+    }
+    const int b = start[k], e = start[k + 1];
+    int r = 0;
+    for (int q = b; q < e; ++q) r += tmp[q] < s;
+    sorted[b + r] = s;
+}
+
+// mode 0: count the row of every slot; mode 1: write it into the ELL tile rows (width w, stencil
+// order) -- per-slot overflow (>= 512, main.cpp:1609-1611) raises the error flag
+template <int DIM>
+__global__ __launch_bounds__(256) void k_sinit_search(DevParams P, int ns, const double4* __restrict__ x0,
+                                                      const int* __restrict__ start,
+                                                      const int* __restrict__ sorted, int* __restrict__ ocnt,
+                                                      int* __restrict__ ell, int w, int mode,
+                                                      DevState* __restrict__ st)
+{
+#pragma clang fp contract(off)
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ns) return;
+    const double4 xi = x0[s];
+    const int cx = cell_axis(xi.x, P.corg[0], P.dw[0], P.ginv[0], P.gc[0]);
+    const int cy = cell_axis(xi.y, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
+    const int cz = DIM == 3 ? cell_axis(xi.z, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
+    // stencil half-widths in cells: 2 across (cells >= rc/2), P.sa along the contiguous axis
+    const int ry = DIM == 3 ? 2 : P.sa, rz = DIM == 3 ? P.sa : 0;
+    int c = 0;
+    for (int dx = -2; dx <= 2; ++dx) {
+        const int jx = wrap_cell(cx + dx, P.gc[0]);
+        for (int dy = -ry; dy <= ry; ++dy) {
+            const int jy = wrap_cell(cy + dy, P.gc[1]);
+            for (int dz = -rz; dz <= rz; ++dz) {
+                const int jz = DIM == 3 ? wrap_cell(cz + dz, P.gc[2]) : 0;
+                const int cell = (jx * P.gc[1] + jy) * P.gc[2] + jz;
+                for (int q = start[cell], e = start[cell + 1]; q < e; ++q) {
+                    const int t = sorted[q];
+                    if (t == s) continue;
+                    const double4 xj = x0[t];
+                    const double q0 = image_exact<false>(xj.x - xi.x, P.dw[0], P.hw[0], P.w075[0]);
+                    const double q1 = image_exact<false>(xj.y - xi.y, P.dw[1], P.hw[1], P.w075[1]);
+                    const double q2 = DIM == 3 ? image_exact<false>(xj.z - xi.z, P.dw[2], P.hw[2], P.w075[2]) : 0.0;
+                    if (r2_exact(q0, q1, q2) <= P.rc2) {
+                        if (mode == 1 && c < w) ell[sell(s, w, c)] = t;
+                        ++c;
+                    }
+                }
+            }
+        }
+    }
+    if (mode == 0) {
+        ocnt[s] = c;
+        if (c >= kMaxNeighbor) atomicOr(&st->overflow, 1);
+    }
+}
+
+// ascending order inside each ELL row (insertion sort in place; rows are <= ~80 long)
+__global__ __launch_bounds__(256) void k_sinit_sort_rows(int ns, const int* __restrict__ cnt, int* __restrict__ ell,
+                                                         int w)
+{
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ns) return;
+    const int n = cnt[s];
+    for (int a = 1; a < n; ++a) {
+        const int v = ell[sell(s, w, a)];
+        int b = a - 1;
+        while (b >= 0 && ell[sell(s, w, b)] > v) {
+            ell[sell(s, w, b + 1)] = ell[sell(s, w, b)];
+            --b;
+        }
+        ell[sell(s, w, b + 1)] = v;
+    }
+}
+
+// transpose: mode 0 counts the in-degree, mode 1 appends s to the in-row of every t it lists
+__global__ __launch_bounds__(256) void k_sinit_transpose(int ns, const int* __restrict__ ocnt,
+                                                         const int* __restrict__ eo, int wo,
+                                                         int* __restrict__ icnt, int* __restrict__ ei, int wi,
+                                                         int mode)
+{
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ns) return;
+    const int n = ocnt[s];
+    for (int k = 0; k < n; ++k) {
+        const int t = eo[sell(s, wo, k)];
+        const int pos = atomicAdd(&icnt[t], 1);
+        if (mode == 1) ei[sell(t, wi, pos)] = s;
+    }
+}
+
+// calculateNormalizer (main.cpp:2555-2651) over the sorted row: the 3x3 accumulation in both
+// dimensions (the TWO_DIMENSION typo of 2545), 2-D inverse with the identity fallback, 3-D
+// cofactor inverse (left unchanged when det = 0, like the reference); plus the fixed sum of
+// w_sj x0_sj that the P_s half of the gather-form stress force uses
+template <int DIM>
+__global__ __launch_bounds__(256) void k_sinit_normalizer(DevParams P, int ns, const double4* __restrict__ x0,
+                                                          const int* __restrict__ ocnt,
+                                                          const int* __restrict__ eo, int wo,
+                                                          double* __restrict__ L, double4* __restrict__ wx0)
+{
+#pragma clang fp contract(off)
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ns) return;
+    const double4 xi = x0[s];
+    double N[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
+    double c3[3] = {0.0, 0.0, 0.0};
+    const int n = ocnt[s];
+    for (int k = 0; k < n; ++k) {
+        const double4 xj = x0[eo[sell(s, wo, k)]];
+        const double4 pr = struct_pair<DIM>(P, xi, xj);
+        // the accumulation runs over all three components: in 2-D the z image of equal z is 0
+        const double q[3] = {pr.x, pr.y, image_exact<false>(xj.z - xi.z, P.dw[2], P.hw[2], P.w075[2])};
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) N[a][b] += pr.w * q[a] * q[b];
+        c3[0] += pr.w * pr.x;
+        c3[1] += pr.w * pr.y;
+        c3[2] += pr.w * pr.z;
+    }
+    if (DIM == 2) {
+        const double a = N[0][0], b = N[0][1], cc = N[1][0], d = N[1][1];
+        const double det = a * d - b * cc;
+        if (det != 0.0) {
+            N[0][0] = d / det; N[0][1] = -b / det; N[1][0] = -cc / det; N[1][1] = a / det;
+        } else {
+            N[0][0] = 1.0; N[0][1] = 0.0; N[1][0] = 0.0; N[1][1] = 1.0;
+        }
+    } else {
+        const double det = N[0][0] * (N[1][1] * N[2][2] - N[1][2] * N[2][1])
+                         - N[0][1] * (N[1][0] * N[2][2] - N[1][2] * N[2][0])
+                         + N[0][2] * (N[1][0] * N[2][1] - N[1][1] * N[2][0]);
+        if (det != 0.0) {
+            double adj[3][3];
+            adj[0][0] = N[1][1] * N[2][2] - N[1][2] * N[2][1];
+            adj[0][1] = -N[1][0] * N[2][2] + N[1][2] * N[2][0];
+            adj[0][2] = N[1][0] * N[2][1] - N[1][1] * N[2][0];
+            adj[1][0] = -N[0][1] * N[2][2] + N[0][2] * N[2][1];
+            adj[1][1] = N[0][0] * N[2][2] - N[0][2] * N[2][0];
+            adj[1][2] = -N[0][0] * N[2][1] + N[0][1] * N[2][0];
+            adj[2][0] = N[0][1] * N[1][2] - N[0][2] * N[1][1];
+            adj[2][1] = -N[0][0] * N[1][2] + N[0][2] * N[1][0];
+            adj[2][2] = N[0][0] * N[1][1] - N[0][1] * N[1][0];
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) N[a][b] = adj[a][b] / det;
+        }
+    }
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) L[(size_t)s * 9 + 3 * a + b] = N[a][b];
+    wx0[s] = make_double4(c3[0], c3[1], c3[2], 0.0);
+}
+
 // ------------------------------------------------------------------ slab decomposition -----
 // Multi-GPU redistribution (mph_dist.hip).  Every B entry is classified by its slab coordinate
 // after this step's wall motion + periodic wrap; a stable partition then writes the owned and
@@ -1910,6 +2093,71 @@ void launch_structure(const Launch& L)
         launch_struct_stress(L);
         launch_struct_velocity(L, sub == L.P->substeps - 1);
     }
+}
+
+int launch_struct_init(const Launch& L, int ns, const double4* x0, int* key, int* slot, int* tmp, int* sorted,
+                       int* ocnt, int* icnt, int** eo, int* wo, int** ei, int* wi, double* Lm, double4* wx0,
+                       void* (*alloc)(void*, size_t), void* actx)
+{
+    Profiler* prof = L.prof;
+    const DevParams& P = *L.P;
+    if (ns <= 0) return 0;
+    const dim3 g(blocks(ns, 256)), b(256);
+    // bin the slots on the grid (L.cnt is zero between steps and the scan re-zeroes it)
+    MPH_LAUNCH("sinit_bin", L.stream, k_sinit_bin, g, b, 0, L.stream, P, ns, x0, key, L.cnt, slot);
+    launch_scan(L.cnt, P.ncell, L.bsum, L.start, ns, L.stream, prof);
+    MPH_LAUNCH("sinit_place", L.stream, k_sinit_place, g, b, 0, L.stream, ns, key, slot, L.start, tmp, sorted, 0);
+    MPH_LAUNCH("sinit_place", L.stream, k_sinit_place, g, b, 0, L.stream, ns, key, slot, L.start, tmp, sorted, 1);
+    if (P.dim == 3)
+        MPH_LAUNCH("sinit_search", L.stream, k_sinit_search<3>, g, b, 0, L.stream, P, ns, x0, L.start, sorted, ocnt,
+                   (int*)nullptr, 0, 0, L.st);
+    else
+        MPH_LAUNCH("sinit_search", L.stream, k_sinit_search<2>, g, b, 0, L.stream, P, ns, x0, L.start, sorted, ocnt,
+                   (int*)nullptr, 0, 0, L.st);
+    // ELL width = the longest row (one host read at initialisation)
+    std::vector<int> h(ns);
+    if (hipMemcpyAsync(h.data(), ocnt, sizeof(int) * ns, hipMemcpyDeviceToHost, L.stream) != hipSuccess ||
+        hipStreamSynchronize(L.stream) != hipSuccess)
+        return -1;
+    int w = 1;
+    for (int v : h) w = v > w ? v : w;
+    if (w >= kMaxNeighbor) return -2;
+    const size_t ntile = ((size_t)ns + 63) / 64;
+    *eo = (int*)alloc(actx, ntile * w * 64 * sizeof(int));
+    if (!*eo) return -3;
+    if (hipMemsetAsync(*eo, 0, ntile * w * 64 * sizeof(int), L.stream) != hipSuccess) return -1;
+    if (P.dim == 3)
+        MPH_LAUNCH("sinit_search", L.stream, k_sinit_search<3>, g, b, 0, L.stream, P, ns, x0, L.start, sorted, ocnt,
+                   *eo, w, 1, L.st);
+    else
+        MPH_LAUNCH("sinit_search", L.stream, k_sinit_search<2>, g, b, 0, L.stream, P, ns, x0, L.start, sorted, ocnt,
+                   *eo, w, 1, L.st);
+    MPH_LAUNCH("sinit_sort_rows", L.stream, k_sinit_sort_rows, g, b, 0, L.stream, ns, ocnt, *eo, w);
+    *wo = w;
+    // transpose: in-degrees, width, then the rows (atomic order) sorted ascending
+    if (hipMemsetAsync(icnt, 0, sizeof(int) * ns, L.stream) != hipSuccess) return -1;
+    MPH_LAUNCH("sinit_transpose", L.stream, k_sinit_transpose, g, b, 0, L.stream, ns, ocnt, *eo, w, icnt,
+               (int*)nullptr, 0, 0);
+    if (hipMemcpyAsync(h.data(), icnt, sizeof(int) * ns, hipMemcpyDeviceToHost, L.stream) != hipSuccess ||
+        hipStreamSynchronize(L.stream) != hipSuccess)
+        return -1;
+    int wi2 = 1;
+    for (int v : h) wi2 = v > wi2 ? v : wi2;
+    *ei = (int*)alloc(actx, ntile * wi2 * 64 * sizeof(int));
+    if (!*ei) return -3;
+    if (hipMemsetAsync(*ei, 0, ntile * wi2 * 64 * sizeof(int), L.stream) != hipSuccess) return -1;
+    if (hipMemsetAsync(icnt, 0, sizeof(int) * ns, L.stream) != hipSuccess) return -1;
+    MPH_LAUNCH("sinit_transpose", L.stream, k_sinit_transpose, g, b, 0, L.stream, ns, ocnt, *eo, w, icnt, *ei,
+               wi2, 1);
+    MPH_LAUNCH("sinit_sort_rows", L.stream, k_sinit_sort_rows, g, b, 0, L.stream, ns, icnt, *ei, wi2);
+    *wi = wi2;
+    if (P.dim == 3)
+        MPH_LAUNCH("sinit_normalizer", L.stream, k_sinit_normalizer<3>, g, b, 0, L.stream, P, ns, x0, ocnt, *eo, w,
+                   Lm, wx0);
+    else
+        MPH_LAUNCH("sinit_normalizer", L.stream, k_sinit_normalizer<2>, g, b, 0, L.stream, P, ns, x0, ocnt, *eo, w,
+                   Lm, wx0);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 void launch_struct_pack(const Launch& L, const double4* src, int w, const int* idx, int m, double4* buf)

@@ -233,3 +233,39 @@ def test_gpu_vtu_matches_state(tmp_path):
         np.testing.assert_array_equal(d["force"], f32(s.get("Force")))
         np.testing.assert_array_equal(d["neighbor"], s.get("NeighborCount"))
         np.testing.assert_array_equal(d["label"], parts.property)
+
+
+@pytest.mark.parametrize("case", ["bar2d", "bar3d", "gate3d_sub", "gate2d_sub", "hydro2d", "turek2d"])
+def test_gpu_structure_init_equals_host_build(case, monkeypatch):
+    """calculateInitialNeighbor + calculateNormalizer run on the device (launch_struct_init) for a
+    single context: the counts, Normalizer and Lame constants equal the host build
+    (mph_structure_init, pinned to the reference by the s0 goldens) bit for bit, and the lists
+    (sorted like the host's) give bitwise the same steps as a context built on the host."""
+    from particlemethod_fsi_amd import solver
+    import ctypes
+    cfg, parts = cases.get(case).build()
+    n = parts.n
+    isnc = np.zeros(n, np.int32)
+    nrm = np.zeros((n, 3, 3))
+    ll, lm = np.zeros(n), np.zeros(n)
+    prop = np.ascontiguousarray(parts.property, np.int32)
+    x0 = np.ascontiguousarray(parts.initial_position)
+    assert solver.load_library().mph_structure_init(ctypes.byref(cfg), n, prop.ctypes.data, x0.ctypes.data,
+                                                    isnc.ctypes.data, nrm.ctypes.data, ll.ctypes.data,
+                                                    lm.ctypes.data) == 0
+    outs = []
+    for mode in ("device", "host"):
+        if mode == "host":
+            monkeypatch.setenv("MPH_STRUCT_INIT", "host")
+        with MphSolver(cfg, parts) as s:
+            got = {f: s.get(f) for f in ("InitialStructureNeighborCount", "Normalizer", "LambdaLames", "MuLames")}
+            s.step(5)
+            got["Position"] = s.get("Position")
+            got["Stress"] = s.get("Stress")
+            outs.append(got)
+    dev, host = outs
+    assert np.array_equal(dev["InitialStructureNeighborCount"], isnc)
+    assert np.array_equal(dev["Normalizer"], nrm)
+    assert np.array_equal(dev["LambdaLames"], ll) and np.array_equal(dev["MuLames"], lm)
+    for f in dev:
+        assert np.array_equal(dev[f], host[f]), f
