@@ -211,8 +211,12 @@ int mph_structure_init(const MphConfig* cfg, int n, const int* property, const d
  * the reference's initialisation sums (main.cpp:534-570).                                    */
 int mph_create(MphCtx** ctx, const MphConfig* cfg, int n, const int* property,
                const double* pos, const double* pos0, const double* vel, int device);
-/* Advance nsteps time steps (main.cpp:597-686 each).  Steps are replayed from a captured
- * hipGraph; returns MPH_ERR_NEIGHBOR_OVERFLOW if any particle reached 512 neighbours.        */
+/* Advance nsteps time steps (main.cpp:597-686 each).  Steps are replayed from captured
+ * hipGraphs of 8 and 1 steps; returns MPH_ERR_NEIGHBOR_OVERFLOW if any particle reached 512
+ * neighbours.  The output-only fields (Force, Acceleration, DensityA, VolStrainP, DivergenceP,
+ * and GravityCenter/PressureA without surface tension) are stored by the last step of each
+ * replayed batch, so after a successful mph_step they hold that step's values; after an error
+ * they are undefined (the state itself -- Position, Velocity -- is the failing step's).        */
 int mph_step(MphCtx* ctx, int nsteps);
 int mph_synchronize(MphCtx* ctx);
 /* Copy a field to host, AoS, original particle order.                                      */

@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 
@@ -2029,6 +2030,12 @@ void launch_pass_b(const Launch& L, int phase)
     Profiler* prof = L.prof;
     const DevParams& P = *L.P;
     if (P.n == 0) return;
+    // pass B reads GravityCenter and PressureA of every neighbour with surface tension; enqueue_step
+    // may leave them unstored on the non-last steps of a batch only without it
+    if (P.surface && !(L.gx && L.gy && L.gz && L.pa)) {
+        std::fprintf(stderr, "mph: launch_pass_b with surface tension needs GravityCenter/PressureA\n");
+        std::abort();
+    }
 #define MPH_PASS_B(S, D)                                                                            \
     MPH_LAUNCH("pass_b", L.stream, (k_pass_b<S, D>), dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, \
                L.T, L.A, L.rec, L.fpart, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, L.force, L.acc, L.B, phase, \
