@@ -78,6 +78,7 @@ struct MphCtx {
     int *key = nullptr, *slot = nullptr, *tmp = nullptr, *cnt = nullptr, *start = nullptr, *bsum = nullptr;
     double *vir = nullptr, *vpres = nullptr;   // VirialStress [cap][9] / VirialPressure (A order), lazy
     int *nbr = nullptr, *ncount = nullptr;
+    int2* seg_hdr = nullptr;     // per-wave list headers (column-segmented lists)
     double *pres = nullptr, *gx = nullptr, *gy = nullptr, *gz = nullptr, *pa = nullptr;
     double4 *force = nullptr, *acc = nullptr, *fpart = nullptr, *rec = nullptr;
     double *dens_a = nullptr, *vstrain = nullptr, *divp = nullptr;

@@ -599,7 +599,14 @@ int dist_step(MphCtx* c, int nsteps, Profiler* prof)
     MphDist& D = *c->dist;
     int left = nsteps;
     if (D.graphs && !prof) {
-        if (!c->graph1) MPH_CK(dist_capture(c, 1, &c->graph1));
+        // a capture the runtime refuses (an RCCL build without graph support) falls back to the
+        // same steps as direct launches, reported by mph_dist_info
+        if (!c->graph1 && dist_capture(c, 1, &c->graph1) != MPH_OK) {
+            (void)hipGetLastError();
+            D.graphs = false;
+            c->err.clear();
+            return dist_step(c, nsteps, prof);
+        }
         if (!c->graph8 && nsteps >= 8) MPH_CK(dist_capture(c, 8, &c->graph8));
         while (left >= 8) { MPH_HIP_OK(c, hipGraphLaunch(c->graph8, c->stream)); left -= 8; }
         while (left > 0) { MPH_HIP_OK(c, hipGraphLaunch(c->graph1, c->stream)); left -= 1; }

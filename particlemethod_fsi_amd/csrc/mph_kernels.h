@@ -79,6 +79,7 @@ struct Launch {
     int* dst_of = nullptr;        // slab mode: pre-sort index -> sorted index (else rank_of[id])
     int *key = nullptr, *slot = nullptr, *tmp = nullptr, *cnt = nullptr, *start = nullptr, *bsum = nullptr;
     int *nbr = nullptr, *ncount = nullptr;
+    int2* hdr = nullptr;          // per-wave headers of the column-segmented lists (kSegHdr each)
     // pass A products (A order): pressure values, gravity centre (GC, PressureA), sums
     double *pres = nullptr, *gx = nullptr, *gy = nullptr, *gz = nullptr, *pa = nullptr;
     double *dens_a = nullptr, *vstrain = nullptr, *divp = nullptr;

@@ -196,6 +196,32 @@ __device__ __forceinline__ const int* ell_row(const int* nbr, int i)
     return nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
 }
 
+// Column-segmented neighbour list of an interior wavefront (MPH_SEG).  The search visits the
+// stencil columns in order; per column the wave's candidates form one window [mn, mn + span) of
+// the cell-sorted arrays.  Each column gets a segment of W slots (W = the most any lane accepted
+// there), slot k of lane l at seg[k][l] (uint16): the offset of the neighbour in the window (8 bits)
+// and its type (bits 8-10), or kSegNone in the padding.  A column whose window exceeds the staging
+// capacity is "wide": two slots per entry, the low and high halves of the sorted index (type in
+// bits 12-14 of the high half).  Per wave the header holds, per column, {mn, span | W << 16 |
+// wide << 31}, and in entry kSegCols the list format (1 = segmented, 0 = the ELL rows).  The
+// entries of a lane come in the same order as in its ELL row (column order, ascending index), so
+// both formats give bit-identical sums.  The segments reuse the wave's ELL tile (128 KB).
+#ifndef MPH_SEG
+#define MPH_SEG 0   // measured slower: pass A 0.44 -> 0.92 ms at D1M
+#endif
+constexpr int kSegCols = kSegHdr - 1;              // stencil columns (3-D; 2-D uses 5)
+constexpr int kSegCap = kTile * kMaxNeighbor * 4 / (2 * kTile);   // 1024 slots of 64 x uint16
+constexpr unsigned short kSegNone = 0xFFFF;
+
+__device__ __forceinline__ unsigned short* seg_tile(int* nbr, int i)
+{
+    return reinterpret_cast<unsigned short*>(nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor));
+}
+__device__ __forceinline__ const unsigned short* seg_tile(const int* nbr, int i)
+{
+    return reinterpret_cast<const unsigned short*>(nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor));
+}
+
 // ------------------------------------------------------------------------- sort phase -------
 
 // calculateWall (main.cpp:3031-3060) + calculatePeriodicBoundary (3322-3333) + cell histogram.
@@ -751,10 +777,11 @@ __device__ __forceinline__ int wave_max(int v)
 // texture-address unit was the bound; a staged column costs 4.  Same candidates, same order,
 // same FP64 test as scan_candidates, so the list is identical.  Every lane of the wave must call
 // this (act = live particle); the column loop and the staging are wave-uniform.
-template <int DIM, int SB = MPH_SB, int CAP = MPH_LDS_CAP>
+template <int DIM, bool SEG, int SB = MPH_SB, int CAP = MPH_LDS_CAP>
 __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa& A, const int* start,
                                                    int i, bool act, double xi, double yi, double zi,
-                                                   int cx, int cy, int cz, int* out, double* sx)
+                                                   int cx, int cy, int cz, int* out, double* sx,
+                                                   unsigned short* seg, int2* hdr, int* seg_overflow)
 {
     double* sy = sx + (CAP + SB);
     double* sz = sx + 2 * (CAP + SB);
@@ -800,6 +827,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     // staged and tested (the per-column chain start[] -> window -> staging loads is latency bound)
     int nb_jb, nb_je;
     col_range(0, nb_jb, nb_je);
+    int slot = 0;   // SEG: first slot of this column's segment
     for (int col = 0; col < NCOL; ++col) {
         const int jb = nb_jb, je = nb_je;
         if (MPH_SEARCH_PREFETCH && col + 1 < NCOL) col_range(col + 1, nb_jb, nb_je);
@@ -807,8 +835,12 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
         const int mn = wave_min(any ? jb : 0x7fffffff);
         const int mx = wave_max(any ? je : -1);
         if (!MPH_SEARCH_PREFETCH && col + 1 < NCOL) col_range(col + 1, nb_jb, nb_je);
-        if (mx <= mn) continue;   // wave-uniform: no lane has candidates in this column
+        if (mx <= mn) {   // wave-uniform: no lane has candidates in this column
+            if (SEG && lane == 0) hdr[col] = make_int2(0, 0);
+            continue;
+        }
         const int span = mx - mn;
+        const int cnt0 = cnt;   // SEG: this lane's entries before the column
         if (MPH_DIAG_SEARCH & 2) { cnt += span & 1; continue; }
         if (span <= CAP) {
             for (int t = lane; t < span; t += 64) {
@@ -838,8 +870,13 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                     const bool a = accept_interior(P, xs[u] - xi, ys[u] - yi, zs[u] - zi, lo2, hi2) &
                                    (j < je) & (j != i);
                     if (a) {
-                        if (!MPH_DIAG_NOSTORE)
+                        if (SEG) {
+                            const int sl = slot + (cnt - cnt0);
+                            if (sl < kSegCap)
+                                seg[(size_t)sl * kTile + lane] = (unsigned short)((j - mn) | (st[k0 + u] << 8));
+                        } else if (!MPH_DIAG_NOSTORE) {
                             list_store(out + min(cnt, kMaxNeighbor - 1) * kTile, nbr_entry(j, st[k0 + u]));
+                        }
                         ++cnt;
                     }
                 }
@@ -859,20 +896,40 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                 for (int u = 0; u < SB; ++u) {
                     const int j = j0 + u;
                     if (accept_interior(P, xs[u] - xi, ys[u] - yi, zs[u] - zi, lo2, hi2) && j < je && j != i) {
-                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) list_store(out + cnt * kTile, nbr_entry(j, A.type[j]));
+                        if (SEG) {
+                            const int sl = slot + 2 * (cnt - cnt0);
+                            if (sl + 1 < kSegCap) {
+                                seg[(size_t)sl * kTile + lane] = (unsigned short)(j & 0xFFFF);
+                                seg[(size_t)(sl + 1) * kTile + lane] = (unsigned short)((j >> 16) | (A.type[j] << 12));
+                            }
+                        } else if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) {
+                            list_store(out + cnt * kTile, nbr_entry(j, A.type[j]));
+                        }
                         ++cnt;
                     }
                 }
             }
         }
+        if (SEG) {
+            // close the column's segment: W = the most entries any lane has in it; the others pad
+            const bool wide = span > CAP;
+            const int mine = cnt - cnt0;
+            const int w = wave_max(mine);
+            const int per = wide ? 2 : 1;
+            for (int k = mine * per; k < w * per; ++k)
+                if (slot + k < kSegCap) seg[(size_t)(slot + k) * kTile + lane] = kSegNone;
+            if (lane == 0) hdr[col] = make_int2(mn, (span & 0xFFFF) | (w << 16) | (wide ? (int)0x80000000 : 0));
+            slot += w * per;
+        }
     }
+    if (SEG && slot > kSegCap) *seg_overflow = 1;
     return cnt;
 }
 
 template <int DIM>
 __global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int* __restrict__ start,
                                                    int* __restrict__ nbr, int* __restrict__ ncount,
-                                                   DevState* __restrict__ st)
+                                                   int2* __restrict__ hdr, DevState* __restrict__ st)
 {
     const int n = dev_n(P);
     if ((int)blockIdx.x >= live_blocks(n)) return;
@@ -886,16 +943,31 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int
     const int cy = cell_axis(yi, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
     const int cz = DIM == 3 ? cell_axis(zi, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
     int* out = nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
+    int2* h = hdr ? hdr + (size_t)(i >> 6) * kSegHdr : nullptr;
+    int seg_over = 0;
     if (MPH_SEARCH_LDS && fast) {
         __shared__ double stage[4][3 * (MPH_LDS_CAP + MPH_SB) + (MPH_LDS_CAP + MPH_SB + 1) / 2];
-        cnt = scan_candidates_lds<DIM>(P, A, start, i, live, xi, yi, zi, cx, cy, cz, out,
-                                       stage[threadIdx.x >> 6]);
+        if (MPH_SEG && h) {
+            cnt = scan_candidates_lds<DIM, true>(P, A, start, i, live, xi, yi, zi, cx, cy, cz, out,
+                                                 stage[threadIdx.x >> 6], seg_tile(nbr, i), h, &seg_over);
+            if ((threadIdx.x & 63) == 0) h[kSegCols] = make_int2(1, 0);
+        } else {
+            cnt = scan_candidates_lds<DIM, false>(P, A, start, i, live, xi, yi, zi, cx, cy, cz, out,
+                                                  stage[threadIdx.x >> 6], nullptr, nullptr, nullptr);
+            if (h && (threadIdx.x & 63) == 0) h[kSegCols] = make_int2(0, 0);
+        }
         if (live) ncount[i] = cnt;
-    } else if (live && !(MPH_DIAG_SEARCH & 4)) {
-        cnt = fast ? scan_candidates<DIM, true>(P, A, start, i, xi, yi, zi, cx, cy, cz, out)
-                   : scan_candidates<DIM, false>(P, A, start, i, xi, yi, zi, cx, cy, cz, out);
-        ncount[i] = cnt;
+    } else {
+        if (live && !(MPH_DIAG_SEARCH & 4)) {
+            cnt = fast ? scan_candidates<DIM, true>(P, A, start, i, xi, yi, zi, cx, cy, cz, out)
+                       : scan_candidates<DIM, false>(P, A, start, i, xi, yi, zi, cx, cy, cz, out);
+            ncount[i] = cnt;
+        }
+        if (h && (threadIdx.x & 63) == 0) h[kSegCols] = make_int2(0, 0);
     }
+    // a segmented list past the tile's 1024 slots (far beyond any physical state: ~100 used at
+    // D1M) is reported like a neighbour overflow
+    if (seg_over) atomicOr(&st->overflow, 1);
     // overflow flag (main.cpp:1766-1768 is the reference's limit).  No per-step statistics here:
     // one same-address device atomic per wave serialises at ~11 ns each (21.8k waves at D1M took
     // 0.5 ms); mph_neighbor_stats reduces ncount on demand.
@@ -955,6 +1027,91 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
     }
 }
 
+// Pass A over a column-segmented list (interior waves): per stencil column the wave stages its
+// window of 48-byte records in LDS with coalesced loads and every lane reads its neighbours from
+// there -- instead of per-lane gathers whose 64 lanes touch ~41 cache lines per 16-byte load (the
+// per-CU L1 tag rate bound pass A).  Wide columns (window beyond the staging capacity) gather
+// from global memory.  Every lane of the wave takes part (live = it has a particle).
+template <int DIM, int U = MPH_UA, int CAP = MPH_LDS_CAP>
+__device__ __forceinline__ void pass_a_seg(const DevParams& P, const double* s_ratio, const double* s_mu,
+                                           const Soa& A, const unsigned short* seg, const int2* hdr, bool live,
+                                           int ti, bool solid, double xi, double yi, double zi, double vxi,
+                                           double vyi, double vzi, PassA& o, double2* stage)
+{
+    constexpr int NCOL = DIM == 3 ? 25 : 5;
+    const int lane = threadIdx.x & 63;
+    int slot = 0;
+    for (int col = 0; col < NCOL; ++col) {
+        const int2 h = hdr[col];
+        const int w = (h.y >> 16) & 0x7FFF;
+        if (w == 0) continue;
+        const int mn = h.x;
+        if (h.y >= 0) {
+            const int span = h.y & 0xFFFF;
+            const double2* src = A.p6 + 3 * (size_t)mn;
+            for (int t = lane; t < 3 * span; t += 64) stage[t] = src[t];
+            __builtin_amdgcn_wave_barrier();
+            for (int k0 = 0; k0 < w; k0 += U) {
+                unsigned e[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    e[u] = k0 + u < w ? seg[(size_t)min(slot + k0 + u, kSegCap - 1) * kTile + lane] : kSegNone;
+                double X[U], Y[U], Z[U], VX[U], VY[U], VZ[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int q = e[u] == kSegNone ? 0 : (int)(e[u] & 0xFF);
+                    const double2 a = stage[3 * q], b = stage[3 * q + 1], c = stage[3 * q + 2];
+                    X[u] = a.x; Y[u] = a.y; Z[u] = b.x;
+                    VX[u] = b.y; VY[u] = c.x; VZ[u] = c.y;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (!live || e[u] == kSegNone) continue;
+                    const double q0 = image_exact<true>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
+                    const double q1 = image_exact<true>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
+                    const double q2 = image_exact<true>(Z[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
+                    pass_a_term<true>(P, s_ratio, s_mu, ti, (int)((e[u] >> 8) & 7), solid, q0, q1, q2,
+                                      r2_exact(q0, q1, q2), VX[u] - vxi, VY[u] - vyi, VZ[u] - vzi, o);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();   // every lane done reading before the next staging
+            slot += w;
+        } else {
+            for (int k0 = 0; k0 < w; k0 += U) {
+                int jj[U], TT[U];
+                bool ok[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int sl = min(slot + 2 * (k0 + u), kSegCap - 2);
+                    const unsigned lo = k0 + u < w ? seg[(size_t)sl * kTile + lane] : 0u;
+                    const unsigned hi = k0 + u < w ? seg[(size_t)(sl + 1) * kTile + lane] : kSegNone;
+                    ok[u] = hi != kSegNone;
+                    jj[u] = ok[u] ? (int)(lo | ((hi & 0xFFF) << 16)) : mn;
+                    TT[u] = (int)(hi >> 12) & 7;
+                }
+                double X[U], Y[U], Z[U], VX[U], VY[U], VZ[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const double2* q = A.p6 + 3 * (size_t)jj[u];
+                    const double2 a = q[0], b = q[1], c = q[2];
+                    X[u] = a.x; Y[u] = a.y; Z[u] = b.x;
+                    VX[u] = b.y; VY[u] = c.x; VZ[u] = c.y;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (!live || !ok[u]) continue;
+                    const double q0 = image_exact<true>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
+                    const double q1 = image_exact<true>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
+                    const double q2 = image_exact<true>(Z[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
+                    pass_a_term<true>(P, s_ratio, s_mu, ti, TT[u], solid, q0, q1, q2, r2_exact(q0, q1, q2),
+                                      VX[u] - vxi, VY[u] - vyi, VZ[u] - vzi, o);
+                }
+            }
+            slot += 2 * w;
+        }
+    }
+}
+
 #ifndef MPH_PA_WPE
 #define MPH_PA_WPE 0
 #endif
@@ -966,7 +1123,8 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
 template <int DIM>
 __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const DevTables* __restrict__ T, Soa A,
                                                 const int* __restrict__ nbr,
-                                                const int* __restrict__ ncount, PassAOut pout)
+                                                const int* __restrict__ ncount, const int2* __restrict__ hdr,
+                                                PassAOut pout)
 {
     const int n = dev_n(P);
     if ((int)blockIdx.x >= live_blocks(n)) return;
@@ -981,6 +1139,18 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
     const bool live = i < n;
     const int ii = live ? i : n - 1;
     const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
+    const int2* h = hdr ? hdr + (size_t)(i >> 6) * kSegHdr : nullptr;
+    if (MPH_SEG && h && h[kSegCols].x == 1) {   // wave-uniform: this wave's list is column-segmented
+        __shared__ double2 stage[4][3 * MPH_LDS_CAP];
+        const double vxi = A.vx[ii], vyi = A.vy[ii], vzi = A.vz[ii];
+        const int ti = A.type[ii];
+        const bool solid = dev_is_struct(ti);
+        PassA o;
+        pass_a_seg<DIM>(P, s_ratio, s_mu, A, seg_tile(nbr, i), h, live, ti, solid, xi, yi, zi, vxi, vyi,
+                        vzi, o, stage[threadIdx.x >> 6]);
+        if (live) pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
+        return;
+    }
     const bool fast = wave_interior(P, live, xi, yi, zi);
     if (!live) return;
     const double vxi = A.vx[i], vyi = A.vy[i], vzi = A.vz[i];
@@ -1013,6 +1183,63 @@ __device__ __forceinline__ double4 struct_disp(const DevParams& P, double4 x, do
 #ifndef MPH_PB_REC
 #define MPH_PB_REC 1
 #endif
+// One neighbour's pair forces for pass B (see k_pass_b): PressureP's P_j half, and with surface
+// tension PressureA and DiffuseInterface; structure i takes non-structure j only.
+template <bool FAST, bool SURF, int DIM>
+__device__ __forceinline__ void pass_b_term(const DevParams& P, const double* s_ratio, const double* gx,
+                                            const double* gy, const double* gz, const double* pa, int j, int tj,
+                                            double X, double Y, double Z, double PJ, int ti, bool solid,
+                                            double xi, double yi, double zi, double gxi, double gyi, double gzi,
+                                            double pai, double ai, double dscale, double cpv, double& f0,
+                                            double& f1, double& f2)
+{
+    if (solid && dev_is_struct(tj)) return;
+    const double q0 = image_exact<FAST>(X - xi, P.dw[0], P.hw[0], P.w075[0]);
+    const double q1 = image_exact<FAST>(Y - yi, P.dw[1], P.hw[1], P.w075[1]);
+    const double q2 = image_exact<FAST || DIM == 2>(Z - zi, P.dw[2], P.hw[2], P.w075[2]);
+    const double r2 = r2_exact(q0, q1, q2);
+    if (!SURF || solid) {
+        if (r2 < P.rp2) {
+            double r, ir;
+            rsqrt_pair(r2, r, ir);
+            const double c = PJ * (cpv * (1.0 - r * P.inv_rp)) * ir;
+            f0 += c * q0;
+            f1 += c * q1;
+            f2 += c * q2;
+        }
+        return;
+    }
+    double r, ir;
+    rsqrt_pair(r2, r, ir);
+    double c = 0.0;
+    if (r2 < P.rp2) c += PJ * (cpv * (1.0 - r * P.inv_rp)) * ir;
+    const double rij = s_ratio[ti * kTypes + tj];
+    const double rji = s_ratio[tj * kTypes + ti];
+    const double gxj = gx[j], gyj = gy[j], gzj = gz[j], paj = pa[j];
+    if (r2 < P.ra2) {
+        const double t = r * P.inv_ra;
+        const double dwa = P.cda * (1.0 - t) * (1.0 - 3.0 * t);
+        c += (pai * rij + paj * rji) * dwa * ir * P.vol;
+    }
+    if (r2 < P.rg2) {
+        const double omt = 1.0 - r * P.inv_rg;
+        const double wg = P.cg * omt * omt;
+        const double dwg = P.cdg * omt;
+        const double wij = rij * wg, wji = rji * wg;
+        f0 -= (ai * gxj * wji - ai * gxi * wij) * dscale;
+        f1 -= (ai * gyj * wji - ai * gyi * wij) * dscale;
+        f2 -= (ai * gzj * wji - ai * gzi * wij) * dscale;
+        const double dwij = rij * dwg, dwji = rji * dwg;
+        const double gr = (ai * gxj * dwji - ai * gxi * dwij) * q0 +
+                          (ai * gyj * dwji - ai * gyi * dwij) * q1 +
+                          (ai * gzj * dwji - ai * gzi * dwij) * q2;
+        c -= gr * ir * dscale;
+    }
+    f0 += c * q0;
+    f1 += c * q1;
+    f2 += c * q2;
+}
+
 template <bool FAST, bool SURF, int DIM, int U = MPH_UB>
 __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_ratio, const Soa& A,
                                             const double4* rec, const double* pres, const double* gx,
@@ -1046,55 +1273,81 @@ __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-        if (k0 + u >= cnt) break;
-        if (MPH_DIAG_GATHER == 2) { f0 += X[u] + Y[u] + Z[u] + PJ[u] + TT[u]; continue; }
-        const int tj = TT[u];
-        if (solid && dev_is_struct(tj)) continue;
-        const double q0 = image_exact<FAST>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
-        const double q1 = image_exact<FAST>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
-        const double q2 = image_exact<FAST || DIM == 2>(Z[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
-        const double r2 = r2_exact(q0, q1, q2);
-        if (!SURF || solid) {
-            if (r2 < P.rp2) {
-                double r, ir;
-                rsqrt_pair(r2, r, ir);
-                const double c = PJ[u] * (cpv * (1.0 - r * P.inv_rp)) * ir;
-                f0 += c * q0;
-                f1 += c * q1;
-                f2 += c * q2;
+            if (k0 + u >= cnt) break;
+            if (MPH_DIAG_GATHER == 2) { f0 += X[u] + Y[u] + Z[u] + PJ[u] + TT[u]; continue; }
+            pass_b_term<FAST, SURF, DIM>(P, s_ratio, gx, gy, gz, pa, jj[u], TT[u], X[u], Y[u], Z[u], PJ[u], ti,
+                                         solid, xi, yi, zi, gxi, gyi, gzi, pai, ai, dscale, cpv, f0, f1, f2);
+        }
+    }
+}
+
+// Pass B over a column-segmented list (interior waves): the 32-byte records {x, y, z, P} of each
+// column window staged in LDS (pass_a_seg); wide columns gather from global memory.
+template <bool SURF, int DIM, int U = MPH_UB, int CAP = MPH_LDS_CAP>
+__device__ __forceinline__ void pass_b_seg(const DevParams& P, const double* s_ratio, const double4* rec,
+                                           const double* gx, const double* gy, const double* gz,
+                                           const double* pa, const unsigned short* seg, const int2* hdr,
+                                           bool live, int ti, bool solid, double xi, double yi, double zi,
+                                           double gxi, double gyi, double gzi, double pai, double ai,
+                                           double& f0, double& f1, double& f2, double4* stage)
+{
+    constexpr int NCOL = DIM == 3 ? 25 : 5;
+    const double dscale = P.rg / P.r2g * (P.vol / P.dx);
+    const double cpv = P.cdp * P.vol;
+    const int lane = threadIdx.x & 63;
+    int slot = 0;
+    for (int col = 0; col < NCOL; ++col) {
+        const int2 h = hdr[col];
+        const int w = (h.y >> 16) & 0x7FFF;
+        if (w == 0) continue;
+        const int mn = h.x;
+        if (h.y >= 0) {
+            const int span = h.y & 0xFFFF;
+            for (int t = lane; t < span; t += 64) stage[t] = rec[mn + t];
+            __builtin_amdgcn_wave_barrier();
+            for (int k0 = 0; k0 < w; k0 += U) {
+                unsigned e[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    e[u] = k0 + u < w ? seg[(size_t)min(slot + k0 + u, kSegCap - 1) * kTile + lane] : kSegNone;
+                double4 R[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) R[u] = stage[e[u] == kSegNone ? 0 : (int)(e[u] & 0xFF)];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (!live || e[u] == kSegNone) continue;
+                    pass_b_term<true, SURF, DIM>(P, s_ratio, gx, gy, gz, pa, mn + (int)(e[u] & 0xFF),
+                                                 (int)((e[u] >> 8) & 7), R[u].x, R[u].y, R[u].z, R[u].w, ti, solid,
+                                                 xi, yi, zi, gxi, gyi, gzi, pai, ai, dscale, cpv, f0, f1, f2);
+                }
             }
-            continue;
-        }
-        const int j = jj[u];
-        double r, ir;
-        rsqrt_pair(r2, r, ir);
-        double c = 0.0;
-        if (r2 < P.rp2) c += PJ[u] * (cpv * (1.0 - r * P.inv_rp)) * ir;
-        const double rij = s_ratio[ti * kTypes + tj];
-        const double rji = s_ratio[tj * kTypes + ti];
-        const double gxj = gx[j], gyj = gy[j], gzj = gz[j], paj = pa[j];
-        if (r2 < P.ra2) {
-            const double t = r * P.inv_ra;
-            const double dwa = P.cda * (1.0 - t) * (1.0 - 3.0 * t);
-            c += (pai * rij + paj * rji) * dwa * ir * P.vol;
-        }
-        if (r2 < P.rg2) {
-            const double omt = 1.0 - r * P.inv_rg;
-            const double wg = P.cg * omt * omt;
-            const double dwg = P.cdg * omt;
-            const double wij = rij * wg, wji = rji * wg;
-            f0 -= (ai * gxj * wji - ai * gxi * wij) * dscale;
-            f1 -= (ai * gyj * wji - ai * gyi * wij) * dscale;
-            f2 -= (ai * gzj * wji - ai * gzi * wij) * dscale;
-            const double dwij = rij * dwg, dwji = rji * dwg;
-            const double gr = (ai * gxj * dwji - ai * gxi * dwij) * q0 +
-                              (ai * gyj * dwji - ai * gyi * dwij) * q1 +
-                              (ai * gzj * dwji - ai * gzi * dwij) * q2;
-            c -= gr * ir * dscale;
-        }
-        f0 += c * q0;
-        f1 += c * q1;
-        f2 += c * q2;
+            __builtin_amdgcn_wave_barrier();
+            slot += w;
+        } else {
+            for (int k0 = 0; k0 < w; k0 += U) {
+                int jj[U], TT[U];
+                bool ok[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int sl = min(slot + 2 * (k0 + u), kSegCap - 2);
+                    const unsigned lo = k0 + u < w ? seg[(size_t)sl * kTile + lane] : 0u;
+                    const unsigned hi = k0 + u < w ? seg[(size_t)(sl + 1) * kTile + lane] : kSegNone;
+                    ok[u] = hi != kSegNone;
+                    jj[u] = ok[u] ? (int)(lo | ((hi & 0xFFF) << 16)) : mn;
+                    TT[u] = (int)(hi >> 12) & 7;
+                }
+                double4 R[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) R[u] = rec[jj[u]];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (!live || !ok[u]) continue;
+                    pass_b_term<true, SURF, DIM>(P, s_ratio, gx, gy, gz, pa, jj[u], TT[u], R[u].x, R[u].y, R[u].z,
+                                                 R[u].w, ti, solid, xi, yi, zi, gxi, gyi, gzi, pai, ai, dscale, cpv,
+                                                 f0, f1, f2);
+                }
+            }
+            slot += 2 * w;
         }
     }
 }
@@ -1113,7 +1366,7 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
                                                 const double* __restrict__ gz,
                                                 const double* __restrict__ pa,
                                                 const int* __restrict__ nbr,
-                                                const int* __restrict__ ncount,
+                                                const int* __restrict__ ncount, const int2* __restrict__ hdr,
                                                 double4* __restrict__ force, double4* __restrict__ acc,
                                                 Soa B, int phase, StructHook H)
 {
@@ -1135,25 +1388,35 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
         const bool inner = c - P.slab_lo > P.slab_h && P.slab_hi - c > P.slab_h;
         live = live && (phase == 1 ? inner : !inner);
     }
-    const bool fast = wave_interior(P, live, xi, yi, zi);
-    if (!live) return;
-    const int ti = A.type[i];
+    const int2* h = hdr ? hdr + (size_t)(i >> 6) * kSegHdr : nullptr;
+    const bool segmented = MPH_SEG && h && h[kSegCols].x == 1;   // wave-uniform
+    const bool fast = segmented || wave_interior(P, live, xi, yi, zi);
+    if (!segmented && !live) return;
+    const int ti = A.type[ii];
     const bool solid = dev_is_struct(ti);
-    const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
-    const int* row = ell_row(nbr, i);
-    const double4 fp = fpart[i];
+    const double4 fp = fpart[ii];
     double f0 = fp.x, f1 = fp.y, f2 = fp.z;
     double gxi = 0.0, gyi = 0.0, gzi = 0.0, pai = 0.0, ai = 0.0;
     if (SURF) {
-        gxi = gx[i]; gyi = gy[i]; gzi = gz[i]; pai = pa[i];
+        gxi = gx[ii]; gyi = gy[ii]; gzi = gz[ii]; pai = pa[ii];
         ai = T->cofa[ti] * P.cofk * P.cofk;
     }
-    if (fast)
-        pass_b_loop<true, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, row, cnt, ti, solid, xi, yi, zi,
-                                     gxi, gyi, gzi, pai, ai, f0, f1, f2);
-    else
-        pass_b_loop<false, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, row, cnt, ti, solid, xi, yi, zi,
-                                      gxi, gyi, gzi, pai, ai, f0, f1, f2);
+    if (segmented) {
+        // every lane of the wave stages; the lanes without a particle of this phase only help
+        __shared__ double4 stage[4][MPH_LDS_CAP];
+        pass_b_seg<SURF, DIM>(P, s_ratio, rec, gx, gy, gz, pa, seg_tile(nbr, i), h, live, ti, solid, xi, yi, zi,
+                              gxi, gyi, gzi, pai, ai, f0, f1, f2, stage[threadIdx.x >> 6]);
+        if (!live) return;
+    } else {
+        const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
+        const int* row = ell_row(nbr, i);
+        if (fast)
+            pass_b_loop<true, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, row, cnt, ti, solid, xi, yi,
+                                         zi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
+        else
+            pass_b_loop<false, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, row, cnt, ti, solid, xi, yi,
+                                          zi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
+    }
     const double vxi = A.vx[i], vyi = A.vy[i], vzi = A.vz[i];
     double vo0 = vxi, vo1 = vyi, vo2 = vzi;
     double xo0 = xi, xo1 = yi, xo2 = zi;
@@ -1212,8 +1475,8 @@ __global__ __launch_bounds__(256) void k_virial(DevParams P, const DevTables* __
                                                 const double* __restrict__ pres, const double* __restrict__ pa,
                                                 const double* __restrict__ gx, const double* __restrict__ gy,
                                                 const double* __restrict__ gz, const int* __restrict__ nbr,
-                                                const int* __restrict__ ncount, double* __restrict__ vir,
-                                                double* __restrict__ vpres)
+                                                const int* __restrict__ ncount, const int2* __restrict__ hdr,
+                                                double* __restrict__ vir, double* __restrict__ vpres)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.n) return;
@@ -1228,9 +1491,43 @@ __global__ __launch_bounds__(256) void k_virial(DevParams P, const DevTables* __
     double S[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
     const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
     const int* row = ell_row(nbr, i);
+    // either list format (the neighbours come in the same order): ELL row, or the lane's column
+    // segments decoded per entry
+    const int2* h = hdr ? hdr + (size_t)(i >> 6) * kSegHdr : nullptr;
+    const bool segmented = MPH_SEG && h && h[kSegCols].x == 1;
+    const unsigned short* seg = seg_tile(nbr, i);
+    const int lane = i & 63;
+    int col = 0, slot = 0, used = 0;
     for (int k = 0; k < cnt; ++k) {
-        const int e = row[k * kTile];
-        const int j = e & kIndexMask, tj = e >> kTypeShift;
+        int j, tj;
+        if (!segmented) {
+            const int e = row[k * kTile];
+            j = e & kIndexMask;
+            tj = e >> kTypeShift;
+        } else {
+            // next real entry of this lane: walk the segments (padding skipped)
+            for (;;) {
+                const int2 hc = h[col];
+                const int w = (hc.y >> 16) & 0x7FFF;
+                const bool wide = hc.y < 0;
+                if (used >= w) { slot += wide ? 2 * w : w; used = 0; ++col; continue; }
+                if (wide) {
+                    const unsigned lo = seg[(size_t)(slot + 2 * used) * kTile + lane];
+                    const unsigned hi = seg[(size_t)(slot + 2 * used + 1) * kTile + lane];
+                    ++used;
+                    if (hi == kSegNone) continue;
+                    j = (int)(lo | ((hi & 0xFFF) << 16));
+                    tj = (int)(hi >> 12) & 7;
+                } else {
+                    const unsigned e = seg[(size_t)(slot + used) * kTile + lane];
+                    ++used;
+                    if (e == kSegNone) continue;
+                    j = hc.x + (int)(e & 0xFF);
+                    tj = (int)(e >> 8) & 7;
+                }
+                break;
+            }
+        }
         double q[3];
         q[0] = image_exact<false>(B.x[j] - xi, P.dw[0], P.hw[0], P.w075[0]);
         q[1] = image_exact<false>(B.y[j] - yi, P.dw[1], P.hw[1], P.w075[1]);
@@ -1991,10 +2288,10 @@ void launch_neighbors(const Launch& L)
     if (P.n == 0) return;
     if (P.dim == 3)
         MPH_LAUNCH("neighbors", L.stream, k_neighbors<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.A,
-                   L.start, L.nbr, L.ncount, L.st);
+                   L.start, L.nbr, L.ncount, L.hdr, L.st);
     else
         MPH_LAUNCH("neighbors", L.stream, k_neighbors<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.A,
-                   L.start, L.nbr, L.ncount, L.st);
+                   L.start, L.nbr, L.ncount, L.hdr, L.st);
 }
 
 void launch_pass_a(const Launch& L)
@@ -2005,10 +2302,10 @@ void launch_pass_a(const Launch& L)
     const PassAOut po = pass_a_out(L);
     if (P.dim == 3)
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, po);
+                   L.A, L.nbr, L.ncount, L.hdr, po);
     else
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, po);
+                   L.A, L.nbr, L.ncount, L.hdr, po);
 }
 
 static StructHook struct_hook(const Launch& L)
@@ -2038,7 +2335,8 @@ void launch_pass_b(const Launch& L, int phase)
     }
 #define MPH_PASS_B(S, D)                                                                            \
     MPH_LAUNCH("pass_b", L.stream, (k_pass_b<S, D>), dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, \
-               L.T, L.A, L.rec, L.fpart, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, L.force, L.acc, L.B, phase, \
+               L.T, L.A, L.rec, L.fpart, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, L.hdr, L.force, L.acc, L.B, \
+               phase, \
                struct_hook(L))
     if (P.surface) {
         if (P.dim == 3) MPH_PASS_B(true, 3); else MPH_PASS_B(true, 2);
@@ -2055,10 +2353,10 @@ void launch_virial(const Launch& L, const Soa& X, double* vir, double* vpres)
     if (P.n == 0) return;
     if (P.dim == 3)
         MPH_LAUNCH("virial", L.stream, k_virial<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T, L.A, X,
-                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, vir, vpres);
+                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, L.hdr, vir, vpres);
     else
         MPH_LAUNCH("virial", L.stream, k_virial<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T, L.A, X,
-                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, vir, vpres);
+                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, L.hdr, vir, vpres);
 }
 
 void launch_struct_stress(const Launch& L)

@@ -17,6 +17,9 @@ constexpr int kContigSub = 2;   // cells along the contiguous axis are 1/kContig
 constexpr int kTypeShift = 28;
 constexpr int kIndexMask = (1 << kTypeShift) - 1;
 constexpr int kPad = 8;         // extra elements behind every per-particle array (vector over-reads)
+// per-wave header of the column-segmented neighbour list (mph_kernels.hip, MPH_SEG): one entry per
+// stencil column (25 in 3-D) plus the list format
+constexpr int kSegHdr = 26;
 
 inline bool is_fluid(int t) { return t >= 0 && t < 2; }   // main.cpp:69-70
 inline bool is_struct(int t) { return t >= 2 && t < 4; }  // main.cpp:71-72
