@@ -943,18 +943,22 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int
     const int cy = cell_axis(yi, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
     const int cz = DIM == 3 ? cell_axis(zi, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
     int* out = nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
+#if MPH_SEG
     int2* h = hdr ? hdr + (size_t)(i >> 6) * kSegHdr : nullptr;
     int seg_over = 0;
+#endif
     if (MPH_SEARCH_LDS && fast) {
         __shared__ double stage[4][3 * (MPH_LDS_CAP + MPH_SB) + (MPH_LDS_CAP + MPH_SB + 1) / 2];
-        if (MPH_SEG && h) {
+#if MPH_SEG
+        if (h) {
             cnt = scan_candidates_lds<DIM, true>(P, A, start, i, live, xi, yi, zi, cx, cy, cz, out,
                                                  stage[threadIdx.x >> 6], seg_tile(nbr, i), h, &seg_over);
             if ((threadIdx.x & 63) == 0) h[kSegCols] = make_int2(1, 0);
-        } else {
+        } else
+#endif
+        {
             cnt = scan_candidates_lds<DIM, false>(P, A, start, i, live, xi, yi, zi, cx, cy, cz, out,
                                                   stage[threadIdx.x >> 6], nullptr, nullptr, nullptr);
-            if (h && (threadIdx.x & 63) == 0) h[kSegCols] = make_int2(0, 0);
         }
         if (live) ncount[i] = cnt;
     } else {
@@ -963,11 +967,15 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int
                        : scan_candidates<DIM, false>(P, A, start, i, xi, yi, zi, cx, cy, cz, out);
             ncount[i] = cnt;
         }
+#if MPH_SEG
         if (h && (threadIdx.x & 63) == 0) h[kSegCols] = make_int2(0, 0);
+#endif
     }
+#if MPH_SEG
     // a segmented list past the tile's 1024 slots (far beyond any physical state: ~100 used at
     // D1M) is reported like a neighbour overflow
     if (seg_over) atomicOr(&st->overflow, 1);
+#endif
     // overflow flag (main.cpp:1766-1768 is the reference's limit).  No per-step statistics here:
     // one same-address device atomic per wave serialises at ~11 ns each (21.8k waves at D1M took
     // 0.5 ms); mph_neighbor_stats reduces ncount on demand.
@@ -2288,10 +2296,10 @@ void launch_neighbors(const Launch& L)
     if (P.n == 0) return;
     if (P.dim == 3)
         MPH_LAUNCH("neighbors", L.stream, k_neighbors<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.A,
-                   L.start, L.nbr, L.ncount, L.hdr, L.st);
+                   L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.st);
     else
         MPH_LAUNCH("neighbors", L.stream, k_neighbors<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.A,
-                   L.start, L.nbr, L.ncount, L.hdr, L.st);
+                   L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.st);
 }
 
 void launch_pass_a(const Launch& L)
@@ -2302,10 +2310,10 @@ void launch_pass_a(const Launch& L)
     const PassAOut po = pass_a_out(L);
     if (P.dim == 3)
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, L.hdr, po);
+                   L.A, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, po);
     else
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, L.hdr, po);
+                   L.A, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, po);
 }
 
 static StructHook struct_hook(const Launch& L)
@@ -2335,7 +2343,7 @@ void launch_pass_b(const Launch& L, int phase)
     }
 #define MPH_PASS_B(S, D)                                                                            \
     MPH_LAUNCH("pass_b", L.stream, (k_pass_b<S, D>), dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, \
-               L.T, L.A, L.rec, L.fpart, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, L.hdr, L.force, L.acc, L.B, \
+               L.T, L.A, L.rec, L.fpart, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.force, L.acc, L.B, \
                phase, \
                struct_hook(L))
     if (P.surface) {
@@ -2353,10 +2361,10 @@ void launch_virial(const Launch& L, const Soa& X, double* vir, double* vpres)
     if (P.n == 0) return;
     if (P.dim == 3)
         MPH_LAUNCH("virial", L.stream, k_virial<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T, L.A, X,
-                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, L.hdr, vir, vpres);
+                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, vir, vpres);
     else
         MPH_LAUNCH("virial", L.stream, k_virial<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T, L.A, X,
-                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, L.hdr, vir, vpres);
+                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, vir, vpres);
 }
 
 void launch_struct_stress(const Launch& L)
