@@ -1,0 +1,123 @@
+"""GPU: edge cases of the hot path and of the C ABI's error behaviour.
+
+The reference has no tests; these follow its own limits and quirks:
+  * a particle with >= 512 neighbours (MAX_NEIGHBOR_COUNT, main.cpp:100, 1766-1768: the reference
+    keeps counting and later reads past the row) is MPH_ERR_NEIGHBOR_OVERFLOW here, never a fault;
+  * empty and single-particle inputs (a lone fluid particle only falls: Kappa is zeroed on tension,
+    main.cpp:2113, so P = 0 and the force is m g -- checked bit for bit);
+  * a domain narrower than the cell stencil and too many slabs are MPH_ERR_DOMAIN;
+  * invalid arguments are MPH_ERR_ARG;
+  * non-default type choices (fluid type 0, walls type 5) against the oracle.
+"""
+import numpy as np
+import pytest
+
+from particlemethod_fsi_amd import MphSolver, cases, mphio
+from particlemethod_fsi_amd.mphio import Cuboid
+from particlemethod_fsi_amd.solver import MphError
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(cuboids, lower, upper, dim=2, module="dam", spacing=0.001, **data):
+    c = cases.Case("edge", dim, module, spacing, lower, upper, cuboids, data_changes=data)
+    return c.build()
+
+
+def test_neighbor_overflow_is_an_error_not_a_fault():
+    # 30 x 30 particles at 0.2 dx: the central ones have ~530 neighbours within 2.6 dx
+    cfg, parts = _case([Cuboid(1, (0.1, 0.1, 0.0), (0.106, 0.106, 0.0002), 0.0002)],
+                       (0.0, 0.0, 0.0), (0.2, 0.2, 0.0002))
+    assert parts.n == 900
+    with pytest.raises(MphError) as e:
+        MphSolver(cfg, parts)
+    assert e.value.code == -3
+
+
+def test_empty_input():
+    cfg, parts = _case([], (0.0, 0.0, 0.0), (0.05, 0.05, 0.001))
+    assert parts.n == 0
+    with MphSolver(cfg, parts) as s:
+        s.step(9)
+        assert s.get("Position").shape == (0, 3)
+        t = 0.0
+        for _ in range(9):
+            t += cfg.dt
+        assert s.time == t
+
+
+def test_single_fluid_particle_falls_bitwise():
+    cfg, parts = _case([Cuboid(1, (0.02, 0.03, 0.0), (0.021, 0.031, 0.001), 0.001)],
+                       (0.0, 0.0, 0.0), (0.05, 0.05, 0.001))
+    assert parts.n == 1
+    steps = 20
+    with MphSolver(cfg, parts) as s:
+        s.step(steps)
+        x, v = s.get("Position")[0], s.get("Velocity")[0]
+        assert int(s.get("NeighborCount")[0]) == 0
+        assert float(s.get("PressureP")[0]) == 0.0
+    # calculateGravity (2917-2936), Acceleration (2938-2956), Convection (1892-1907) in FP64:
+    # F = m g; v += F / m * Dt; x += v * Dt
+    m = cfg.density[1] * cfg.particle_spacing * cfg.particle_spacing
+    xr = parts.position[0].copy()
+    vr = parts.velocity[0].copy()
+    for _ in range(steps):
+        for d in range(3):
+            f = m * cfg.gravity[d]
+            vr[d] = vr[d] + f / m * cfg.dt
+            xr[d] = xr[d] + vr[d] * cfg.dt
+    assert np.array_equal(v, vr), (v, vr)
+    assert np.array_equal(x, xr), (x, xr)
+
+
+def test_domain_narrower_than_the_stencil_is_an_error():
+    # 4 mm wide: fewer than 2.5 cutoffs (2.6 mm) across
+    cfg, parts = _case([Cuboid(1, (0.0, 0.0, 0.0), (0.004, 0.01, 0.001), 0.001)],
+                       (0.0, 0.0, 0.0), (0.004, 0.05, 0.001))
+    with pytest.raises(MphError) as e:
+        MphSolver(cfg, parts)
+    assert e.value.code == -7
+
+
+def test_too_many_slabs_is_an_error():
+    from particlemethod_fsi_amd.solver import Slab
+    cfg, parts = cases.get("channel3d").build()
+    # 24 slabs of a 36 mm periodic axis: each thinner than two halo widths
+    slab = Slab(0, 24, 2, exchange=lambda *a: None)
+    with pytest.raises(MphError) as e:
+        MphSolver(cfg, parts, slab=slab)
+    assert e.value.code == -7
+
+
+def test_invalid_arguments():
+    cfg, parts = cases.get("dam2d").build()
+    bad = mphio.Particles(parts.property.copy(), parts.position, parts.initial_position, parts.velocity)
+    bad.property[5] = 7   # TYPE_COUNT is 6 (main.cpp:68)
+    with pytest.raises(MphError) as e:
+        MphSolver(cfg, bad)
+    assert e.value.code == -1
+    cfg2 = cfg.copy()
+    cfg2.dt = 0.0
+    with pytest.raises(MphError) as e:
+        MphSolver(cfg2, parts)
+    assert e.value.code == -1
+
+
+def test_fluid_type0_walls_type5_match_oracle():
+    """The type classes are ranges (fluid [0,2), walls [4,6), main.cpp:68-74): the dam with fluid
+    type 0 and type-5 walls (Density 6000, its own viscosities) against the oracle."""
+    from oracle_bindings import OracleSolver
+    src = cases.get("dam2d")
+    cubs = [Cuboid(0 if c.type == 1 else 5, c.lower, c.upper, c.space) for c in src.cuboids]
+    cfg, parts = _case(cubs, src.lower, src.upper, module="bar")
+    o = OracleSolver(cfg, parts)
+    o.init()
+    with MphSolver(cfg, parts) as s:
+        for _ in range(3):
+            s.step(5)
+            o.step(5)
+            assert np.array_equal(s.get("NeighborCount"), o.get("NeighborCount"))
+            assert float(np.max(np.abs(s.get("Position") - o.get("Position")))) <= 1e-12
+            assert float(np.max(np.abs(s.get("Velocity") - o.get("Velocity")))) <= 1e-9
+            P, Po = s.get("PressureP"), o.get("PressureP")
+            assert float(np.max(np.abs(P - Po))) <= 1e-8 * float(np.max(np.abs(Po))) + 1e-9
