@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <string>
 #include <thread>
 #include <vector>
@@ -37,6 +38,9 @@ struct MphDist {
     // transport: RCCL communicator, or a host callback (tests / hosts without RCCL)
     bool rccl = false;
     bool graphs = false;          // steps replayed from captured graphs (RCCL transport)
+    // pass B of the inner particles overlaps the pass-A halo (MPH_SLAB_OVERLAP=0: halo, then one
+    // pass B over all particles)
+    bool overlap = !(std::getenv("MPH_SLAB_OVERLAP") && std::string(std::getenv("MPH_SLAB_OVERLAP")) == "0");
     char uid[128] = {0};          // ncclUniqueId
     void* comm = nullptr;         // ncclComm_t
     mph_host_exchange_fn host_fn = nullptr;
@@ -106,7 +110,7 @@ void ctx_fill_launch(MphCtx* c);
 // cells between a fast-path interior particle and a grid face along axis d: stencil half-width + 1
 inline int stencil_margin(const DevParams& P, int d)
 {
-    const int ca = P.dim == 3 ? 2 : 1;
+    const int ca = contig_axis(P.dim, P.perm);
     return (d == ca ? P.sa : 2) + 1;
 }
 int ctx_state_status(MphCtx* c, const DevState& hs);   // kernel error flags -> MphStatus

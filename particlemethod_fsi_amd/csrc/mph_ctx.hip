@@ -276,7 +276,18 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     make_dev_params(c->cfg, c->h, n, ns, c->P);
     const double rc = std::sqrt(c->P.rc2);
     {
-        int r = choose_grid(c->h, cfg->dim, rc, kContigSub, c->P.gc, c->P.ginv, err);
+        // z slabs of a 3-D problem: z in the middle of the cell order, so the ghosts beyond both
+        // faces are long runs (whole wavefronts) at the ends of every plane (DevParams.perm;
+        // MPH_SLAB_PERM=0 keeps (x, y, z); =1..4 force an order on any 3-D context, =force
+        // orders a single 3-D context the z-slab way -- A/B timing and the parity tests)
+        const char* pe = std::getenv("MPH_SLAB_PERM");
+        const std::string pv = pe ? pe : "";
+        const bool zslab = cfg->dim == 3 && c->dist && c->dist->g.axis == 2;
+        const bool forced = pv.size() == 1 && pv[0] >= '1' && pv[0] <= '4';
+        c->P.perm = 0;
+        if (cfg->dim == 3 && (forced || pv == "force" || (zslab && pv != "0")))
+            c->P.perm = forced ? pv[0] - '0' : choose_cell_order(c->h, n, pos, rc);
+        int r = choose_grid(c->h, cfg->dim, rc, kContigSub, c->P.gc, c->P.ginv, err, c->P.perm);
         if (r != MPH_OK) return fail(c, r, err);
     }
     // interior box for the wave-uniform fast minimum image (k_neighbors / passes): >= 3 cells

@@ -565,6 +565,11 @@ int dist_enqueue_step(MphCtx* c, Profiler* prof)
     // the pass-A halo travels on stream2 while pass B runs the particles that have no ghost
     // neighbours; the near-face particles follow once the halo has landed (inner pass B is
     // enqueued first, so that a host-staged exchange, which blocks the host, also overlaps with it)
+    if (!D.overlap) {   // MPH_SLAB_OVERLAP=0: halo first, then one pass B over every particle
+        MPH_CK(halo_exchange(c, prof, c->stream));
+        launch_pass_b(L, 0);
+        return struct_substeps(c, prof);
+    }
     MPH_HIP_OK(c, hipEventRecord(D.ev_a, c->stream));
     launch_pass_b(L, 1);
     MPH_HIP_OK(c, hipStreamWaitEvent(D.stream2, D.ev_a, 0));

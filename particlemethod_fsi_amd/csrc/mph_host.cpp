@@ -624,14 +624,38 @@ void fill_scalars(const HostDerived& h, const MphConfig& c, double* o)
     o[33] = h.cell_n[0]; o[34] = h.cell_n[1]; o[35] = h.cell_n[2];
 }
 
+// Cell order of a z-slab context: (y, z, x) (perm 3) or (x, z, y) (perm 4), i.e. which of x and
+// y is the contiguous axis.
+// A wavefront is a run of consecutive sorted particles along the contiguous axis; the search
+// takes its fast wave-uniform path only when every lane is a few cells clear of the periodic
+// faces (DevParams.inner_lo/hi), so a contiguous axis whose particle runs reach a face (the
+// bottom wall of a tank at the domain edge, say) slows every column that touches it.  Pick the
+// axis with fewer particles within 2 rc of its faces, then the one with the longer runs.
+int choose_cell_order(const HostDerived& h, int n, const double* pos, double rc)
+{
+    long near[2] = {0, 0};
+    double lo[2] = {1e300, 1e300}, hi[2] = {-1e300, -1e300};
+    for (int i = 0; i < n; ++i) {
+        for (int d = 0; d < 2; ++d) {
+            const double a = pos[3 * (size_t)i + d];
+            if (a - h.dmin[d] < 2.0 * rc || h.dmax[d] - a < 2.0 * rc) ++near[d];
+            lo[d] = std::min(lo[d], a);
+            hi[d] = std::max(hi[d], a);
+        }
+    }
+    if (near[0] != near[1]) return near[0] < near[1] ? 3 : 4;
+    return (hi[0] - lo[0]) >= (hi[1] - lo[1]) ? 3 : 4;
+}
+
 // GPU linked-cell grid: cells of width >= rc/2 along the two outer axes (a +-2-cell stencil
 // covers the acceptance sphere) and >= rc/(2 sub) along the contiguous axis (z in 3-D, y in 2-D;
 // a +-2 sub stencil, scanned as one contiguous index range per column, so thinner cells there
 // only sharpen the cutoff trimming of each column).  Cell counts divide the periodic width
 // exactly; every axis needs enough cells that the stencil never visits a cell twice.
-int choose_grid(const HostDerived& h, int dim, double rc, int sub, int gc[3], double ginv[3], std::string& err)
+int choose_grid(const HostDerived& h, int dim, double rc, int sub, int gc[3], double ginv[3], std::string& err,
+                int perm)
 {
-    const int ca = dim == 3 ? 2 : 1;
+    const int ca = contig_axis(dim, perm);   // the contiguous (half-width) axis
     for (int d = 0; d < 3; ++d) {
         if (d == 2 && dim == 2) { gc[d] = 1; ginv[d] = 1.0 / h.dw[d]; continue; }
         const int s = d == ca ? sub : 1;

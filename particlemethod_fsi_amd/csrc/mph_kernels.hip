@@ -137,13 +137,35 @@ __device__ __forceinline__ int cell_axis(double x, double org, double w, double 
     return (int)t;
 }
 
+// linear cell index in the cell order DevParams.perm (order_axis; the last axis contiguous, with
+// half-width cells)
+__device__ __forceinline__ int cell_index(const DevParams& P, int cx, int cy, int cz)
+{
+    const int* g = P.gc;
+    switch (P.perm) {
+    case 1: return (cz * g[0] + cx) * g[1] + cy;   // (z, x, y)
+    case 2: return (cz * g[1] + cy) * g[0] + cx;   // (z, y, x)
+    case 3: return (cy * g[2] + cz) * g[0] + cx;   // (y, z, x)
+    case 4: return (cx * g[2] + cz) * g[1] + cy;   // (x, z, y)
+    default: return (cx * g[1] + cy) * g[2] + cz;  // (x, y, z)
+    }
+}
+
 __device__ __forceinline__ int cell_id(const DevParams& P, double x, double y, double z)
 {
     const int cx = cell_axis(x, P.corg[0], P.dw[0], P.ginv[0], P.gc[0]);
     const int cy = cell_axis(y, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
     const int cz = P.dim == 3 ? cell_axis(z, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
-    return (cx * P.gc[1] + cy) * P.gc[2] + cz;
+    return cell_index(P, cx, cy, cz);
 }
+
+// Logical axes of the cell order for the search: the two column axes (A0 slowest, A1) and the
+// contiguous axis A2 (cells half as wide); 2-D: x columns, y contiguous.
+template <int DIM, int PERM> struct CellAxes {
+    static constexpr int A0 = DIM == 3 ? order_axis(PERM, 0) : 0;
+    static constexpr int A1 = DIM == 3 ? order_axis(PERM, 1) : 1;
+    static constexpr int A2 = DIM == 3 ? order_axis(PERM, 2) : 1;
+};
 
 __device__ __forceinline__ bool dev_is_struct(int t) { return t == 2 || t == 3; }
 __device__ __forceinline__ bool dev_is_fluid(int t) { return t == 0 || t == 1; }
@@ -646,40 +668,42 @@ __device__ __forceinline__ bool accept_interior(const DevParams& P, double dx, d
     return a;
 }
 
-template <int DIM, bool FAST, int SB = MPH_SB>
+template <int DIM, bool FAST, int PERM, int SB = MPH_SB>
 __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A, const int* start,
                                                int i, double xi, double yi, double zi, int cx,
                                                int cy, int cz, int* out)
 {
+    using X = CellAxes<DIM, PERM>;
     int cnt = 0;
     constexpr int NCOL = DIM == 3 ? 25 : 5;
-    const int gca = DIM == 3 ? P.gc[2] : P.gc[1];   // contiguous axis
-    const int cca = DIM == 3 ? cz : cy;
+    const int cc[3] = {cx, cy, cz};
+    const int gca = P.gc[X::A2];   // contiguous axis
+    const int cca = cc[X::A2];
     // Column trimming: skip the cells of a column (and whole columns) that lie entirely beyond
     // the cutoff.  Conservative (cutoff enlarged by 1e-6 relative, far above the roundoff of the
     // cell geometry), so the accepted set and its order are unchanged.
     const double rcm2 = P.rc2 * (1.0 + 4e-6);
-    const double cw0 = 1.0 / P.ginv[0], cw1 = 1.0 / P.ginv[1];
-    const double ux = grid_offset(xi, P.corg[0], P.dw[0]);
-    const double uy = grid_offset(yi, P.corg[1], P.dw[1]);
-    const double uz = DIM == 3 ? grid_offset(zi, P.corg[2], P.dw[2]) : 0.0;
-    const double ua = DIM == 3 ? uz : uy;             // offset along the contiguous axis
+    const double cw0 = 1.0 / P.ginv[X::A0], cw1 = 1.0 / P.ginv[X::A1];
+    const double uu[3] = {grid_offset(xi, P.corg[0], P.dw[0]), grid_offset(yi, P.corg[1], P.dw[1]),
+                          DIM == 3 ? grid_offset(zi, P.corg[2], P.dw[2]) : 0.0};
+    const double ua = uu[X::A2];                      // offset along the contiguous axis
     const double lo2 = P.rc2 * (1.0 - 1e-10), hi2 = P.rc2 * (1.0 + 1e-10);
-    const double ginva = DIM == 3 ? P.ginv[2] : P.ginv[1];
+    const double ginva = P.ginv[X::A2];
     for (int col = 0; col < NCOL; ++col) {
         int base;
         double d2;
         if (DIM == 3) {
             const int dxc = col / 5 - 2, dyc = col % 5 - 2;
-            const double gx = cell_gap(ux, cx, dxc, cw0), gy = cell_gap(uy, cy, dyc, cw1);
+            const int c0 = cc[X::A0], c1 = cc[X::A1];
+            const double gx = cell_gap(uu[X::A0], c0, dxc, cw0), gy = cell_gap(uu[X::A1], c1, dyc, cw1);
             d2 = gx * gx + gy * gy;
             if (d2 > rcm2) continue;
-            const int jx = FAST ? cx + dxc : wrap_cell(cx + dxc, P.gc[0]);
-            const int jy = FAST ? cy + dyc : wrap_cell(cy + dyc, P.gc[1]);
-            base = (jx * P.gc[1] + jy) * P.gc[2];
+            const int jx = FAST ? c0 + dxc : wrap_cell(c0 + dxc, P.gc[X::A0]);
+            const int jy = FAST ? c1 + dyc : wrap_cell(c1 + dyc, P.gc[X::A1]);
+            base = (jx * P.gc[X::A1] + jy) * P.gc[X::A2];
         } else {
             const int dxc = col - 2;
-            const double gx = cell_gap(ux, cx, dxc, cw0);
+            const double gx = cell_gap(uu[0], cx, dxc, cw0);
             d2 = gx * gx;
             if (d2 > rcm2) continue;
             base = (FAST ? cx + dxc : wrap_cell(cx + dxc, P.gc[0])) * P.gc[1];
@@ -777,7 +801,7 @@ __device__ __forceinline__ int wave_max(int v)
 // texture-address unit was the bound; a staged column costs 4.  Same candidates, same order,
 // same FP64 test as scan_candidates, so the list is identical.  Every lane of the wave must call
 // this (act = live particle); the column loop and the staging are wave-uniform.
-template <int DIM, bool SEG, int SB = MPH_SB, int CAP = MPH_LDS_CAP>
+template <int DIM, bool SEG, int PERM, int SB = MPH_SB, int CAP = MPH_LDS_CAP>
 __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa& A, const int* start,
                                                    int i, bool act, double xi, double yi, double zi,
                                                    int cx, int cy, int cz, int* out, double* sx,
@@ -788,28 +812,30 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     int* st = reinterpret_cast<int*>(sx + 3 * (CAP + SB));
     const int lane = threadIdx.x & 63;
     const double lo2 = P.rc2 * (1.0 - 1e-10), hi2 = P.rc2 * (1.0 + 1e-10);
+    using X = CellAxes<DIM, PERM>;
     int cnt = 0;
     constexpr int NCOL = DIM == 3 ? 25 : 5;
-    const int cca = DIM == 3 ? cz : cy;
+    const int cc[3] = {cx, cy, cz};
+    const int cca = cc[X::A2];
     const double rcm2 = P.rc2 * (1.0 + 4e-6);
-    const double cw0 = 1.0 / P.ginv[0], cw1 = 1.0 / P.ginv[1];
-    const double ux = grid_offset(xi, P.corg[0], P.dw[0]);
-    const double uy = grid_offset(yi, P.corg[1], P.dw[1]);
-    const double uz = DIM == 3 ? grid_offset(zi, P.corg[2], P.dw[2]) : 0.0;
-    const double ua = DIM == 3 ? uz : uy;
-    const double ginva = DIM == 3 ? P.ginv[2] : P.ginv[1];
+    const double cw0 = 1.0 / P.ginv[X::A0], cw1 = 1.0 / P.ginv[X::A1];
+    const double uu[3] = {grid_offset(xi, P.corg[0], P.dw[0]), grid_offset(yi, P.corg[1], P.dw[1]),
+                          DIM == 3 ? grid_offset(zi, P.corg[2], P.dw[2]) : 0.0};
+    const double ua = uu[X::A2];
+    const double ginva = P.ginv[X::A2];
     // candidate range of this lane in stencil column col (cell ranges -> start[] loads)
     auto col_range = [&](int col, int& jb, int& je) {
         int base;
         double d2;
         if (DIM == 3) {
             const int dxc = col / 5 - 2, dyc = col % 5 - 2;
-            const double gx = cell_gap(ux, cx, dxc, cw0), gy = cell_gap(uy, cy, dyc, cw1);
+            const int c0 = cc[X::A0], c1 = cc[X::A1];
+            const double gx = cell_gap(uu[X::A0], c0, dxc, cw0), gy = cell_gap(uu[X::A1], c1, dyc, cw1);
             d2 = gx * gx + gy * gy;
-            base = ((cx + dxc) * P.gc[1] + cy + dyc) * P.gc[2];
+            base = ((c0 + dxc) * P.gc[X::A1] + c1 + dyc) * P.gc[X::A2];
         } else {
             const int dxc = col - 2;
-            const double gx = cell_gap(ux, cx, dxc, cw0);
+            const double gx = cell_gap(uu[0], cx, dxc, cw0);
             d2 = gx * gx;
             base = (cx + dxc) * P.gc[1];
         }
@@ -926,18 +952,33 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     return cnt;
 }
 
-template <int DIM>
-__global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int* __restrict__ start,
-                                                   int* __restrict__ nbr, int* __restrict__ ncount,
-                                                   int2* __restrict__ hdr, DevState* __restrict__ st)
+// Slab mode: true when no lane of the wave holds an owned particle (ghost ids are negative).
+// With the (z, x, y) cell order of z slabs (DevParams.perm) the ghosts beyond the two faces fill
+// whole wavefronts at the ends of the sorted arrays; their lists and pass-A/pass-B sums are not
+// needed (their pass-A values arrive in the halo, their pass-B results are dropped), so the list
+// kernels skip them.
+__device__ __forceinline__ bool wave_all_ghosts(const DevParams& P, const Soa& A, bool live, int ii)
+{
+    if (P.slab_axis < 0) return false;
+    return __all(!live || A.id[ii] < 0);
+}
+
+template <int DIM, int PERM>
+__device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A, const int* start, int* nbr,
+                                               int* ncount, int2* hdr, DevState* st, double* stage)
 {
     const int n = dev_n(P);
-    if ((int)blockIdx.x >= live_blocks(n)) return;
     const int i = xcd_block(blockIdx.x, live_blocks(n)) * blockDim.x + threadIdx.x;
     const bool live = i < n;
     const int ii = live ? i : n - 1;
+    if (wave_all_ghosts(P, A, live, ii)) {
+        if (live) ncount[i] = 0;
+        return;
+    }
+    // the ghost lanes of a mixed wave take no part either (empty list)
+    const bool own = live && !(P.slab_axis >= 0 && A.id[ii] < 0);
     const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
-    const bool fast = wave_interior(P, live, xi, yi, zi);
+    const bool fast = wave_interior(P, own, xi, yi, zi);
     int cnt = 0;
     const int cx = cell_axis(xi, P.corg[0], P.dw[0], P.ginv[0], P.gc[0]);
     const int cy = cell_axis(yi, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
@@ -948,25 +989,23 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int
     int seg_over = 0;
 #endif
     if (MPH_SEARCH_LDS && fast) {
-        __shared__ double stage[4][3 * (MPH_LDS_CAP + MPH_SB) + (MPH_LDS_CAP + MPH_SB + 1) / 2];
 #if MPH_SEG
         if (h) {
-            cnt = scan_candidates_lds<DIM, true>(P, A, start, i, live, xi, yi, zi, cx, cy, cz, out,
-                                                 stage[threadIdx.x >> 6], seg_tile(nbr, i), h, &seg_over);
+            cnt = scan_candidates_lds<DIM, true, PERM>(P, A, start, i, own, xi, yi, zi, cx, cy, cz, out,
+                                                       stage, seg_tile(nbr, i), h, &seg_over);
             if ((threadIdx.x & 63) == 0) h[kSegCols] = make_int2(1, 0);
         } else
 #endif
         {
-            cnt = scan_candidates_lds<DIM, false>(P, A, start, i, live, xi, yi, zi, cx, cy, cz, out,
-                                                  stage[threadIdx.x >> 6], nullptr, nullptr, nullptr);
+            cnt = scan_candidates_lds<DIM, false, PERM>(P, A, start, i, own, xi, yi, zi, cx, cy, cz, out,
+                                                        stage, nullptr, nullptr, nullptr);
         }
         if (live) ncount[i] = cnt;
     } else {
-        if (live && !(MPH_DIAG_SEARCH & 4)) {
-            cnt = fast ? scan_candidates<DIM, true>(P, A, start, i, xi, yi, zi, cx, cy, cz, out)
-                       : scan_candidates<DIM, false>(P, A, start, i, xi, yi, zi, cx, cy, cz, out);
-            ncount[i] = cnt;
-        }
+        if (own && !(MPH_DIAG_SEARCH & 4))
+            cnt = fast ? scan_candidates<DIM, true, PERM>(P, A, start, i, xi, yi, zi, cx, cy, cz, out)
+                       : scan_candidates<DIM, false, PERM>(P, A, start, i, xi, yi, zi, cx, cy, cz, out);
+        if (live && !(MPH_DIAG_SEARCH & 4)) ncount[i] = cnt;
 #if MPH_SEG
         if (h && (threadIdx.x & 63) == 0) h[kSegCols] = make_int2(0, 0);
 #endif
@@ -980,6 +1019,17 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int
     // one same-address device atomic per wave serialises at ~11 ns each (21.8k waves at D1M took
     // 0.5 ms); mph_neighbor_stats reduces ncount on demand.
     if (cnt > kMaxNeighbor) atomicOr(&st->overflow, 1);
+}
+
+// one kernel per cell order (PERM 1: (z, x, y) for z slabs), so each keeps its own register budget
+template <int DIM, int PERM>
+__global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int* __restrict__ start,
+                                                   int* __restrict__ nbr, int* __restrict__ ncount,
+                                                   int2* __restrict__ hdr, DevState* __restrict__ st)
+{
+    if ((int)blockIdx.x >= live_blocks(dev_n(P))) return;
+    __shared__ double stage[4][3 * (MPH_LDS_CAP + MPH_SB) + (MPH_LDS_CAP + MPH_SB + 1) / 2];
+    neighbors_body<DIM, PERM>(P, A, start, nbr, ncount, hdr, st, stage[threadIdx.x >> 6]);
 }
 
 // ---------------------------------------------------------------------------- pass A -------
@@ -1147,6 +1197,16 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
     const bool live = i < n;
     const int ii = live ? i : n - 1;
     const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
+    if (wave_all_ghosts(P, A, live, ii)) {
+        // ghosts: PressureP (+ GravityCenter, PressureA) arrive in the halo, which also fills the
+        // .w of the pass-B record; its position part is written here
+        if (live && pout.rec) pout.rec[i] = make_double4(xi, yi, zi, 0.0);
+        return;
+    }
+    // likewise the ghost lanes of a mixed wave
+    const bool ghost = live && P.slab_axis >= 0 && A.id[ii] < 0;
+    if (ghost && pout.rec) pout.rec[i] = make_double4(xi, yi, zi, 0.0);
+    const bool own = live && !ghost;
     const int2* h = hdr ? hdr + (size_t)(i >> 6) * kSegHdr : nullptr;
     if (MPH_SEG && h && h[kSegCols].x == 1) {   // wave-uniform: this wave's list is column-segmented
         __shared__ double2 stage[4][3 * MPH_LDS_CAP];
@@ -1154,13 +1214,13 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
         const int ti = A.type[ii];
         const bool solid = dev_is_struct(ti);
         PassA o;
-        pass_a_seg<DIM>(P, s_ratio, s_mu, A, seg_tile(nbr, i), h, live, ti, solid, xi, yi, zi, vxi, vyi,
+        pass_a_seg<DIM>(P, s_ratio, s_mu, A, seg_tile(nbr, i), h, own, ti, solid, xi, yi, zi, vxi, vyi,
                         vzi, o, stage[threadIdx.x >> 6]);
-        if (live) pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
+        if (own) pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
         return;
     }
-    const bool fast = wave_interior(P, live, xi, yi, zi);
-    if (!live) return;
+    const bool fast = wave_interior(P, own, xi, yi, zi);
+    if (!own) return;
     const double vxi = A.vx[i], vyi = A.vy[i], vzi = A.vz[i];
     const int ti = A.type[i];
     const bool solid = dev_is_struct(ti);
@@ -1389,12 +1449,22 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
     const int ii = i < n ? i : n - 1;
     const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
     bool live = i < n;
+    if (wave_all_ghosts(P, A, live, ii)) {
+        if (live) B.id[i] = A.id[i];
+        return;
+    }
+    if (live && P.slab_axis >= 0 && A.id[ii] < 0) {   // a ghost lane of a mixed wave
+        B.id[i] = A.id[i];
+        live = false;
+    }
     if (phase) {
-        // slab mode: phase 1 = particles whose neighbours are all owned (run while the halo of
-        // pass-A values is in flight), phase 2 = the rest (after the halo arrived)
+        // slab mode: phase 1 = the wavefronts whose particles have no ghost neighbour (run while
+        // the halo of pass-A values is in flight), phase 2 = the rest, after the halo arrived --
+        // split by whole waves, so that no wave runs its list loop twice
         const double c = P.slab_axis == 0 ? xi : (P.slab_axis == 1 ? yi : zi);
         const bool inner = c - P.slab_lo > P.slab_h && P.slab_hi - c > P.slab_h;
-        live = live && (phase == 1 ? inner : !inner);
+        const bool wave_inner = __all(!live || inner);
+        if (phase == 1 ? !wave_inner : wave_inner) return;
     }
     const int2* h = hdr ? hdr + (size_t)(i >> 6) * kSegHdr : nullptr;
     const bool segmented = MPH_SEG && h && h[kSegCols].x == 1;   // wave-uniform
@@ -1890,15 +1960,16 @@ __global__ __launch_bounds__(256) void k_sinit_search(DevParams P, int ns, const
     const int cy = cell_axis(xi.y, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
     const int cz = DIM == 3 ? cell_axis(xi.z, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
     // stencil half-widths in cells: 2 across (cells >= rc/2), P.sa along the contiguous axis
-    const int ry = DIM == 3 ? 2 : P.sa, rz = DIM == 3 ? P.sa : 0;
+    const int ca = contig_axis(DIM, P.perm);
+    const int rx = ca == 0 ? P.sa : 2, ry = ca == 1 ? P.sa : 2, rz = DIM == 3 ? (ca == 2 ? P.sa : 2) : 0;
     int c = 0;
-    for (int dx = -2; dx <= 2; ++dx) {
+    for (int dx = -rx; dx <= rx; ++dx) {
         const int jx = wrap_cell(cx + dx, P.gc[0]);
         for (int dy = -ry; dy <= ry; ++dy) {
             const int jy = wrap_cell(cy + dy, P.gc[1]);
             for (int dz = -rz; dz <= rz; ++dz) {
                 const int jz = DIM == 3 ? wrap_cell(cz + dz, P.gc[2]) : 0;
-                const int cell = (jx * P.gc[1] + jy) * P.gc[2] + jz;
+                const int cell = cell_index(P, jx, jy, jz);
                 for (int q = start[cell], e = start[cell + 1]; q < e; ++q) {
                     const int t = sorted[q];
                     if (t == s) continue;
@@ -2294,12 +2365,21 @@ void launch_neighbors(const Launch& L)
     Profiler* prof = L.prof;
     const DevParams& P = *L.P;
     if (P.n == 0) return;
-    if (P.dim == 3)
-        MPH_LAUNCH("neighbors", L.stream, k_neighbors<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.A,
-                   L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.st);
-    else
-        MPH_LAUNCH("neighbors", L.stream, k_neighbors<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.A,
-                   L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.st);
+#define MPH_NEIGHBORS(PERM)                                                                                  \
+    MPH_LAUNCH("neighbors", L.stream, (k_neighbors<3, PERM>), dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, \
+               L.A, L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.st)
+    if (P.dim == 3) {
+        switch (P.perm) {
+        case 1: MPH_NEIGHBORS(1); break;
+        case 2: MPH_NEIGHBORS(2); break;
+        case 3: MPH_NEIGHBORS(3); break;
+        case 4: MPH_NEIGHBORS(4); break;
+        default: MPH_NEIGHBORS(0); break;
+        }
+    } else
+        MPH_LAUNCH("neighbors", L.stream, (k_neighbors<2, 0>), dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P,
+                   L.A, L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.st);
+#undef MPH_NEIGHBORS
 }
 
 void launch_pass_a(const Launch& L)
@@ -2342,7 +2422,7 @@ void launch_pass_b(const Launch& L, int phase)
         std::abort();
     }
 #define MPH_PASS_B(S, D)                                                                            \
-    MPH_LAUNCH("pass_b", L.stream, (k_pass_b<S, D>), dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, \
+    MPH_LAUNCH(phase == 2 ? "pass_b_face" : "pass_b", L.stream, (k_pass_b<S, D>), dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, \
                L.T, L.A, L.rec, L.fpart, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.force, L.acc, L.B, \
                phase, \
                struct_hook(L))

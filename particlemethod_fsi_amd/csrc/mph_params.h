@@ -25,6 +25,19 @@ inline bool is_fluid(int t) { return t >= 0 && t < 2; }   // main.cpp:69-70
 inline bool is_struct(int t) { return t >= 2 && t < 4; }  // main.cpp:71-72
 inline bool is_wall(int t) { return t >= 4 && t < 6; }    // main.cpp:73-74
 
+// Axis of the 3-D cell order DevParams.perm at position k (0 slowest, 2 contiguous):
+// 0 (x, y, z); for z slabs 1 (z, x, y), 2 (z, y, x), 3 (y, z, x), 4 (x, z, y)
+inline constexpr int order_axis(int perm, int k)
+{
+    return perm == 1 ? (k == 0 ? 2 : k == 1 ? 0 : 1)
+         : perm == 2 ? (k == 0 ? 2 : k == 1 ? 1 : 0)
+         : perm == 3 ? (k == 0 ? 1 : k == 1 ? 2 : 0)
+         : perm == 4 ? (k == 0 ? 0 : k == 1 ? 2 : 1)
+                     : k;
+}
+// the contiguous (half-width-cell) axis of the cell order
+inline constexpr int contig_axis(int dim, int perm) { return dim == 2 ? 1 : order_axis(perm, 2); }
+
 // Every constant the reference derives in initializeWeight/Fluid/Wall/Domain
 // (main.cpp:1191-1469), in the reference's own arithmetic, plus what the GPU path precomputes.
 // Passed by value as a kernel argument (kernarg segment -> scalar loads).
@@ -42,6 +55,12 @@ struct DevParams {
     int ncell;         // gc[0]*gc[1]*gc[2]
     int substeps;      // (int)(Dt/Elastic_Dt + 0.5), main.cpp:653
     int sa;            // stencil half-width (cells) along the contiguous axis (2 * kContigSub)
+    // linear order of the 3-D cell grid (order_axis above): 0 = (x, y, z) with z contiguous; z
+    // slabs (mph_dist.hip) put z in the middle, 3 = (y, z, x) or 4 = (x, z, y), so that the ghosts
+    // beyond both faces form long runs at the two ends of every plane of the slowest axis (whole
+    // wavefronts the list kernels skip) while every XCD's contiguous share of the sorted arrays
+    // stays a band of that slowest axis through the whole slab (L2 locality); 1, 2 put z slowest
+    int perm;
     int fast_ok;       // every active axis has > 12 GPU cells: interior waves may skip the
                        // periodic branch of the minimum image (see k_neighbors)
     double inner_lo[3], inner_hi[3];   // interior box: >= 3 GPU cells from every periodic face

@@ -269,3 +269,27 @@ def test_gpu_structure_init_equals_host_build(case, monkeypatch):
     assert np.array_equal(dev["LambdaLames"], ll) and np.array_equal(dev["MuLames"], lm)
     for f in dev:
         assert np.array_equal(dev[f], host[f]), f
+
+
+CASES_3D = [c for c in CASES if cases.get(c).dim == 3]
+
+
+@pytest.mark.parametrize("perm", [1, 2, 3, 4])
+@pytest.mark.parametrize("case", CASES_3D)
+def test_gpu_cell_orders_match_golden(case, perm, monkeypatch):
+    """Every cell order of the z-slab contexts (DevParams.perm, forced on a single context through
+    MPH_SLAB_PERM) gives the reference's neighbour counts and fields within the same tolerances:
+    the order changes which cells are contiguous and the order of each neighbour list, nothing
+    else."""
+    monkeypatch.setenv("MPH_SLAB_PERM", str(perm))
+    g = Golden(case)
+    cfg, parts = cases.get(case).build()
+    with MphSolver(cfg, parts) as s:
+        for fn in cases.get(case).init_calls:
+            s.set_initial_velocity_profile()
+        compare(g, s, 0)
+        done = 0
+        for step in g.steps[:2]:
+            s.step(step - done)
+            done = step
+            compare(g, s, step)

@@ -1,0 +1,126 @@
+"""Clean per-slab kernel timings of the multi-GPU path on ONE GPU.
+
+The 8-rank rehearsal (tools/gpu_dist_rehearsal.sh) runs eight processes on one card at once, so
+their kernels overlap and the per-kernel times it reports are inflated by the others.  Here the
+N slab contexts live in one process, one thread each, and move their messages through an
+in-process host exchange; a token serialises the GPU phases between exchanges (a context has
+synchronised its stream before it calls the host exchange, and each thread synchronises before
+it gives the token back at the end of a call), so every rank's kernels run alone on the card and
+the HIP-event profile of each rank is what that rank would see on its own GPU.
+
+usage: python tools/slab_serial.py [--case d16m] [--ranks 8] [--steps 4] [--warmup 2]
+prints one JSON line: per-rank kernel averages, held/owned counts, their GPU time per step.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import queue
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from particlemethod_fsi_amd import MphSolver, cases, solver  # noqa: E402
+from particlemethod_fsi_amd.dist import build_local  # noqa: E402
+
+SLAB_AXIS = {2: 0, 3: 2}
+
+
+class Token:
+    """The GPU: held by one rank thread while it launches work."""
+
+    def __init__(self):
+        self.lock = threading.Lock()
+
+
+class InProcExchange:
+    """mph_host_exchange_fn between threads: send_l -> left neighbour's recv_r, send_r -> right
+    neighbour's recv_l; gives the token back while it waits for its peers."""
+
+    def __init__(self, rank, nranks, boxes, token):
+        self.rank, self.nranks, self.boxes, self.token = rank, nranks, boxes, token
+        self.left, self.right = (rank - 1) % nranks, (rank + 1) % nranks
+
+    def __call__(self, send_l, send_r, recv_l, recv_r):
+        self.token.lock.release()
+        try:
+            if len(send_l):
+                self.boxes[(self.rank, self.left, "L")].put(bytes(send_l))
+            if len(send_r):
+                self.boxes[(self.rank, self.right, "R")].put(bytes(send_r))
+            if len(recv_r):
+                b = self.boxes[(self.right, self.rank, "L")].get(timeout=300)
+                recv_r[:len(b)] = b
+            if len(recv_l):
+                b = self.boxes[(self.left, self.rank, "R")].get(timeout=300)
+                recv_l[:len(b)] = b
+        finally:
+            self.token.lock.acquire()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--case", default="d16m")
+    ap.add_argument("--ranks", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--warmup", type=int, default=2)
+    args = ap.parse_args()
+    case = cases.get(args.case)
+    axis = SLAB_AXIS[case.dim]
+    R = args.ranks
+    token = Token()
+    boxes = {}
+    for r in range(R):
+        for d, peer in (("L", (r - 1) % R), ("R", (r + 1) % R)):
+            boxes[(r, peer, d)] = queue.Queue()
+    locals_ = [build_local(case, r, R, axis) for r in range(R)]
+    out = [None] * R
+    errs = []
+
+    def run(r):
+        try:
+            cfg, parts, ids, n_glob = locals_[r]
+            ex = InProcExchange(r, R, boxes, token)
+            with token.lock:
+                s = MphSolver(cfg, parts, device=0,
+                              slab=solver.Slab(r, R, axis, exchange=ex, ids=ids, n_glob=n_glob))
+                s.synchronize()
+            with token.lock:
+                s.step(args.warmup)
+                s.synchronize()
+            with token.lock:
+                t0 = time.perf_counter()
+                prof = s.profile(args.steps)
+                s.synchronize()
+                wall = time.perf_counter() - t0
+            info = s.dist_info()
+            out[r] = {"rank": r, "owned": len(s.owned_ids()), "held": info["held"],
+                      "kernels_ms": {k: round(v["avg_ms"], 5) for k, v in prof.items()},
+                      "ms_per_step": {k: round(v["avg_ms"] * v["launches"] / args.steps, 5)
+                                      for k, v in prof.items()},
+                      "gpu_ms_per_step": sum(v["avg_ms"] * v["launches"] for v in prof.values()) / args.steps,
+                      "wall_s": wall}
+            with token.lock:
+                s.close()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs.append((r, repr(e)))
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(R)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        print(json.dumps({"errors": errs}))
+        sys.exit(1)
+    worst = max(o["gpu_ms_per_step"] for o in out)
+    print(json.dumps({"case": args.case, "ranks": R, "perm": os.environ.get("MPH_SLAB_PERM", "default"),
+                      "max_rank_gpu_ms_per_step": worst, "per_rank": out}))
+
+
+if __name__ == "__main__":
+    main()
