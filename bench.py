@@ -180,6 +180,7 @@ def main():
     from particlemethod_fsi_amd import MphSolver, cases
 
     dist = None
+    cuts = None
     case_name = args.case
     if world > 1:
         # one process per GPU; torch.distributed (gloo) is only the control plane (rendezvous,
@@ -195,11 +196,14 @@ def main():
 
     case = cases.get(case_name)
     if dist is not None:
-        from particlemethod_fsi_amd.dist import build_local, gloo_slab, rccl_slab
+        from particlemethod_fsi_amd.dist import balanced_cuts, build_local, gloo_slab, rccl_slab
         axis = SLAB_AXIS[case.dim]
-        cfg, parts, ids, n_total = build_local(case, rank, world, axis)
+        # slab boundaries at the particle-count quantiles (equal shares; MPH_SLAB_EQUAL=1: equal widths)
+        cuts = None if os.environ.get("MPH_SLAB_EQUAL") == "1" else balanced_cuts(case, world, axis)
+        cfg, parts, ids, n_total = build_local(case, rank, world, axis, cuts)
         mk = gloo_slab if os.environ.get("MPH_SLAB_TRANSPORT") == "host" else rccl_slab
-        solver = MphSolver(cfg, parts, device=device, slab=mk(rank, world, axis, ids=ids, n_glob=n_total))
+        solver = MphSolver(cfg, parts, device=device,
+                           slab=mk(rank, world, axis, ids=ids, n_glob=n_total, cuts=cuts))
         del parts, ids
         n_local = len(solver.owned_ids())
     else:
@@ -286,8 +290,11 @@ def main():
         "config": {"workload": "%s: %s, %d particles, ~%d per GPU"
                                % (case_name, case.describe(), n_total, n_total // world),
                    "particles": n_total, "dim": case.dim, "module": case.module, "dt": cfg.dt,
-                   "parallelism": "single" if world == 1 else "slab%d-%s (%s halo exchange)" % (
-                       world, "xyz"[SLAB_AXIS[case.dim]], "host-staged" if os.environ.get("MPH_SLAB_TRANSPORT") == "host" else "RCCL")},
+                   "parallelism": "single" if world == 1 else "slab%d-%s (%s halo exchange, %s)" % (
+                       world, "xyz"[SLAB_AXIS[case.dim]],
+                       "host-staged" if os.environ.get("MPH_SLAB_TRANSPORT") == "host" else "RCCL",
+                       "equal widths" if cuts is None else "cuts at particle-count quantiles"),
+                "slab_cuts": None if cuts is None else [round(float(x), 9) for x in cuts]},
         "achieved_hbm_gbps_alg": B_ALG_STEP * value / 1e9,
         "achieved_hbm_gbps_measured": (step_bytes / (elapsed / args.steps) / 1e9) if step_bytes else None,
         "hbm_measured": ({"bytes_per_step": step_bytes, "bytes_per_particle_step": step_bytes / n_total,

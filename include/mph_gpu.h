@@ -317,12 +317,18 @@ typedef struct MphSlabOptions {
     void* host_user;
     int n_glob;                        /* 0: the arrays hold every particle (n == n_glob)       */
     const int* ids;
+    /* NULL: nranks equal slabs; else the nranks - 1 interior boundaries along the axis, strictly
+     * ascending inside the domain (slab r = [cuts[r-1], cuts[r]), the first and last reaching
+     * the domain faces), the same array on every rank -- e.g. particle-count quantiles, so that
+     * the ranks hold equal shares (balanced_cuts in particlemethod_fsi_amd/dist.py)           */
+    const double* cuts;
 } MphSlabOptions;
 int mph_create_slab(MphCtx** ctx, const MphConfig* cfg, int n, const int* property, const double* pos,
                     const double* pos0, const double* vel, int device, const MphSlabOptions* opt);
 /* Host-only: the periodic window [lo, hi) (out2) along `axis` that rank `rank` of `nranks` needs
- * at slab-local creation: its slab widened by two halo widths on each side.                   */
-int mph_slab_window(const MphConfig* cfg, int rank, int nranks, int axis, double* out2);
+ * at slab-local creation: its slab widened by two halo widths on each side.  cuts: as in
+ * MphSlabOptions (NULL: equal slabs).                                                         */
+int mph_slab_window(const MphConfig* cfg, int rank, int nranks, int axis, const double* cuts, double* out2);
 /* One-rank RCCL communicator on `device` whose two neighbours are itself: checks that the
  * exchange delivers each message to the right buffer (the per-peer ordering nranks == 2 relies
  * on) without a second GPU.  Returns 0 on success.                                            */
@@ -335,10 +341,11 @@ int mph_dist_info(const MphCtx* ctx, int* out8);
 /* Particles currently owned by this rank (after the last migration); their original indices.  */
 int mph_owned_count(const MphCtx* ctx);
 int mph_owned_ids(MphCtx* ctx, int* out_ids);
-/* Host-only: the slab bounds [lo, hi) of `rank` and the halo width along `axis` that
- * mph_create_dist would use (out3 = {lo, hi, h}), and whether a rank owns coordinate c.      */
-int mph_slab_bounds(const MphConfig* cfg, int rank, int nranks, int axis, double* out3);
-int mph_slab_owner(const MphConfig* cfg, int nranks, int axis, double c);
+/* Host-only: the slab bounds [lo, hi) of `rank` and the halo width along `axis` that a slab
+ * context would use (out3 = {lo, hi, h}), and which rank owns coordinate c.  cuts: as in
+ * MphSlabOptions (NULL: equal slabs).                                                         */
+int mph_slab_bounds(const MphConfig* cfg, int rank, int nranks, int axis, const double* cuts, double* out3);
+int mph_slab_owner(const MphConfig* cfg, int nranks, int axis, const double* cuts, double c);
 
 #ifdef __cplusplus
 }

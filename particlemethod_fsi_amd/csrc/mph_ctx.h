@@ -17,6 +17,7 @@
 struct MphDist {
     int rank = 0, nranks = 1, left = 0, right = 0;
     mph::SlabGeom g{};
+    std::vector<double> cuts;     // interior slab boundaries (MphSlabOptions.cuts); empty: equal widths
     int cap = 0;                  // capacity of every local per-particle array
     int n_own = 0;                // owned particles after the last redistribution (host mirror)
     // Every size of a step lives on the device (DistLayout), so a step has no host round trip and

@@ -65,23 +65,45 @@ constexpr double kStructMargin = 4.0;   // x ParticleSpacing: elastic particle d
             return ctx_fail(ctx, MPH_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
     } while (0)
 
-// Slab of `rank`: equal widths along `axis`; hi(r) and lo(r+1) are the same expression.
-void slab_of(const HostDerived& h, int axis, int rank, int nranks, double& lo, double& hi)
+// Slab of `rank` along `axis`: equal widths, or the caller's cuts (nranks - 1 interior
+// coordinates, ascending; MphSlabOptions.cuts); hi(r) and lo(r+1) are the same expression.
+void slab_of(const HostDerived& h, int axis, int rank, int nranks, const double* cuts, double& lo, double& hi)
 {
     const double W = h.dw[axis];
+    if (cuts) {
+        lo = rank == 0 ? h.dmin[axis] : cuts[rank - 1];
+        hi = rank == nranks - 1 ? h.dmax[axis] : cuts[rank];
+        return;
+    }
     lo = rank == 0 ? h.dmin[axis] : h.dmin[axis] + W * rank / nranks;
     hi = rank == nranks - 1 ? h.dmax[axis] : h.dmin[axis] + W * (rank + 1) / nranks;
 }
 
-SlabGeom make_geom(const HostDerived& h, int axis, int rank, int nranks, double halo)
+// cuts strictly ascending inside the domain (NULL: equal widths)
+int check_cuts(const HostDerived& h, int axis, int nranks, const double* cuts, std::string& err)
+{
+    if (!cuts) return MPH_OK;
+    for (int k = 0; k < nranks - 1; ++k) {
+        const double lo = k == 0 ? h.dmin[axis] : cuts[k - 1];
+        if (!(cuts[k] > lo) || !(cuts[k] < h.dmax[axis])) {
+            err = "slab cuts must ascend strictly inside the domain";
+            return MPH_ERR_ARG;
+        }
+    }
+    return MPH_OK;
+}
+
+const double* dist_cuts(const MphDist& D) { return D.cuts.empty() ? nullptr : D.cuts.data(); }
+
+SlabGeom make_geom(const HostDerived& h, int axis, int rank, int nranks, const double* cuts, double halo)
 {
     SlabGeom g{};
     g.axis = axis;
     g.w = h.dw[axis];
     const int l = (rank + nranks - 1) % nranks, r = (rank + 1) % nranks;
-    slab_of(h, axis, rank, nranks, g.lo, g.hi);
-    slab_of(h, axis, l, nranks, g.llo, g.lhi);
-    slab_of(h, axis, r, nranks, g.rlo, g.rhi);
+    slab_of(h, axis, rank, nranks, cuts, g.lo, g.hi);
+    slab_of(h, axis, l, nranks, cuts, g.llo, g.lhi);
+    slab_of(h, axis, r, nranks, cuts, g.rlo, g.rhi);
     g.first = rank == 0; g.last = rank == nranks - 1;
     g.lfirst = l == 0; g.llast = l == nranks - 1;
     g.rfirst = r == 0; g.rlast = r == nranks - 1;
@@ -99,22 +121,22 @@ double wrap_coord(const HostDerived& h, int axis, double x)
 
 double halo_width(const DevParams& P) { return std::sqrt(P.rc2) * (1.0 + 1e-6); }
 
-int owner_rank(const HostDerived& h, int axis, int nranks, double x)
+int owner_rank(const HostDerived& h, int axis, int nranks, const double* cuts, double x)
 {
     const double a = wrap_coord(h, axis, x);
     for (int r = 0; r < nranks; ++r) {
         double lo, hi;
-        slab_of(h, axis, r, nranks, lo, hi);
+        slab_of(h, axis, r, nranks, cuts, lo, hi);
         if (slab_owns(a, lo, hi, r == 0, r == nranks - 1)) return r;
     }
     return nranks - 1;
 }
 
 // signed periodic offset of x from the centre of rank r's slab
-double slab_offset(const HostDerived& h, int axis, int r, int nranks, double x)
+double slab_offset(const HostDerived& h, int axis, int r, int nranks, const double* cuts, double x)
 {
     double lo, hi;
-    slab_of(h, axis, r, nranks, lo, hi);
+    slab_of(h, axis, r, nranks, cuts, lo, hi);
     const double W = h.dw[axis];
     double off = x - 0.5 * (lo + hi);
     off -= W * std::floor(off / W + 0.5);
@@ -346,15 +368,20 @@ int dist_setup(MphCtx* c, const double* pos, std::vector<int>& owned)
     const bool has_struct = !c->S.orig.empty();
     const double smargin = has_struct ? kStructMargin * h.dx : 0.0;
     const double halo = halo_width(c->P) + smargin;
-    D.g = make_geom(h, axis, D.rank, D.nranks, halo);
+    MPH_CK(ctx_fail(c, check_cuts(h, axis, D.nranks, dist_cuts(D), err), err));
+    D.g = make_geom(h, axis, D.rank, D.nranks, dist_cuts(D), halo);
     D.g.smargin = smargin;
     const double W = h.dw[axis];
     const double cw = W / c->P.gc[axis];
     // slabs must be wider than two halos plus a migration margin, so that a band particle is
     // mirrored to one neighbour only and a migrant reaches only the adjacent slab
-    if (W / D.nranks < 2.0 * halo + 2.0 * h.dx)
-        return ctx_fail(c, MPH_ERR_DOMAIN, "slab width " + std::to_string(W / D.nranks) +
-                                               " below two halo widths (" + std::to_string(2.0 * halo) + ")");
+    for (int r = 0; r < D.nranks; ++r) {
+        double lo, hi;
+        slab_of(h, axis, r, D.nranks, dist_cuts(D), lo, hi);
+        if (hi - lo < 2.0 * halo + 2.0 * h.dx)
+            return ctx_fail(c, MPH_ERR_DOMAIN, "slab width " + std::to_string(hi - lo) + " below two halo widths (" +
+                                                   std::to_string(2.0 * halo) + ")");
+    }
     // local window grid along the slab axis: [lo - h - cw, hi + h + cw)
     const double wlo = D.g.lo - halo - cw, whi = D.g.hi + halo + cw;
     const int gloc = (int)std::ceil((whi - wlo) / cw);
@@ -377,7 +404,8 @@ int dist_setup(MphCtx* c, const double* pos, std::vector<int>& owned)
         const double a = wrap_coord(h, axis, pos[3 * (size_t)i + axis]);
         if (is_struct(c->prop[i])) {
             // static owner: the slab of the InitialPosition
-            if (owner_rank(h, axis, D.nranks, c->pos0[3 * (size_t)i + axis]) == D.rank) owned.push_back(i);
+            if (owner_rank(h, axis, D.nranks, dist_cuts(D), c->pos0[3 * (size_t)i + axis]) == D.rank)
+                owned.push_back(i);
             else ++near;
             continue;
         }
@@ -405,7 +433,8 @@ int dist_struct_setup(MphCtx* c, std::vector<int>& lsl, int& n_own)
     const int axis = D.g.axis, R = D.nranks;
     const int ns = (int)S.orig.size();
     std::vector<int> owner(ns);
-    for (int s = 0; s < ns; ++s) owner[s] = owner_rank(h, axis, R, c->pos0[3 * (size_t)S.orig[s] + axis]);
+    const double* cuts = dist_cuts(D);
+    for (int s = 0; s < ns; ++s) owner[s] = owner_rank(h, axis, R, cuts, c->pos0[3 * (size_t)S.orig[s] + axis]);
     // ghost slots of rank r: the list neighbours (out- and in-lists) of its owned slots that other
     // ranks own, split by side (periodic offset of x0 from r's slab centre), ascending slot id
     std::string err;
@@ -417,7 +446,7 @@ int dist_struct_setup(MphCtx* c, std::vector<int>& lsl, int& n_own)
         auto visit = [&](int j) {
             if (owner[j] == r || seen[j]) return;
             seen[j] = 1;
-            const bool lside = slab_offset(h, axis, r, R, c->pos0[3 * (size_t)S.orig[j] + axis]) < 0.0;
+            const bool lside = slab_offset(h, axis, r, R, cuts, c->pos0[3 * (size_t)S.orig[j] + axis]) < 0.0;
             if (owner[j] != (lside ? left : right)) err = "structure list spans more than one slab";
             (lside ? gl : gr).push_back(j);
         };
@@ -680,6 +709,7 @@ int mph_create_slab(MphCtx** ctx, const MphConfig* cfg, int n, const int* proper
     D->rank = opt->rank;
     D->nranks = opt->nranks;
     D->g.axis = opt->axis;
+    if (opt->cuts) D->cuts.assign(opt->cuts, opt->cuts + std::max(opt->nranks - 1, 0));
     if (opt->unique_id128) {
         D->rccl = true;
         D->graphs = std::getenv("MPH_SLAB_GRAPHS") == nullptr || std::string(std::getenv("MPH_SLAB_GRAPHS")) != "0";
@@ -822,22 +852,24 @@ int mph_owned_ids(MphCtx* c, int* out)
     return k == c->dist->n_own ? MPH_OK : ctx_fail(c, MPH_ERR_CAPACITY, "owned id count mismatch");
 }
 
-int mph_slab_bounds(const MphConfig* cfg, int rank, int nranks, int axis, double* out3)
+int mph_slab_bounds(const MphConfig* cfg, int rank, int nranks, int axis, const double* cuts, double* out3)
 {
     if (!cfg || !out3 || nranks < 1 || rank < 0 || rank >= nranks || axis < 0 || axis > 2) return MPH_ERR_ARG;
     HostDerived h{};
     derive_constants(*cfg, h);
+    std::string err;
+    if (check_cuts(h, axis, nranks, cuts, err) != MPH_OK) return MPH_ERR_ARG;
     DevParams P{};
     make_dev_params(*cfg, h, 0, 0, P);
-    slab_of(h, axis, rank, nranks, out3[0], out3[1]);
+    slab_of(h, axis, rank, nranks, cuts, out3[0], out3[1]);
     out3[2] = halo_width(P);
     return MPH_OK;
 }
 
-int mph_slab_window(const MphConfig* cfg, int rank, int nranks, int axis, double* out2)
+int mph_slab_window(const MphConfig* cfg, int rank, int nranks, int axis, const double* cuts, double* out2)
 {
     double b[3];
-    const int rc = mph_slab_bounds(cfg, rank, nranks, axis, b);
+    const int rc = mph_slab_bounds(cfg, rank, nranks, axis, cuts, b);
     if (rc != MPH_OK) return rc;
     if (!out2) return MPH_ERR_ARG;
     // two halo widths, each including the elastic particles' displacement margin, so that the
@@ -849,15 +881,17 @@ int mph_slab_window(const MphConfig* cfg, int rank, int nranks, int axis, double
     return MPH_OK;
 }
 
-int mph_slab_owner(const MphConfig* cfg, int nranks, int axis, double x)
+int mph_slab_owner(const MphConfig* cfg, int nranks, int axis, const double* cuts, double x)
 {
     if (!cfg || nranks < 1 || axis < 0 || axis > 2) return MPH_ERR_ARG;
     HostDerived h{};
     derive_constants(*cfg, h);
+    std::string err;
+    if (check_cuts(h, axis, nranks, cuts, err) != MPH_OK) return MPH_ERR_ARG;
     const double a = wrap_coord(h, axis, x);
     for (int r = 0; r < nranks; ++r) {
         double lo, hi;
-        slab_of(h, axis, r, nranks, lo, hi);
+        slab_of(h, axis, r, nranks, cuts, lo, hi);
         if (slab_owns(a, lo, hi, r == 0, r == nranks - 1)) return r;
     }
     return MPH_ERR_DOMAIN;

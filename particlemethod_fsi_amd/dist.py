@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from . import solver
+from . import mphio, solver
 
 
 class GlooExchange:
@@ -54,24 +54,45 @@ class GlooExchange:
             np.frombuffer(mv, dtype=np.uint8)[:] = b.numpy()
 
 
-def rccl_slab(rank: int, nranks: int, axis: int, group=None, ids=None, n_glob: int = 0) -> solver.Slab:
+def rccl_slab(rank: int, nranks: int, axis: int, group=None, ids=None, n_glob: int = 0, cuts=None) -> solver.Slab:
     """Slab options with an RCCL communicator: rank 0 makes the unique id, everyone receives it
     through torch.distributed (any backend)."""
     import torch.distributed as dist
     obj = [solver.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0, group=group)
-    return solver.Slab(rank, nranks, axis, uid=obj[0], ids=ids, n_glob=n_glob)
+    return solver.Slab(rank, nranks, axis, uid=obj[0], ids=ids, n_glob=n_glob, cuts=cuts)
 
 
-def gloo_slab(rank: int, nranks: int, axis: int, group=None, ids=None, n_glob: int = 0) -> solver.Slab:
-    return solver.Slab(rank, nranks, axis, exchange=GlooExchange(rank, nranks, group), ids=ids, n_glob=n_glob)
+def gloo_slab(rank: int, nranks: int, axis: int, group=None, ids=None, n_glob: int = 0, cuts=None) -> solver.Slab:
+    return solver.Slab(rank, nranks, axis, exchange=GlooExchange(rank, nranks, group), ids=ids, n_glob=n_glob,
+                       cuts=cuts)
 
 
-def build_local(case, rank: int, nranks: int, axis: int):
-    """This rank's share of a registered case for slab-local creation: (cfg, particles of its
-    window, their original indices, total count) -- generated without the rest of the problem."""
+def balanced_cuts(case, nranks: int, axis: int) -> np.ndarray:
+    """Interior slab boundaries (MphSlabOptions.cuts) that give every rank the same share of the
+    initial particles: count quantiles of the case's lattice planes along `axis`
+    (mphio.plane_counts), each cut halfway between two planes.  Deterministic, so every rank
+    computes the same array."""
     cfg, _ = case._config()
-    lo, hi = solver.slab_window(cfg, rank, nranks, axis)
+    dmin = cfg.domain_min[axis]
+    W = cfg.domain_max[axis] - dmin
+    v, c = mphio.plane_counts(case.cuboids, axis, dmin, W)
+    cum = np.cumsum(c)
+    total = int(cum[-1]) if len(cum) else 0
+    cuts = []
+    for k in range(1, nranks):
+        p = int(np.searchsorted(cum, total * k / nranks))   # first plane reaching the quantile
+        p = min(p, len(v) - 2)
+        cuts.append(0.5 * (v[p] + v[p + 1]))
+    return np.array(cuts, np.float64)
+
+
+def build_local(case, rank: int, nranks: int, axis: int, cuts=None):
+    """This rank's share of a registered case for slab-local creation: (cfg, particles of its
+    window, their original indices, total count) -- generated without the rest of the problem.
+    cuts: the slab boundaries the contexts will use (None: equal slabs)."""
+    cfg, _ = case._config()
+    lo, hi = solver.slab_window(cfg, rank, nranks, axis, cuts)
     return case.build_window(axis, lo, hi)
 
 

@@ -288,6 +288,27 @@ def generate_window(cuboids: list[Cuboid], axis: int, lo: float, hi: float, dmin
     return parts, idx, base
 
 
+def plane_counts(cuboids: list[Cuboid], axis: int, dmin: float, width: float):
+    """(coordinates, counts): the lattice planes of ``generate(cuboids)`` along ``axis`` (wrapped
+    into the periodic domain [dmin, dmin + width), ascending) and the particles on each -- the
+    particle distribution along a slab axis without generating the particles."""
+    vals, cnts = [], []
+    for cub in cuboids:
+        ax = [np.array([_e(v) for v in _axis_values(cub.lower[d], cub.upper[d], cub.space)])
+              for d in range(3)]
+        per = len(ax[(axis + 1) % 3]) * len(ax[(axis + 2) % 3])
+        u = ax[axis] - dmin
+        vals.append(u - width * np.floor(u / width) + dmin)
+        cnts.append(np.full(len(ax[axis]), per, np.int64))
+    if not vals:
+        return np.zeros(0), np.zeros(0, np.int64)
+    v, c = np.concatenate(vals), np.concatenate(cnts)
+    order = np.argsort(v, kind="stable")
+    v, c = v[order], c[order]
+    uv, inv = np.unique(v, return_inverse=True)
+    return uv, np.bincount(inv, weights=c).astype(np.int64)
+
+
 def format_grid(p: Particles, spacing: float, lower, upper, time: float = 0.0) -> str:
     """Text of the generator's ``writefile`` (generator.cpp:839-862); ``time`` is the first line
     (0 from the generator; a .prof restart carries its Time, main.cpp:797, 961)."""

@@ -68,7 +68,8 @@ class MphSlabOptions(ctypes.Structure):
     """include/mph_gpu.h MphSlabOptions."""
     _fields_ = [("rank", ctypes.c_int), ("nranks", ctypes.c_int), ("axis", ctypes.c_int),
                 ("unique_id128", ctypes.c_char_p), ("host_fn", HOST_EXCHANGE_FN),
-                ("host_user", ctypes.c_void_p), ("n_glob", ctypes.c_int), ("ids", ctypes.c_void_p)]
+                ("host_user", ctypes.c_void_p), ("n_glob", ctypes.c_int), ("ids", ctypes.c_void_p),
+                ("cuts", ctypes.c_void_p)]
 
 
 class MphError(RuntimeError):
@@ -127,8 +128,8 @@ def load_library() -> ctypes.CDLL:
         "mph_create_dist_host": (ip, [ctypes.POINTER(vp), cfgp, ip, vp, vp, vp, vp, ip, ip, ip, ip,
                                       HOST_EXCHANGE_FN, vp]),
         "mph_owned_ids": (ip, [vp, vp]),
-        "mph_slab_bounds": (ip, [cfgp, ip, ip, ip, vp]),
-        "mph_slab_owner": (ip, [cfgp, ip, ip, dp]),
+        "mph_slab_bounds": (ip, [cfgp, ip, ip, ip, vp, vp]),
+        "mph_slab_owner": (ip, [cfgp, ip, ip, vp, dp]),
         "mph_dist_selftest": (ip, [ip]),
         "mph_derive_scalars": (ip, [cfgp, vp]),
         "mph_structure_init": (ip, [cfgp, ip, vp, vp, vp, vp, vp, vp]),
@@ -143,7 +144,7 @@ def load_library() -> ctypes.CDLL:
         "mph_set_initial_velocity_profile": (ip, [vp]),
         "mph_dist_info": (ip, [vp, vp]),
         "mph_create_slab": (ip, [ctypes.POINTER(vp), cfgp, ip, vp, vp, vp, vp, ip, ctypes.POINTER(MphSlabOptions)]),
-        "mph_slab_window": (ip, [cfgp, ip, ip, ip, vp]),
+        "mph_slab_window": (ip, [cfgp, ip, ip, ip, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -213,22 +214,35 @@ def _check(rc, ctx=None):
     return rc
 
 
-def slab_bounds(cfg: mphio.MphConfig, rank: int, nranks: int, axis: int):
-    """(lo, hi, halo) of a rank's slab, as mph_create_dist computes them (host only)."""
+def _cuts(cuts, nranks: int):
+    """(array kept alive, pointer or None) for MphSlabOptions.cuts / the host helpers."""
+    if cuts is None:
+        return None, None
+    c = np.ascontiguousarray(cuts, np.float64)
+    if c.shape != (nranks - 1,):
+        raise ValueError("cuts: %d interior boundaries expected for %d slabs" % (nranks - 1, nranks))
+    return c, c.ctypes.data
+
+
+def slab_bounds(cfg: mphio.MphConfig, rank: int, nranks: int, axis: int, cuts=None):
+    """(lo, hi, halo) of a rank's slab, as a slab context computes them (host only)."""
     out = np.zeros(3)
-    _check(load_library().mph_slab_bounds(ctypes.byref(cfg), rank, nranks, axis, out.ctypes.data))
+    c, p = _cuts(cuts, nranks)
+    _check(load_library().mph_slab_bounds(ctypes.byref(cfg), rank, nranks, axis, p, out.ctypes.data))
     return float(out[0]), float(out[1]), float(out[2])
 
 
-def slab_window(cfg: mphio.MphConfig, rank: int, nranks: int, axis: int):
+def slab_window(cfg: mphio.MphConfig, rank: int, nranks: int, axis: int, cuts=None):
     """(lo, hi): the periodic window of particles a rank needs for slab-local creation."""
     out = np.zeros(2)
-    _check(load_library().mph_slab_window(ctypes.byref(cfg), rank, nranks, axis, out.ctypes.data))
+    c, p = _cuts(cuts, nranks)
+    _check(load_library().mph_slab_window(ctypes.byref(cfg), rank, nranks, axis, p, out.ctypes.data))
     return float(out[0]), float(out[1])
 
 
-def slab_owner(cfg: mphio.MphConfig, nranks: int, axis: int, x: float) -> int:
-    return _check(load_library().mph_slab_owner(ctypes.byref(cfg), nranks, axis, float(x)))
+def slab_owner(cfg: mphio.MphConfig, nranks: int, axis: int, x: float, cuts=None) -> int:
+    c, p = _cuts(cuts, nranks)
+    return _check(load_library().mph_slab_owner(ctypes.byref(cfg), nranks, axis, p, float(x)))
 
 
 class Slab:
@@ -237,14 +251,17 @@ class Slab:
     `exchange(send_l, send_r, recv_l, recv_r)` over memoryviews (mph_create_dist_host)."""
 
     def __init__(self, rank: int, nranks: int, axis: int, uid: bytes | None = None, exchange=None,
-                 ids: np.ndarray | None = None, n_glob: int = 0):
+                 ids: np.ndarray | None = None, n_glob: int = 0, cuts=None):
         """ids/n_glob: slab-local creation -- the particles handed to MphSolver are only this
-        rank's window (slab_window), with their original indices ids among n_glob."""
+        rank's window (slab_window), with their original indices ids among n_glob.
+        cuts: the nranks - 1 interior slab boundaries (None: equal slabs), the same on every rank
+        (dist.balanced_cuts)."""
         if (uid is None) == (exchange is None):
             raise ValueError("Slab needs exactly one of uid (RCCL) or exchange (host transport)")
         self.rank, self.nranks, self.axis, self.uid, self.exchange = rank, nranks, axis, uid, exchange
         self.ids = None if ids is None else np.ascontiguousarray(ids, np.int32)
         self.n_glob = int(n_glob) if ids is not None else 0
+        self.cuts = _cuts(cuts, nranks)[0]
 
 
 def unique_id() -> bytes:
@@ -290,6 +307,8 @@ class MphSolver:
                 opt.ids = slab.ids.ctypes.data
                 self._keep_ids = slab.ids
                 self.n = slab.n_glob
+            if slab.cuts is not None:
+                opt.cuts = slab.cuts.ctypes.data
             rc = L.mph_create_slab(ctypes.byref(h), ctypes.byref(self.cfg), parts.n, *ptrs, int(device),
                                    ctypes.byref(opt))
         if rc < 0:

@@ -27,21 +27,35 @@ def _init(rank, world, port):
     return dist
 
 
-def gpu_worker(rank, world, port, case, checkpoints, fields, out_path, local=False):
+def make_cuts(c, world, axis, mode):
+    """Slab boundaries of a test run: None (equal slabs), "balanced" (dist.balanced_cuts, as
+    bench.py) or "skew" (equal cuts moved alternately by a tenth of a slab width)."""
+    if mode is None:
+        return None
+    from particlemethod_fsi_amd.dist import balanced_cuts
+    if mode == "balanced":
+        return balanced_cuts(c, world, axis)
+    cfg, _ = c._config()
+    dmin, W = cfg.domain_min[axis], cfg.domain_max[axis] - cfg.domain_min[axis]
+    return np.array([dmin + W * k / world + (0.1 if k % 2 else -0.1) * W / world for k in range(1, world)])
+
+
+def gpu_worker(rank, world, port, case, checkpoints, fields, out_path, local=False, cuts_mode=None):
     """Run `case` as rank `rank` of `world` on cuda:0; at every checkpoint (cumulative step
     count) gather `fields` over the ranks; rank 0 saves them to out_path (.npz).  local: the rank
-    is created from its own window of the case only (slab-local creation)."""
+    is created from its own window of the case only (slab-local creation); cuts_mode: make_cuts."""
     dist = _init(rank, world, port)
     from particlemethod_fsi_amd import MphSolver, cases
     from particlemethod_fsi_amd.dist import build_local, gather_field, gloo_slab
     c = cases.get(case)
     axis = SLAB_AXIS[case]
+    cuts = make_cuts(c, world, axis, cuts_mode)
     if local:
-        cfg, parts, ids, n_glob = build_local(c, rank, world, axis)
-        slab = gloo_slab(rank, world, axis, ids=ids, n_glob=n_glob)
+        cfg, parts, ids, n_glob = build_local(c, rank, world, axis, cuts)
+        slab = gloo_slab(rank, world, axis, ids=ids, n_glob=n_glob, cuts=cuts)
     else:
         cfg, parts = c.build()
-        slab = gloo_slab(rank, world, axis)
+        slab = gloo_slab(rank, world, axis, cuts=cuts)
     res = {}
     with MphSolver(cfg, parts, device=0, slab=slab) as s:
         def owner_map():
@@ -136,7 +150,7 @@ def band_worker(rank, world, port, case, out_path):
     dist.destroy_process_group()
 
 
-def gpu_rank_worker(rank, world, port, case, axis, nsteps, fields, out_dir, transport="host"):
+def gpu_rank_worker(rank, world, port, case, axis, nsteps, fields, out_dir, transport="host", cuts_mode=None):
     """One slab rank of a large case on cuda:0 (several ranks share the GPU), created from its own
     window of the case only (slab-local creation): run `nsteps`, then save this rank's owned
     particle ids and their `fields` to out_dir/rank<r>.npz (no gather through the process group,
@@ -145,9 +159,10 @@ def gpu_rank_worker(rank, world, port, case, axis, nsteps, fields, out_dir, tran
     from particlemethod_fsi_amd import MphSolver, cases
     from particlemethod_fsi_amd.dist import build_local, gloo_slab, rccl_slab
     c = cases.get(case)
-    cfg, parts, ids, n_glob = build_local(c, rank, world, axis)
+    cuts = make_cuts(c, world, axis, cuts_mode)
+    cfg, parts, ids, n_glob = build_local(c, rank, world, axis, cuts)
     mk = gloo_slab if transport == "host" else rccl_slab
-    with MphSolver(cfg, parts, device=0, slab=mk(rank, world, axis, ids=ids, n_glob=n_glob)) as s:
+    with MphSolver(cfg, parts, device=0, slab=mk(rank, world, axis, ids=ids, n_glob=n_glob, cuts=cuts)) as s:
         del parts
         s.step(nsteps)
         ids = s.owned_ids()

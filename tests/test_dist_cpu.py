@@ -75,3 +75,39 @@ def test_halo_band_contains_all_neighbours(tmp_path, world):
     assert res[:, 0].sum() == n             # ownership is a partition
     assert (res[:, 1] == 0).all(), res       # no owned particle misses a neighbour
     assert (res[:, 2] > 0).all()             # dam2d's fluid spans the slab faces
+
+
+@pytest.mark.parametrize("case,nranks", [("d16m", 8), ("d16m", 2), ("d1m", 4), ("dam2d", 3)])
+def test_balanced_cuts_equalise_shares(case, nranks):
+    """dist.balanced_cuts (bench.py's slab boundaries): the cuts ascend inside the domain, the
+    library's bounds/owner functions follow them, and the initial particles split into shares
+    within one lattice plane of equal."""
+    from particlemethod_fsi_amd import mphio
+    from particlemethod_fsi_amd.dist import balanced_cuts
+    c = cases.get(case)
+    axis = 2 if c.dim == 3 else 0
+    cfg, _ = c._config()
+    cuts = balanced_cuts(c, nranks, axis)
+    assert cuts.shape == (nranks - 1,) and np.all(np.diff(cuts) > 0)
+    b = [solver.slab_bounds(cfg, r, nranks, axis, cuts) for r in range(nranks)]
+    assert b[0][0] == cfg.domain_min[axis] and b[-1][1] == cfg.domain_max[axis]
+    for r in range(nranks - 1):
+        assert b[r][1] == b[r + 1][0] == cuts[r]
+    dmin = cfg.domain_min[axis]
+    v, n = mphio.plane_counts(c.cuboids, axis, dmin, cfg.domain_max[axis] - dmin)
+    owner = np.array([solver.slab_owner(cfg, nranks, axis, x, cuts) for x in v])
+    share = np.bincount(owner, weights=n, minlength=nranks)
+    assert share.sum() == n.sum()
+    assert share.max() - share.min() <= 2 * n.max(), share
+    # equal slabs are the cuts=None default
+    assert solver.slab_bounds(cfg, 1, nranks, axis) == solver.slab_bounds(cfg, 1, nranks, axis, None)
+
+
+def test_bad_cuts_rejected():
+    cfg, _ = cases.get("d1m").build()
+    with pytest.raises(solver.MphError):
+        solver.slab_bounds(cfg, 0, 3, 2, [0.05, 0.02])        # not ascending
+    with pytest.raises(solver.MphError):
+        solver.slab_owner(cfg, 2, 2, 0.0, [cfg.domain_max[2] + 1.0])   # outside the domain
+    with pytest.raises(ValueError):
+        solver.slab_window(cfg, 0, 3, 2, [0.05])              # wrong length

@@ -62,11 +62,13 @@ def test_d16m_single_context_rerun_time_and_counts():
 
 
 def test_d16m_slab8_matches_single_context(tmp_path):
+    """The 8-slab configuration of bench.py --gpus 8 (slab-local creation, cuts at the
+    particle-count quantiles) against one context over all 16.2M particles."""
     world = 8
     ctx = mp.get_context("spawn")
     port = _free_port()
     ps = [ctx.Process(target=dist_worker.gpu_rank_worker,
-                      args=(r, world, port, "d16m", 2, STEPS, FIELDS, str(tmp_path)))
+                      args=(r, world, port, "d16m", 2, STEPS, FIELDS, str(tmp_path), "host", "balanced"))
           for r in range(world)]
     for p in ps:
         p.start()

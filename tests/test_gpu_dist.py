@@ -37,10 +37,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def run_slab(case, world, checkpoints, out, fields=FIELDS, local=False):
+def run_slab(case, world, checkpoints, out, fields=FIELDS, local=False, cuts_mode=None):
     ctx = mp.get_context("spawn")
     port = _free_port()
-    ps = [ctx.Process(target=dist_worker.gpu_worker, args=(r, world, port, case, checkpoints, fields, out, local))
+    ps = [ctx.Process(target=dist_worker.gpu_worker,
+                      args=(r, world, port, case, checkpoints, fields, out, local, cuts_mode))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -73,15 +74,17 @@ def close(f, a, b, rel=1e-8):
 STRUCT_REL = {"DivergenceP": 1e-6}
 
 
-@pytest.mark.parametrize("case,world,local", [("channel3d", 2, False), ("channel3d", 3, False),
-                                              ("channel2d", 4, False), ("channel3d_st", 2, False),
-                                              ("dam2d", 2, False), ("channel3d", 3, True),
-                                              ("channel2d", 4, True)])
-def test_slab_ranks_match_oracle(tmp_path, case, world, local):
-    """local: every rank is created from its own window of the case (slab-local creation)."""
+@pytest.mark.parametrize("case,world,local,cuts", [("channel3d", 2, False, None), ("channel3d", 3, False, None),
+                                                   ("channel2d", 4, False, None), ("channel3d_st", 2, False, None),
+                                                   ("dam2d", 2, False, None), ("channel3d", 3, True, None),
+                                                   ("channel2d", 4, True, None), ("channel3d", 3, True, "skew"),
+                                                   ("channel2d", 4, False, "skew"), ("dam2d", 3, True, "balanced")])
+def test_slab_ranks_match_oracle(tmp_path, case, world, local, cuts):
+    """local: every rank is created from its own window of the case (slab-local creation);
+    cuts: unequal slabs (MphSlabOptions.cuts)."""
     from oracle_bindings import OracleSolver
     checkpoints = [1, 5, 20]
-    r = run_slab(case, world, checkpoints, str(tmp_path / "slab.npz"), local=local)
+    r = run_slab(case, world, checkpoints, str(tmp_path / "slab.npz"), local=local, cuts_mode=cuts)
     cfg, parts = cases.get(case).build()
     assert (r["owner0"] >= 0).all()
     o = OracleSolver(cfg, parts)
@@ -102,16 +105,18 @@ def test_slab_ranks_match_oracle(tmp_path, case, world, local):
         assert moved, "no particle migrated between slabs"
 
 
-@pytest.mark.parametrize("case,world,local", [("bar2d", 2, False), ("bar2d", 3, False), ("bar3d", 2, False),
-                                              ("gate2d_sub", 2, False), ("bar2d", 3, True),
-                                              ("gate2d_sub", 2, True)])
-def test_slab_structure_ranks_match_oracle(tmp_path, case, world, local):
+@pytest.mark.parametrize("case,world,local,cuts", [("bar2d", 2, False, None), ("bar2d", 3, False, None),
+                                                   ("bar3d", 2, False, None), ("gate2d_sub", 2, False, None),
+                                                   ("bar2d", 3, True, None), ("gate2d_sub", 2, True, None),
+                                                   ("bar2d", 3, True, "skew")])
+def test_slab_structure_ranks_match_oracle(tmp_path, case, world, local, cuts):
     """Elastic-solid particles across slab faces: static owners by InitialPosition, ghost slots of
     the fixed Lagrangian lists exchanged before every stress / velocity half-substep.  local: the
-    structure lists are built from each rank's window only."""
+    structure lists are built from each rank's window only; cuts: unequal slabs."""
     from oracle_bindings import OracleSolver
     checkpoints = [1, 10, 30]
-    r = run_slab(case, world, checkpoints, str(tmp_path / "slab.npz"), STRUCT_FIELDS, local=local)
+    r = run_slab(case, world, checkpoints, str(tmp_path / "slab.npz"), STRUCT_FIELDS, local=local,
+                 cuts_mode=cuts)
     cfg, parts = cases.get(case).build()
     o = OracleSolver(cfg, parts)
     o.init()
