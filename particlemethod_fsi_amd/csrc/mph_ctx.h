@@ -84,6 +84,7 @@ struct MphCtx {
     double *vir = nullptr, *vpres = nullptr;   // VirialStress [cap][9] / VirialPressure (A order), lazy
     int *nbr = nullptr, *ncount = nullptr;
     int2* seg_hdr = nullptr;     // per-wave list headers (column-segmented lists)
+    int* list_hdr = nullptr;     // per-wave headers of the compact 16-bit lists (kLhdr ints each)
     double *pres = nullptr, *gx = nullptr, *gy = nullptr, *gz = nullptr, *pa = nullptr;
     double4 *force = nullptr, *acc = nullptr, *fpart = nullptr, *rec = nullptr;
     double *dens_a = nullptr, *vstrain = nullptr, *divp = nullptr;

@@ -68,7 +68,7 @@ void ctx_fill_launch(MphCtx* c)
     // returned through A.id), so k_rank_scatter skips that scatter; slab mode uses dst_of.
     L.A = c->A; L.B = c->B; L.rank_of = nullptr; L.dst_of = nullptr;
     L.key = c->key; L.slot = c->slot; L.tmp = c->tmp; L.cnt = c->cnt; L.start = c->start; L.bsum = c->bsum;
-    L.nbr = c->nbr; L.ncount = c->ncount; L.hdr = c->seg_hdr;
+    L.nbr = c->nbr; L.ncount = c->ncount; L.hdr = c->seg_hdr; L.lhdr = c->list_hdr;
     L.pres = c->pres; L.gx = c->gx; L.gy = c->gy; L.gz = c->gz; L.pa = c->pa;
     L.force = c->force; L.acc = c->acc; L.fpart = c->fpart; L.rec = c->rec;
     L.dens_a = c->dens_a; L.vstrain = c->vstrain; L.divp = c->divp;
@@ -346,6 +346,7 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     CK(dalloc(c, &c->bsum, (size_t)c->P.ncell / 4096 + 2));
     CK(dalloc(c, &c->nbr, ntile * kTile * kMaxNeighbor)); CK(dalloc(c, &c->ncount, cap));
     CK(dalloc(c, &c->seg_hdr, ntile * kSegHdr));
+    CK(dalloc(c, &c->list_hdr, ntile * kLhdr));
     CK(dalloc(c, &c->pres, cap)); CK(dalloc(c, &c->gx, cap)); CK(dalloc(c, &c->gy, cap)); CK(dalloc(c, &c->gz, cap));
     CK(dalloc(c, &c->pa, cap)); CK(dalloc(c, &c->force, cap)); CK(dalloc(c, &c->acc, cap));
     CK(dalloc(c, &c->fpart, cap)); CK(dalloc(c, &c->rec, cap));

@@ -80,6 +80,7 @@ struct Launch {
     int *key = nullptr, *slot = nullptr, *tmp = nullptr, *cnt = nullptr, *start = nullptr, *bsum = nullptr;
     int *nbr = nullptr, *ncount = nullptr;
     int2* hdr = nullptr;          // per-wave headers of the column-segmented lists (kSegHdr each)
+    int* lhdr = nullptr;          // per-wave headers of the compact 16-bit lists (kLhdr each)
     // pass A products (A order): pressure values, gravity centre (GC, PressureA), sums
     double *pres = nullptr, *gx = nullptr, *gy = nullptr, *gz = nullptr, *pa = nullptr;
     double *dens_a = nullptr, *vstrain = nullptr, *divp = nullptr;

@@ -211,11 +211,80 @@ __device__ __forceinline__ int list_load(const int* p)
 {
     return MPH_LIST_NT ? __builtin_nontemporal_load(p) : *p;
 }
-__device__ __forceinline__ void list_store(int* p, int v) { *p = v; }
+#ifndef MPH_LIST_NT_STORE
+#define MPH_LIST_NT_STORE 0
+#endif
+__device__ __forceinline__ void list_store(int* p, int v)
+{
+    if (MPH_LIST_NT_STORE) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 
 __device__ __forceinline__ const int* ell_row(const int* nbr, int i)
 {
     return nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
+}
+
+// Compact neighbour list (MPH_LIST16, the default for interior waves).  The stencil's columns
+// fall into 5 groups (3-D: the 5 columns of one slowest-axis offset, which are consecutive in
+// cell order; 2-D: each column), so every neighbour of a group lies in a short index range from
+// the group's wave-wide first candidate.  Entry k of a lane is 16 bits -- the offset from its
+// group's base (13 bits) and the neighbour's type (3 bits) -- two entries per 32-bit word at
+// word[k / 2][lane] of the wave's tile (same order as the ELL row, so sums are bit-identical).
+// Per wave the header (kLhdr ints) holds the 5 group bases, the format flag (1 = compact,
+// 0 = the 32-bit ELL row: waves near a periodic face or whose group ranges are too long) and,
+// per lane, the count at the end of groups 0-3 (4 bytes).  Half the list bytes of the ELL rows.
+#ifndef MPH_LIST16
+#define MPH_LIST16 1
+#endif
+constexpr int kOff16 = 13;                  // offset bits of a compact entry (type above)
+constexpr int kSpan16 = (1 << kOff16) - 1;  // longest group range a compact wave may have
+
+struct NbrList {
+    const int* tile;                // the wave's list tile (wave-uniform)
+    int lane;
+    int b0, b1, b2, b3, b4;         // group bases (wave-uniform)
+    unsigned ends;                  // the lane's counts at the ends of groups 0-3 (bytes)
+    bool c16;                       // wave-uniform format flag
+};
+
+__device__ __forceinline__ NbrList nbr_list(const int* nbr, const int* lhdr, int i)
+{
+    NbrList L;
+    const int tile = __builtin_amdgcn_readfirstlane(i >> 6);
+    L.tile = nbr + (size_t)tile * (kTile * kMaxNeighbor);
+    L.lane = i & 63;
+    const int* h = lhdr ? lhdr + (size_t)tile * kLhdr : nullptr;
+    L.c16 = MPH_LIST16 && h && h[5] == 1;
+    L.b0 = L.b1 = L.b2 = L.b3 = L.b4 = 0;
+    L.ends = 0;
+    if (L.c16) {
+        L.b0 = h[0]; L.b1 = h[1]; L.b2 = h[2]; L.b3 = h[3]; L.b4 = h[4];
+        L.ends = (unsigned)h[8 + (i & 63)];
+    }
+    return L;
+}
+
+// entry k of the lane: neighbour index j and type t
+template <bool C16>
+__device__ __forceinline__ void nbr_at(NbrList L, int k, int& j, int& t)
+{
+    if (C16) {
+        const unsigned w = reinterpret_cast<const unsigned*>(L.tile)[(k >> 1) * kTile + L.lane];
+        const unsigned e = (k & 1) ? (w >> 16) : (w & 0xFFFFu);
+        const unsigned uk = (unsigned)k;
+        int b = L.b0;
+        b = uk >= (L.ends & 0xFFu) ? L.b1 : b;
+        b = uk >= ((L.ends >> 8) & 0xFFu) ? L.b2 : b;
+        b = uk >= ((L.ends >> 16) & 0xFFu) ? L.b3 : b;
+        b = uk >= (L.ends >> 24) ? L.b4 : b;
+        j = b + (int)(e & kSpan16);
+        t = (int)(e >> kOff16);
+    } else {
+        const int e = list_load(L.tile + k * kTile + L.lane);
+        j = e & kIndexMask;
+        t = e >> kTypeShift;
+    }
 }
 
 // Column-segmented neighbour list of an interior wavefront (MPH_SEG).  The search visits the
@@ -805,7 +874,8 @@ template <int DIM, bool SEG, int PERM, int SB = MPH_SB, int CAP = MPH_LDS_CAP>
 __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa& A, const int* start,
                                                    int i, bool act, double xi, double yi, double zi,
                                                    int cx, int cy, int cz, int* out, double* sx,
-                                                   unsigned short* seg, int2* hdr, int* seg_overflow)
+                                                   unsigned short* seg, int2* hdr, int* seg_overflow,
+                                                   int* lh = nullptr, unsigned short* o16 = nullptr)
 {
     double* sy = sx + (CAP + SB);
     double* sz = sx + 2 * (CAP + SB);
@@ -849,12 +919,51 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             je = start[base + hi + 1];
         }
     };
+    // compact list (nbr_list): the wave-wide index range of every column group, from the cell
+    // ranges of its first and last column (no column wraps: the wave is interior)
+    const bool want16 = MPH_LIST16 && !SEG && lh != nullptr;
+    bool c16 = false;
+    int g0 = 0, g1 = 0, g2 = 0, g3 = 0, g4 = 0, gbase = 0;
+    if (want16) {
+        bool ok = true;
+#pragma unroll
+        for (int g = 0; g < 5; ++g) {
+            int lo = 0x7fffffff, hi = -1;
+            if (act) {
+                if (DIM == 3) {
+                    const int a0 = cc[X::A0] + g - 2, c1 = cc[X::A1];
+                    lo = start[((a0 * P.gc[X::A1] + c1 - 2) * P.gc[X::A2]) + cca - P.sa];
+                    hi = start[((a0 * P.gc[X::A1] + c1 + 2) * P.gc[X::A2]) + cca + P.sa + 1];
+                } else {
+                    lo = start[(cx + g - 2) * P.gc[1] + cca - P.sa];
+                    hi = start[(cx + g - 2) * P.gc[1] + cca + P.sa + 1];
+                }
+            }
+            const int mn = wave_min(lo), mx = wave_max(hi);
+            ok = ok && (mx <= mn || mx - mn <= kSpan16 + 1);
+            const int b = mx > mn ? mn : 0;
+            if (g == 0) g0 = b;
+            if (g == 1) g1 = b;
+            if (g == 2) g2 = b;
+            if (g == 3) g3 = b;
+            if (g == 4) g4 = b;
+        }
+        c16 = ok;
+    }
+    unsigned ends = 0;
     // software pipeline: the start[] loads of column col + 1 are in flight while column col is
     // staged and tested (the per-column chain start[] -> window -> staging loads is latency bound)
     int nb_jb, nb_je;
     col_range(0, nb_jb, nb_je);
     int slot = 0;   // SEG: first slot of this column's segment
     for (int col = 0; col < NCOL; ++col) {
+        if (c16) {
+            // entering group g: the count so far ends group g - 1
+            const bool first = DIM == 3 ? col % 5 == 0 : true;
+            const int g = DIM == 3 ? col / 5 : col;
+            if (first && g > 0) ends |= (unsigned)min(cnt, 255) << (8 * (g - 1));
+            if (first) gbase = g == 0 ? g0 : g == 1 ? g1 : g == 2 ? g2 : g == 3 ? g3 : g4;
+        }
         const int jb = nb_jb, je = nb_je;
         if (MPH_SEARCH_PREFETCH && col + 1 < NCOL) col_range(col + 1, nb_jb, nb_je);
         const bool any = je > jb;
@@ -900,6 +1009,10 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                             const int sl = slot + (cnt - cnt0);
                             if (sl < kSegCap)
                                 seg[(size_t)sl * kTile + lane] = (unsigned short)((j - mn) | (st[k0 + u] << 8));
+                        } else if (c16) {
+                            const int k = min(cnt, kMaxNeighbor - 1);
+                            o16[(((k >> 1) * kTile + lane) << 1) + (k & 1)] =
+                                (unsigned short)((j - gbase) | (st[k0 + u] << kOff16));
                         } else if (!MPH_DIAG_NOSTORE) {
                             list_store(out + min(cnt, kMaxNeighbor - 1) * kTile, nbr_entry(j, st[k0 + u]));
                         }
@@ -928,6 +1041,10 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                                 seg[(size_t)sl * kTile + lane] = (unsigned short)(j & 0xFFFF);
                                 seg[(size_t)(sl + 1) * kTile + lane] = (unsigned short)((j >> 16) | (A.type[j] << 12));
                             }
+                        } else if (c16) {
+                            if (cnt < kMaxNeighbor)
+                                o16[(((cnt >> 1) * kTile + lane) << 1) + (cnt & 1)] =
+                                    (unsigned short)((j - gbase) | (A.type[j] << kOff16));
                         } else if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) {
                             list_store(out + cnt * kTile, nbr_entry(j, A.type[j]));
                         }
@@ -949,6 +1066,14 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
         }
     }
     if (SEG && slot > kSegCap) *seg_overflow = 1;
+    if (c16) {
+        // group ends of this lane, the bases and the format flag of the wave
+        lh[8 + lane] = (int)ends;
+        if (lane == 0) {
+            lh[0] = g0; lh[1] = g1; lh[2] = g2; lh[3] = g3; lh[4] = g4;
+            lh[5] = 1;
+        }
+    }
     return cnt;
 }
 
@@ -965,12 +1090,16 @@ __device__ __forceinline__ bool wave_all_ghosts(const DevParams& P, const Soa& A
 
 template <int DIM, int PERM>
 __device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A, const int* start, int* nbr,
-                                               int* ncount, int2* hdr, DevState* st, double* stage)
+                                               int* ncount, int2* hdr, int* lhdr, DevState* st, double* stage)
 {
     const int n = dev_n(P);
     const int i = xcd_block(blockIdx.x, live_blocks(n)) * blockDim.x + threadIdx.x;
     const bool live = i < n;
     const int ii = live ? i : n - 1;
+    // list format of the wave: the 32-bit ELL row unless the interior search below goes compact
+    const int tile = __builtin_amdgcn_readfirstlane(i >> 6);
+    int* lh = lhdr ? lhdr + (size_t)tile * kLhdr : nullptr;
+    if (lh && (threadIdx.x & 63) == 0) lh[5] = 0;
     if (wave_all_ghosts(P, A, live, ii)) {
         if (live) ncount[i] = 0;
         return;
@@ -998,7 +1127,9 @@ __device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A,
 #endif
         {
             cnt = scan_candidates_lds<DIM, false, PERM>(P, A, start, i, own, xi, yi, zi, cx, cy, cz, out,
-                                                        stage, nullptr, nullptr, nullptr);
+                                                        stage, nullptr, nullptr, nullptr, lh,
+                                                        reinterpret_cast<unsigned short*>(
+                                                            nbr + (size_t)tile * (kTile * kMaxNeighbor)));
         }
         if (live) ncount[i] = cnt;
     } else {
@@ -1025,11 +1156,12 @@ __device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A,
 template <int DIM, int PERM>
 __global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int* __restrict__ start,
                                                    int* __restrict__ nbr, int* __restrict__ ncount,
-                                                   int2* __restrict__ hdr, DevState* __restrict__ st)
+                                                   int2* __restrict__ hdr, int* __restrict__ lhdr,
+                                                   DevState* __restrict__ st)
 {
     if ((int)blockIdx.x >= live_blocks(dev_n(P))) return;
     __shared__ double stage[4][3 * (MPH_LDS_CAP + MPH_SB) + (MPH_LDS_CAP + MPH_SB + 1) / 2];
-    neighbors_body<DIM, PERM>(P, A, start, nbr, ncount, hdr, st, stage[threadIdx.x >> 6]);
+    neighbors_body<DIM, PERM>(P, A, start, nbr, ncount, hdr, lhdr, st, stage[threadIdx.x >> 6]);
 }
 
 // ---------------------------------------------------------------------------- pass A -------
@@ -1042,10 +1174,10 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int
 #ifndef MPH_UB
 #define MPH_UB 8
 #endif
-template <bool FAST, int DIM, int U = MPH_UA>
+template <bool FAST, bool C16, int DIM, int U = MPH_UA>
 __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_ratio, const double* s_mu,
                                             const Soa& A,
-                                            const int* row, int cnt, int ti, bool solid, double xi,
+                                            NbrList NL, int cnt, int ti, bool solid, double xi,
                                             double yi, double zi, double vxi, double vyi, double vzi,
                                             PassA& o)
 {
@@ -1055,9 +1187,7 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
         int TT[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int e = list_load(row + (k0 + u < cnt ? k0 + u : cnt - 1) * kTile);
-            jj[u] = e & kIndexMask;
-            TT[u] = e >> kTypeShift;
+            nbr_at<C16>(NL, k0 + u < cnt ? k0 + u : cnt - 1, jj[u], TT[u]);
             if (MPH_DIAG_GATHER == 1) jj[u] = min((int)(blockIdx.x * blockDim.x + threadIdx.x) ^ 1, dev_n(P) - 1);
         }
 #pragma unroll
@@ -1085,6 +1215,12 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
     }
 }
 
+// MPH_SEG_GATHER: how the segmented passes read a column's records -- 0 staged in LDS, 1 AoS
+// gathers from global memory, 2 SoA gathers (the lanes' k-th entries of a column are aligned,
+// so the 64 lanes touch a few consecutive lines per 8-byte load)
+#ifndef MPH_SEG_GATHER
+#define MPH_SEG_GATHER 0
+#endif
 // Pass A over a column-segmented list (interior waves): per stencil column the wave stages its
 // window of 48-byte records in LDS with coalesced loads and every lane reads its neighbours from
 // there -- instead of per-lane gathers whose 64 lanes touch ~41 cache lines per 16-byte load (the
@@ -1107,8 +1243,10 @@ __device__ __forceinline__ void pass_a_seg(const DevParams& P, const double* s_r
         if (h.y >= 0) {
             const int span = h.y & 0xFFFF;
             const double2* src = A.p6 + 3 * (size_t)mn;
-            for (int t = lane; t < 3 * span; t += 64) stage[t] = src[t];
-            __builtin_amdgcn_wave_barrier();
+            if (MPH_SEG_GATHER == 0) {
+                for (int t = lane; t < 3 * span; t += 64) stage[t] = src[t];
+                __builtin_amdgcn_wave_barrier();
+            }
             for (int k0 = 0; k0 < w; k0 += U) {
                 unsigned e[U];
 #pragma unroll
@@ -1118,7 +1256,14 @@ __device__ __forceinline__ void pass_a_seg(const DevParams& P, const double* s_r
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const int q = e[u] == kSegNone ? 0 : (int)(e[u] & 0xFF);
-                    const double2 a = stage[3 * q], b = stage[3 * q + 1], c = stage[3 * q + 2];
+                    if (MPH_SEG_GATHER == 2) {   // column-aligned lanes: coherent 8-byte SoA gathers
+                        const int j = mn + q;
+                        X[u] = A.x[j]; Y[u] = A.y[j]; Z[u] = A.z[j];
+                        VX[u] = A.vx[j]; VY[u] = A.vy[j]; VZ[u] = A.vz[j];
+                        continue;
+                    }
+                    const double2* r = MPH_SEG_GATHER == 1 ? src : stage;
+                    const double2 a = r[3 * q], b = r[3 * q + 1], c = r[3 * q + 2];
                     X[u] = a.x; Y[u] = a.y; Z[u] = b.x;
                     VX[u] = b.y; VY[u] = c.x; VZ[u] = c.y;
                 }
@@ -1132,7 +1277,7 @@ __device__ __forceinline__ void pass_a_seg(const DevParams& P, const double* s_r
                                       r2_exact(q0, q1, q2), VX[u] - vxi, VY[u] - vyi, VZ[u] - vzi, o);
                 }
             }
-            __builtin_amdgcn_wave_barrier();   // every lane done reading before the next staging
+            if (MPH_SEG_GATHER == 0) __builtin_amdgcn_wave_barrier();   // reads done before the next staging
             slot += w;
         } else {
             for (int k0 = 0; k0 < w; k0 += U) {
@@ -1171,7 +1316,7 @@ __device__ __forceinline__ void pass_a_seg(const DevParams& P, const double* s_r
 }
 
 #ifndef MPH_PA_WPE
-#define MPH_PA_WPE 0
+#define MPH_PA_WPE 3   // pass A at <= 168 VGPRs: 3 waves per SIMD
 #endif
 #if MPH_PA_WPE
 #define MPH_PA_ATTR __attribute__((amdgpu_waves_per_eu(MPH_PA_WPE)))
@@ -1182,7 +1327,7 @@ template <int DIM>
 __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const DevTables* __restrict__ T, Soa A,
                                                 const int* __restrict__ nbr,
                                                 const int* __restrict__ ncount, const int2* __restrict__ hdr,
-                                                PassAOut pout)
+                                                const int* __restrict__ lhdr, PassAOut pout)
 {
     const int n = dev_n(P);
     if ((int)blockIdx.x >= live_blocks(n)) return;
@@ -1225,10 +1370,14 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
     const int ti = A.type[i];
     const bool solid = dev_is_struct(ti);
     const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
-    const int* row = ell_row(nbr, i);
+    const NbrList NL = nbr_list(nbr, lhdr, i);
     PassA o;
-    if (fast) pass_a_loop<true, DIM>(P, s_ratio, s_mu, A, row, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
-    else pass_a_loop<false, DIM>(P, s_ratio, s_mu, A, row, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+    if (NL.c16)   // compact lists come from interior searches only
+        pass_a_loop<true, true, DIM>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+    else if (fast)
+        pass_a_loop<true, false, DIM>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+    else
+        pass_a_loop<false, false, DIM>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
     pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
 }
 
@@ -1308,11 +1457,11 @@ __device__ __forceinline__ void pass_b_term(const DevParams& P, const double* s_
     f2 += c * q2;
 }
 
-template <bool FAST, bool SURF, int DIM, int U = MPH_UB>
+template <bool FAST, bool C16, bool SURF, int DIM, int U = MPH_UB>
 __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_ratio, const Soa& A,
                                             const double4* rec, const double* pres, const double* gx,
                                             const double* gy, const double* gz, const double* pa,
-                                            const int* row, int cnt, int ti, bool solid, double xi,
+                                            NbrList NL, int cnt, int ti, bool solid, double xi,
                                             double yi, double zi, double gxi, double gyi, double gzi,
                                             double pai, double ai, double& f0, double& f1, double& f2)
 {
@@ -1324,9 +1473,7 @@ __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_
         int TT[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int e = list_load(row + (k0 + u < cnt ? k0 + u : cnt - 1) * kTile);
-            jj[u] = e & kIndexMask;
-            TT[u] = e >> kTypeShift;
+            nbr_at<C16>(NL, k0 + u < cnt ? k0 + u : cnt - 1, jj[u], TT[u]);
             if (MPH_DIAG_GATHER == 1) jj[u] = min((int)(blockIdx.x * blockDim.x + threadIdx.x) ^ 1, dev_n(P) - 1);
         }
 #pragma unroll
@@ -1435,6 +1582,7 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
                                                 const double* __restrict__ pa,
                                                 const int* __restrict__ nbr,
                                                 const int* __restrict__ ncount, const int2* __restrict__ hdr,
+                                                const int* __restrict__ lhdr,
                                                 double4* __restrict__ force, double4* __restrict__ acc,
                                                 Soa B, int phase, StructHook H)
 {
@@ -1487,13 +1635,16 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
         if (!live) return;
     } else {
         const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
-        const int* row = ell_row(nbr, i);
-        if (fast)
-            pass_b_loop<true, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, row, cnt, ti, solid, xi, yi,
-                                         zi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
+        const NbrList NL = nbr_list(nbr, lhdr, i);
+        if (NL.c16)   // compact lists come from interior searches only
+            pass_b_loop<true, true, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, NL, cnt, ti, solid, xi,
+                                               yi, zi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
+        else if (fast)
+            pass_b_loop<true, false, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, NL, cnt, ti, solid, xi,
+                                                yi, zi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
         else
-            pass_b_loop<false, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, row, cnt, ti, solid, xi, yi,
-                                          zi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
+            pass_b_loop<false, false, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, NL, cnt, ti, solid, xi,
+                                                 yi, zi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
     }
     const double vxi = A.vx[i], vyi = A.vy[i], vzi = A.vz[i];
     double vo0 = vxi, vo1 = vyi, vo2 = vzi;
@@ -1554,6 +1705,7 @@ __global__ __launch_bounds__(256) void k_virial(DevParams P, const DevTables* __
                                                 const double* __restrict__ gx, const double* __restrict__ gy,
                                                 const double* __restrict__ gz, const int* __restrict__ nbr,
                                                 const int* __restrict__ ncount, const int2* __restrict__ hdr,
+                                                const int* __restrict__ lhdr,
                                                 double* __restrict__ vir, double* __restrict__ vpres)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1575,10 +1727,13 @@ __global__ __launch_bounds__(256) void k_virial(DevParams P, const DevTables* __
     const bool segmented = MPH_SEG && h && h[kSegCols].x == 1;
     const unsigned short* seg = seg_tile(nbr, i);
     const int lane = i & 63;
+    const NbrList NL = nbr_list(nbr, lhdr, i);
     int col = 0, slot = 0, used = 0;
     for (int k = 0; k < cnt; ++k) {
         int j, tj;
-        if (!segmented) {
+        if (NL.c16) {
+            nbr_at<true>(NL, k, j, tj);
+        } else if (!segmented) {
             const int e = row[k * kTile];
             j = e & kIndexMask;
             tj = e >> kTypeShift;
@@ -2367,7 +2522,7 @@ void launch_neighbors(const Launch& L)
     if (P.n == 0) return;
 #define MPH_NEIGHBORS(PERM)                                                                                  \
     MPH_LAUNCH("neighbors", L.stream, (k_neighbors<3, PERM>), dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, \
-               L.A, L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.st)
+               L.A, L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, L.st)
     if (P.dim == 3) {
         switch (P.perm) {
         case 1: MPH_NEIGHBORS(1); break;
@@ -2378,7 +2533,7 @@ void launch_neighbors(const Launch& L)
         }
     } else
         MPH_LAUNCH("neighbors", L.stream, (k_neighbors<2, 0>), dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P,
-                   L.A, L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.st);
+                   L.A, L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, L.st);
 #undef MPH_NEIGHBORS
 }
 
@@ -2390,10 +2545,10 @@ void launch_pass_a(const Launch& L)
     const PassAOut po = pass_a_out(L);
     if (P.dim == 3)
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, po);
+                   L.A, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, po);
     else
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, po);
+                   L.A, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, po);
 }
 
 static StructHook struct_hook(const Launch& L)
@@ -2423,7 +2578,7 @@ void launch_pass_b(const Launch& L, int phase)
     }
 #define MPH_PASS_B(S, D)                                                                            \
     MPH_LAUNCH(phase == 2 ? "pass_b_face" : "pass_b", L.stream, (k_pass_b<S, D>), dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, \
-               L.T, L.A, L.rec, L.fpart, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.force, L.acc, L.B, \
+               L.T, L.A, L.rec, L.fpart, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, L.force, L.acc, L.B, \
                phase, \
                struct_hook(L))
     if (P.surface) {
@@ -2441,10 +2596,10 @@ void launch_virial(const Launch& L, const Soa& X, double* vir, double* vpres)
     if (P.n == 0) return;
     if (P.dim == 3)
         MPH_LAUNCH("virial", L.stream, k_virial<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T, L.A, X,
-                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, vir, vpres);
+                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, vir, vpres);
     else
         MPH_LAUNCH("virial", L.stream, k_virial<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T, L.A, X,
-                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, vir, vpres);
+                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, vir, vpres);
 }
 
 void launch_struct_stress(const Launch& L)

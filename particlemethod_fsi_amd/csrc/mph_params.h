@@ -20,6 +20,9 @@ constexpr int kPad = 8;         // extra elements behind every per-particle arra
 // per-wave header of the column-segmented neighbour list (mph_kernels.hip, MPH_SEG): one entry per
 // stencil column (25 in 3-D) plus the list format
 constexpr int kSegHdr = 26;
+// Compact neighbour list of a wavefront (mph_kernels.hip, MPH_LIST16): ints per wave header --
+// 5 group bases, the format flag, 2 spare, then the 64 lanes' group ends
+constexpr int kLhdr = 8 + 64;
 
 inline bool is_fluid(int t) { return t >= 0 && t < 2; }   // main.cpp:69-70
 inline bool is_struct(int t) { return t >= 2 && t < 4; }  // main.cpp:71-72
