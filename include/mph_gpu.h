@@ -338,6 +338,10 @@ int mph_dist_selftest(int device);
  * local array capacity, largest send / receive message capacity (particles), particles held
  * (owned + ghosts)}.                                                                          */
 int mph_dist_info(const MphCtx* ctx, int* out8);
+/* Neighbour-list formats of the last search: out2 = {wavefronts with the compact 16-bit list,
+ * wavefronts in all} (the others, near a periodic face or with long group ranges, keep 32-bit
+ * ELL rows; MPH_LIST16=0 at creation disables the compact format).                           */
+int mph_list_formats(MphCtx* ctx, int* out2);
 /* Particles currently owned by this rank (after the last migration); their original indices.  */
 int mph_owned_count(const MphCtx* ctx);
 int mph_owned_ids(MphCtx* ctx, int* out_ids);

@@ -68,7 +68,10 @@ void ctx_fill_launch(MphCtx* c)
     // returned through A.id), so k_rank_scatter skips that scatter; slab mode uses dst_of.
     L.A = c->A; L.B = c->B; L.rank_of = nullptr; L.dst_of = nullptr;
     L.key = c->key; L.slot = c->slot; L.tmp = c->tmp; L.cnt = c->cnt; L.start = c->start; L.bsum = c->bsum;
-    L.nbr = c->nbr; L.ncount = c->ncount; L.hdr = c->seg_hdr; L.lhdr = c->list_hdr;
+    L.nbr = c->nbr; L.ncount = c->ncount; L.hdr = c->seg_hdr;
+    // compact 16-bit lists of interior wavefronts (MPH_LIST16=0: 32-bit ELL rows everywhere)
+    const char* l16 = std::getenv("MPH_LIST16");
+    L.lhdr = (l16 && std::string(l16) == "0") ? nullptr : c->list_hdr;
     L.pres = c->pres; L.gx = c->gx; L.gy = c->gy; L.gz = c->gz; L.pa = c->pa;
     L.force = c->force; L.acc = c->acc; L.fpart = c->fpart; L.rec = c->rec;
     L.dens_a = c->dens_a; L.vstrain = c->vstrain; L.divp = c->divp;
@@ -897,6 +900,22 @@ int mph_neighbor_stats(MphCtx* c, double* mean, int* mx)
     for (int v : h) { sum += v; m = v > m ? v : m; }
     *mean = c->n ? (double)sum / c->n : 0.0;
     *mx = m;
+    return MPH_OK;
+}
+
+int mph_list_formats(MphCtx* c, int* out2)
+{
+    if (!c || !out2) return MPH_ERR_ARG;
+    HIP_OK(c, hipSetDevice(c->device));
+    const int nt = (c->n + kTile - 1) / kTile;
+    int compact = 0;
+    if (nt && c->L.lhdr) {
+        std::vector<int> h((size_t)nt * kLhdr);
+        HIP_OK(c, hipMemcpy(h.data(), c->list_hdr, sizeof(int) * h.size(), hipMemcpyDeviceToHost));
+        for (int t = 0; t < nt; ++t) compact += h[(size_t)t * kLhdr + 5] == 1;
+    }
+    out2[0] = compact;
+    out2[1] = nt;
     return MPH_OK;
 }
 

@@ -56,6 +56,7 @@ EXPORTED_SYMBOLS = [
     "mph_config_sizeof", "mph_write_vtk_async", "mph_output_wait", "mph_write_grid_binary",
     "mph_write_vtu_arrays", "mph_write_vtu", "mph_velocity_profile_arrays",
     "mph_set_initial_velocity_profile", "mph_dist_info", "mph_create_slab", "mph_slab_window",
+    "mph_list_formats",
 ]
 
 # mph_host_exchange_fn (include/mph_gpu.h): (user, send_l, n, send_r, n, recv_l, n, recv_r, n)
@@ -143,6 +144,7 @@ def load_library() -> ctypes.CDLL:
         "mph_velocity_profile_arrays": (ip, [cfgp, dp, ip, vp, vp, vp, vp]),
         "mph_set_initial_velocity_profile": (ip, [vp]),
         "mph_dist_info": (ip, [vp, vp]),
+        "mph_list_formats": (ip, [vp, vp]),
         "mph_create_slab": (ip, [ctypes.POINTER(vp), cfgp, ip, vp, vp, vp, vp, ip, ctypes.POINTER(MphSlabOptions)]),
         "mph_slab_window": (ip, [cfgp, ip, ip, ip, vp, vp]),
     }
@@ -411,6 +413,12 @@ class MphSolver:
         out = np.zeros(max(self.n, 1), np.int32)
         _check(self._L.mph_owned_ids(self._h, out.ctypes.data), self._h)
         return out[:k].copy()
+
+    def list_formats(self) -> tuple:
+        """(wavefronts with compact 16-bit neighbour lists, all wavefronts) of the last search."""
+        a = np.zeros(2, np.int32)
+        _check(self._L.mph_list_formats(self._h, a.ctypes.data), self._h)
+        return int(a[0]), int(a[1])
 
     def dist_info(self) -> dict:
         """Slab-mode facts (mph_dist_info): communicator size, transport, graph replay, capacities."""

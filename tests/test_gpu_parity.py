@@ -293,3 +293,25 @@ def test_gpu_cell_orders_match_golden(case, perm, monkeypatch):
             s.step(step - done)
             done = step
             compare(g, s, step)
+
+
+@pytest.mark.parametrize("case", ["box3d", "gate3d", "d1m"])
+def test_gpu_compact_lists_bitwise_equal_ell(case, monkeypatch):
+    """The compact 16-bit neighbour lists (MPH_LIST16, default) hold the same neighbours in the same
+    order as the 32-bit ELL rows, so every field after several steps is bit-identical with
+    MPH_LIST16=0; and the interior wavefronts of the large case do use the compact format."""
+    cfg, parts = cases.get(case).build()
+    fields = ["Position", "Velocity", "PressureP", "NeighborCount", "Force", "DensityA", "VolStrainP"]
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MPH_LIST16", mode)
+        with MphSolver(cfg, parts) as s:
+            s.step(5)
+            out[mode] = {f: s.get(f) for f in fields}
+            compact, waves = s.list_formats()
+            if mode == "0":
+                assert compact == 0
+            elif case == "d1m":
+                assert compact > 0.5 * waves, (compact, waves)
+    for f in fields:
+        assert np.array_equal(out["1"][f], out["0"][f]), f
