@@ -283,6 +283,8 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         // faces are long runs (whole wavefronts) at the ends of every plane (DevParams.perm;
         // MPH_SLAB_PERM=0 keeps (x, y, z); =1..4 force an order on any 3-D context, =force
         // orders a single 3-D context the z-slab way -- A/B timing and the parity tests)
+        const char* lm = std::getenv("MPH_LIST16_MAX");
+        c->P.l16max = lm ? std::max(0, std::min(255, std::atoi(lm))) : 255;
         const char* pe = std::getenv("MPH_SLAB_PERM");
         const std::string pv = pe ? pe : "";
         const bool zslab = cfg->dim == 3 && c->dist && c->dist->g.axis == 2;

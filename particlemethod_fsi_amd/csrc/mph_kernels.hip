@@ -233,7 +233,8 @@ __device__ __forceinline__ const int* ell_row(const int* nbr, int i)
 // word[k / 2][lane] of the wave's tile (same order as the ELL row, so sums are bit-identical).
 // Per wave the header (kLhdr ints) holds the 5 group bases, the format flag (1 = compact,
 // 0 = the 32-bit ELL row: waves near a periodic face or whose group ranges are too long) and,
-// per lane, the count at the end of groups 0-3 (4 bytes).  Half the list bytes of the ELL rows.
+// per lane, the count at the end of groups 0-3 (bytes; a wave with more than 255 neighbours on a
+// lane, which the reference allows up to 511, is searched again into ELL rows: k_neighbors REDO).  Half the list bytes of the ELL rows.
 #ifndef MPH_LIST16
 #define MPH_LIST16 1
 #endif
@@ -1067,6 +1068,12 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     }
     if (SEG && slot > kSegCap) *seg_overflow = 1;
     if (c16) {
+        // the group ends are bytes: a wave with a lane past 255 neighbours (the reference allows
+        // 511) is marked for the ELL search of launch_neighbors' second launch (k_neighbors REDO)
+        if (wave_max(cnt) > P.l16max) {
+            if (lane == 0) lh[5] = 2;
+            return cnt;
+        }
         // group ends of this lane, the bases and the format flag of the wave
         lh[8 + lane] = (int)ends;
         if (lane == 0) {
@@ -1088,7 +1095,7 @@ __device__ __forceinline__ bool wave_all_ghosts(const DevParams& P, const Soa& A
     return __all(!live || A.id[ii] < 0);
 }
 
-template <int DIM, int PERM>
+template <int DIM, int PERM, int REDO>
 __device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A, const int* start, int* nbr,
                                                int* ncount, int2* hdr, int* lhdr, DevState* st, double* stage)
 {
@@ -1099,7 +1106,13 @@ __device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A,
     // list format of the wave: the 32-bit ELL row unless the interior search below goes compact
     const int tile = __builtin_amdgcn_readfirstlane(i >> 6);
     int* lh = lhdr ? lhdr + (size_t)tile * kLhdr : nullptr;
-    if (lh && (threadIdx.x & 63) == 0) lh[5] = 0;
+    if (REDO) {
+        // second launch: only the waves the first one marked (a lane past 255 neighbours), now
+        // into ELL rows
+        if (!lh || lh[5] != 2) return;
+        lh = nullptr;
+    }
+    if (lhdr && (threadIdx.x & 63) == 0) lhdr[(size_t)tile * kLhdr + 5] = 0;
     if (wave_all_ghosts(P, A, live, ii)) {
         if (live) ncount[i] = 0;
         return;
@@ -1152,8 +1165,9 @@ __device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A,
     if (cnt > kMaxNeighbor) atomicOr(&st->overflow, 1);
 }
 
-// one kernel per cell order (PERM 1: (z, x, y) for z slabs), so each keeps its own register budget
-template <int DIM, int PERM>
+// one kernel per cell order (DevParams.perm), so each keeps its own register budget; REDO: the
+// second launch over the waves whose compact list did not fit (see scan_candidates_lds)
+template <int DIM, int PERM, int REDO = 0>
 __global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int* __restrict__ start,
                                                    int* __restrict__ nbr, int* __restrict__ ncount,
                                                    int2* __restrict__ hdr, int* __restrict__ lhdr,
@@ -1161,7 +1175,7 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int
 {
     if ((int)blockIdx.x >= live_blocks(dev_n(P))) return;
     __shared__ double stage[4][3 * (MPH_LDS_CAP + MPH_SB) + (MPH_LDS_CAP + MPH_SB + 1) / 2];
-    neighbors_body<DIM, PERM>(P, A, start, nbr, ncount, hdr, lhdr, st, stage[threadIdx.x >> 6]);
+    neighbors_body<DIM, PERM, REDO>(P, A, start, nbr, ncount, hdr, lhdr, st, stage[threadIdx.x >> 6]);
 }
 
 // ---------------------------------------------------------------------------- pass A -------
@@ -2520,20 +2534,27 @@ void launch_neighbors(const Launch& L)
     Profiler* prof = L.prof;
     const DevParams& P = *L.P;
     if (P.n == 0) return;
-#define MPH_NEIGHBORS(PERM)                                                                                  \
-    MPH_LAUNCH("neighbors", L.stream, (k_neighbors<3, PERM>), dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, \
-               L.A, L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, L.st)
+    // the second launch (REDO) only when compact lists are on; its waves exit at once unless the
+    // first marked them
+#define MPH_NEIGHBORS(D, PERM)                                                                               \
+    do {                                                                                                     \
+        MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM>), dim3(blocks(P.n, 256)), dim3(256), 0,     \
+                   L.stream, P, L.A, L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, L.st);   \
+        if (L.lhdr)                                                                                          \
+            MPH_LAUNCH("neighbors_redo", L.stream, (k_neighbors<D, PERM, 1>), dim3(blocks(P.n, 256)),       \
+                       dim3(256), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, nullptr, L.lhdr, L.st);   \
+    } while (0)
     if (P.dim == 3) {
         switch (P.perm) {
-        case 1: MPH_NEIGHBORS(1); break;
-        case 2: MPH_NEIGHBORS(2); break;
-        case 3: MPH_NEIGHBORS(3); break;
-        case 4: MPH_NEIGHBORS(4); break;
-        default: MPH_NEIGHBORS(0); break;
+        case 1: MPH_NEIGHBORS(3, 1); break;
+        case 2: MPH_NEIGHBORS(3, 2); break;
+        case 3: MPH_NEIGHBORS(3, 3); break;
+        case 4: MPH_NEIGHBORS(3, 4); break;
+        default: MPH_NEIGHBORS(3, 0); break;
         }
-    } else
-        MPH_LAUNCH("neighbors", L.stream, (k_neighbors<2, 0>), dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P,
-                   L.A, L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, L.st);
+    } else {
+        MPH_NEIGHBORS(2, 0);
+    }
 #undef MPH_NEIGHBORS
 }
 

@@ -21,7 +21,7 @@ constexpr int kPad = 8;         // extra elements behind every per-particle arra
 // stencil column (25 in 3-D) plus the list format
 constexpr int kSegHdr = 26;
 // Compact neighbour list of a wavefront (mph_kernels.hip, MPH_LIST16): ints per wave header --
-// 5 group bases, the format flag, 2 spare, then the 64 lanes' group ends
+// 5 group bases, the format flag, 2 spare, then the 64 lanes' group ends (4 bytes each)
 constexpr int kLhdr = 8 + 64;
 
 inline bool is_fluid(int t) { return t >= 0 && t < 2; }   // main.cpp:69-70
@@ -64,6 +64,8 @@ struct DevParams {
     // wavefronts the list kernels skip) while every XCD's contiguous share of the sorted arrays
     // stays a band of that slowest axis through the whole slab (L2 locality); 1, 2 put z slowest
     int perm;
+    int l16max;        // most neighbours a lane of a compact-list wave may have (255: byte group
+                       // ends; lower only to test the ELL redo, MPH_LIST16_MAX)
     int fast_ok;       // every active axis has > 12 GPU cells: interior waves may skip the
                        // periodic branch of the minimum image (see k_neighbors)
     double inner_lo[3], inner_hi[3];   // interior box: >= 3 GPU cells from every periodic face
