@@ -1097,21 +1097,16 @@ __device__ __forceinline__ bool wave_all_ghosts(const DevParams& P, const Soa& A
 
 template <int DIM, int PERM, int REDO>
 __device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A, const int* start, int* nbr,
-                                               int* ncount, int2* hdr, int* lhdr, DevState* st, double* stage)
+                                               int* ncount, int2* hdr, int* lhdr, DevState* st, double* stage,
+                                               int i)
 {
     const int n = dev_n(P);
-    const int i = xcd_block(blockIdx.x, live_blocks(n)) * blockDim.x + threadIdx.x;
     const bool live = i < n;
     const int ii = live ? i : n - 1;
     // list format of the wave: the 32-bit ELL row unless the interior search below goes compact
     const int tile = __builtin_amdgcn_readfirstlane(i >> 6);
     int* lh = lhdr ? lhdr + (size_t)tile * kLhdr : nullptr;
-    if (REDO) {
-        // second launch: only the waves the first one marked (a lane past 255 neighbours), now
-        // into ELL rows
-        if (!lh || lh[5] != 2) return;
-        lh = nullptr;
-    }
+    if (REDO) lh = nullptr;   // a wave the first launch marked: now into ELL rows
     if (lhdr && (threadIdx.x & 63) == 0) lhdr[(size_t)tile * kLhdr + 5] = 0;
     if (wave_all_ghosts(P, A, live, ii)) {
         if (live) ncount[i] = 0;
@@ -1165,17 +1160,42 @@ __device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A,
     if (cnt > kMaxNeighbor) atomicOr(&st->overflow, 1);
 }
 
-// one kernel per cell order (DevParams.perm), so each keeps its own register budget; REDO: the
-// second launch over the waves whose compact list did not fit (see scan_candidates_lds)
-template <int DIM, int PERM, int REDO = 0>
+// one kernel per cell order (DevParams.perm), so each keeps its own register budget
+template <int DIM, int PERM>
 __global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int* __restrict__ start,
                                                    int* __restrict__ nbr, int* __restrict__ ncount,
                                                    int2* __restrict__ hdr, int* __restrict__ lhdr,
                                                    DevState* __restrict__ st)
 {
-    if ((int)blockIdx.x >= live_blocks(dev_n(P))) return;
+    const int n = dev_n(P);
+    if ((int)blockIdx.x >= live_blocks(n)) return;
     __shared__ double stage[4][3 * (MPH_LDS_CAP + MPH_SB) + (MPH_LDS_CAP + MPH_SB + 1) / 2];
-    neighbors_body<DIM, PERM, REDO>(P, A, start, nbr, ncount, hdr, lhdr, st, stage[threadIdx.x >> 6]);
+    const int i = xcd_block(blockIdx.x, live_blocks(n)) * blockDim.x + threadIdx.x;
+    neighbors_body<DIM, PERM, 0>(P, A, start, nbr, ncount, hdr, lhdr, st, stage[threadIdx.x >> 6], i);
+}
+
+// The second launch, over the waves whose compact list did not fit (scan_candidates_lds marks
+// them): each lane checks one wave's header, and the wave then searches every marked one of its
+// 64 into ELL rows -- a few microseconds when none is marked (grid: one lane per wave of the
+// first launch).
+template <int DIM, int PERM>
+__global__ __launch_bounds__(256) void k_neighbors_redo(DevParams P, Soa A, const int* __restrict__ start,
+                                                        int* __restrict__ nbr, int* __restrict__ ncount,
+                                                        int* __restrict__ lhdr, DevState* __restrict__ st)
+{
+    const int n = dev_n(P);
+    const int ntile = (n + kTile - 1) / kTile;
+    __shared__ double stage[4][3 * (MPH_LDS_CAP + MPH_SB) + (MPH_LDS_CAP + MPH_SB + 1) / 2];
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;   // the wave header this lane checks
+    const bool marked = t < ntile && lhdr[(size_t)t * kLhdr + 5] == 2;
+    unsigned long long m = __ballot(marked);
+    const int first = (t & ~63);
+    while (m) {
+        const int b = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        neighbors_body<DIM, PERM, 1>(P, A, start, nbr, ncount, nullptr, lhdr, st, stage[threadIdx.x >> 6],
+                                     (first + b) * kTile + (threadIdx.x & 63));
+    }
 }
 
 // ---------------------------------------------------------------------------- pass A -------
@@ -2541,8 +2561,9 @@ void launch_neighbors(const Launch& L)
         MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM>), dim3(blocks(P.n, 256)), dim3(256), 0,     \
                    L.stream, P, L.A, L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, L.st);   \
         if (L.lhdr)                                                                                          \
-            MPH_LAUNCH("neighbors_redo", L.stream, (k_neighbors<D, PERM, 1>), dim3(blocks(P.n, 256)),       \
-                       dim3(256), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, nullptr, L.lhdr, L.st);   \
+            MPH_LAUNCH("neighbors_redo", L.stream, (k_neighbors_redo<D, PERM>),                            \
+                       dim3(blocks((P.n + kTile - 1) / kTile, 256)),                                         \
+                       dim3(256), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.lhdr, L.st);            \
     } while (0)
     if (P.dim == 3) {
         switch (P.perm) {

@@ -44,7 +44,7 @@ def main():
     tag = sys.argv[3] if len(sys.argv) > 3 else ""
     fetch = per_kernel(src + "/fetch/*counter_collection.csv")
     write = per_kernel(src + "/write/*counter_collection.csv")
-    names = {"k_neighbors": "neighbors", "k_pass_a": "pass_a", "k_pass_b": "pass_b", "k_prep": "prep",
+    names = {"k_neighbors": "neighbors", "k_neighbors_redo": "neighbors_redo", "k_pass_a": "pass_a", "k_pass_b": "pass_b", "k_prep": "prep",
              "k_rank_scatter": "rank_scatter", "k_scan_down": "scan_down", "k_scan_reduce": "scan_reduce",
              "k_scan_top": "scan_top", "k_place": "place"}
     out = {"_note": "HBM bytes per launch = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE "
