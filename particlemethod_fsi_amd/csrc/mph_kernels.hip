@@ -1071,7 +1071,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
         // the group ends are bytes: a wave with a lane past 255 neighbours (the reference allows
         // 511) is marked for the ELL search of launch_neighbors' second launch (k_neighbors REDO)
         if (wave_max(cnt) > P.l16max) {
-            if (lane == 0) lh[5] = 2;
+            if (lane == 0) lh[5] = 2;   // counted in DevState.list_redo by neighbors_body
             return cnt;
         }
         // group ends of this lane, the bases and the format flag of the wave
@@ -1138,6 +1138,7 @@ __device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A,
                                                         stage, nullptr, nullptr, nullptr, lh,
                                                         reinterpret_cast<unsigned short*>(
                                                             nbr + (size_t)tile * (kTile * kMaxNeighbor)));
+            if (lh && (threadIdx.x & 63) == 0 && lh[5] == 2) atomicAdd(&st->list_redo, 1);
         }
         if (live) ncount[i] = cnt;
     } else {
@@ -1175,27 +1176,31 @@ __global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int
 }
 
 // The second launch, over the waves whose compact list did not fit (scan_candidates_lds marks
-// them): each lane checks one wave's header, and the wave then searches every marked one of its
-// 64 into ELL rows -- a few microseconds when none is marked (grid: one lane per wave of the
-// first launch).
+// them and counts them in DevState.list_redo): one block; it exits at once when the count is zero
+// (the rule: a lane past 255 neighbours, physically far off), else its 4 waves walk every wave
+// header and search the marked ones into ELL rows, then clear the count for the next step.
 template <int DIM, int PERM>
 __global__ __launch_bounds__(256) void k_neighbors_redo(DevParams P, Soa A, const int* __restrict__ start,
                                                         int* __restrict__ nbr, int* __restrict__ ncount,
                                                         int* __restrict__ lhdr, DevState* __restrict__ st)
 {
+    if (st->list_redo == 0) return;
     const int n = dev_n(P);
     const int ntile = (n + kTile - 1) / kTile;
     __shared__ double stage[4][3 * (MPH_LDS_CAP + MPH_SB) + (MPH_LDS_CAP + MPH_SB + 1) / 2];
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;   // the wave header this lane checks
-    const bool marked = t < ntile && lhdr[(size_t)t * kLhdr + 5] == 2;
-    unsigned long long m = __ballot(marked);
-    const int first = (t & ~63);
-    while (m) {
-        const int b = __ffsll((long long)m) - 1;
-        m &= m - 1;
-        neighbors_body<DIM, PERM, 1>(P, A, start, nbr, ncount, nullptr, lhdr, st, stage[threadIdx.x >> 6],
-                                     (first + b) * kTile + (threadIdx.x & 63));
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int t0 = wave * 64; t0 < ntile; t0 += 4 * 64) {
+        const int t = t0 + lane;   // the wave header this lane checks
+        unsigned long long m = __ballot(t < ntile && lhdr[(size_t)t * kLhdr + 5] == 2);
+        while (m) {
+            const int b = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            neighbors_body<DIM, PERM, 1>(P, A, start, nbr, ncount, nullptr, lhdr, st, stage[wave],
+                                         (t0 + b) * kTile + lane);
+        }
     }
+    __syncthreads();
+    if (threadIdx.x == 0) st->list_redo = 0;
 }
 
 // ---------------------------------------------------------------------------- pass A -------
@@ -2561,8 +2566,7 @@ void launch_neighbors(const Launch& L)
         MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM>), dim3(blocks(P.n, 256)), dim3(256), 0,     \
                    L.stream, P, L.A, L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, L.st);   \
         if (L.lhdr)                                                                                          \
-            MPH_LAUNCH("neighbors_redo", L.stream, (k_neighbors_redo<D, PERM>),                            \
-                       dim3(blocks((P.n + kTile - 1) / kTile, 256)),                                         \
+            MPH_LAUNCH("neighbors_redo", L.stream, (k_neighbors_redo<D, PERM>), dim3(1),                  \
                        dim3(256), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.lhdr, L.st);            \
     } while (0)
     if (P.dim == 3) {

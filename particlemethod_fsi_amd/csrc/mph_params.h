@@ -106,6 +106,7 @@ struct DevState {
     double wall_rot[kTypes][3][3];  // WallRotation (initializeWall)
     int overflow;                // error bits: 1 neighbour overflow (> MAX_NEIGHBOR_COUNT),
                                  // 2 slab jump (mph_dist), 4 non-finite position
+    int list_redo;               // waves of this step's search left for k_neighbors_redo
 };
 
 #if defined(__HIPCC__)
