@@ -7,7 +7,9 @@ reference at sizes whose golden files would be too large to commit:
   fsi3d       3-D dam onto an elastic gate, 2,259,700       (configs[3])
   bar2d_400k  2-D elastic cantilever, 400,000 structure     (configs[2])
 
-Two steps each (the oracle needs a few seconds per step on the host cores).  Same tolerances as
+Ten steps each, compared after steps 1, 2, 5 and 10 (the oracle needs about a second per step
+on 16 host cores); sums of the elastic cases at 1e-7 relative, the solid bound of the other
+parity tests.  Same tolerances as
 test_gpu_parity.py: NeighborCount exact, positions 1e-12 m, velocities 1e-9 m/s, sums 1e-8
 relative + roundoff floor.  Plus size-independent properties of the full D1M run: a rerun is
 bitwise identical and the time advances by exactly Dt per step.
@@ -41,9 +43,11 @@ def test_full_size_matches_oracle(case):
     o.init()
     with MphSolver(cfg, parts) as s:
         assert np.array_equal(s.get("NeighborCount"), o.get("NeighborCount"))
-        for k in range(2):
-            s.step(1)
-            o.step(1)
+        done = 0
+        for k in (1, 2, 5, 10):
+            s.step(k - done)
+            o.step(k - done)
+            done = k
             assert np.array_equal(s.get("NeighborCount"), o.get("NeighborCount")), (case, k)
             fields = ["Position", "Velocity", "PressureP", "VolStrainP", "DivergenceP", "Force"]
             if solid.any():
@@ -53,7 +57,11 @@ def test_full_size_matches_oracle(case):
                 if f in ("DeformGradient", "Stress"):
                     a, b = a[solid], b[solid]
                 scale = float(np.max(np.abs(b))) if b.size else 0.0
-                t = {"Position": 1e-12, "Velocity": 1e-9}.get(f, 1e-8 * scale + FLOOR.get(f, 1e-12))
+                # elastic cases run near the solid's stability limit, where reassociation roundoff
+                # grows ~10x per 10 steps: the solid bound of test_gpu_parity / test_gpu_dist
+                # (DivergenceP, a difference of nearly equal sums, 1e-6 as in test_gpu_dist)
+                rel = (1e-6 if f == "DivergenceP" else 1e-7) if solid.any() else 1e-8
+                t = {"Position": 1e-12, "Velocity": 1e-9}.get(f, rel * scale + FLOOR.get(f, 1e-12))
                 err = float(np.max(np.abs(a - b))) if b.size else 0.0
                 assert err <= t, (case, k, f, err, t)
 
