@@ -511,20 +511,34 @@ __global__ __launch_bounds__(1024) void k_scan_top(int* __restrict__ bsum, int n
     }
 }
 
+// top: bsum holds the raw block totals and every block sums its predecessors' itself (no
+// k_scan_top launch; used while the block count is small, kScanFusedTop)
+#ifndef MPH_SCAN_FUSED_TOP
+#define MPH_SCAN_FUSED_TOP 4096
+#endif
+constexpr int kScanFusedTop = MPH_SCAN_FUSED_TOP;
 __global__ __launch_bounds__(kScanThreads) void k_scan_down(int* __restrict__ cnt, int ncell,
                                                             const int* __restrict__ bsum,
                                                             int* __restrict__ start, int n,
-                                                            const int* __restrict__ n_dev)
+                                                            const int* __restrict__ n_dev, int top)
 {
     __shared__ int lds[kScanThreads / 64];
     const int base = blockIdx.x * kScanBlock + threadIdx.x * kScanItems;
     int v[kScanItems];
     load16(cnt, base, ncell, v);
+    int pre = 0;
+    if (top) {
+        int t = 0;
+        for (int b = threadIdx.x; b < (int)blockIdx.x; b += kScanThreads) t += bsum[b];
+        block_exclusive_scan(t, lds, pre);
+    } else {
+        pre = bsum[blockIdx.x];
+    }
     int s = 0;
 #pragma unroll
     for (int k = 0; k < kScanItems; ++k) s += v[k];
     int total;
-    int run = block_exclusive_scan(s, lds, total) + bsum[blockIdx.x];
+    int run = block_exclusive_scan(s, lds, total) + pre;
     int o[kScanItems];
 #pragma unroll
     for (int k = 0; k < kScanItems; ++k) {
@@ -2538,11 +2552,12 @@ void launch_sort(const Launch& L, int mode)
     MPH_LAUNCH("prep", L.stream, k_prep, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.B,
                L.key, L.slot, L.cnt, mode);
     const int nb = blocks(P.ncell, kScanBlock);
+    const int top = nb <= kScanFusedTop;
     MPH_LAUNCH("scan_reduce", L.stream, k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt,
                P.ncell, L.bsum);
-    MPH_LAUNCH("scan_top", L.stream, k_scan_top, dim3(1), dim3(1024), 0, L.stream, L.bsum, nb);
+    if (!top) MPH_LAUNCH("scan_top", L.stream, k_scan_top, dim3(1), dim3(1024), 0, L.stream, L.bsum, nb);
     MPH_LAUNCH("scan_down", L.stream, k_scan_down, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt,
-               P.ncell, L.bsum, L.start, n, P.n_dev);
+               P.ncell, L.bsum, L.start, n, P.n_dev, top);
     MPH_LAUNCH("place", L.stream, k_place, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.key,
                L.slot, L.start, L.tmp, mode);
     MPH_LAUNCH("rank_scatter", L.stream, k_rank_scatter, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P,
@@ -2773,10 +2788,11 @@ void launch_struct_unpack(const Launch& L, const double4* buf, int w, const int*
 void launch_scan(int* cnt, int ncell, int* bsum, int* start, int total, hipStream_t stream, Profiler* prof)
 {
     const int nb = blocks(ncell, kScanBlock);
+    const int top = nb <= kScanFusedTop;
     MPH_LAUNCH("scan_reduce", stream, k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, stream, cnt, ncell, bsum);
-    MPH_LAUNCH("scan_top", stream, k_scan_top, dim3(1), dim3(1024), 0, stream, bsum, nb);
+    if (!top) MPH_LAUNCH("scan_top", stream, k_scan_top, dim3(1), dim3(1024), 0, stream, bsum, nb);
     MPH_LAUNCH("scan_down", stream, k_scan_down, dim3(nb), dim3(kScanThreads), 0, stream, cnt, ncell, bsum,
-               start, total, (const int*)nullptr);
+               start, total, (const int*)nullptr, top);
 }
 
 int dist_blocks(int n) { return blocks(n > 0 ? n : 1, 256); }
