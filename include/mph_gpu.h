@@ -287,7 +287,7 @@ int mph_dist_unique_id(char* out128);
  * `rank` of `nranks`; all ranks pass the full particle set.  Transport: RCCL (ncclSend/Recv
  * with the two periodic neighbours, on the context's stream).  Every size of a step is kept on
  * the device and messages travel with fixed capacities (grown between mph_step batches when a
- * count passes 80 %), so the steps are replayed from captured hipGraphs with no host round trip
+ * count passes 90 %), so the steps are replayed from captured hipGraphs with no host round trip
  * (MPH_SLAB_GRAPHS=0: direct launches).                                                       */
 int mph_create_dist(MphCtx** ctx, const MphConfig* cfg, int n, const int* property,
                     const double* pos, const double* pos0, const double* vel, int device,

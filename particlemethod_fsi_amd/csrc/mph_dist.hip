@@ -16,7 +16,7 @@
 //      the previous step are dropped.
 //   2. stable partition into C = [migR | bandR | inner | bandL | migL]     (scan + scatter)
 //   3. exchange: to the left neighbour [bandL | migL], to the right [migR | bandR] (56 B per
-//      particle, preceded by a 2-int count message); received messages are appended to C:
+//      particle, behind a header with the two class counts); received messages are appended to C:
 //      [.. | from left: their migR (ours now), their bandR (ghosts) | from right: their bandL
 //      (ghosts), their migL (ours now)].  Our own migrants stay in C as ghosts.
 //   4. cell sort of C (owned + ghosts) into A, neighbour search, pass A -- the single-GPU kernels
@@ -56,6 +56,7 @@ using namespace mph;
 namespace {
 
 constexpr size_t kMsgBytes = 56;   // per particle, k_dist_pack layout
+constexpr size_t kMsgHead = 16;    // message header: the two class counts
 constexpr double kStructMargin = 4.0;   // x ParticleSpacing: elastic particle displacement across a face
 
 #define RCCL_OK(ctx, expr)                                                                     \
@@ -203,7 +204,7 @@ T* lay_field(DistLayout* lay, size_t off) { return reinterpret_cast<T*>(reinterp
 
 // Message capacity (particles) of a direction whose live count is c: room to grow by half before
 // the next capacity check (between step batches, dist_sync).
-int msg_capacity(int c) { return c + c / 2 + 4096; }
+int msg_capacity(int c) { return c + c / 4 + 4096; }
 
 // (Re)allocate the four message buffers for the current capacities: redistribution (56 B per
 // particle), pass-A halo (up to 40 B per particle of both directions' capacities), elastic ghosts.
@@ -211,7 +212,7 @@ int msg_alloc(MphCtx* c)
 {
     MphDist& D = *c->dist;
     const size_t most = std::max({D.cap_sl, D.cap_sr, D.cap_rl, D.cap_rr});
-    size_t region = kMsgBytes * most;
+    size_t region = kMsgHead + kMsgBytes * most;
     region = std::max(region, sizeof(double) * 5 * (size_t)std::max(D.cap_sl + D.cap_rl, D.cap_sr + D.cap_rr));
     const size_t smost = std::max({D.nss_l, D.nss_r, D.nsr_l, D.nsr_r});
     region = std::max(region, 3 * sizeof(double4) * smost);
@@ -245,11 +246,13 @@ int redistribute(MphCtx* c, bool move, bool init, Profiler* prof)
     launch_scan(D.bcnt, kSlabClasses * nb, D.bsum, D.boff, 0, c->stream, prof);
     launch_dist_scatter(L, D.cap, D.lay, D.cls, D.boff, D.C, lay_field<int>(D.lay, offsetof(DistLayout, seg)));
     launch_dist_counts(L, D.lay);
-    int* snd = lay_field<int>(D.lay, offsetof(DistLayout, send));
-    int* rcv = lay_field<int>(D.lay, offsetof(DistLayout, recv));
-    MPH_CK(exchange(c, c->stream, snd, 2 * sizeof(int), snd + 2, 2 * sizeof(int), rcv, 2 * sizeof(int), rcv + 2,
-                    2 * sizeof(int)));
     if (init) {
+        // the first redistribution exchanges the counts alone, to size the message buffers; later
+        // ones find them in the message headers (one exchange per redistribution)
+        int* snd = lay_field<int>(D.lay, offsetof(DistLayout, send));
+        int* rcv = lay_field<int>(D.lay, offsetof(DistLayout, recv));
+        MPH_CK(exchange(c, c->stream, snd, 2 * sizeof(int), snd + 2, 2 * sizeof(int), rcv, 2 * sizeof(int),
+                        rcv + 2, 2 * sizeof(int)));
         MPH_HIP_OK(c, hipMemcpyAsync(D.hlay, D.lay, sizeof(DistLayout), hipMemcpyDeviceToHost, c->stream));
         MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
         const DistLayout& h = *D.hlay;
@@ -261,10 +264,11 @@ int redistribute(MphCtx* c, bool move, bool init, Profiler* prof)
     }
     launch_dist_pack(L, D.C, D.lay, 0, D.cap_sl, D.send_l);
     launch_dist_pack(L, D.C, D.lay, 1, D.cap_sr, D.send_r);
-    MPH_CK(exchange(c, c->stream, D.send_l, kMsgBytes * D.cap_sl, D.send_r, kMsgBytes * D.cap_sr, D.recv_l,
-                    kMsgBytes * D.cap_rl, D.recv_r, kMsgBytes * D.cap_rr));
-    launch_dist_unpack(L, D.recv_l, D.lay, 0, D.cap_rl, D.cap, D.C);
-    launch_dist_unpack(L, D.recv_r, D.lay, 1, D.cap_rr, D.cap, D.C);
+    MPH_CK(exchange(c, c->stream, D.send_l, kMsgHead + kMsgBytes * D.cap_sl, D.send_r,
+                    kMsgHead + kMsgBytes * D.cap_sr, D.recv_l, kMsgHead + kMsgBytes * D.cap_rl, D.recv_r,
+                    kMsgHead + kMsgBytes * D.cap_rr));
+    launch_dist_unpack(L, D.recv_l, D.recv_r, D.lay, 0, D.cap_rl, D.cap, D.C);
+    launch_dist_unpack(L, D.recv_l, D.recv_r, D.lay, 1, D.cap_rr, D.cap, D.C);
     return MPH_OK;
 }
 
@@ -544,13 +548,14 @@ int dist_sync(MphCtx* c)
     if (h.hw[4] > D.cap)
         return ctx_fail(c, MPH_ERR_CAPACITY, "slab mode: local particle capacity " + std::to_string(D.cap) +
                                                  " exceeded (" + std::to_string(h.hw[4]) + ")");
-    // capacity check between batches: a direction above 80 % of its message capacity grows (both
+    // capacity check between batches: a direction above 90 % of its message capacity grows (both
     // ranks of the pair see the same counts, so they grow the shared direction alike); the
-    // captured graphs hold the old sizes and are re-captured by the next step
+    // captured graphs hold the old sizes and are re-captured by the next step.  Capacities are
+    // 1.25 c + 4096: every message travels at its capacity (fixed sizes in the graphs)
     int* caps[4] = {&D.cap_sl, &D.cap_sr, &D.cap_rl, &D.cap_rr};
     bool grow = false;
     for (int k = 0; k < 4; ++k)
-        if (h.hw[k] * 5 > *caps[k] * 4) {
+        if ((long long)h.hw[k] * 10 > (long long)*caps[k] * 9) {
             *caps[k] = msg_capacity(h.hw[k]);
             grow = true;
         }

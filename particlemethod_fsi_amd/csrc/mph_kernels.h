@@ -126,8 +126,8 @@ void launch_dist_scatter(const Launch& L, int cap, const DistLayout* lay, const 
                          const Soa& C, int* dseg);
 void launch_dist_counts(const Launch& L, DistLayout* lay);
 void launch_dist_pack(const Launch& L, const Soa& C, DistLayout* lay, int side, int cap_msg, char* buf);
-void launch_dist_unpack(const Launch& L, const char* buf, DistLayout* lay, int side, int cap_msg, int cap,
-                        const Soa& C);
+void launch_dist_unpack(const Launch& L, const char* buf_l, const char* buf_r, DistLayout* lay, int side,
+                        int cap_msg, int cap, const Soa& C);
 void launch_halo_pack(const Launch& L, const int* dst_of, const DistLayout* lay, int dir, int cap,
                       const HaloFields& F, double* buf);
 void launch_halo_unpack(const Launch& L, const double* buf, const int* dst_of, const DistLayout* lay, int dir,

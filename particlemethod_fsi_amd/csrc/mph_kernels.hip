@@ -2387,21 +2387,30 @@ __device__ __forceinline__ void dist_send_range(const DistLayout* lay, int side,
     m = side == 0 ? lay->send[0] + lay->send[1] : lay->send[2] + lay->send[3];
 }
 
-// side 0: from the left (their {migR, bandR}) appended at nc, side 1: from the right after it
-__device__ __forceinline__ void dist_recv_range(const DistLayout* lay, int side, int& off, int& m)
+// side 0: from the left (their {migR, bandR}) appended at nc, side 1: from the right after it;
+// r[4] = the received counts (the message headers)
+__device__ __forceinline__ void dist_recv_range(const DistLayout* lay, const int* r, int side, int& off, int& m)
 {
     const int nc = lay->seg[kSlabDrop];
-    const int fl = lay->recv[0] + lay->recv[1];
+    const int fl = r[0] + r[1];
     off = side == 0 ? nc : nc + fl;
-    m = side == 0 ? fl : lay->recv[2] + lay->recv[3];
+    m = side == 0 ? fl : r[2] + r[3];
 }
 
-// message layout: x[m] y[m] z[m] vx[m] vy[m] vz[m] (double) type[m] id[m] (int) = 56 B/particle
+// message layout: a 16-byte header with the two class counts (so no separate count message is
+// needed per step), then x[m] y[m] z[m] vx[m] vy[m] vz[m] (double) type[m] id[m] (int), 56 B per
+// particle
+constexpr int kMsgHeader = 16;
 __global__ __launch_bounds__(256) void k_dist_pack(Soa C, DistLayout* __restrict__ lay, int side, int cap,
                                                    DevState* __restrict__ st, char* __restrict__ buf)
 {
     int off, m;
     dist_send_range(lay, side, off, m);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        int* h = (int*)buf;
+        h[0] = lay->send[2 * side];
+        h[1] = lay->send[2 * side + 1];
+    }
     if (m > cap) {   // more than the message capacity: an error (MPH_ERR_CAPACITY), never a fault
         if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&st->overflow, 8);
         m = cap;
@@ -2409,7 +2418,7 @@ __global__ __launch_bounds__(256) void k_dist_pack(Soa C, DistLayout* __restrict
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicMax(&lay->hw[side], m);
     if (k >= m) return;
-    double* d = (double*)buf;
+    double* d = (double*)(buf + kMsgHeader);
     int* q = (int*)(d + 6 * (size_t)m);
     const int s = off + k;
     d[k] = C.x[s]; d[m + k] = C.y[s]; d[2 * m + k] = C.z[s];
@@ -2421,12 +2430,18 @@ __global__ __launch_bounds__(256) void k_dist_pack(Soa C, DistLayout* __restrict
 // received message -> C[off, off+m); ownership flips (their migrants are ours, their band
 // particles are our ghosts): id -> -1-id for every entry.  The right-hand message completes the
 // layout: n = kept + received, n_own = the kept owned classes + the received migrants.
-__global__ __launch_bounds__(256) void k_dist_unpack(const char* __restrict__ buf, DistLayout* __restrict__ lay,
-                                                     int side, int cap_msg, int cap, DevState* __restrict__ st,
-                                                     Soa C)
+__global__ __launch_bounds__(256) void k_dist_unpack(const char* __restrict__ buf_l, const char* __restrict__ buf_r,
+                                                     DistLayout* __restrict__ lay, int side, int cap_msg, int cap,
+                                                     DevState* __restrict__ st, Soa C)
 {
+    // the received counts, from the two message headers (from the left: {migR, bandR} of the left
+    // neighbour, from the right: {bandL, migL} of the right neighbour)
+    const int* hl = (const int*)buf_l;
+    const int* hr = (const int*)buf_r;
+    const int r[4] = {hl[0], hl[1], hr[0], hr[1]};
+    const char* buf = side == 0 ? buf_l : buf_r;
     int off, m;
-    dist_recv_range(lay, side, off, m);
+    dist_recv_range(lay, r, side, off, m);
     const int mm = m;   // the sender's count = the stride of its message
     const bool first = blockIdx.x == 0 && threadIdx.x == 0;
     if (mm > cap_msg || off + m > cap) {   // the sender flagged it too; read nothing out of range
@@ -2435,18 +2450,21 @@ __global__ __launch_bounds__(256) void k_dist_unpack(const char* __restrict__ bu
     }
     if (first) {
         atomicMax(&lay->hw[2 + side], mm);
-        if (side == 1) {
+        if (side == 0) {
+            // the layout's receive counts, for the halo ranges of this step
+            lay->recv[0] = r[0]; lay->recv[1] = r[1]; lay->recv[2] = r[2]; lay->recv[3] = r[3];
+        } else {
             const int* seg = lay->seg;
             const int n = min(off + m, cap);
             lay->n = n;
             lay->n_own = (seg[kBandR + 1] - seg[kBandR]) + (seg[kInner + 1] - seg[kInner]) +
-                         (seg[kBandL + 1] - seg[kBandL]) + lay->recv[0] + lay->recv[3];
-            atomicMax(&lay->hw[4], off + (lay->recv[2] + lay->recv[3]));
+                         (seg[kBandL + 1] - seg[kBandL]) + r[0] + r[3];
+            atomicMax(&lay->hw[4], off + (r[2] + r[3]));
         }
     }
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= m) return;
-    const double* d = (const double*)buf;
+    const double* d = (const double*)(buf + kMsgHeader);
     const int* q = (const int*)(d + 6 * (size_t)mm);
     const int s = off + k;
     C.x[s] = d[k]; C.y[s] = d[mm + k]; C.z[s] = d[2 * mm + k];
@@ -2828,12 +2846,12 @@ void launch_dist_pack(const Launch& L, const Soa& C, DistLayout* lay, int side, 
                side, cap_msg, L.st, buf);
 }
 
-void launch_dist_unpack(const Launch& L, const char* buf, DistLayout* lay, int side, int cap_msg, int cap,
-                        const Soa& C)
+void launch_dist_unpack(const Launch& L, const char* buf_l, const char* buf_r, DistLayout* lay, int side,
+                        int cap_msg, int cap, const Soa& C)
 {
     Profiler* prof = L.prof;
-    MPH_LAUNCH("dist_unpack", L.stream, k_dist_unpack, dim3(dist_blocks(cap_msg)), dim3(256), 0, L.stream, buf,
-               lay, side, cap_msg, cap, L.st, C);
+    MPH_LAUNCH("dist_unpack", L.stream, k_dist_unpack, dim3(dist_blocks(cap_msg)), dim3(256), 0, L.stream, buf_l,
+               buf_r, lay, side, cap_msg, cap, L.st, C);
 }
 
 void launch_halo_pack(const Launch& L, const int* dst_of, const DistLayout* lay, int dir, int cap,
