@@ -42,6 +42,11 @@ struct MphDist {
     // pass B of the inner particles overlaps the pass-A halo (MPH_SLAB_OVERLAP=0: halo, then one
     // pass B over all particles)
     bool overlap = !(std::getenv("MPH_SLAB_OVERLAP") && std::string(std::getenv("MPH_SLAB_OVERLAP")) == "0");
+    // early send: within a batch of steps, the redistribution messages of the next step leave
+    // while the interior pass B of this one runs (no elastic particles; MPH_SLAB_EARLY=0: off)
+    bool early = !(std::getenv("MPH_SLAB_EARLY") && std::string(std::getenv("MPH_SLAB_EARLY")) == "0");
+    int* wface = nullptr;                             // face-wavefront flags of the last pass B
+    hipEvent_t ev_s = nullptr, ev_x = nullptr;       // early messages packed / exchanged
     char uid[128] = {0};          // ncclUniqueId
     void* comm = nullptr;         // ncclComm_t
     mph_host_exchange_fn host_fn = nullptr;

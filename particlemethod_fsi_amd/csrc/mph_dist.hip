@@ -236,16 +236,24 @@ int msg_alloc(MphCtx* c)
 // local set (owned and ghosts) in D.C and its sizes in D.lay -- on the device: nothing here reads
 // a size on the host, so the step can be captured.  init: first redistribution of mph_create,
 // which reads the counts once to size the message buffers.
-int redistribute(MphCtx* c, bool move, bool init, Profiler* prof)
+// early_in: the messages left at the end of the previous step (early_send); here only the local
+// partition, then the wait for them and the unpack
+int redistribute(MphCtx* c, bool move, bool init, Profiler* prof, bool early_in = false)
 {
     MphDist& D = *c->dist;
     Launch L = c->L;
     L.prof = prof;
     const int nb = dist_blocks(D.cap);
-    launch_dist_classify(L, D.g, D.cap, D.lay, move ? 1 : 0, D.cls, D.bcnt);
+    launch_dist_classify(L, D.g, D.cap, D.lay, move ? 1 : 0, D.cls, D.bcnt, early_in ? D.wface : nullptr);
     launch_scan(D.bcnt, kSlabClasses * nb, D.bsum, D.boff, 0, c->stream, prof);
     launch_dist_scatter(L, D.cap, D.lay, D.cls, D.boff, D.C, lay_field<int>(D.lay, offsetof(DistLayout, seg)));
     launch_dist_counts(L, D.lay);
+    if (early_in) {
+        MPH_HIP_OK(c, hipStreamWaitEvent(c->stream, D.ev_x, 0));
+        launch_dist_unpack(L, D.recv_l, D.recv_r, D.lay, 0, D.cap_rl, D.cap, D.C);
+        launch_dist_unpack(L, D.recv_l, D.recv_r, D.lay, 1, D.cap_rr, D.cap, D.C);
+        return MPH_OK;
+    }
     if (init) {
         // the first redistribution exchanges the counts alone, to size the message buffers; later
         // ones find them in the message headers (one exchange per redistribution)
@@ -269,6 +277,27 @@ int redistribute(MphCtx* c, bool move, bool init, Profiler* prof)
                     kMsgHead + kMsgBytes * D.cap_rr));
     launch_dist_unpack(L, D.recv_l, D.recv_r, D.lay, 0, D.cap_rl, D.cap, D.C);
     launch_dist_unpack(L, D.recv_l, D.recv_r, D.lay, 1, D.cap_rr, D.cap, D.C);
+    return MPH_OK;
+}
+
+// The next step's redistribution messages, sent from the face wavefronts of this step's pass B
+// on the second stream (joined by the next step's redistribute(early_in)); the same bytes as
+// k_dist_pack would send from C.
+int early_send(MphCtx* c, Profiler* prof)
+{
+    MphDist& D = *c->dist;
+    Launch L = c->L;
+    L.prof = prof;
+    const int nb = dist_blocks(D.cap);
+    launch_dist_early_classify(L, D.g, D.cap, D.lay, D.wface, D.cls, D.bcnt);
+    launch_scan(D.bcnt, kSlabClasses * nb, D.bsum, D.boff, 0, c->stream, prof);
+    launch_dist_early_pack(L, D.cap, D.lay, D.cls, D.boff, D.cap_sl, D.cap_sr, D.send_l, D.send_r);
+    MPH_HIP_OK(c, hipEventRecord(D.ev_s, c->stream));
+    MPH_HIP_OK(c, hipStreamWaitEvent(D.stream2, D.ev_s, 0));
+    MPH_CK(exchange(c, D.stream2, D.send_l, kMsgHead + kMsgBytes * D.cap_sl, D.send_r,
+                    kMsgHead + kMsgBytes * D.cap_sr, D.recv_l, kMsgHead + kMsgBytes * D.cap_rl, D.recv_r,
+                    kMsgHead + kMsgBytes * D.cap_rr));
+    MPH_HIP_OK(c, hipEventRecord(D.ev_x, D.stream2));
     return MPH_OK;
 }
 
@@ -395,7 +424,10 @@ int dist_setup(MphCtx* c, const double* pos, std::vector<int>& owned)
     c->P.slab_axis = axis;
     c->P.slab_lo = D.g.lo;
     c->P.slab_hi = D.g.hi;
-    c->P.slab_h = halo;
+    // pass B's face wavefronts (particles within slab_h of a face, integrated after the halo) also
+    // carry every particle the next redistribution can send: one step moves a particle far less
+    // than the 2 dx margin (checked: k_dist_classify flags a sender outside them)
+    c->P.slab_h = halo + 2.0 * h.dx;
     c->P.gc[axis] = std::min(gloc, c->P.gc[axis] + 1);
     // fast-path interior: >= 3 cells inside both the window and the periodic domain
     c->P.inner_lo[axis] = std::max(wlo, h.dmin[axis]) + m * cw * (1.0 + 1e-9);
@@ -502,6 +534,8 @@ int dist_alloc(MphCtx* c)
     MPH_CK(ctx_dalloc(c, &C.vx, cap)); MPH_CK(ctx_dalloc(c, &C.vy, cap)); MPH_CK(ctx_dalloc(c, &C.vz, cap));
     MPH_CK(ctx_dalloc(c, &C.type, cap)); MPH_CK(ctx_dalloc(c, &C.id, cap));
     MPH_CK(ctx_dalloc(c, &D.cls, cap));
+    MPH_CK(ctx_dalloc(c, &D.wface, (size_t)cap / 64 + 2));
+    MPH_HIP_OK(c, hipMemsetAsync(D.wface, 0, sizeof(int) * ((size_t)cap / 64 + 2), c->stream));
     const size_t nslots = (size_t)kSlabClasses * dist_blocks(cap);
     MPH_CK(ctx_dalloc(c, &D.bcnt, nslots + 1));
     MPH_CK(ctx_dalloc(c, &D.boff, nslots + 1));
@@ -522,6 +556,8 @@ int dist_alloc(MphCtx* c)
     MPH_HIP_OK(c, hipStreamCreateWithFlags(&D.stream2, hipStreamNonBlocking));
     MPH_HIP_OK(c, hipEventCreateWithFlags(&D.ev_a, hipEventDisableTiming));
     MPH_HIP_OK(c, hipEventCreateWithFlags(&D.ev_h, hipEventDisableTiming));
+    MPH_HIP_OK(c, hipEventCreateWithFlags(&D.ev_s, hipEventDisableTiming));
+    MPH_HIP_OK(c, hipEventCreateWithFlags(&D.ev_x, hipEventDisableTiming));
     if (D.rccl) {
         ncclUniqueId id;
         std::memcpy(&id, D.uid, sizeof(id));
@@ -587,15 +623,27 @@ int dist_init(MphCtx* c)
 // One slab step on the context's stream (no host synchronisation inside: RCCL transport steps
 // are captured into graphs by dist_step; the host transport stages each message through host
 // memory and so synchronises in exchange()).
-int dist_enqueue_step(MphCtx* c, Profiler* prof)
+// early_in / early_out: inside a batch of steps, this step's redistribution messages were sent by
+// the previous step / the next step's are sent here (early_send), beside the interior pass B.
+int dist_enqueue_step(MphCtx* c, Profiler* prof, bool early_in, bool early_out)
 {
     Launch L = c->L;
     L.prof = prof;
     MphDist& D = *c->dist;
-    MPH_CK(redistribute(c, true, false, prof));
+    L.wface = D.wface;
+    MPH_CK(redistribute(c, true, false, prof, early_in));
     sort_local(c, 2, prof);
     launch_neighbors(L);
     launch_pass_a(L);
+    if (early_out) {
+        // halo first (the face waves need it), the face waves, the messages of the next step on
+        // the second stream, and the interior waves meanwhile
+        MPH_CK(halo_exchange(c, prof, c->stream));
+        launch_pass_b(L, 2);
+        MPH_CK(early_send(c, prof));
+        launch_pass_b(L, 1);
+        return struct_substeps(c, prof);   // none: early sends only without elastic particles
+    }
     // the pass-A halo travels on stream2 while pass B runs the particles that have no ghost
     // neighbours; the near-face particles follow once the halo has landed (inner pass B is
     // enqueued first, so that a host-staged exchange, which blocks the host, also overlaps with it)
@@ -615,12 +663,22 @@ int dist_enqueue_step(MphCtx* c, Profiler* prof)
     return MPH_OK;
 }
 
+// the early send chains the steps of one batch (one graph or one mph_step call): step k receives
+// early if k > 0 and sends early if k < steps - 1, so every batch ends joined
+bool early_at(const MphCtx* c, int k, int steps, int out)
+{
+    const MphDist& D = *c->dist;
+    if (!D.early || !D.overlap || c->P.n_struct > 0) return false;
+    return out ? k < steps - 1 : k > 0;
+}
+
 int dist_capture(MphCtx* c, int steps, hipGraphExec_t* out)
 {
     hipGraph_t g = nullptr;
     MPH_HIP_OK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     int rc = MPH_OK;
-    for (int k = 0; k < steps && rc == MPH_OK; ++k) rc = dist_enqueue_step(c, nullptr);
+    for (int k = 0; k < steps && rc == MPH_OK; ++k) rc = dist_enqueue_step(c, nullptr, early_at(c, k, steps, 0),
+                                                                           early_at(c, k, steps, 1));
     const hipError_t e = hipStreamEndCapture(c->stream, &g);
     if (rc != MPH_OK) {
         if (g) (void)hipGraphDestroy(g);
@@ -650,7 +708,8 @@ int dist_step(MphCtx* c, int nsteps, Profiler* prof)
         while (left >= 8) { MPH_HIP_OK(c, hipGraphLaunch(c->graph8, c->stream)); left -= 8; }
         while (left > 0) { MPH_HIP_OK(c, hipGraphLaunch(c->graph1, c->stream)); left -= 1; }
     } else {
-        for (; left > 0; --left) MPH_CK(dist_enqueue_step(c, prof));
+        for (int k = 0; k < nsteps; ++k)
+            MPH_CK(dist_enqueue_step(c, prof, early_at(c, k, nsteps, 0), early_at(c, k, nsteps, 1)));
     }
     MPH_HIP_OK(c, hipGetLastError());
     for (int k = 0; k < nsteps; ++k) c->time += c->cfg.dt;
@@ -666,6 +725,8 @@ void dist_free(MphCtx* c)
     if (D->comm) (void)ncclCommDestroy((ncclComm_t)D->comm);
     if (D->ev_a) (void)hipEventDestroy(D->ev_a);
     if (D->ev_h) (void)hipEventDestroy(D->ev_h);
+    if (D->ev_s) (void)hipEventDestroy(D->ev_s);
+    if (D->ev_x) (void)hipEventDestroy(D->ev_x);
     if (D->stream2) (void)hipStreamDestroy(D->stream2);
     if (D->hlay) (void)hipHostFree(D->hlay);
     for (char* b : {D->send_l, D->send_r, D->recv_l, D->recv_r})

@@ -81,6 +81,7 @@ struct Launch {
     int *nbr = nullptr, *ncount = nullptr;
     int2* hdr = nullptr;          // per-wave headers of the column-segmented lists (kSegHdr each)
     int* lhdr = nullptr;          // per-wave headers of the compact 16-bit lists (kLhdr each)
+    int* wface = nullptr;         // slab mode: face-wavefront flags written by pass B (early send)
     // pass A products (A order): pressure values, gravity centre (GC, PressureA), sums
     double *pres = nullptr, *gx = nullptr, *gy = nullptr, *gz = nullptr, *pa = nullptr;
     double *dens_a = nullptr, *vstrain = nullptr, *divp = nullptr;
@@ -121,7 +122,11 @@ int dist_blocks(int n);
 // slab redistribution; every size is read from the device layout (graph-capturable).  cap = local
 // array capacity, cap_msg = capacity (particles) of the message of that side.
 void launch_dist_classify(const Launch& L, const SlabGeom& g, int cap, const DistLayout* lay, int move, int* cls,
-                          int* bcnt);
+                          int* bcnt, const int* wface = nullptr);
+void launch_dist_early_classify(const Launch& L, const SlabGeom& g, int cap, const DistLayout* lay,
+                                const int* wface, int* cls, int* bcnt);
+void launch_dist_early_pack(const Launch& L, int cap, DistLayout* lay, const int* cls, const int* boff, int cap_l,
+                            int cap_r, char* buf_l, char* buf_r);
 void launch_dist_scatter(const Launch& L, int cap, const DistLayout* lay, const int* cls, const int* boff,
                          const Soa& C, int* dseg);
 void launch_dist_counts(const Launch& L, DistLayout* lay);

@@ -1637,7 +1637,7 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
                                                 const int* __restrict__ ncount, const int2* __restrict__ hdr,
                                                 const int* __restrict__ lhdr,
                                                 double4* __restrict__ force, double4* __restrict__ acc,
-                                                Soa B, int phase, StructHook H)
+                                                Soa B, int phase, int* __restrict__ wface, StructHook H)
 {
     const int n = dev_n(P);
     if ((int)blockIdx.x >= live_blocks(n)) return;
@@ -1652,6 +1652,7 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
     bool live = i < n;
     if (wave_all_ghosts(P, A, live, ii)) {
         if (live) B.id[i] = A.id[i];
+        if (phase == 2 && wface && (threadIdx.x & 63) == 0) wface[i >> 6] = 0;
         return;
     }
     if (live && P.slab_axis >= 0 && A.id[ii] < 0) {   // a ghost lane of a mixed wave
@@ -1665,6 +1666,8 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
         const double c = P.slab_axis == 0 ? xi : (P.slab_axis == 1 ? yi : zi);
         const bool inner = c - P.slab_lo > P.slab_h && P.slab_hi - c > P.slab_h;
         const bool wave_inner = __all(!live || inner);
+        // the face waves of this step, for the early send of the redistribution (mph_dist.hip)
+        if (phase == 2 && wface && (threadIdx.x & 63) == 0) wface[i >> 6] = wave_inner ? 0 : 1;
         if (phase == 1 ? !wave_inner : wave_inner) return;
     }
     const int2* h = hdr ? hdr + (size_t)(i >> 6) * kSegHdr : nullptr;
@@ -2301,9 +2304,16 @@ __global__ __launch_bounds__(256) void k_sinit_normalizer(DevParams P, int ns, c
 
 __device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << (threadIdx.x & 63)) - 1ull; }
 
+__device__ __forceinline__ bool dist_sends(int c) { return c == kMigR || c == kBandR || c == kBandL || c == kMigL; }
+constexpr int kMsgHeader = 16;   // redistribution message header: the two class counts
+
+// wface (early send, see k_dist_early_classify): the face wavefronts of the previous step, whose
+// particles were moved and sent already -- not moved again here, and no other particle may be
+// of a sending class (it would have moved more than the face margin: an error)
 __global__ __launch_bounds__(256) void k_dist_classify(DevParams P, DevState* __restrict__ st, SlabGeom g,
                                                        Soa B, const DistLayout* __restrict__ lay, int move,
-                                                       int* __restrict__ cls, int* __restrict__ bcnt, int nb)
+                                                       int* __restrict__ cls, int* __restrict__ bcnt, int nb,
+                                                       const int* __restrict__ wface)
 {
     __shared__ int wc[4][kSlabClasses];
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2313,14 +2323,16 @@ __global__ __launch_bounds__(256) void k_dist_classify(DevParams P, DevState* __
         if (B.id[p] < 0) {
             c = kSlabDrop;
         } else {
+            const bool face = wface && wface[p >> 6] == 1;
             double x = B.x[p], y = B.y[p], z = B.z[p];
-            if (move) move_and_wrap(P, st, B, p, x, y, z);
+            if (move && !face) move_and_wrap(P, st, B, p, x, y, z);
             const double a = g.axis == 0 ? x : (g.axis == 1 ? y : z);
             c = dev_is_struct(B.type[p]) ? slab_class_static(g, a) : slab_class(g, a);
             if (c == kSlabLost) {
                 atomicOr(&st->overflow, 2);
                 c = kInner;
             }
+            if (wface && !face && dist_sends(c)) atomicOr(&st->overflow, 8);
         }
         cls[p] = c;
     }
@@ -2336,6 +2348,91 @@ __global__ __launch_bounds__(256) void k_dist_classify(DevParams P, DevState* __
         for (int w = 0; w < 4; ++w) t += wc[w][threadIdx.x];
         bcnt[threadIdx.x * nb + blockIdx.x] = t;
     }
+}
+
+// Early send (mph_dist.hip): at the end of a step, once pass B has integrated the face wavefronts
+// (wface, written by pass B), their owned particles are moved (calculateWall / periodic wrap, as
+// k_dist_classify would at the next step) and classified; the others count as nothing here.
+__global__ __launch_bounds__(256) void k_dist_early_classify(DevParams P, DevState* __restrict__ st, SlabGeom g,
+                                                             Soa B, const DistLayout* __restrict__ lay,
+                                                             const int* __restrict__ wface,
+                                                             int* __restrict__ cls, int* __restrict__ bcnt, int nb)
+{
+    __shared__ int wc[4][kSlabClasses];
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int n = lay->n;
+    int c = -1;
+    if (p < n && B.id[p] >= 0 && wface[p >> 6] == 1) {
+        double x = B.x[p], y = B.y[p], z = B.z[p];
+        move_and_wrap(P, st, B, p, x, y, z);
+        const double a = g.axis == 0 ? x : (g.axis == 1 ? y : z);
+        c = slab_class(g, a);   // no elastic particles in early-send mode
+        if (c == kSlabLost) c = kInner;   // reported by k_dist_classify at the next step
+    }
+    if (p < n) cls[p] = c;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < kSlabClasses; ++k) {
+        const unsigned long long m = __ballot(c == k);
+        if (lane == 0) wc[wave][k] = __popcll(m);
+    }
+    __syncthreads();
+    if (threadIdx.x < kSlabClasses) {
+        int t = 0;
+        for (int w = 0; w < 4; ++w) t += wc[w][threadIdx.x];
+        bcnt[threadIdx.x * nb + blockIdx.x] = t;
+    }
+}
+
+// The messages straight from B, in the order k_dist_scatter + k_dist_pack give them (stable by
+// B index within each class): to the left [bandL | migL], to the right [migR | bandR], each behind
+// its count header; migrants travel with negated ids, as from C.
+__global__ __launch_bounds__(256) void k_dist_early_pack(Soa B, DistLayout* __restrict__ lay,
+                                                         const int* __restrict__ cls,
+                                                         const int* __restrict__ boff, int nb, int cap_l,
+                                                         int cap_r, DevState* __restrict__ st,
+                                                         char* __restrict__ buf_l, char* __restrict__ buf_r)
+{
+    __shared__ int wc[4][kSlabClasses];
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int n = lay->n;
+    const int c = p < n ? cls[p] : -1;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int rank = 0;
+#pragma unroll
+    for (int k = 0; k < kSlabClasses; ++k) {
+        const unsigned long long m = __ballot(c == k);
+        if (c == k) rank = __popcll(m & lanemask_lt());
+        if (lane == 0) wc[wave][k] = __popcll(m);
+    }
+    __syncthreads();
+    const int sMigR = boff[kMigR * nb], sBandR = boff[kBandR * nb], sInner = boff[kInner * nb];
+    const int sBandL = boff[kBandL * nb], sMigL = boff[kMigL * nb], sDrop = boff[kSlabDrop * nb];
+    const int mr = sInner - sMigR, ml = sDrop - sBandL;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        int* hl = (int*)buf_l;
+        int* hr = (int*)buf_r;
+        hl[0] = sMigL - sBandL; hl[1] = sDrop - sMigL;   // {bandL, migL}
+        hr[0] = sBandR - sMigR; hr[1] = sInner - sBandR; // {migR, bandR}
+        lay->send[0] = hl[0]; lay->send[1] = hl[1]; lay->send[2] = hr[0]; lay->send[3] = hr[1];
+        atomicMax(&lay->hw[0], min(ml, cap_l));
+        atomicMax(&lay->hw[1], min(mr, cap_r));
+        if (ml > cap_l || mr > cap_r) atomicOr(&st->overflow, 8);
+    }
+    if (!dist_sends(c)) return;
+    int o = boff[c * nb + blockIdx.x] + rank;
+    for (int w = 0; w < wave; ++w) o += wc[w][c];
+    const bool left = c == kBandL || c == kMigL;
+    const int m = left ? ml : mr;
+    const int j = left ? o - sBandL : o - sMigR;
+    if (j >= (left ? cap_l : cap_r)) return;
+    double* d = (double*)((left ? buf_l : buf_r) + kMsgHeader);
+    int* q = (int*)(d + 6 * (size_t)m);
+    d[j] = B.x[p]; d[m + j] = B.y[p]; d[2 * m + j] = B.z[p];
+    d[3 * m + j] = B.vx[p]; d[4 * m + j] = B.vy[p]; d[5 * m + j] = B.vz[p];
+    q[j] = B.type[p];
+    const int id = B.id[p];
+    q[m + j] = (c == kMigR || c == kMigL) ? -1 - id : id;
 }
 
 __global__ __launch_bounds__(256) void k_dist_scatter(Soa B, const DistLayout* __restrict__ lay,
@@ -2399,8 +2496,7 @@ __device__ __forceinline__ void dist_recv_range(const DistLayout* lay, const int
 
 // message layout: a 16-byte header with the two class counts (so no separate count message is
 // needed per step), then x[m] y[m] z[m] vx[m] vy[m] vz[m] (double) type[m] id[m] (int), 56 B per
-// particle
-constexpr int kMsgHeader = 16;
+// particle (kMsgHeader above)
 __global__ __launch_bounds__(256) void k_dist_pack(Soa C, DistLayout* __restrict__ lay, int side, int cap,
                                                    DevState* __restrict__ st, char* __restrict__ buf)
 {
@@ -2658,7 +2754,7 @@ void launch_pass_b(const Launch& L, int phase)
 #define MPH_PASS_B(S, D)                                                                            \
     MPH_LAUNCH(phase == 2 ? "pass_b_face" : "pass_b", L.stream, (k_pass_b<S, D>), dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, \
                L.T, L.A, L.rec, L.fpart, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, L.force, L.acc, L.B, \
-               phase, \
+               phase, L.wface, \
                struct_hook(L))
     if (P.surface) {
         if (P.dim == 3) MPH_PASS_B(true, 3); else MPH_PASS_B(true, 2);
@@ -2816,12 +2912,30 @@ void launch_scan(int* cnt, int ncell, int* bsum, int* start, int total, hipStrea
 int dist_blocks(int n) { return blocks(n > 0 ? n : 1, 256); }
 
 void launch_dist_classify(const Launch& L, const SlabGeom& g, int cap, const DistLayout* lay, int move, int* cls,
-                          int* bcnt)
+                          int* bcnt, const int* wface)
 {
     Profiler* prof = L.prof;
     const int nb = dist_blocks(cap);
     MPH_LAUNCH("dist_classify", L.stream, k_dist_classify, dim3(nb), dim3(256), 0, L.stream, *L.P, L.st, g,
-               L.B, lay, move, cls, bcnt, nb);
+               L.B, lay, move, cls, bcnt, nb, wface);
+}
+
+void launch_dist_early_classify(const Launch& L, const SlabGeom& g, int cap, const DistLayout* lay,
+                                const int* wface, int* cls, int* bcnt)
+{
+    Profiler* prof = L.prof;
+    const int nb = dist_blocks(cap);
+    MPH_LAUNCH("dist_early_classify", L.stream, k_dist_early_classify, dim3(nb), dim3(256), 0, L.stream, *L.P,
+               L.st, g, L.B, lay, wface, cls, bcnt, nb);
+}
+
+void launch_dist_early_pack(const Launch& L, int cap, DistLayout* lay, const int* cls, const int* boff, int cap_l,
+                            int cap_r, char* buf_l, char* buf_r)
+{
+    Profiler* prof = L.prof;
+    const int nb = dist_blocks(cap);
+    MPH_LAUNCH("dist_early_pack", L.stream, k_dist_early_pack, dim3(nb), dim3(256), 0, L.stream, L.B, lay, cls,
+               boff, nb, cap_l, cap_r, L.st, buf_l, buf_r);
 }
 
 void launch_dist_scatter(const Launch& L, int cap, const DistLayout* lay, const int* cls, const int* boff,

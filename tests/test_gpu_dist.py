@@ -152,3 +152,17 @@ def test_rccl_exchange_selftest():
     L = load_library()
     rc = L.mph_dist_selftest(0)
     assert rc == 0, (rc, (L.mph_last_error(None) or b"").decode())
+
+
+@pytest.mark.parametrize("case,world", [("channel3d", 3), ("channel2d", 4)])
+def test_slab_early_send_bitwise(tmp_path, case, world, monkeypatch):
+    """The early send of the redistribution messages (MPH_SLAB_EARLY, default on: inside a batch,
+    the next step's messages leave from pass B's face wavefronts while the interior ones run)
+    sends exactly the bytes the late pack would, so every field is bit-identical to
+    MPH_SLAB_EARLY=0 -- over batches of 1, 4 and 15 steps."""
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MPH_SLAB_EARLY", mode)
+        out[mode] = run_slab(case, world, [1, 5, 20], str(tmp_path / ("slab%s.npz" % mode)), local=True)
+    for k in out["1"].files:
+        assert np.array_equal(out["1"][k], out["0"][k]), k
