@@ -704,7 +704,12 @@ int dist_step(MphCtx* c, int nsteps, Profiler* prof)
             c->err.clear();
             return dist_step(c, nsteps, prof);
         }
-        if (!c->graph8 && nsteps >= 8) MPH_CK(dist_capture(c, 8, &c->graph8));
+        if (!c->graph8 && nsteps >= 8 && dist_capture(c, 8, &c->graph8) != MPH_OK) {
+            (void)hipGetLastError();
+            D.graphs = false;
+            c->err.clear();
+            return dist_step(c, nsteps, prof);
+        }
         while (left >= 8) { MPH_HIP_OK(c, hipGraphLaunch(c->graph8, c->stream)); left -= 8; }
         while (left > 0) { MPH_HIP_OK(c, hipGraphLaunch(c->graph1, c->stream)); left -= 1; }
     } else {
@@ -858,6 +863,45 @@ int mph_dist_selftest(int device)
         MPH_HIP_OK(&c, hipMemcpy(gl.data(), rl, nr, hipMemcpyDeviceToHost));
         MPH_HIP_OK(&c, hipMemcpy(gr.data(), rr, nl, hipMemcpyDeviceToHost));
         if (gl != hr || gr != hl) return ctx_fail(&c, MPH_ERR_RCCL, "graph-replayed RCCL exchange delivered wrong bytes");
+        // the early send's pattern (dist_enqueue_step): per step the exchange forks onto a second
+        // stream after an event of the main stream, main-stream work runs beside it, and the
+        // next step joins it -- three chained steps in one captured graph, replayed twice
+        hipStream_t s2 = nullptr;
+        hipEvent_t es = nullptr, ex = nullptr;
+        MPH_HIP_OK(&c, hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+        MPH_HIP_OK(&c, hipEventCreateWithFlags(&es, hipEventDisableTiming));
+        MPH_HIP_OK(&c, hipEventCreateWithFlags(&ex, hipEventDisableTiming));
+        char* side;
+        MPH_CK(ctx_dalloc(&c, &side, 1 << 20));
+        MPH_HIP_OK(&c, hipMemset(rl, 0, nr));
+        MPH_HIP_OK(&c, hipMemset(rr, 0, nl));
+        MPH_HIP_OK(&c, hipStreamBeginCapture(c.stream, hipStreamCaptureModeThreadLocal));
+        int rc2 = MPH_OK;
+        for (int k = 0; k < 3 && rc2 == MPH_OK; ++k) {
+            if (k > 0) (void)hipStreamWaitEvent(c.stream, ex, 0);
+            (void)hipEventRecord(es, c.stream);
+            (void)hipStreamWaitEvent(s2, es, 0);
+            rc2 = exchange(&c, s2, sl, nl, sr, nr, rl, nr, rr, nl);
+            (void)hipEventRecord(ex, s2);
+            (void)hipMemsetAsync(side, k, 1 << 20, c.stream);   // work beside the exchange
+        }
+        (void)hipStreamWaitEvent(c.stream, ex, 0);
+        const hipError_t e2 = hipStreamEndCapture(c.stream, &g);
+        MPH_CK(rc2);
+        MPH_HIP_OK(&c, e2);
+        const hipError_t ei2 = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        MPH_HIP_OK(&c, ei2);
+        for (int rep = 0; rep < 2; ++rep) MPH_HIP_OK(&c, hipGraphLaunch(ge, c.stream));
+        MPH_HIP_OK(&c, hipStreamSynchronize(c.stream));
+        (void)hipGraphExecDestroy(ge);
+        (void)hipEventDestroy(es);
+        (void)hipEventDestroy(ex);
+        (void)hipStreamDestroy(s2);
+        MPH_HIP_OK(&c, hipMemcpy(gl.data(), rl, nr, hipMemcpyDeviceToHost));
+        MPH_HIP_OK(&c, hipMemcpy(gr.data(), rr, nl, hipMemcpyDeviceToHost));
+        if (gl != hr || gr != hl)
+            return ctx_fail(&c, MPH_ERR_RCCL, "forked graph-replayed RCCL exchanges delivered wrong bytes");
         return MPH_OK;
     };
     status = run();
