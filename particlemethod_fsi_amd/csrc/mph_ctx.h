@@ -118,7 +118,7 @@ void ctx_fill_launch(MphCtx* c);
 inline int stencil_margin(const DevParams& P, int d)
 {
     const int ca = contig_axis(P.dim, P.perm);
-    return (d == ca ? P.sa : 2) + 1;
+    return (d == ca ? P.sa : kReach) + 1;
 }
 int ctx_state_status(MphCtx* c, const DevState& hs);   // kernel error flags -> MphStatus
 

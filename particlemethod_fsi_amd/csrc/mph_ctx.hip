@@ -69,9 +69,11 @@ void ctx_fill_launch(MphCtx* c)
     L.A = c->A; L.B = c->B; L.rank_of = nullptr; L.dst_of = nullptr;
     L.key = c->key; L.slot = c->slot; L.tmp = c->tmp; L.cnt = c->cnt; L.start = c->start; L.bsum = c->bsum;
     L.nbr = c->nbr; L.ncount = c->ncount; L.hdr = c->seg_hdr;
-    // compact 16-bit lists of interior wavefronts (MPH_LIST16=0: 32-bit ELL rows everywhere)
+    // compact 16-bit lists of interior wavefronts (MPH_LIST16=1), or 32-bit ELL rows everywhere
+    // (MPH_LIST16=0); unset: kListCompact
     const char* l16 = std::getenv("MPH_LIST16");
-    L.lhdr = (l16 && std::string(l16) == "0") ? nullptr : c->list_hdr;
+    const bool compact = l16 && *l16 ? std::string(l16) != "0" : kListCompact;
+    L.lhdr = compact ? c->list_hdr : nullptr;
     L.pres = c->pres; L.gx = c->gx; L.gy = c->gy; L.gz = c->gz; L.pa = c->pa;
     L.force = c->force; L.acc = c->acc; L.fpart = c->fpart; L.rec = c->rec;
     L.dens_a = c->dens_a; L.vstrain = c->vstrain; L.divp = c->divp;
@@ -284,7 +286,7 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         // MPH_SLAB_PERM=0 keeps (x, y, z); =1..4 force an order on any 3-D context, =force
         // orders a single 3-D context the z-slab way -- A/B timing and the parity tests)
         const char* lm = std::getenv("MPH_LIST16_MAX");
-        c->P.l16max = lm ? std::max(0, std::min(255, std::atoi(lm))) : 255;
+        c->P.l16max = lm ? std::max(0, std::min(127, std::atoi(lm))) : 127;
         const char* pe = std::getenv("MPH_SLAB_PERM");
         const std::string pv = pe ? pe : "";
         const bool zslab = cfg->dim == 3 && c->dist && c->dist->g.axis == 2;
@@ -292,14 +294,14 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         c->P.perm = 0;
         if (cfg->dim == 3 && (forced || pv == "force" || (zslab && pv != "0")))
             c->P.perm = forced ? pv[0] - '0' : choose_cell_order(c->h, n, pos, rc);
-        int r = choose_grid(c->h, cfg->dim, rc, kContigSub, c->P.gc, c->P.ginv, err, c->P.perm);
+        int r = choose_grid(c->h, cfg->dim, rc, kContigReach, c->P.gc, c->P.ginv, err, c->P.perm);
         if (r != MPH_OK) return fail(c, r, err);
     }
     // interior box for the wave-uniform fast minimum image (k_neighbors / passes): >= 3 cells
     // (+1e-9 relative margin) from every periodic face; needs > 12 cells on every active axis
     // (stencil half-width + 1 cells from every periodic face; the candidate offsets then stay
     // below a quarter of the domain width, which needs > 4 x that many cells on every axis)
-    c->P.sa = 2 * kContigSub;
+    c->P.sa = kContigReach;
     c->P.fast_ok = 1;
     for (int d = 0; d < 3; ++d) {
         if (d == 2 && cfg->dim == 2) { c->P.inner_lo[d] = -1e300; c->P.inner_hi[d] = 1e300; continue; }
@@ -914,7 +916,7 @@ int mph_list_formats(MphCtx* c, int* out2)
     if (nt && c->L.lhdr) {
         std::vector<int> h((size_t)nt * kLhdr);
         HIP_OK(c, hipMemcpy(h.data(), c->list_hdr, sizeof(int) * h.size(), hipMemcpyDeviceToHost));
-        for (int t = 0; t < nt; ++t) compact += h[(size_t)t * kLhdr + 5] == 1;
+        for (int t = 0; t < nt; ++t) compact += h[(size_t)t * kLhdr + kHdrFlag] == 1;
     }
     out2[0] = compact;
     out2[1] = nt;

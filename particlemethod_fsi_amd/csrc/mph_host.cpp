@@ -647,21 +647,26 @@ int choose_cell_order(const HostDerived& h, int n, const double* pos, double rc)
     return (hi[0] - lo[0]) >= (hi[1] - lo[1]) ? 3 : 4;
 }
 
-// GPU linked-cell grid: cells of width >= rc/2 along the two outer axes (a +-2-cell stencil
-// covers the acceptance sphere) and >= rc/(2 sub) along the contiguous axis (z in 3-D, y in 2-D;
-// a +-2 sub stencil, scanned as one contiguous index range per column, so thinner cells there
+// GPU linked-cell grid: cells of width >= rc/kReach along the two outer axes (a +-kReach stencil
+// covers the acceptance sphere) and >= rc/sa along the contiguous axis (z in 3-D, y in 2-D;
+// a +-sa stencil, scanned as one contiguous index range per column, so thinner cells there
 // only sharpen the cutoff trimming of each column).  Cell counts divide the periodic width
 // exactly; every axis needs enough cells that the stencil never visits a cell twice.
-int choose_grid(const HostDerived& h, int dim, double rc, int sub, int gc[3], double ginv[3], std::string& err,
+int choose_grid(const HostDerived& h, int dim, double rc, int sa, int gc[3], double ginv[3], std::string& err,
                 int perm)
 {
     const int ca = contig_axis(dim, perm);   // the contiguous (half-width) axis
     for (int d = 0; d < 3; ++d) {
         if (d == 2 && dim == 2) { gc[d] = 1; ginv[d] = 1.0 / h.dw[d]; continue; }
-        const int s = d == ca ? sub : 1;
-        const double target = 0.5 * rc / s * (1.0 + 1e-6);
+        // the domain rule is the one of rc/2 cells on every axis (>= 5 of them), whatever kReach
+        if ((int)std::floor(h.dw[d] / (0.5 * rc * (1.0 + 1e-6))) < 5) {
+            err = "domain axis " + std::to_string(d) + " narrower than 2.5 x cutoff";
+            return MPH_ERR_DOMAIN;
+        }
+        const int reach = d == ca ? sa : kReach;
+        const double target = rc / reach * (1.0 + 1e-6);
         const int nc = (int)std::floor(h.dw[d] / target);
-        if (nc < 4 * s + 1) {
+        if (nc < 2 * reach + 1) {
             err = "domain axis " + std::to_string(d) + " narrower than 2.5 x cutoff";
             return MPH_ERR_DOMAIN;
         }

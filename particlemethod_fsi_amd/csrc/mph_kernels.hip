@@ -226,14 +226,15 @@ __device__ __forceinline__ const int* ell_row(const int* nbr, int i)
 }
 
 // Compact neighbour list (MPH_LIST16, the default for interior waves).  The stencil's columns
-// fall into 5 groups (3-D: the 5 columns of one slowest-axis offset, which are consecutive in
-// cell order; 2-D: each column), so every neighbour of a group lies in a short index range from
-// the group's wave-wide first candidate.  Entry k of a lane is 16 bits -- the offset from its
-// group's base (13 bits) and the neighbour's type (3 bits) -- two entries per 32-bit word at
-// word[k / 2][lane] of the wave's tile (same order as the ELL row, so sums are bit-identical).
-// Per wave the header (kLhdr ints) holds the 5 group bases, the format flag (1 = compact,
-// 0 = the 32-bit ELL row: waves near a periodic face or whose group ranges are too long) and,
-// per lane, the count at the end of groups 0-3 (bytes; a wave with more than 255 neighbours on a
+// fall into kGroups groups (3-D: the 2 kReach + 1 columns of one slowest-axis offset, which are
+// consecutive in cell order; 2-D: each column), so every neighbour of a group lies in a short
+// index range from the group's wave-wide first candidate.  Entry k of a lane is 16 bits -- the
+// offset from its group's base (13 bits) and the neighbour's type (3 bits) -- two entries per
+// 32-bit word at word[k / 2][lane] of the wave's tile (same order as the ELL row, so sums are
+// bit-identical).  Per wave the header (kLhdr ints) holds the group bases, the format flag
+// (kHdrFlag; 1 = compact, 0 = the 32-bit ELL row: waves near a periodic face or whose group
+// ranges are too long) and, per lane, the count at the end of every group but the last (bytes; a
+// wave with more than 255 neighbours on a
 // lane, which the reference allows up to 511, is searched again into ELL rows: k_neighbors REDO).  Half the list bytes of the ELL rows.
 #ifndef MPH_LIST16
 #define MPH_LIST16 1
@@ -241,44 +242,70 @@ __device__ __forceinline__ const int* ell_row(const int* nbr, int i)
 constexpr int kOff16 = 13;                  // offset bits of a compact entry (type above)
 constexpr int kSpan16 = (1 << kOff16) - 1;  // longest group range a compact wave may have
 
+#ifndef MPH_GB_LDS
+#define MPH_GB_LDS 1   // group base of an entry read from LDS (else a select tree)
+#endif
 struct NbrList {
     const int* tile;                // the wave's list tile (wave-uniform)
     int lane;
-    int b0, b1, b2, b3, b4;         // group bases (wave-uniform)
-    unsigned ends;                  // the lane's counts at the ends of groups 0-3 (bytes)
+    const int* gb;                  // the wave's group bases, staged in LDS (kGroups ints)
+    int b[kGroups];                 // the same, wave-uniform (MPH_GB_LDS=0: selected by compares)
+    // the lane's counts at the ends of groups 0-3 and 4-5, one byte each (<= 127; unused bytes 127)
+    unsigned ends, ends2;
     bool c16;                       // wave-uniform format flag
 };
 
-__device__ __forceinline__ NbrList nbr_list(const int* nbr, const int* lhdr, int i)
+// sb: kGroups ints of LDS for this wave.  Every active lane stores the (wave-uniform) bases, so
+// the lanes that have already left do not matter.
+__device__ __forceinline__ NbrList nbr_list(const int* nbr, const int* lhdr, int i, int* sb)
 {
     NbrList L;
     const int tile = __builtin_amdgcn_readfirstlane(i >> 6);
     L.tile = nbr + (size_t)tile * (kTile * kMaxNeighbor);
     L.lane = i & 63;
+    L.gb = sb;
     const int* h = lhdr ? lhdr + (size_t)tile * kLhdr : nullptr;
-    L.c16 = MPH_LIST16 && h && h[5] == 1;
-    L.b0 = L.b1 = L.b2 = L.b3 = L.b4 = 0;
-    L.ends = 0;
+    L.c16 = MPH_LIST16 && h && h[kHdrFlag] == 1;
+    L.ends = L.ends2 = 0x7F7F7F7Fu;
+#pragma unroll
+    for (int g = 0; g < kGroups; ++g) L.b[g] = 0;
     if (L.c16) {
-        L.b0 = h[0]; L.b1 = h[1]; L.b2 = h[2]; L.b3 = h[3]; L.b4 = h[4];
+#pragma unroll
+        for (int g = 0; g < kGroups; ++g) {
+            L.b[g] = h[g];
+            if (MPH_GB_LDS) sb[g] = h[g];
+        }
+        if (MPH_GB_LDS) __builtin_amdgcn_wave_barrier();
         L.ends = (unsigned)h[8 + (i & 63)];
+        if (kGroups > 5) L.ends2 = (unsigned)h[8 + 64 + (i & 63)];
     }
     return L;
 }
 
-// entry k of the lane: neighbour index j and type t
+// entry k of the lane: neighbour index j and type t.  The group of entry k is the number of
+// group ends <= k: with k and the ends below 128, (k | 0x80) - end per byte keeps its top bit
+// exactly when k >= end, so two subtractions and popcounts count them for all 6 ends at once.
 template <bool C16>
-__device__ __forceinline__ void nbr_at(NbrList L, int k, int& j, int& t)
+__device__ __forceinline__ void nbr_at(const NbrList& L, int k, int& j, int& t)
 {
     if (C16) {
         const unsigned w = reinterpret_cast<const unsigned*>(L.tile)[(k >> 1) * kTile + L.lane];
         const unsigned e = (k & 1) ? (w >> 16) : (w & 0xFFFFu);
-        const unsigned uk = (unsigned)k;
-        int b = L.b0;
-        b = uk >= (L.ends & 0xFFu) ? L.b1 : b;
-        b = uk >= ((L.ends >> 8) & 0xFFu) ? L.b2 : b;
-        b = uk >= ((L.ends >> 16) & 0xFFu) ? L.b3 : b;
-        b = uk >= (L.ends >> 24) ? L.b4 : b;
+        const unsigned kk = ((unsigned)k * 0x01010101u) | 0x80808080u;
+        int g = __popc((kk - L.ends) & 0x80808080u);
+        if (kGroups > 5) g += __popc((kk - L.ends2) & 0x80808080u);
+        int b;
+        if (MPH_GB_LDS) {
+            b = L.gb[g];
+        } else {   // binary select tree over the uniform bases
+            const int s0 = (g & 1) ? L.b[1] : L.b[0];
+            const int s1 = (g & 1) ? L.b[3] : L.b[2];
+            const int s2 = (g & 1) ? L.b[kGroups > 5 ? 5 : 4] : L.b[4];
+            const int s3 = L.b[kGroups - 1];
+            const int t0 = (g & 2) ? s1 : s0;
+            const int t1 = (g & 2) ? s3 : s2;
+            b = (g & 4) ? t1 : t0;
+        }
         j = b + (int)(e & kSpan16);
         t = (int)(e >> kOff16);
     } else {
@@ -759,7 +786,7 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
 {
     using X = CellAxes<DIM, PERM>;
     int cnt = 0;
-    constexpr int NCOL = DIM == 3 ? 25 : 5;
+    constexpr int NCOL = DIM == 3 ? kGroups * kGroups : kGroups;
     const int cc[3] = {cx, cy, cz};
     const int gca = P.gc[X::A2];   // contiguous axis
     const int cca = cc[X::A2];
@@ -777,7 +804,7 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
         int base;
         double d2;
         if (DIM == 3) {
-            const int dxc = col / 5 - 2, dyc = col % 5 - 2;
+            const int dxc = col / kGroups - kReach, dyc = col % kGroups - kReach;
             const int c0 = cc[X::A0], c1 = cc[X::A1];
             const double gx = cell_gap(uu[X::A0], c0, dxc, cw0), gy = cell_gap(uu[X::A1], c1, dyc, cw1);
             d2 = gx * gx + gy * gy;
@@ -786,7 +813,7 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
             const int jy = FAST ? c1 + dyc : wrap_cell(c1 + dyc, P.gc[X::A1]);
             base = (jx * P.gc[X::A1] + jy) * P.gc[X::A2];
         } else {
-            const int dxc = col - 2;
+            const int dxc = col - kReach;
             const double gx = cell_gap(uu[0], cx, dxc, cw0);
             d2 = gx * gx;
             if (d2 > rcm2) continue;
@@ -899,7 +926,8 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     const double lo2 = P.rc2 * (1.0 - 1e-10), hi2 = P.rc2 * (1.0 + 1e-10);
     using X = CellAxes<DIM, PERM>;
     int cnt = 0;
-    constexpr int NCOL = DIM == 3 ? 25 : 5;
+    constexpr int NCOL = DIM == 3 ? kGroups * kGroups : kGroups;
+    static_assert(!SEG || NCOL <= kSegCols, "the segmented list header has 25 columns (MPH_R=2)");
     const int cc[3] = {cx, cy, cz};
     const int cca = cc[X::A2];
     const double rcm2 = P.rc2 * (1.0 + 4e-6);
@@ -913,13 +941,13 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
         int base;
         double d2;
         if (DIM == 3) {
-            const int dxc = col / 5 - 2, dyc = col % 5 - 2;
+            const int dxc = col / kGroups - kReach, dyc = col % kGroups - kReach;
             const int c0 = cc[X::A0], c1 = cc[X::A1];
             const double gx = cell_gap(uu[X::A0], c0, dxc, cw0), gy = cell_gap(uu[X::A1], c1, dyc, cw1);
             d2 = gx * gx + gy * gy;
             base = ((c0 + dxc) * P.gc[X::A1] + c1 + dyc) * P.gc[X::A2];
         } else {
-            const int dxc = col - 2;
+            const int dxc = col - kReach;
             const double gx = cell_gap(uu[0], cx, dxc, cw0);
             d2 = gx * gx;
             base = (cx + dxc) * P.gc[1];
@@ -938,34 +966,35 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     // ranges of its first and last column (no column wraps: the wave is interior)
     const bool want16 = MPH_LIST16 && !SEG && lh != nullptr;
     bool c16 = false;
-    int g0 = 0, g1 = 0, g2 = 0, g3 = 0, g4 = 0, gbase = 0;
+    int gb[kGroups], gbase = 0;   // wave-uniform group bases
     if (want16) {
         bool ok = true;
 #pragma unroll
-        for (int g = 0; g < 5; ++g) {
+        for (int g = 0; g < kGroups; ++g) {
             int lo = 0x7fffffff, hi = -1;
             if (act) {
                 if (DIM == 3) {
-                    const int a0 = cc[X::A0] + g - 2, c1 = cc[X::A1];
-                    lo = start[((a0 * P.gc[X::A1] + c1 - 2) * P.gc[X::A2]) + cca - P.sa];
-                    hi = start[((a0 * P.gc[X::A1] + c1 + 2) * P.gc[X::A2]) + cca + P.sa + 1];
+                    const int a0 = cc[X::A0] + g - kReach, c1 = cc[X::A1];
+                    lo = start[((a0 * P.gc[X::A1] + c1 - kReach) * P.gc[X::A2]) + cca - P.sa];
+                    hi = start[((a0 * P.gc[X::A1] + c1 + kReach) * P.gc[X::A2]) + cca + P.sa + 1];
                 } else {
-                    lo = start[(cx + g - 2) * P.gc[1] + cca - P.sa];
-                    hi = start[(cx + g - 2) * P.gc[1] + cca + P.sa + 1];
+                    lo = start[(cx + g - kReach) * P.gc[1] + cca - P.sa];
+                    hi = start[(cx + g - kReach) * P.gc[1] + cca + P.sa + 1];
                 }
             }
             const int mn = wave_min(lo), mx = wave_max(hi);
             ok = ok && (mx <= mn || mx - mn <= kSpan16 + 1);
-            const int b = mx > mn ? mn : 0;
-            if (g == 0) g0 = b;
-            if (g == 1) g1 = b;
-            if (g == 2) g2 = b;
-            if (g == 3) g3 = b;
-            if (g == 4) g4 = b;
+            gb[g] = mx > mn ? mn : 0;
         }
         c16 = ok;
     }
-    unsigned ends = 0;
+    // the lane's group ends go straight to the header (byte g - 1: the count at the end of group
+    // g - 1; unused bytes 127, nbr_at), so they hold no registers during the column loop
+    unsigned char* ends8 = c16 ? reinterpret_cast<unsigned char*>(lh + 8 + lane) : nullptr;
+    if (c16) {
+        lh[8 + lane] = 0x7F7F7F7F;
+        if (kGroups > 5) lh[8 + 64 + lane] = 0x7F7F7F7F;
+    }
     // software pipeline: the start[] loads of column col + 1 are in flight while column col is
     // staged and tested (the per-column chain start[] -> window -> staging loads is latency bound)
     int nb_jb, nb_je;
@@ -974,10 +1003,14 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     for (int col = 0; col < NCOL; ++col) {
         if (c16) {
             // entering group g: the count so far ends group g - 1
-            const bool first = DIM == 3 ? col % 5 == 0 : true;
-            const int g = DIM == 3 ? col / 5 : col;
-            if (first && g > 0) ends |= (unsigned)min(cnt, 255) << (8 * (g - 1));
-            if (first) gbase = g == 0 ? g0 : g == 1 ? g1 : g == 2 ? g2 : g == 3 ? g3 : g4;
+            const bool first = DIM == 3 ? col % kGroups == 0 : true;
+            const int g = DIM == 3 ? col / kGroups : col;
+            if (first && g > 0) ends8[g <= 4 ? g - 1 : 4 * 64 + g - 5] = (unsigned char)min(cnt, 127);
+            if (first) {
+#pragma unroll
+                for (int q = 0; q < kGroups; ++q)
+                    if (q == g) gbase = gb[q];
+            }
         }
         const int jb = nb_jb, je = nb_je;
         if (MPH_SEARCH_PREFETCH && col + 1 < NCOL) col_range(col + 1, nb_jb, nb_je);
@@ -1082,17 +1115,18 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     }
     if (SEG && slot > kSegCap) *seg_overflow = 1;
     if (c16) {
-        // the group ends are bytes: a wave with a lane past 255 neighbours (the reference allows
-        // 511) is marked for the ELL search of launch_neighbors' second launch (k_neighbors REDO)
+        // the group ends are bytes below 128 (nbr_at): a wave with a lane past 127 neighbours (the
+        // reference allows 511) is marked for the ELL search of launch_neighbors' second launch
+        // (k_neighbors REDO)
         if (wave_max(cnt) > P.l16max) {
-            if (lane == 0) lh[5] = 2;   // counted in DevState.list_redo by neighbors_body
+            if (lane == 0) lh[kHdrFlag] = 2;   // counted in DevState.list_redo by neighbors_body
             return cnt;
         }
-        // group ends of this lane, the bases and the format flag of the wave
-        lh[8 + lane] = (int)ends;
+        // the bases and the format flag of the wave
         if (lane == 0) {
-            lh[0] = g0; lh[1] = g1; lh[2] = g2; lh[3] = g3; lh[4] = g4;
-            lh[5] = 1;
+#pragma unroll
+            for (int g = 0; g < kGroups; ++g) lh[g] = gb[g];
+            lh[kHdrFlag] = 1;
         }
     }
     return cnt;
@@ -1121,7 +1155,7 @@ __device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A,
     const int tile = __builtin_amdgcn_readfirstlane(i >> 6);
     int* lh = lhdr ? lhdr + (size_t)tile * kLhdr : nullptr;
     if (REDO) lh = nullptr;   // a wave the first launch marked: now into ELL rows
-    if (lhdr && (threadIdx.x & 63) == 0) lhdr[(size_t)tile * kLhdr + 5] = 0;
+    if (lhdr && (threadIdx.x & 63) == 0) lhdr[(size_t)tile * kLhdr + kHdrFlag] = 0;
     if (wave_all_ghosts(P, A, live, ii)) {
         if (live) ncount[i] = 0;
         return;
@@ -1152,7 +1186,7 @@ __device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A,
                                                         stage, nullptr, nullptr, nullptr, lh,
                                                         reinterpret_cast<unsigned short*>(
                                                             nbr + (size_t)tile * (kTile * kMaxNeighbor)));
-            if (lh && (threadIdx.x & 63) == 0 && lh[5] == 2) atomicAdd(&st->list_redo, 1);
+            if (lh && (threadIdx.x & 63) == 0 && lh[kHdrFlag] == 2) atomicAdd(&st->list_redo, 1);
         }
         if (live) ncount[i] = cnt;
     } else {
@@ -1175,9 +1209,13 @@ __device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A,
     if (cnt > kMaxNeighbor) atomicOr(&st->overflow, 1);
 }
 
-// one kernel per cell order (DevParams.perm), so each keeps its own register budget
+// one kernel per cell order (DevParams.perm), so each keeps its own register budget; held to 80
+// VGPRs (6 waves per SIMD: the search waits on its start[] and staging loads)
+#ifndef MPH_NB_WPE
+#define MPH_NB_WPE 6
+#endif
 template <int DIM, int PERM>
-__global__ __launch_bounds__(256) void k_neighbors(DevParams P, Soa A, const int* __restrict__ start,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MPH_NB_WPE))) void k_neighbors(DevParams P, Soa A, const int* __restrict__ start,
                                                    int* __restrict__ nbr, int* __restrict__ ncount,
                                                    int2* __restrict__ hdr, int* __restrict__ lhdr,
                                                    DevState* __restrict__ st)
@@ -1205,7 +1243,7 @@ __global__ __launch_bounds__(256) void k_neighbors_redo(DevParams P, Soa A, cons
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int t0 = wave * 64; t0 < ntile; t0 += 4 * 64) {
         const int t = t0 + lane;   // the wave header this lane checks
-        unsigned long long m = __ballot(t < ntile && lhdr[(size_t)t * kLhdr + 5] == 2);
+        unsigned long long m = __ballot(t < ntile && lhdr[(size_t)t * kLhdr + kHdrFlag] == 2);
         while (m) {
             const int b = __ffsll((long long)m) - 1;
             m &= m - 1;
@@ -1423,7 +1461,8 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
     const int ti = A.type[i];
     const bool solid = dev_is_struct(ti);
     const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
-    const NbrList NL = nbr_list(nbr, lhdr, i);
+    __shared__ int s_gb[4][8];
+    const NbrList NL = nbr_list(nbr, lhdr, i, s_gb[threadIdx.x >> 6]);
     PassA o;
     if (NL.c16)   // compact lists come from interior searches only
         pass_a_loop<true, true, DIM>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
@@ -1691,7 +1730,8 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
         if (!live) return;
     } else {
         const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
-        const NbrList NL = nbr_list(nbr, lhdr, i);
+        __shared__ int s_gb[4][8];
+        const NbrList NL = nbr_list(nbr, lhdr, i, s_gb[threadIdx.x >> 6]);
         if (NL.c16)   // compact lists come from interior searches only
             pass_b_loop<true, true, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, NL, cnt, ti, solid, xi,
                                                yi, zi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
@@ -1783,7 +1823,8 @@ __global__ __launch_bounds__(256) void k_virial(DevParams P, const DevTables* __
     const bool segmented = MPH_SEG && h && h[kSegCols].x == 1;
     const unsigned short* seg = seg_tile(nbr, i);
     const int lane = i & 63;
-    const NbrList NL = nbr_list(nbr, lhdr, i);
+    __shared__ int s_gb[4][8];
+    const NbrList NL = nbr_list(nbr, lhdr, i, s_gb[threadIdx.x >> 6]);
     int col = 0, slot = 0, used = 0;
     for (int k = 0; k < cnt; ++k) {
         int j, tj;
@@ -2170,9 +2211,10 @@ __global__ __launch_bounds__(256) void k_sinit_search(DevParams P, int ns, const
     const int cx = cell_axis(xi.x, P.corg[0], P.dw[0], P.ginv[0], P.gc[0]);
     const int cy = cell_axis(xi.y, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
     const int cz = DIM == 3 ? cell_axis(xi.z, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
-    // stencil half-widths in cells: 2 across (cells >= rc/2), P.sa along the contiguous axis
+    // stencil half-widths in cells: kReach across (cells >= rc/kReach), P.sa along the contiguous axis
     const int ca = contig_axis(DIM, P.perm);
-    const int rx = ca == 0 ? P.sa : 2, ry = ca == 1 ? P.sa : 2, rz = DIM == 3 ? (ca == 2 ? P.sa : 2) : 0;
+    const int rx = ca == 0 ? P.sa : kReach, ry = ca == 1 ? P.sa : kReach,
+              rz = DIM == 3 ? (ca == 2 ? P.sa : kReach) : 0;
     int c = 0;
     for (int dx = -rx; dx <= rx; ++dx) {
         const int jx = wrap_cell(cx + dx, P.gc[0]);

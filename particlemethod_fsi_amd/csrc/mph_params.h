@@ -11,7 +11,23 @@ namespace mph {
 constexpr int kTypes = MPH_TYPE_COUNT;
 constexpr int kMaxNeighbor = MPH_MAX_NEIGHBOR_COUNT;
 constexpr int kTile = 64;  // ELL neighbour-list tile = one wavefront of i-particles
-constexpr int kContigSub = 2;   // cells along the contiguous axis are 1/kContigSub as wide
+// Stencil reach along the contiguous axis: cells there are >= rc / kContigReach wide, and a
+// column is the one index range of +-kContigReach cells (thin cells only sharpen the cutoff
+// trimming of each column)
+#ifndef MPH_SA
+#define MPH_SA 3
+#endif
+constexpr int kContigReach = MPH_SA;
+// Stencil reach across the two outer (column) axes: cells there are >= rc / kReach wide, so a
+// +-kReach stencil of (2 kReach + 1)^2 columns covers the acceptance sphere.  kReach = 3 makes the
+// cells (rc / 3 = 0.87 dx at RadiusRatio 2.5) narrower than the lattice spacing, so a cell row
+// holds one lattice line and a wavefront is a run along that line: the 64 lanes' k-th neighbours
+// are then consecutive particles of one neighbour row (coherent gathers in the list passes).
+#ifndef MPH_R
+#define MPH_R 3
+#endif
+constexpr int kReach = MPH_R;
+constexpr int kGroups = 2 * kReach + 1;   // compact-list groups: one per slowest-axis offset
 // ELL list entry = sorted index | (type << kTypeShift): pass A reads the neighbour's type with
 // its index instead of gathering it (requires fewer than 2^28 particles per context)
 constexpr int kTypeShift = 28;
@@ -21,8 +37,18 @@ constexpr int kPad = 8;         // extra elements behind every per-particle arra
 // stencil column (25 in 3-D) plus the list format
 constexpr int kSegHdr = 26;
 // Compact neighbour list of a wavefront (mph_kernels.hip, MPH_LIST16): ints per wave header --
-// 5 group bases, the format flag, 2 spare, then the 64 lanes' group ends (4 bytes each)
-constexpr int kLhdr = 8 + 64;
+// kGroups (<= 7) group bases, the format flag at kHdrFlag, then the 64 lanes' group ends: the
+// ends of groups 0-3 (4 bytes) at [8 + lane], of groups 4-5 at [8 + 64 + lane]
+constexpr int kHdrFlag = 7;
+// the default list format: compact pays at kReach = 2 (D1M -1 %, D16M -6 %); at kReach = 3 the
+// passes' gathers are coherent and the 16-bit decode (group of the entry, then its base) costs
+// more than the list bytes it saves (D1M pass A 0.381 -> 0.416 ms)
+#ifndef MPH_LIST_COMPACT
+#define MPH_LIST_COMPACT (MPH_R == 2)
+#endif
+constexpr bool kListCompact = MPH_LIST_COMPACT;
+constexpr int kLhdr = 8 + 2 * 64;
+static_assert(kGroups <= kHdrFlag, "group bases overlap the format flag");
 
 inline bool is_fluid(int t) { return t >= 0 && t < 2; }   // main.cpp:69-70
 inline bool is_struct(int t) { return t >= 2 && t < 4; }  // main.cpp:71-72
@@ -57,14 +83,14 @@ struct DevParams {
     int gc[3];         // GPU linked-cell grid (gc[2] == 1 in 2-D)
     int ncell;         // gc[0]*gc[1]*gc[2]
     int substeps;      // (int)(Dt/Elastic_Dt + 0.5), main.cpp:653
-    int sa;            // stencil half-width (cells) along the contiguous axis (2 * kContigSub)
+    int sa;            // stencil half-width (cells) along the contiguous axis (kContigReach)
     // linear order of the 3-D cell grid (order_axis above): 0 = (x, y, z) with z contiguous; z
     // slabs (mph_dist.hip) put z in the middle, 3 = (y, z, x) or 4 = (x, z, y), so that the ghosts
     // beyond both faces form long runs at the two ends of every plane of the slowest axis (whole
     // wavefronts the list kernels skip) while every XCD's contiguous share of the sorted arrays
     // stays a band of that slowest axis through the whole slab (L2 locality); 1, 2 put z slowest
     int perm;
-    int l16max;        // most neighbours a lane of a compact-list wave may have (255: byte group
+    int l16max;        // most neighbours a lane of a compact-list wave may have (127: byte group
                        // ends; lower only to test the ELL redo, MPH_LIST16_MAX)
     int fast_ok;       // every active axis has > 12 GPU cells: interior waves may skip the
                        // periodic branch of the minimum image (see k_neighbors)

@@ -297,17 +297,17 @@ def test_gpu_cell_orders_match_golden(case, perm, monkeypatch):
 
 @pytest.mark.parametrize("case", ["box3d", "gate3d", "d1m"])
 def test_gpu_compact_lists_bitwise_equal_ell(case, monkeypatch):
-    """The compact 16-bit neighbour lists (MPH_LIST16, default) hold the same neighbours in the same
+    """The compact 16-bit neighbour lists (MPH_LIST16=1) hold the same neighbours in the same
     order as the 32-bit ELL rows, so every field after several steps is bit-identical with
     MPH_LIST16=0; and the interior wavefronts of the large case do use the compact format.
-    Mode "redo": a lane limit of 60 (MPH_LIST16_MAX, 255 in production) sends most waves through
+    Mode "redo": a lane limit of 60 (MPH_LIST16_MAX, 127 in production) sends most waves through
     the second, ELL search launch (k_neighbors REDO) -- same results again."""
     cfg, parts = cases.get(case).build()
     fields = ["Position", "Velocity", "PressureP", "NeighborCount", "Force", "DensityA", "VolStrainP"]
     out = {}
     for mode in ("1", "redo", "0"):
         monkeypatch.setenv("MPH_LIST16", "0" if mode == "0" else "1")
-        monkeypatch.setenv("MPH_LIST16_MAX", "60" if mode == "redo" else "255")
+        monkeypatch.setenv("MPH_LIST16_MAX", "60" if mode == "redo" else "127")
         with MphSolver(cfg, parts) as s:
             s.step(5)
             out[mode] = {f: s.get(f) for f in fields}
