@@ -668,12 +668,13 @@ __device__ __forceinline__ void pass_a_term(const DevParams& P, const double* s_
     const double dot = dvx * q0 + dvy * q1 + dvz * q2;
     if (r2 <= P.rp2) {
         const double omt = 1.0 - r * P.inv_rp;
+        const double u = P.cdp * omt * ir;   // dw_p(r) / r
         o.vs += P.cp * omt * omt;
-        o.dv -= dot * ir * (P.cdp * omt);
+        o.dv -= dot * u;
         // strict test of the force loops (2402), and structure i sees only non-structure j
         // (InterfaceForce 2439-2472)
         if (FORCE && r2 < P.rp2 && !(solid && dev_is_struct(tj))) {
-            const double c = P.cdp * omt * ir * P.vol;
+            const double c = u * P.vol;
             o.s0 += c * q0;
             o.s1 += c * q1;
             o.s2 += c * q2;
@@ -694,8 +695,8 @@ __device__ __forceinline__ void pass_a_term(const DevParams& P, const double* s_
             o.g2 += q2 * w;
         }
         if (FORCE && r2 < P.rv2) {
-            const double dwij = -P.cdv * (1.0 - r * P.inv_rv);
-            const double c = P.cvis * s_mu[ti * kTypes + tj] * dot * dwij * (ir * ir * ir) * P.vol;
+            // s_mu holds -cvis cdv vol mu_ij (k_pass_a): dw_v(r) = -cdv (1 - r / rv)
+            const double c = s_mu[ti * kTypes + tj] * (1.0 - r * P.inv_rv) * dot * (ir * ir * ir);
             o.v0 += c * q0;
             o.v1 += c * q1;
             o.v2 += c * q2;
@@ -936,26 +937,37 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                           DIM == 3 ? grid_offset(zi, P.corg[2], P.dw[2]) : 0.0};
     const double ua = uu[X::A2];
     const double ginva = P.ginv[X::A2];
-    // candidate range of this lane in stencil column col (cell ranges -> start[] loads)
+    // candidate range of this lane in stencil column col (cell ranges -> start[] loads).  The
+    // trimming is only a bound (the exact test decides), so it runs in FP32, rounded outwards: the
+    // squared cell gaps down, the cutoff and the half range up, so every range holds the one of the
+    // FP64 bound (same candidates, same list).  The gap along the slowest axis changes once per
+    // group of columns (the columns are visited in order).
+    constexpr float kDn = 1.0f - 1.0f / (1 << 20), kUp = 1.0f + 1.0f / (1 << 19);
+    const float rcm2f = (float)rcm2 * kUp;
+    float gx2f = 0.0f;
     auto col_range = [&](int col, int& jb, int& je) {
         int base;
-        double d2;
+        float d2f;
         if (DIM == 3) {
             const int dxc = col / kGroups - kReach, dyc = col % kGroups - kReach;
             const int c0 = cc[X::A0], c1 = cc[X::A1];
-            const double gx = cell_gap(uu[X::A0], c0, dxc, cw0), gy = cell_gap(uu[X::A1], c1, dyc, cw1);
-            d2 = gx * gx + gy * gy;
+            if (dyc == -kReach) {
+                const float gx = (float)cell_gap(uu[X::A0], c0, dxc, cw0);
+                gx2f = gx * gx * kDn;
+            }
+            const float gy = (float)cell_gap(uu[X::A1], c1, dyc, cw1);
+            d2f = (gx2f + gy * gy * kDn) * kDn;
             base = ((c0 + dxc) * P.gc[X::A1] + c1 + dyc) * P.gc[X::A2];
         } else {
             const int dxc = col - kReach;
-            const double gx = cell_gap(uu[0], cx, dxc, cw0);
-            d2 = gx * gx;
+            const float gx = (float)cell_gap(uu[0], cx, dxc, cw0);
+            d2f = gx * gx * kDn;
             base = (cx + dxc) * P.gc[1];
         }
         jb = 0;
         je = 0;
-        if (act && d2 <= rcm2) {
-            const double ra = sqrt(rcm2 - d2);
+        if (act && d2f <= rcm2f) {
+            const double ra = (double)(__fsqrt_rn(rcm2f - d2f) * kUp);
             const int lo = (int)fmax(floor((ua - ra) * ginva), (double)(cca - P.sa));
             const int hi = (int)fmin(floor((ua + ra) * ginva), (double)(cca + P.sa));
             jb = start[base + lo];
@@ -1260,7 +1272,7 @@ __global__ __launch_bounds__(256) void k_neighbors_redo(DevParams P, Soa A, cons
 // List pass: the neighbour loops gather U neighbours' fields
 // before the first use (all loads in flight at once; the loops are memory-latency bound).
 #ifndef MPH_UA
-#define MPH_UA 8
+#define MPH_UA 5   // pass A (with MPH_PA_WPE 4; coherent gathers at kReach 3: 0.355 ms against 0.376 at U = 8, 3 waves)
 #endif
 #ifndef MPH_UB
 #define MPH_UB 8
@@ -1407,7 +1419,7 @@ __device__ __forceinline__ void pass_a_seg(const DevParams& P, const double* s_r
 }
 
 #ifndef MPH_PA_WPE
-#define MPH_PA_WPE 3   // pass A at <= 168 VGPRs: 3 waves per SIMD
+#define MPH_PA_WPE 4   // pass A at <= 128 VGPRs: 4 waves per SIMD
 #endif
 #if MPH_PA_WPE
 #define MPH_PA_ATTR __attribute__((amdgpu_waves_per_eu(MPH_PA_WPE)))
@@ -1426,7 +1438,7 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
     __shared__ double s_mu[kTypes * kTypes];
     if (threadIdx.x < kTypes * kTypes) {
         s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
-        s_mu[threadIdx.x] = T->mu_ij[threadIdx.x];
+        s_mu[threadIdx.x] = T->mu_ij[threadIdx.x] * (-P.cvis * P.cdv * P.vol);   // pass_a_term's viscous factor
     }
     __syncthreads();
     const int i = xcd_block(blockIdx.x, live_blocks(n)) * blockDim.x + threadIdx.x;
