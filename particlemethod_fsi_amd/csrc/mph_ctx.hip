@@ -73,7 +73,7 @@ void ctx_fill_launch(MphCtx* c)
     // (MPH_LIST16=0); unset: kListCompact
     const char* l16 = std::getenv("MPH_LIST16");
     const bool compact = l16 && *l16 ? std::string(l16) != "0" : kListCompact;
-    L.lhdr = compact ? c->list_hdr : nullptr;
+    L.lhdr = compact && pass_a_equal_radii(c->P) ? c->list_hdr : nullptr;
     L.pres = c->pres; L.gx = c->gx; L.gy = c->gy; L.gz = c->gz; L.pa = c->pa;
     L.force = c->force; L.acc = c->acc; L.fpart = c->fpart; L.rec = c->rec;
     L.dens_a = c->dens_a; L.vstrain = c->vstrain; L.divp = c->divp;

@@ -460,8 +460,11 @@ __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __res
 
 // Exclusive scan of the cell histogram: 3 launches (block reduce, top-level scan, down-sweep).
 constexpr int kScanThreads = 256;
-constexpr int kScanItems = 16;
-constexpr int kScanBlock = kScanThreads * kScanItems;   // 4096 cells per block
+#ifndef MPH_SCAN_ITEMS
+#define MPH_SCAN_ITEMS 16
+#endif
+constexpr int kScanItems = MPH_SCAN_ITEMS;   // cells per thread (a multiple of 4)
+constexpr int kScanBlock = kScanThreads * kScanItems;   // 4096 cells per block (bsum arrays: ncell / 4096 + 2)
 
 __device__ __forceinline__ int block_exclusive_scan(int v, int* lds, int& total)
 {
@@ -658,7 +661,7 @@ struct PassA {
 // One neighbour's contribution to DensityA (2141-2171), GravityCenter (2174-2210), DensityP
 // (2314-2341), DivergenceP (2343-2379), and (FORCE) the P_i half of the pressure force and the
 // viscous force; (dvx, dvy, dvz) = v_j - v_i.
-template <bool FORCE>
+template <bool FORCE, bool EQR = false>
 __device__ __forceinline__ void pass_a_term(const DevParams& P, const double* s_ratio, const double* s_mu, int ti,
                                             int tj, bool solid, double q0, double q1, double q2, double r2,
                                             double dvx, double dvy, double dvz, PassA& o)
@@ -666,6 +669,40 @@ __device__ __forceinline__ void pass_a_term(const DevParams& P, const double* s_
     double r, ir;
     rsqrt_pair(r2, r, ir);
     const double dot = dvx * q0 + dvy * q1 + dvz * q2;
+    if (EQR) {
+        // RadiusA = RadiusP = RadiusV (pass_a_equal_radii): one cutoff test and one 1 - r/h for
+        // all four kernels; same expressions otherwise
+        if (r2 <= P.rp2) {
+            const double t = r * P.inv_rp;
+            const double omt = 1.0 - t;
+            const double omt2 = omt * omt;
+            const double u = P.cdp * omt * ir;
+            o.vs += P.cp * omt2;
+            o.dv -= dot * u;
+            const bool strict = r2 < P.rp2;
+            if (FORCE && strict && !(solid && dev_is_struct(tj))) {
+                const double c = u * P.vol;
+                o.s0 += c * q0;
+                o.s1 += c * q1;
+                o.s2 += c * q2;
+            }
+            if (!solid) {
+                const double ratio = s_ratio[ti * kTypes + tj];
+                o.da += ratio * (P.ca * t * omt2);
+                const double w = ratio * (P.cg * omt2) * (P.rg / P.r2g);
+                o.g0 += q0 * w;
+                o.g1 += q1 * w;
+                o.g2 += q2 * w;
+                if (FORCE && strict) {
+                    const double c = s_mu[ti * kTypes + tj] * omt * dot * (ir * ir * ir);
+                    o.v0 += c * q0;
+                    o.v1 += c * q1;
+                    o.v2 += c * q2;
+                }
+            }
+        }
+        return;
+    }
     if (r2 <= P.rp2) {
         const double omt = 1.0 - r * P.inv_rp;
         const double u = P.cdp * omt * ir;   // dw_p(r) / r
@@ -771,7 +808,7 @@ __device__ __forceinline__ bool accept_interior(const DevParams& P, double dx, d
 {
     const double r2a = fma(dx, dx, fma(dy, dy, dz * dz));
     bool a = r2a <= lo2;
-    if (r2a > lo2 && r2a <= hi2) {
+    if (!a && r2a <= hi2) {   // two compares: the band is "<= hi2 and not <= lo2"
         const double q0 = image_exact<true>(dx, P.dw[0], P.hw[0], P.w075[0]);
         const double q1 = image_exact<true>(dy, P.dw[1], P.hw[1], P.w075[1]);
         const double q2 = image_exact<true>(dz, P.dw[2], P.hw[2], P.w075[2]);
@@ -1277,7 +1314,7 @@ __global__ __launch_bounds__(256) void k_neighbors_redo(DevParams P, Soa A, cons
 #ifndef MPH_UB
 #define MPH_UB 8
 #endif
-template <bool FAST, bool C16, int DIM, int U = MPH_UA>
+template <bool FAST, bool C16, int DIM, bool EQR, int U = MPH_UA>
 __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_ratio, const double* s_mu,
                                             const Soa& A,
                                             NbrList NL, int cnt, int ti, bool solid, double xi,
@@ -1312,8 +1349,8 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
             const double q0 = image_exact<FAST>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
             const double q1 = image_exact<FAST>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
             const double q2 = image_exact<FAST || DIM == 2>(Z[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
-            pass_a_term<true>(P, s_ratio, s_mu, ti, TT[u], solid, q0, q1, q2, r2_exact(q0, q1, q2), VX[u] - vxi,
-                              VY[u] - vyi, VZ[u] - vzi, o);
+            pass_a_term<true, EQR>(P, s_ratio, s_mu, ti, TT[u], solid, q0, q1, q2, r2_exact(q0, q1, q2), VX[u] - vxi,
+                                   VY[u] - vyi, VZ[u] - vzi, o);
         }
     }
 }
@@ -1476,12 +1513,19 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
     __shared__ int s_gb[4][8];
     const NbrList NL = nbr_list(nbr, lhdr, i, s_gb[threadIdx.x >> 6]);
     PassA o;
+    // wave-uniform: equal radii (every BASELINE config) take the single-cutoff form of the sums
+    const bool eqr = pass_a_equal_radii(P);
+    // (compact lists are only built at equal radii, launch_neighbors, so both list formats of an
+    // interior wave take the same form and stay bit-identical; waves at a periodic face, ELL rows
+    // in both formats, keep the general form)
     if (NL.c16)   // compact lists come from interior searches only
-        pass_a_loop<true, true, DIM>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+        pass_a_loop<true, true, DIM, true>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+    else if (fast && eqr)
+        pass_a_loop<true, false, DIM, true>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
     else if (fast)
-        pass_a_loop<true, false, DIM>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+        pass_a_loop<true, false, DIM, false>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
     else
-        pass_a_loop<false, false, DIM>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+        pass_a_loop<false, false, DIM, false>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
     pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
 }
 

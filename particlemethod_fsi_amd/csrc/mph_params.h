@@ -141,6 +141,17 @@ struct DevState {
 #define MPH_HD
 #endif
 
+// Pass A's single-cutoff form (pass_a_term<.., true>) when RadiusA = RadiusP = RadiusV (RadiusG =
+// RadiusA, main.cpp:1195-1198), as in every BASELINE config; compact lists are built only then
+// (ctx_fill_launch), so both list formats of an interior wave take the same form.
+#ifndef MPH_PA_EQR
+#define MPH_PA_EQR 1
+#endif
+MPH_HD inline bool pass_a_equal_radii(const DevParams& P)
+{
+    return MPH_PA_EQR && P.ra == P.rp && P.rv == P.rp && P.rg == P.rp;
+}
+
 // Slab decomposition along one axis (multi-GPU, mph_dist.hip).  Rank r owns the particles whose
 // (periodically wrapped) coordinate c satisfies lo <= c < hi, with the first/last rank also
 // owning any roundoff spill below dmin / above dmax.  `h` is the halo width (>= the neighbour
