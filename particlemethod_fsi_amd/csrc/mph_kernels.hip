@@ -904,6 +904,9 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
     return cnt;
 }
 
+#ifndef MPH_WIN_BALLOT
+#define MPH_WIN_BALLOT 1   // search window bounds from the first/last active lanes (verified)
+#endif
 #ifndef MPH_DPP_REDUCE
 #define MPH_DPP_REDUCE 1   // wave min/max by DPP row shifts + row broadcasts (else ds_bpermute)
 #endif
@@ -1064,8 +1067,22 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
         const int jb = nb_jb, je = nb_je;
         if (MPH_SEARCH_PREFETCH && col + 1 < NCOL) col_range(col + 1, nb_jb, nb_je);
         const bool any = je > jb;
-        const int mn = wave_min(any ? jb : 0x7fffffff);
-        const int mx = wave_max(any ? je : -1);
+        // the wave's window [mn, mx): the lanes are in cell order, so the first lane with candidates
+        // normally has the lowest jb and the last the highest je -- read those two lanes, and take
+        // the DPP reductions only when a lane says otherwise (wave-uniform check)
+        const unsigned long long am = __ballot(any);
+        int mn = 0x7fffffff, mx = -1;
+        if (am && !MPH_WIN_BALLOT) {
+            mn = wave_min(any ? jb : 0x7fffffff);
+            mx = wave_max(any ? je : -1);
+        } else if (am) {
+            mn = __builtin_amdgcn_readlane(jb, __ffsll((long long)am) - 1);
+            mx = __builtin_amdgcn_readlane(je, 63 - __clzll(am));
+            if (__ballot(any && (jb < mn || je > mx))) {
+                mn = wave_min(any ? jb : 0x7fffffff);
+                mx = wave_max(any ? je : -1);
+            }
+        }
         if (!MPH_SEARCH_PREFETCH && col + 1 < NCOL) col_range(col + 1, nb_jb, nb_je);
         if (mx <= mn) {   // wave-uniform: no lane has candidates in this column
             if (SEG && lane == 0) hdr[col] = make_int2(0, 0);
