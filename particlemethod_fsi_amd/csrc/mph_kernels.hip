@@ -200,6 +200,19 @@ __device__ __forceinline__ int live_blocks(int n) { return (n + 255) >> 8; }
 
 __device__ __forceinline__ int nbr_entry(int j, int type) { return j | (type << kTypeShift); }
 
+// Velocity of sorted particle i for the list passes: from its 48-byte gather record {x, y, z, vx,
+// vy, vz} (k_rank_scatter then skips the SoA velocity stores), or the SoA arrays.
+__device__ __forceinline__ void own_velocity(const Soa& A, int i, double& vx, double& vy, double& vz)
+{
+    if (MPH_AOS_GATHER && A.p6) {
+        const double2* q = A.p6 + 3 * (size_t)i;
+        const double2 b = q[1], c = q[2];
+        vx = b.y; vy = c.x; vz = c.y;
+    } else {
+        vx = A.vx[i]; vy = A.vy[i]; vz = A.vz[i];
+    }
+}
+
 // The ELL list is written once per step and read once per pass.  MPH_LIST_NT=1 makes the pass
 // reads non-temporal (D1M: pass A -1 %, within noise); non-temporal list *stores* in the search
 // lose the write combining of the scattered 4-byte entries (search 0.41 -> 0.77 ms), so the
@@ -633,9 +646,14 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
     A.x[dst] = B.x[p];
     A.y[dst] = B.y[p];
     A.z[dst] = B.z[p];
-    A.vx[dst] = B.vx[p];
-    A.vy[dst] = B.vy[p];
-    A.vz[dst] = B.vz[p];
+    // the sorted velocities are read only through the 48-byte records (own_velocity below), unless
+    // the passes gather SoA (MPH_AOS_GATHER=0, or the segmented lists of MPH_SEG), or in slab mode
+    // (dist_init copies the sorted set into B)
+    if (!MPH_AOS_GATHER || MPH_SEG || !A.p6 || dst_of) {
+        A.vx[dst] = B.vx[p];
+        A.vy[dst] = B.vy[p];
+        A.vz[dst] = B.vz[p];
+    }
     A.type[dst] = B.type[p];
     const int id = B.id[p];
     A.id[dst] = id;
@@ -1512,7 +1530,8 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
     const int2* h = hdr ? hdr + (size_t)(i >> 6) * kSegHdr : nullptr;
     if (MPH_SEG && h && h[kSegCols].x == 1) {   // wave-uniform: this wave's list is column-segmented
         __shared__ double2 stage[4][3 * MPH_LDS_CAP];
-        const double vxi = A.vx[ii], vyi = A.vy[ii], vzi = A.vz[ii];
+        double vxi, vyi, vzi;
+        own_velocity(A, ii, vxi, vyi, vzi);
         const int ti = A.type[ii];
         const bool solid = dev_is_struct(ti);
         PassA o;
@@ -1523,7 +1542,8 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
     }
     const bool fast = wave_interior(P, own, xi, yi, zi);
     if (!own) return;
-    const double vxi = A.vx[i], vyi = A.vy[i], vzi = A.vz[i];
+    double vxi, vyi, vzi;
+    own_velocity(A, i, vxi, vyi, vzi);
     const int ti = A.type[i];
     const bool solid = dev_is_struct(ti);
     const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
@@ -1815,7 +1835,8 @@ __global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __
             pass_b_loop<false, false, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, NL, cnt, ti, solid, xi,
                                                  yi, zi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
     }
-    const double vxi = A.vx[i], vyi = A.vy[i], vzi = A.vz[i];
+    double vxi, vyi, vzi;
+    own_velocity(A, i, vxi, vyi, vzi);
     double vo0 = vxi, vo1 = vyi, vo2 = vzi;
     double xo0 = xi, xo1 = yi, xo2 = zi;
     double4 ao = make_double4(0.0, 0.0, 0.0, 0.0);
