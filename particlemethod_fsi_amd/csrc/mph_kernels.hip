@@ -1604,7 +1604,8 @@ __device__ __forceinline__ void pass_b_term(const DevParams& P, const double* s_
         if (r2 < P.rp2) {
             double r, ir;
             rsqrt_pair(r2, r, ir);
-            const double c = PJ * (cpv * (1.0 - r * P.inv_rp)) * ir;
+            // dw_p(r) / r = cdp (1 - r / rp) / r = cdp (1/r - 1/rp): r itself is not needed
+            const double c = PJ * cpv * (ir - P.inv_rp);
             f0 += c * q0;
             f1 += c * q1;
             f2 += c * q2;
