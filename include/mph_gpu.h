@@ -340,7 +340,8 @@ int mph_dist_selftest(int device);
 int mph_dist_info(const MphCtx* ctx, int* out8);
 /* Neighbour-list formats of the last search: out2 = {wavefronts with the compact 16-bit list,
  * wavefronts in all} (the others, near a periodic face or with long group ranges, keep 32-bit
- * ELL rows; MPH_LIST16=0 at creation disables the compact format).                           */
+ * ELL rows).  The compact format is opt-in at the default stencil (MPH_LIST16=1 at creation,
+ * equal radii only; MPH_LIST16=0 forces ELL rows everywhere).                                 */
 int mph_list_formats(MphCtx* ctx, int* out2);
 /* Particles currently owned by this rank (after the last migration); their original indices.  */
 int mph_owned_count(const MphCtx* ctx);
