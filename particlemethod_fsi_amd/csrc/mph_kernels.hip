@@ -1758,7 +1758,15 @@ __device__ __forceinline__ void pass_b_seg(const DevParams& P, const double* s_r
 // Gravity (2917-2936), Acceleration/kick (2938-2956) and Convection/drift (1892-1907).  The sums
 // start from pass A's fpart (P_i half of the pressure force + viscous force).
 template <bool SURF, int DIM>
-__global__ __launch_bounds__(256) void k_pass_b(DevParams P, const DevTables* __restrict__ T, Soa A,
+#ifndef MPH_PB_WPE
+#define MPH_PB_WPE 0   // pass B occupancy hint (0: the compiler's choice, 112 VGPRs / 4 waves at U = 8)
+#endif
+#if MPH_PB_WPE
+#define MPH_PB_ATTR __attribute__((amdgpu_waves_per_eu(MPH_PB_WPE)))
+#else
+#define MPH_PB_ATTR
+#endif
+__global__ __launch_bounds__(256) MPH_PB_ATTR void k_pass_b(DevParams P, const DevTables* __restrict__ T, Soa A,
                                                 const double4* __restrict__ rec,
                                                 const double4* __restrict__ fpart,
                                                 const double* __restrict__ pres,
