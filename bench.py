@@ -21,10 +21,13 @@ particles and that the NeighborCount total matches the single-GPU run's at the s
 (profiles/d16m_ncount_sum.json), so a scaling run is also a correctness run.
 MPH_SLAB_TRANSPORT=host switches the halo transport to host staging over gloo (diagnostics).
 
-Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel's algorithmic HBM bytes per
-launch (SURVEY 8d per-particle figures) over its HIP-event-timed average
-launch duration; `cpu_baseline` times the reference solver itself (oracle/_ref, built from
-/root/reference) on a bounded sample of the same workload on this host's cores.
+Rank 0 prints ONE JSON line.  `roofline` is the dominant stage's algorithmic HBM bytes per step
+(SURVEY 8d per-particle figures: pass 1 = neighbour search + pass A, 92 B; pass 2 = pass B, 140 B;
+grid build, 140 B; DESIGN.md section 3) over the HIP-event-timed time of the kernels that carry it;
+`roofline.step_frac` is the whole step's 372 B per particle at the measured rate, and
+`neighbor_list` the list bytes SURVEY's figures leave out.  `cpu_baseline` times the reference
+solver itself (oracle/_ref, built from /root/reference) on a bounded sample of the same workload
+on this host's cores.
 """
 from __future__ import annotations
 
@@ -43,6 +46,14 @@ HBM_PEAK_GBPS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level
 FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector spec
 # algorithmic bytes per particle per launch
 ALG_BYTES = {"pass_a": 92.0, "neighbors_pass_a": 92.0, "pass_b": 140.0, "sort": 140.0}
+# SURVEY 8d's stages and the kernels that carry them: "pass 1" (read x, v, type; write PressureP,
+# PressureA, GravityCenter: 92 B) is the neighbour search and pass A together (or their fused
+# form), "pass 2" (140 B) is pass B, the grid build + reorder (140 B) the sort kernels
+STAGES = {
+    "neighbors+pass_a": (92.0, ("neighbors", "neighbors_redo", "search_pass_a", "pass_a")),
+    "pass_b": (140.0, ("pass_b", "pass_b_inner", "pass_b_face")),
+    "sort": (140.0, ("prep", "scan_reduce", "scan_top", "scan_down", "place", "rank_scatter")),
+}
 # elastic substep kernels, per structure particle and launch (SURVEY 8d "500 + 8 n_s" split by
 # kernel; n_s = mean InitialStructureNeighborCount; output-only DeformGradient/Strain/Stress
 # excluded as for the fluid passes):
@@ -157,7 +168,8 @@ def slab_checks(solver, dist, n_total, case_name, steps_done):
             expected = int(table[steps_done])
     except (OSError, ValueError, KeyError):
         pass
-    return {"rccl_nranks": info["nranks"], "transport": "rccl" if info["rccl"] else "host-staged",
+    return {"slab_ranks": info["nranks"], "rccl_nranks": info["rccl_ranks"],
+            "transport": "rccl" if info["rccl_ranks"] else "host-staged",
             "graphs": bool(info["graphs"]), "partition_ok": bool(partition), "owned_total": int(tot[0]),
             "steps_done": steps_done, "neighbor_count_sum": int(tot[2]),
             "neighbor_count_sum_single_gpu": expected,
@@ -251,13 +263,38 @@ def main():
             return (a + b * mean_ns) * ns
         return ALG_BYTES[k] * n_local
 
-    # dominant kernel by total time per step among those with an algorithmic byte count
-    dom = max((k for k in prof if k in ALG_BYTES or k in STRUCT_BYTES),
-              key=lambda k: prof[k]["avg_ms"] * prof[k]["launches"])
-    step_ms = sum(v["avg_ms"] * v["launches"] for v in prof.values()) / args.profile_steps
-    alg_bytes = alg_bytes_of(dom)
-    achieved = alg_bytes / (prof[dom]["avg_ms"] * 1e-3) / 1e9
-    traffic = load_pmc("pmc_traffic", case_name, dom, "hbm_bytes_per_launch")
+    # dominant stage by total time per step: SURVEY 8d's stages (STAGES, each the sum of its
+    # kernels' HIP-event time per step) and the elastic substep kernels
+    steps_prof = max(1, args.profile_steps)
+    units = {}
+    for st, (b, ks) in STAGES.items():
+        ms = sum(prof[k]["avg_ms"] * prof[k]["launches"] for k in ks if k in prof) / steps_prof
+        if ms > 0:
+            units[st] = {"ms": ms, "bytes": b * n_local, "kernels": [k for k in ks if k in prof]}
+    for k in STRUCT_BYTES:
+        if k in prof:
+            units[k] = {"ms": prof[k]["avg_ms"], "bytes": alg_bytes_of(k), "kernels": [k],
+                        "per_launch": True, "launches_per_step": prof[k]["launches"] / steps_prof}
+    dom = max(units, key=lambda u: units[u]["ms"] * units[u].get("launches_per_step", 1.0))
+    step_ms = sum(v["avg_ms"] * v["launches"] for v in prof.values()) / steps_prof
+    alg_bytes = units[dom]["bytes"]
+    achieved = alg_bytes / (units[dom]["ms"] * 1e-3) / 1e9
+    # PMC bytes of the same kernels per step (committed rocprofv3 summary of this case)
+    traffic = None
+    tr = [load_pmc("pmc_traffic", case_name, k, "hbm_bytes_per_launch") for k in units[dom]["kernels"]
+          if k != "neighbors_redo"]
+    if tr and all(t is not None for t in tr):
+        traffic = float(sum(tr))
+    # the neighbour list, which SURVEY's 372 B leave out: written by the search, read by both
+    # passes; algorithmic 4 B per entry against the search's measured WRITE_SIZE
+    list_info = None
+    if world == 1:
+        list_alg = 4.0 * mean_nb * n_local
+        wr = load_pmc("pmc_traffic", case_name, "neighbors", "write_kib")
+        list_info = {"entries_per_particle": mean_nb, "alg_bytes_written": list_alg,
+                     "alg_bytes_read_by_passes": 2.0 * list_alg,
+                     "search_write_bytes_measured": wr * 1024.0 if wr else None,
+                     "write_amplification": (wr * 1024.0 / list_alg) if wr else None}
     # measured HBM traffic of a whole step: rocprofv3 FETCH_SIZE/WRITE_SIZE per kernel in the timed
     # region's store pattern (tools/profile.sh + tools/pmc_traffic.py, calibration
     # profiles/pmc_calib.json), over this run's own step time
@@ -306,10 +343,16 @@ def main():
                                         "particle-step) x rate: a label for the north-star target, not "
                                         "HBM traffic" % ((B_GATHER_3D if case.dim == 3 else 12e3) / 1e3)},
         "neighbors": {"mean": mean_nb, "max": max_nb},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS,
+        "roofline": {"bound": "hbm", "kernel": dom, "kernels": units[dom]["kernels"],
+                     "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
-                     "avg_launch_ms": prof[dom]["avg_ms"]},
+                     "avg_launch_ms": units[dom]["ms"],
+                     "step_frac": B_ALG_STEP * value / world / (HBM_PEAK_GBPS * 1e9),
+                     "stages": {u: {"ms": round(v["ms"], 5),
+                                    "frac": v["bytes"] / (v["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+                                for u, v in units.items()}},
+        "neighbor_list": list_info,
         "fp64": ({"peak_tflops": FP64_PEAK_TFLOPS, "source": "profiles/pmc_fp64.json (64 x "
                   "SQ_INSTS_VALU_FLOPS_FP64 per launch, masked lanes included)",
                   "kernels": {k: {a: round(b, 4) for a, b in v.items()} for k, v in fp64.items()}}

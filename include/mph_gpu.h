@@ -40,7 +40,9 @@ extern "C" {
 
 #define MPH_TYPE_COUNT 6            /* main.cpp:68 */
 #define MPH_MAX_NEIGHBOR_COUNT 512  /* main.cpp:100 (semantic limit; overflow is an error here) */
-#define MPH_ABI_VERSION 2
+/* Bumped on every incompatible change of a declaration below (3: mph_slab_bounds/_owner/_window
+ * take `cuts`; mph_dist_info slot 0/2 meaning); bindings compare mph_abi_version() with it.     */
+#define MPH_ABI_VERSION 3
 
 /* Compile-time case modules of the reference (main.cpp:54-59) as a runtime switch.  The module
  * selects the clamp rule of updateElasticPosition (main.cpp:1918-2044).                        */
@@ -113,6 +115,8 @@ typedef struct MphConfig {
 
 /* sizeof(MphConfig) as compiled into the library (FFI bindings check their mirror against it). */
 int mph_config_sizeof(void);
+/* MPH_ABI_VERSION as compiled into the library.                                              */
+int mph_abi_version(void);
 
 /* Per-particle arrays readable with mph_get (original particle order). */
 typedef enum MphField {
@@ -286,8 +290,9 @@ int mph_dist_unique_id(char* out128);
 /* Same as mph_create, but this rank owns only the particles whose slab (along `axis`) is
  * `rank` of `nranks`; all ranks pass the full particle set.  Transport: RCCL (ncclSend/Recv
  * with the two periodic neighbours, on the context's stream).  Every size of a step is kept on
- * the device and messages travel with fixed capacities (grown between mph_step batches when a
- * count passes 90 %), so the steps are replayed from captured hipGraphs with no host round trip
+ * the device and messages travel with fixed capacities of 1.25 c + 4096 particles for a count c
+ * (checked every 32 steps, also inside one mph_step call, and grown when a count passed 90 %), so
+ * the steps are replayed from captured hipGraphs with no host round trip in between
  * (MPH_SLAB_GRAPHS=0: direct launches).                                                       */
 int mph_create_dist(MphCtx** ctx, const MphConfig* cfg, int n, const int* property,
                     const double* pos, const double* pos0, const double* vel, int device,
@@ -333,8 +338,9 @@ int mph_slab_window(const MphConfig* cfg, int rank, int nranks, int axis, const 
  * exchange delivers each message to the right buffer (the per-peer ordering nranks == 2 relies
  * on) without a second GPU.  Returns 0 on success.                                            */
 int mph_dist_selftest(int device);
-/* Slab-mode facts for reports: out8 = {ranks in the communicator (ncclCommCount; 1 without
- * slabs), rank, RCCL transport (1) or host-staged (0), steps replayed from captured graphs,
+/* Slab-mode facts for reports: out8 = {slab ranks of the decomposition (1 without slabs), rank,
+ * size of the RCCL communicator (ncclCommCount; 0 under the host-staged transport), steps
+ * replayed from captured graphs,
  * local array capacity, largest send / receive message capacity (particles), particles held
  * (owned + ghosts)}.                                                                          */
 int mph_dist_info(const MphCtx* ctx, int* out8);

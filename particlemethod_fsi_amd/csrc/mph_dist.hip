@@ -202,9 +202,32 @@ int exchange(MphCtx* c, hipStream_t stream, const void* send_l, size_t bsl, cons
 template <typename T>
 T* lay_field(DistLayout* lay, size_t off) { return reinterpret_cast<T*>(reinterpret_cast<char*>(lay) + off); }
 
-// Message capacity (particles) of a direction whose live count is c: room to grow by half before
-// the next capacity check (between step batches, dist_sync).
-int msg_capacity(int c) { return c + c / 4 + 4096; }
+// Message capacity (particles) of a direction whose live count is c: 25 % + 4096 particles of room
+// to grow before the next capacity check (dist_sync, at most kSyncSteps steps later).  The slack
+// can be lowered (MPH_SLAB_MSG_SLACK, tests of the growth path); both ranks of a pair read the same
+// environment, so they still derive equal capacities for their shared direction.
+int msg_slack()
+{
+    static const int s = [] {
+        const char* e = std::getenv("MPH_SLAB_MSG_SLACK");
+        return e ? std::max(0, std::atoi(e)) : 4096;
+    }();
+    return s;
+}
+int msg_capacity(int c)
+{
+    // MPH_SLAB_MSG_CAP: one fixed capacity for every direction (tests of the overflow report)
+    static const int fixed = [] {
+        const char* e = std::getenv("MPH_SLAB_MSG_CAP");
+        return e ? std::max(0, std::atoi(e)) : 0;
+    }();
+    return fixed > 0 ? fixed : c + c / 4 + msg_slack();
+}
+
+// Steps between two capacity checks inside one mph_step call: a long call (the steps between two
+// VTK outputs) must not outrun its message capacities while the flow changes, so dist_step
+// replays at most this many steps before dist_sync reads the high-water marks and grows them.
+constexpr int kSyncSteps = 32;
 
 // (Re)allocate the four message buffers for the current capacities: redistribution (56 B per
 // particle), pass-A halo (up to 40 B per particle of both directions' capacities), elastic ghosts.
@@ -691,7 +714,20 @@ int dist_capture(MphCtx* c, int steps, hipGraphExec_t* out)
     return MPH_OK;
 }
 
+int dist_step_batch(MphCtx* c, int nsteps, Profiler* prof);
+
 int dist_step(MphCtx* c, int nsteps, Profiler* prof)
+{
+    // sub-batches of kSyncSteps (a multiple of the 8-step graph), each ending in dist_sync
+    for (int done = 0; done < nsteps;) {
+        const int k = std::min(kSyncSteps, nsteps - done);
+        MPH_CK(dist_step_batch(c, k, prof));
+        done += k;
+    }
+    return MPH_OK;
+}
+
+int dist_step_batch(MphCtx* c, int nsteps, Profiler* prof)
 {
     MphDist& D = *c->dist;
     int left = nsteps;
@@ -702,13 +738,13 @@ int dist_step(MphCtx* c, int nsteps, Profiler* prof)
             (void)hipGetLastError();
             D.graphs = false;
             c->err.clear();
-            return dist_step(c, nsteps, prof);
+            return dist_step_batch(c, nsteps, prof);
         }
         if (!c->graph8 && nsteps >= 8 && dist_capture(c, 8, &c->graph8) != MPH_OK) {
             (void)hipGetLastError();
             D.graphs = false;
             c->err.clear();
-            return dist_step(c, nsteps, prof);
+            return dist_step_batch(c, nsteps, prof);
         }
         while (left >= 8) { MPH_HIP_OK(c, hipGraphLaunch(c->graph8, c->stream)); left -= 8; }
         while (left > 0) { MPH_HIP_OK(c, hipGraphLaunch(c->graph1, c->stream)); left -= 1; }
@@ -922,11 +958,12 @@ int mph_dist_info(const MphCtx* c, int* out8)
         return MPH_OK;
     }
     const MphDist& D = *c->dist;
-    int count = D.nranks;
+    // the RCCL communicator's own size (0 under the host-staged transport, which has none)
+    int count = 0;
     if (D.rccl && D.comm && ncclCommCount((ncclComm_t)D.comm, &count) != ncclSuccess) count = -1;
-    out8[0] = count;
+    out8[0] = D.nranks;
     out8[1] = D.rank;
-    out8[2] = D.rccl ? 1 : 0;
+    out8[2] = count;
     out8[3] = D.graphs ? 1 : 0;
     out8[4] = D.cap;
     out8[5] = std::max(D.cap_sl, D.cap_sr);

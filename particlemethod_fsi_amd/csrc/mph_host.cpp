@@ -19,6 +19,8 @@ using namespace mph;
 
 extern "C" int mph_config_sizeof(void) { return (int)sizeof(MphConfig); }
 
+extern "C" int mph_abi_version(void) { return MPH_ABI_VERSION; }
+
 extern "C" int mph_config_default(MphConfig* cfg, int dim, int module)
 {
     if (!cfg || (dim != 2 && dim != 3) || module < 0 || module > MPH_MODULE_NONE) return MPH_ERR_ARG;

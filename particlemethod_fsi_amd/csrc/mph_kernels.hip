@@ -2568,9 +2568,13 @@ __global__ __launch_bounds__(256) void k_dist_early_pack(Soa B, DistLayout* __re
     int o = boff[c * nb + blockIdx.x] + rank;
     for (int w = 0; w < wave; ++w) o += wc[w][c];
     const bool left = c == kBandL || c == kMigL;
-    const int m = left ? ml : mr;
+    // the stride is clamped to the capacity like k_dist_pack's (the header keeps the true counts,
+    // so a receiver skips an overfull message): an overflow is MPH_ERR_CAPACITY, never a write
+    // past the buffer
+    const int cap = left ? cap_l : cap_r;
+    const int m = min(left ? ml : mr, cap);
     const int j = left ? o - sBandL : o - sMigR;
-    if (j >= (left ? cap_l : cap_r)) return;
+    if (j >= m) return;
     double* d = (double*)((left ? buf_l : buf_r) + kMsgHeader);
     int* q = (int*)(d + 6 * (size_t)m);
     d[j] = B.x[p]; d[m + j] = B.y[p]; d[2 * m + j] = B.z[p];

@@ -200,14 +200,29 @@ def read_grid_file(path: str, cfg: MphConfig) -> Particles:
 # generator (generator/generator.cpp): Cuboid primitive + .grid writer
 # ------------------------------------------------------------------------------------------
 
+# generator.cpp's shapes, in the order genparticle visits them (654-826): every Cuboid block of
+# the .boid file first, then every Cuboid2, Cyboid, Cyboid2, Recboid, Recboid2 block
+SHAPES = ("cuboid", "cuboid2", "cyboid", "cyboid2", "recboid", "recboid2")
+
+
 @dataclass
 class Cuboid:
-    """One ``StartCuboid ... EndCuboid`` block of a ``.boid`` file (generator.cpp:22-30)."""
+    """One ``Start<Shape> ... End<Shape>`` block of a ``.boid`` file (generator.cpp:22-78).
+
+    kind: "cuboid" (lattice from lower + 0.5 s to upper - 0.49 s on every axis, 663-665),
+    "cuboid2" (x and y from lower + 0.01 s to upper, z as cuboid; 689-691), "cyboid" (the cuboid
+    lattice inside the spherical shell ratio * w0/2 < r <= w0/2 about the centre; 714-725),
+    "cyboid2" (the cuboid2 lattice inside the xy ring of generator.cpp:752), "recboid" (the cuboid2
+    lattice where tan(angle) > y/x; 775-784), "recboid2" (the cuboid2 lattice rotated about z by
+    angle; 807-811).  Angles in degrees, converted with 3.1415/180 like the generator."""
     type: int
     lower: tuple
     upper: tuple
     space: float
     velocity: tuple = (0.0, 0.0, 0.0)
+    kind: str = "cuboid"
+    ratio: float = 0.0
+    angle: float = 0.0
 
 
 def _c_round(x: float) -> int:
@@ -215,17 +230,26 @@ def _c_round(x: float) -> int:
     return int(math.floor(x + 0.5)) if x >= 0 else -int(math.floor(-x + 0.5))
 
 
-def _axis_values(lo: float, hi: float, space: float) -> list[float]:
-    # generator.cpp:659-665 -- accumulate px += spacing from lower + 0.5*spacing
+def _axis_values(lo: float, hi: float, space: float, start: float = 0.5, stop: float = 0.49,
+                 stop_space: float | None = None) -> list[float]:
+    # generator.cpp:659-665 (and the other shapes' loops): count = round(width / space), spacing
+    # = width / count, p accumulated by p += spacing from lower + start * spacing while
+    # p < upper - stop * spacing (Recboid's y loop scales its stop by the x spacing, 776, 808)
     width = hi - lo
     count = _c_round(width / space)
     sp = width / count
+    lim = hi - stop * (sp if stop_space is None else stop_space)
     vals = []
-    p = lo + 0.5 * sp
-    while p < hi - 0.49 * sp:
+    p = lo + start * sp
+    while p < lim:
         vals.append(p)
         p += sp
     return vals
+
+
+def _spacing(lo: float, hi: float, space: float) -> float:
+    width = hi - lo
+    return width / _c_round(width / space)
 
 
 def _e(x: float) -> float:
@@ -233,18 +257,68 @@ def _e(x: float) -> float:
     return float("%e" % x)
 
 
+def _shape_points(cub: Cuboid) -> np.ndarray:
+    """Unrounded positions of one non-cuboid block, in the generator's loop order (x outermost),
+    with its own double arithmetic (no FMA: the generator is built with g++ -g, makefile:8)."""
+    k = cub.kind
+    lo, hi, s = cub.lower, cub.upper, cub.space
+    if k == "cyboid":
+        ax = [_axis_values(lo[d], hi[d], s) for d in range(3)]
+    else:
+        sx = _spacing(lo[0], hi[0], s)
+        ax = [_axis_values(lo[0], hi[0], s, 0.01, 0.0),
+              _axis_values(lo[1], hi[1], s, 0.01, 0.0, stop_space=sx if k.startswith("recboid") else None),
+              _axis_values(lo[2], hi[2], s)]
+    X, Y, Z = np.meshgrid(np.array(ax[0]), np.array(ax[1]), np.array(ax[2]), indexing="ij")
+    px, py, pz = X.ravel(), Y.ravel(), Z.ravel()
+    w = [hi[d] - lo[d] for d in range(3)]
+    if k == "cuboid2":
+        return np.stack([px, py, pz], axis=1)
+    if k == "cyboid":
+        c = [0.5 * (hi[d] + lo[d]) for d in range(3)]
+        x, y, z = px - c[0], py - c[1], pz - c[2]
+        r2 = x * x + y * y + z * z
+        inner = 0.25 * w[0] * w[0] * cub.ratio * cub.ratio
+        outer = 0.25 * w[0] * w[0]
+        keep = (r2 > inner) & (r2 <= outer)
+        return np.stack([px[keep], py[keep], pz[keep]], axis=1)
+    if k == "cyboid2":
+        c = [0.5 * (hi[d] + lo[d]) for d in range(2)]
+        x, y = px - c[0], py - c[1]
+        q = x * x + y * y
+        outer = 0.5 * 0.5 * 0.5 * 0.5 * w[0] * w[0] * w[1] * w[1]
+        inner = outer * cub.ratio * cub.ratio * cub.ratio * cub.ratio
+        keep = (q <= outer) & (q > inner)
+        return np.stack([px[keep], py[keep], pz[keep]], axis=1)
+    a = cub.angle * 3.1415 / 180
+    if k == "recboid":
+        with np.errstate(divide="ignore", invalid="ignore"):
+            keep = math.tan(a) > py / px    # y / 0: +-inf or NaN as in C
+        return np.stack([px[keep], py[keep], pz[keep]], axis=1)
+    if k == "recboid2":
+        ca, sa = math.cos(a), math.sin(a)
+        return np.stack([px * ca - py * sa, px * sa + py * ca, pz], axis=1)
+    raise ValueError("unknown generator shape %r" % k)
+
+
 def generate(cuboids: list[Cuboid]) -> Particles:
-    """``genparticle`` for Cuboid blocks (generator.cpp:654-677), values rounded through the
-    ``%e`` text of ``writefile`` exactly as the solver will read them."""
+    """``genparticle`` (generator.cpp:654-835): every shape kind in the generator's order, values
+    rounded through the ``%e`` text of ``writefile`` exactly as the solver will read them."""
     props, pos, vel = [], [], []
-    for cub in cuboids:
-        ax = [np.array([_e(v) for v in _axis_values(cub.lower[d], cub.upper[d], cub.space)])
-              for d in range(3)]
-        X, Y, Z = np.meshgrid(ax[0], ax[1], ax[2], indexing="ij")
-        p = np.stack([X.ravel(), Y.ravel(), Z.ravel()], axis=1)
-        pos.append(p)
-        props.append(np.full(p.shape[0], cub.type, dtype=np.int32))
-        vel.append(np.tile(np.array([_e(v) for v in cub.velocity]), (p.shape[0], 1)))
+    for kind in SHAPES:
+        for cub in cuboids:
+            if cub.kind != kind:
+                continue
+            if kind == "cuboid":
+                ax = [np.array([_e(v) for v in _axis_values(cub.lower[d], cub.upper[d], cub.space)])
+                      for d in range(3)]
+                X, Y, Z = np.meshgrid(ax[0], ax[1], ax[2], indexing="ij")
+                p = np.stack([X.ravel(), Y.ravel(), Z.ravel()], axis=1)
+            else:
+                p = np.vectorize(_e, otypes=[np.float64])(_shape_points(cub)).reshape(-1, 3)
+            pos.append(p)
+            props.append(np.full(p.shape[0], cub.type, dtype=np.int32))
+            vel.append(np.tile(np.array([_e(v) for v in cub.velocity]), (p.shape[0], 1)))
     P = np.concatenate(pos) if pos else np.zeros((0, 3))
     return Particles(property=np.concatenate(props) if props else np.zeros(0, np.int32),
                      position=np.ascontiguousarray(P), initial_position=P.copy(),
@@ -258,6 +332,18 @@ def generate_window(cuboids: list[Cuboid], axis: int, lo: float, hi: float, dmin
     the original indices of the kept particles (ascending) and the total count.  Cuboid lattices
     are separable, so the window only filters the value list of one axis."""
     span = hi - lo
+    if any(c.kind != "cuboid" for c in cuboids):
+        # the other shapes are not separable: generate them all and keep the window's particles
+        parts = generate(cuboids)
+        a = parts.position[:, axis]
+        u = a - dmin
+        u = u - width * np.floor(u / width) + dmin
+        off = (u - lo) - width * np.floor((u - lo) / width)
+        idx = np.nonzero(off < span)[0] if span < width else np.arange(parts.n)
+        sub = Particles(property=parts.property[idx], position=np.ascontiguousarray(parts.position[idx]),
+                        initial_position=np.ascontiguousarray(parts.initial_position[idx]),
+                        velocity=np.ascontiguousarray(parts.velocity[idx]))
+        return sub, idx.astype(np.int32), parts.n
     props, pos, vel, ids = [], [], [], []
     base = 0
     for cub in cuboids:
@@ -293,6 +379,11 @@ def plane_counts(cuboids: list[Cuboid], axis: int, dmin: float, width: float):
     into the periodic domain [dmin, dmin + width), ascending) and the particles on each -- the
     particle distribution along a slab axis without generating the particles."""
     vals, cnts = [], []
+    if any(c.kind != "cuboid" for c in cuboids):
+        u = generate(cuboids).position[:, axis] - dmin
+        v = u - width * np.floor(u / width) + dmin
+        uv, inv = np.unique(v, return_inverse=True)
+        return uv, np.bincount(inv).astype(np.int64)
     for cub in cuboids:
         ax = [np.array([_e(v) for v in _axis_values(cub.lower[d], cub.upper[d], cub.space)])
               for d in range(3)]
@@ -323,34 +414,81 @@ def format_grid(p: Particles, spacing: float, lower, upper, time: float = 0.0) -
     return "".join(out)
 
 
+# block keywords of each shape (generator.cpp:186-652); every one is required by the generator
+_BOID_KEYS = {
+    "cuboid": ("Spacing", "Type", "RigidType", "Lower", "Upper", "Velocity", "Enthalpy"),
+    "cuboid2": ("Spacing", "Type", "Lower", "Upper", "Velocity", "Enthalpy"),
+    "cyboid": ("Spacing", "Type", "RigidType", "Lower", "Upper", "Velocity", "Enthalpy", "Ratio"),
+    "cyboid2": ("Spacing", "Type", "Lower", "Upper", "Velocity", "Enthalpy", "Ratio"),
+    "recboid": ("Spacing", "Type", "Lower", "Upper", "Velocity", "Enthalpy", "Angle"),
+    "recboid2": ("Spacing", "Type", "Lower", "Upper", "Velocity", "Enthalpy", "Angle"),
+}
+_BOID_START = {"Start" + k[0].upper() + k[1:]: k for k in _BOID_KEYS}
+
+
+class BoidError(ValueError):
+    """A .boid file the reference generator would not read completely (generator.cpp:128-184:
+    it stops at the first malformed block and writes the particles read so far)."""
+
+
 def parse_boid(text: str):
-    """Minimal ``.boid`` parser for Cuboid blocks (generator.cpp:128-184, readCuboid)."""
+    """``.boid`` parser (generator.cpp:128-652, readfile and read<Shape>): the domain lines and
+    every Cuboid/Cuboid2/Cyboid/Cyboid2/Recboid/Recboid2 block, whose keywords are read as a
+    token stream up to the block's End keyword.  Where the reference silently stops (a block with
+    an unknown keyword or a missing one) or skips (an unknown Start* block), this raises BoidError
+    instead of returning a grid with particles missing.  Returns (spacing, lower, upper, blocks)."""
     spacing, lower, upper, cubs = None, None, None, []
-    lines = iter(text.splitlines())
-    for line in lines:
+    lines = text.splitlines()
+    i = 0
+    while i < len(lines):
+        line = lines[i]
+        i += 1
         tok = line.split()
-        if not tok or tok[0].startswith("#"):
+        if not tok or line.startswith("#"):
             continue
-        if tok[0] == "ParticleDistance":
+        key = tok[0]
+        if key == "ParticleDistance":
             spacing = float(tok[1])
-        elif tok[0] == "LowerDomain":
+        elif key == "LowerDomain":
             lower = tuple(float(t) for t in tok[1:4])
-        elif tok[0] == "UpperDomain":
+        elif key == "UpperDomain":
             upper = tuple(float(t) for t in tok[1:4])
-        elif tok[0] == "StartCuboid":
-            c = {"Velocity": (0.0, 0.0, 0.0)}
-            for inner in lines:
-                t2 = inner.split()
-                if not t2:
-                    continue
-                if t2[0] == "EndCuboid":
+        elif key in _BOID_START:
+            kind = _BOID_START[key]
+            end = "End" + key[len("Start"):]
+            # the block body is a whitespace token stream (fscanf "%s"), from the next line on
+            words = []
+            while i < len(lines):
+                w = lines[i].split()
+                i += 1
+                if end in w:
+                    words += w[:w.index(end)]
                     break
-                if t2[0] in ("Lower", "Upper", "Velocity"):
-                    c[t2[0]] = tuple(float(t) for t in t2[1:4])
-                elif t2[0] in ("Spacing",):
-                    c["Spacing"] = float(t2[1])
-                elif t2[0] == "Type":
-                    c["Type"] = int(t2[1])
-            cubs.append(Cuboid(type=c["Type"], lower=c["Lower"], upper=c["Upper"],
-                               space=c["Spacing"], velocity=c["Velocity"]))
+                words += w
+            else:
+                raise BoidError("%s without %s" % (key, end))
+            vals, k = {}, 0
+            n_of = {"Lower": 3, "Upper": 3, "Velocity": 3}
+            while k < len(words):
+                w = words[k]
+                if w not in _BOID_KEYS[kind]:
+                    raise BoidError("%s: no such indication %r (generator.cpp)" % (key, w))
+                m = n_of.get(w, 1)
+                try:
+                    v = [float(t) for t in words[k + 1:k + 1 + m]] if w != "Type" and w != "RigidType" \
+                        else [int(words[k + 1])]
+                except (ValueError, IndexError):
+                    raise BoidError("%s: bad value for %s" % (key, w)) from None
+                if len(v) != m:
+                    raise BoidError("%s: bad value for %s" % (key, w))
+                vals[w] = v
+                k += 1 + m
+            missing = [w for w in _BOID_KEYS[kind] if w not in vals]
+            if missing:
+                raise BoidError("%s: missing %s (the generator would stop reading here)" % (key, ", ".join(missing)))
+            cubs.append(Cuboid(type=vals["Type"][0], lower=tuple(vals["Lower"]), upper=tuple(vals["Upper"]),
+                               space=vals["Spacing"][0], velocity=tuple(vals["Velocity"]), kind=kind,
+                               ratio=vals.get("Ratio", [0.0])[0], angle=vals.get("Angle", [0.0])[0]))
+        elif key.startswith("Start"):
+            raise BoidError("unknown block %r (the generator reads %s)" % (key, ", ".join(_BOID_START)))
     return spacing, lower, upper, cubs

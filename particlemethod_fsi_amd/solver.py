@@ -56,8 +56,10 @@ EXPORTED_SYMBOLS = [
     "mph_config_sizeof", "mph_write_vtk_async", "mph_output_wait", "mph_write_grid_binary",
     "mph_write_vtu_arrays", "mph_write_vtu", "mph_velocity_profile_arrays",
     "mph_set_initial_velocity_profile", "mph_dist_info", "mph_create_slab", "mph_slab_window",
-    "mph_list_formats",
+    "mph_list_formats", "mph_abi_version",
 ]
+
+ABI_VERSION = 3   # MPH_ABI_VERSION of include/mph_gpu.h that these bindings follow
 
 # mph_host_exchange_fn (include/mph_gpu.h): (user, send_l, n, send_r, n, recv_l, n, recv_r, n)
 HOST_EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
@@ -136,6 +138,7 @@ def load_library() -> ctypes.CDLL:
         "mph_structure_init": (ip, [cfgp, ip, vp, vp, vp, vp, vp, vp]),
         "mph_compute_virial": (ip, [vp]),
         "mph_config_sizeof": (ip, []),
+        "mph_abi_version": (ip, []),
         "mph_write_grid_binary": (ip, [ctypes.c_char_p, cfgp, ip, vp, vp, vp, vp]),
         "mph_write_vtk_async": (ip, [vp, ctypes.c_char_p]),
         "mph_write_vtu_arrays": (ip, [ctypes.c_char_p, ip] + [vp] * 10),
@@ -152,6 +155,11 @@ def load_library() -> ctypes.CDLL:
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
+    if L.mph_abi_version() != ABI_VERSION:
+        raise ImportError("%s has C ABI version %d, these bindings expect %d (rebuild the library)"
+                          % (LIB_PATH, L.mph_abi_version(), ABI_VERSION))
+    if L.mph_config_sizeof() != ctypes.sizeof(mphio.MphConfig):
+        raise ImportError("MphConfig layout mismatch between %s and mphio.MphConfig" % LIB_PATH)
     _lib = L
     return L
 
@@ -421,10 +429,11 @@ class MphSolver:
         return int(a[0]), int(a[1])
 
     def dist_info(self) -> dict:
-        """Slab-mode facts (mph_dist_info): communicator size, transport, graph replay, capacities."""
+        """Slab-mode facts (mph_dist_info): slab ranks, RCCL communicator size (0: host-staged),
+        graph replay, capacities."""
         a = np.zeros(8, np.int32)
         _check(self._L.mph_dist_info(self._h, a.ctypes.data), self._h)
-        keys = ["nranks", "rank", "rccl", "graphs", "cap", "cap_send", "cap_recv", "held"]
+        keys = ["nranks", "rank", "rccl_ranks", "graphs", "cap", "cap_send", "cap_recv", "held"]
         return {k: int(v) for k, v in zip(keys, a)}
 
     def compute_virial(self):

@@ -172,3 +172,34 @@ def gpu_rank_worker(rank, world, port, case, axis, nsteps, fields, out_dir, tran
     np.savez(os.path.join(out_dir, "rank%d.npz" % rank), **res)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def gpu_capacity_worker(rank, world, port, case, batches, out_dir):
+    """Slab rank of `case` on cuda:0 (host-staged transport): run the step batches (one mph_step
+    call each), after each one record the message capacities of mph_dist_info, and stop at the
+    first error with its status code; rank r saves rank<r>.npz (caps [batch, 2], code, fields)."""
+    dist = _init(rank, world, port)
+    from particlemethod_fsi_amd import MphSolver, cases
+    from particlemethod_fsi_amd.dist import gloo_slab
+    from particlemethod_fsi_amd.solver import MphError
+    c = cases.get(case)
+    axis = SLAB_AXIS[case]
+    cfg, parts = c.build()
+    caps, code, res = [], 0, {}
+    with MphSolver(cfg, parts, device=0, slab=gloo_slab(rank, world, axis)) as s:
+        info = s.dist_info()
+        caps.append([info["cap_send"], info["cap_recv"]])   # as created
+        try:
+            for k in batches:
+                s.step(k)
+                info = s.dist_info()
+                caps.append([info["cap_send"], info["cap_recv"]])
+            ids = s.owned_ids()
+            res = {"ids": ids, "Position": s.get("Position")[ids], "Velocity": s.get("Velocity")[ids],
+                   "PressureP": s.get("PressureP")[ids], "NeighborCount": s.get("NeighborCount")[ids]}
+        except MphError as e:
+            code = e.code
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), caps=np.array(caps, np.int64).reshape(-1, 2),
+             code=np.array([code]), **res)
+    dist.barrier()
+    dist.destroy_process_group()

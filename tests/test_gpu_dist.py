@@ -166,3 +166,49 @@ def test_slab_early_send_bitwise(tmp_path, case, world, monkeypatch):
         out[mode] = run_slab(case, world, [1, 5, 20], str(tmp_path / ("slab%s.npz" % mode)), local=True)
     for k in out["1"].files:
         assert np.array_equal(out["1"][k], out["0"][k]), k
+
+
+def _run_capacity(tmp_path, tag, case, world, batches):
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    d = tmp_path / tag
+    d.mkdir()
+    ps = [ctx.Process(target=dist_worker.gpu_capacity_worker, args=(r, world, port, case, batches, str(d)))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(300)
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    return [dict(np.load(str(d / ("rank%d.npz" % r)))) for r in range(world)]
+
+
+def test_slab_message_capacity_growth(tmp_path, monkeypatch):
+    """Message capacities grow between capacity checks (every 32 steps, also inside one mph_step
+    call): with no slack (MPH_SLAB_MSG_SLACK=0) the buffers start at 1.25 x the first counts and
+    are re-allocated as the channel's face counts rise; the results are bit-identical to the
+    default slack's, which never grows here."""
+    batches = [40, 9]
+    monkeypatch.setenv("MPH_SLAB_MSG_SLACK", "0")
+    tight = _run_capacity(tmp_path, "tight", "channel3d", 3, batches)
+    monkeypatch.delenv("MPH_SLAB_MSG_SLACK")
+    loose = _run_capacity(tmp_path, "loose", "channel3d", 3, batches)
+    for r in range(3):
+        assert int(tight[r]["code"][0]) == 0 and int(loose[r]["code"][0]) == 0
+        assert tight[r]["caps"].max() < loose[r]["caps"].min()   # no slack: far smaller buffers
+        for f in ("ids", "Position", "Velocity", "PressureP", "NeighborCount"):
+            assert np.array_equal(tight[r][f], loose[r][f]), (r, f)
+    # at least one direction of one rank grew after the first check
+    assert any((t["caps"][-1] > t["caps"][0]).any() for t in tight), [t["caps"].tolist() for t in tight]
+
+
+def test_slab_message_overflow_reported(tmp_path, monkeypatch):
+    """A redistribution message larger than its capacity (MPH_SLAB_MSG_CAP forces 64 particles)
+    ends in MPH_ERR_CAPACITY on the ranks -- the late and the early pack both clamp their writes to
+    the buffer, so there is no fault and the process stays usable."""
+    monkeypatch.setenv("MPH_SLAB_MSG_CAP", "64")
+    res = _run_capacity(tmp_path, "over", "channel3d", 2, [4])
+    assert all(int(r["code"][0]) == -11 for r in res), [int(r["code"][0]) for r in res]

@@ -5,6 +5,7 @@ import gzip
 import hashlib
 import os
 import re
+import sys
 import tempfile
 
 import numpy as np
@@ -269,3 +270,58 @@ def test_generator_tool(tmp_path):
     _, p_b = solver.read_case_files(dp, gb, c.dim, c.module)
     for a, b in ((p_t.property, p_b.property), (p_t.position, p_b.position), (p_t.velocity, p_b.velocity)):
         np.testing.assert_array_equal(a, b)
+
+
+# --- generator shapes (generator.cpp:154-175 parsing, 654-835 lattices) -------------------------
+
+BOID_DIR = os.path.join(ROOT, "tests", "golden", "boid")
+REF_GEN = os.path.join(ROOT, "oracle", "_ref", "mph_reference_generator")
+
+
+@pytest.mark.parametrize("name", ["shapes2d.boid", "shapes3d.boid"])
+def test_generator_shapes_byte_identical(name):
+    """Every shape of the reference generator (Cuboid, Cuboid2, Cyboid, Cyboid2, Recboid,
+    Recboid2; interleaved in the file, emitted grouped by shape like genparticle): the .grid text
+    of mphio equals the reference generator's -- against the committed digest of its output
+    (tests/golden/make_generator_golden.py) and, where it is built here, against a live run."""
+    import json
+    text = open(os.path.join(BOID_DIR, name)).read()
+    spacing, lower, upper, blocks = mphio.parse_boid(text)
+    assert {b.kind for b in blocks} == set(mphio.SHAPES)
+    grid = mphio.format_grid(mphio.generate(blocks), spacing, lower, upper)
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "generator_grids.json")))[name]
+    assert int(grid.splitlines()[1].split()[0]) == gold["n"]
+    assert hashlib.sha256(grid.encode()).hexdigest() == gold["sha256"]
+    if os.path.exists(REF_GEN):
+        sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+        from make_generator_golden import reference_grid
+        assert grid == reference_grid(os.path.join(BOID_DIR, name))
+
+
+def test_generator_shapes_slab_window_and_planes():
+    """Slab-local creation of the non-cuboid shapes: the window's particles and their original
+    indices are those of the full set, and the plane counts add up to it."""
+    _, _, _, blocks = mphio.parse_boid(open(os.path.join(BOID_DIR, "shapes3d.boid")).read())
+    full = mphio.generate(blocks)
+    parts, ids, n = mphio.generate_window(blocks, 2, -0.01, 0.02, -0.1, 0.2)
+    assert n == full.n and len(ids) == parts.n > 0
+    np.testing.assert_array_equal(parts.position, full.position[ids])
+    z = full.position[:, 2]
+    assert parts.n == int(((z >= -0.01) & (z < 0.02)).sum())
+    v, c = mphio.plane_counts(blocks, 2, -0.1, 0.2)
+    assert int(c.sum()) == full.n and np.all(np.diff(v) > 0)
+
+
+@pytest.mark.parametrize("bad,msg", [
+    ("StartSphere\n Spacing 0.001\nEndSphere\n", "unknown block"),
+    ("StartCuboid\n Spacing 0.001\n Type 1\n RigidType 0\n Lower 0 0 0\n Upper 1 1 1\n Velocity 0 0 0\n"
+     "EndCuboid\n", "missing Enthalpy"),
+    ("StartCyboid2\n Spacing 0.001\n Type 1\n Colour 3\nEndCyboid2\n", "no such indication"),
+    ("StartRecboid\n Spacing 0.001\n", "without EndRecboid"),
+])
+def test_boid_parser_refuses_what_the_generator_would_drop(bad, msg):
+    """The reference generator silently skips an unknown Start* block and stops reading at a
+    malformed one (writing the particles read so far); parse_boid raises instead."""
+    head = "ParticleDistance 0.001\nLowerDomain 0 0 0\nUpperDomain 1 1 1\n"
+    with pytest.raises(mphio.BoidError, match=msg):
+        mphio.parse_boid(head + bad)
