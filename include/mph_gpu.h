@@ -235,6 +235,10 @@ int mph_particle_count(const MphCtx* ctx);
 double mph_time(const MphCtx* ctx);
 /* Derived scalar constants, same slots as oracle/ref_harness.inc ref_scalars (36 doubles).  */
 int mph_get_scalars(const MphCtx* ctx, double* out36);
+/* The output files of the whole problem.  Slab mode: collective calls (every rank at the same
+ * step); each rank's owned particles are gathered on rank 0 (RCCL: one receive per rank; host
+ * transport: along the ring of neighbour exchanges), which writes `path` -- the same bytes as a
+ * single context holding the same state; the other ranks write nothing.                        */
 int mph_write_prof(MphCtx* ctx, const char* path);
 int mph_write_vtk(MphCtx* ctx, const char* path);
 int mph_write_vtu(MphCtx* ctx, const char* path);   /* mph_write_vtu_arrays of the current state */
@@ -255,7 +259,8 @@ void mph_destroy(MphCtx* ctx);
  * pressure (PressureP, PressureA), viscous and diffuse-interface pair forces over the step's
  * neighbour list at the post-step positions and velocities, and VirialPressureAtParticle
  * = -tr/dim.  Results are read with mph_get(MPH_FIELD_VIRIAL_STRESS / _PRESSURE); zeros until
- * the first call.  Single-context mode only (slab mode: MPH_ERR_UNSUPPORTED).             */
+ * the first call.  Slab mode: collective; every rank computes its owned particles, after one halo
+ * exchange of the ghosts' post-step positions and velocities.                               */
 int mph_compute_virial(MphCtx* ctx);
 
 /* ---- measurement ---------------------------------------------------------------------------- */
@@ -272,7 +277,8 @@ int mph_neighbor_stats(MphCtx* ctx, double* mean, int* max);
 
 /* The reference runs one process over all particles (OpenMP/OpenACC, main.cpp:597-686); it has
  * no domain decomposition.  These entry points add one: the periodic domain is cut into
- * `nranks` equal slabs along `axis`; each rank owns the particles inside its slab, mirrors the
+ * `nranks` slabs along `axis` (equal widths, or the caller's cuts: MphSlabOptions.cuts); each rank
+ * owns the particles inside its slab, mirrors the
  * ones within one cutoff of a face to that neighbour as ghosts, and hands particles that crossed
  * a face to the neighbour at the start of the next step.  Per step: one exchange of
  * (x, v, type, id) for migrants + ghosts before the cell sort, one of the pass-A values

@@ -139,6 +139,11 @@ int dist_alloc(MphCtx* c);                                               // exch
 int dist_init(MphCtx* c);                                                // first exchange + init sums
 int dist_step(MphCtx* c, int nsteps, Profiler* prof = nullptr);
 int dist_sync(MphCtx* c);                // host mirror of the layout + error flags after a batch
+// output in slab mode (collective): every rank's owned records gathered on rank 0, which writes
+// `path` with the single-context writers (kind: kOut*); the virial over the owned particles
+constexpr int kOutProf = 0, kOutVtk = 1, kOutVtu = 2, kOutVtkAsync = 3;
+int dist_write_output(MphCtx* c, const char* path, int kind);
+int dist_virial(MphCtx* c);
 void dist_free(MphCtx* c);
 
 }  // namespace mph

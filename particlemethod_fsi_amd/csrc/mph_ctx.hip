@@ -59,6 +59,7 @@ int ctx_state_status(MphCtx* c, const DevState& hs)
 void ctx_fill_launch(MphCtx* c)
 {
     Launch& L = c->L;
+    set_uniforms(c->P);
     L.P = &c->P;
     L.T = c->dT;
     L.st = c->dst;
@@ -74,6 +75,9 @@ void ctx_fill_launch(MphCtx* c)
     const char* l16 = std::getenv("MPH_LIST16");
     const bool compact = l16 && *l16 ? std::string(l16) != "0" : kListCompact;
     L.lhdr = compact && pass_a_equal_radii(c->P) ? c->list_hdr : nullptr;
+    // the fused search + pass A (k_search_pass_a) unless MPH_FUSED=0 at creation (A/B, tests)
+    const char* fu = std::getenv("MPH_FUSED");
+    L.fused = fu && *fu ? fu[0] != '0' : kFusedDefault;
     L.pres = c->pres; L.gx = c->gx; L.gy = c->gy; L.gz = c->gz; L.pa = c->pa;
     L.force = c->force; L.acc = c->acc; L.fpart = c->fpart; L.rec = c->rec;
     L.dens_a = c->dens_a; L.vstrain = c->vstrain; L.divp = c->divp;
@@ -105,14 +109,13 @@ void fill_launch(MphCtx* c) { ctx_fill_launch(c); }
 void enqueue_step(const Launch& L, bool last)
 {
     launch_sort(L, 1);
-    launch_neighbors(L);
     if (last) {
-        launch_pass_a(L);
+        launch_search_pass_a(L);
     } else {
         Launch La = L;
         La.dens_a = La.vstrain = La.divp = nullptr;
         if (!L.P->surface) La.gx = La.gy = La.gz = La.pa = nullptr;
-        launch_pass_a(La);
+        launch_search_pass_a(La);
     }
     if (last) {
         launch_pass_b(L);
@@ -296,6 +299,7 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
             c->P.perm = forced ? pv[0] - '0' : choose_cell_order(c->h, n, pos, rc);
         int r = choose_grid(c->h, cfg->dim, rc, kContigReach, c->P.gc, c->P.ginv, err, c->P.perm);
         if (r != MPH_OK) return fail(c, r, err);
+        set_uniforms(c->P);
     }
     // interior box for the wave-uniform fast minimum image (k_neighbors / passes): >= 3 cells
     // (+1e-9 relative margin) from every periodic face; needs > 12 cells on every active axis
@@ -536,8 +540,7 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     } else {
         // initialisation sums, main.cpp:565-568 (calculateNeighbor, DensityA, GravityCenter, DensityP)
         launch_sort(c->L, 0);
-        launch_neighbors(c->L);
-        launch_pass_a(c->L);
+        launch_search_pass_a(c->L);
     }
     HIP_OK(c, hipGetLastError());
     HIP_OK(c, hipStreamSynchronize(c->stream));
@@ -715,13 +718,14 @@ int mph_get(MphCtx* c, int field, void* out)
 int mph_compute_virial(MphCtx* c)
 {
     if (!c) return MPH_ERR_ARG;
-    if (c->dist) return fail(c, MPH_ERR_UNSUPPORTED, "mph_compute_virial: single-context mode only");
     HIP_OK(c, hipSetDevice(c->device));
     if (!c->vir) {
-        const size_t cap = (size_t)std::max(c->n, 1);
+        // slab mode: the array capacity (c->P.n), the held count changes every step
+        const size_t cap = (size_t)std::max(c->dist ? c->P.n : c->n, 1);
         CK(dalloc(c, &c->vir, 9 * cap));
         CK(dalloc(c, &c->vpres, cap));
     }
+    if (c->dist) return dist_virial(c);
     // after a step the integrated state B is in A (list) order; before the first step A is current
     launch_virial(c->L, c->stepped ? c->B : c->A, c->vir, c->vpres);
     HIP_OK(c, hipGetLastError());
@@ -776,7 +780,7 @@ int mph_set_initial_velocity_profile(MphCtx* c)
 int mph_write_prof(MphCtx* c, const char* path)
 {
     if (!c || !path) return MPH_ERR_ARG;
-    if (c->dist) return fail(c, MPH_ERR_UNSUPPORTED, "slab mode: gather the owned entries (mph_get) and use mph_write_prof_arrays");
+    if (c->dist) return dist_write_output(c, path, kOutProf);   // collective; rank 0 writes
     const int n = c->n_glob;
     std::vector<double> pos(3 * (size_t)n), vel(3 * (size_t)n);
     CK(mph_get(c, MPH_FIELD_POSITION, pos.data()));
@@ -788,7 +792,7 @@ int mph_write_prof(MphCtx* c, const char* path)
 static int write_vtk_any(MphCtx* c, const char* path, bool xml)
 {
     if (!c || !path) return MPH_ERR_ARG;
-    if (c->dist) return fail(c, MPH_ERR_UNSUPPORTED, "slab mode: gather the owned entries (mph_get) and use mph_write_vtk_arrays");
+    if (c->dist) return dist_write_output(c, path, xml ? kOutVtu : kOutVtk);   // collective; rank 0 writes
     const size_t n = (size_t)c->n_glob;
     std::vector<double> pos(3 * n), vel(3 * n), acc(3 * n), force(3 * n), stress(9 * n), strain(9 * n);
     std::vector<int> isnc(n), nc(n);
@@ -822,8 +826,8 @@ int mph_output_wait(MphCtx* c)
 int mph_write_vtk_async(MphCtx* c, const char* path)
 {
     if (!c || !path) return MPH_ERR_ARG;
-    if (c->dist) return fail(c, MPH_ERR_UNSUPPORTED, "slab mode: gather the owned entries (mph_get) and use mph_write_vtk_arrays");
     CK(mph_output_wait(c));   // at most one file in flight
+    if (c->dist) return dist_write_output(c, path, kOutVtkAsync);   // collective; rank 0 formats and writes
     struct Snap {
         std::string path;
         std::vector<double> pos, pos0, vel, acc, force, stress, strain;

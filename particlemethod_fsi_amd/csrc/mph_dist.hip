@@ -46,6 +46,8 @@
 #include <cstddef>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -349,13 +351,13 @@ HaloFields halo_fields(MphCtx* c)
 
 // Step 5: the pass-A values of every neighbour's ghosts (ranges from the device layout, fixed
 // message capacities: to/from the left cap_sl + cap_rl particles, to/from the right cap_sr + cap_rr).
-int halo_exchange(MphCtx* c, Profiler* prof, hipStream_t stream)
+int halo_exchange(MphCtx* c, Profiler* prof, hipStream_t stream, const HaloFields* fields = nullptr)
 {
     MphDist& D = *c->dist;
     Launch L = c->L;
     L.prof = prof;
     L.stream = stream;
-    const HaloFields F = halo_fields(c);
+    const HaloFields F = fields ? *fields : halo_fields(c);
     const int capl = D.cap_sl + D.cap_rl, capr = D.cap_sr + D.cap_rr;
     double* sl = (double*)D.send_l;
     double* sr = (double*)D.send_r;
@@ -634,8 +636,7 @@ int dist_init(MphCtx* c)
     // on owned + ghosts (no motion, no time advance)
     MPH_CK(redistribute(c, false, true, nullptr));
     sort_local(c, 0, nullptr);
-    launch_neighbors(c->L);
-    launch_pass_a(c->L);
+    launch_search_pass_a(c->L);
     MPH_CK(dist_sync(c));
     // the integrated-state set B starts as the sorted local set (owned + ghosts, ids signed)
     MPH_CK(copy_soa(c, c->B, c->A, c->n));
@@ -656,8 +657,7 @@ int dist_enqueue_step(MphCtx* c, Profiler* prof, bool early_in, bool early_out)
     L.wface = D.wface;
     MPH_CK(redistribute(c, true, false, prof, early_in));
     sort_local(c, 2, prof);
-    launch_neighbors(L);
-    launch_pass_a(L);
+    launch_search_pass_a(L);
     if (early_out) {
         // halo first (the face waves need it), the face waves, the messages of the next step on
         // the second stream, and the interior waves meanwhile
@@ -756,6 +756,274 @@ int dist_step_batch(MphCtx* c, int nsteps, Profiler* prof)
     for (int k = 0; k < nsteps; ++k) c->time += c->cfg.dt;
     c->stepped = true;
     return dist_sync(c);
+}
+
+// ---- output in slab mode (collective calls: every rank enters them at the same step) ---------
+//
+// The reference writes .prof before a step, runs calculateVirialStressAtParticle and writes .vtk
+// after one (main.cpp:583-589, 672-683, 957-1189), always for the whole problem.  Here every rank
+// packs the records of the particles it owns, rank 0 gathers them (RCCL: one receive from every
+// rank; host transport: forwarded along the ring of neighbour exchanges), restores the original
+// order and writes the file with the single-context writers, so the bytes are the reference's.
+
+// rank 0 receives the concatenation of every rank's bytes in rank order; the others get nothing
+int dist_gather_root(MphCtx* c, const std::vector<char>& mine, std::vector<char>& all)
+{
+    MphDist& D = *c->dist;
+    const int R = D.nranks;
+    all.clear();
+    if (R == 1) {
+        all = mine;
+        return MPH_OK;
+    }
+    if (D.rccl) {
+        struct DevBuf {
+            void* p = nullptr;
+            ~DevBuf() { if (p) (void)hipFree(p); }
+        } dsz, dsend, drecv;
+        MPH_HIP_OK(c, hipMalloc(&dsz.p, sizeof(long long) * R));
+        long long* sz = (long long*)dsz.p;
+        const long long my = (long long)mine.size();
+        MPH_HIP_OK(c, hipMemcpyAsync(sz + D.rank, &my, sizeof(my), hipMemcpyHostToDevice, c->stream));
+        RCCL_OK(c, ncclAllGather(sz + D.rank, sz, 1, ncclInt64, (ncclComm_t)D.comm, c->stream));
+        std::vector<long long> h(R);
+        MPH_HIP_OK(c, hipMemcpyAsync(h.data(), sz, sizeof(long long) * R, hipMemcpyDeviceToHost, c->stream));
+        MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
+        long long total = 0;
+        std::vector<long long> off(R);
+        for (int r = 0; r < R; ++r) { off[r] = total; total += h[r]; }
+        if (D.rank != 0 && my > 0) {
+            MPH_HIP_OK(c, hipMalloc(&dsend.p, (size_t)my));
+            MPH_HIP_OK(c, hipMemcpy(dsend.p, mine.data(), (size_t)my, hipMemcpyHostToDevice));
+        }
+        if (D.rank == 0 && total > my) MPH_HIP_OK(c, hipMalloc(&drecv.p, (size_t)(total - my)));
+        RCCL_OK(c, ncclGroupStart());
+        for (int r = 1; r < R; ++r) {
+            if (!h[r]) continue;
+            if (D.rank == 0)
+                RCCL_OK(c, ncclRecv((char*)drecv.p + (off[r] - my), (size_t)h[r], ncclChar, r, (ncclComm_t)D.comm,
+                                    c->stream));
+            else if (D.rank == r)
+                RCCL_OK(c, ncclSend(dsend.p, (size_t)h[r], ncclChar, 0, (ncclComm_t)D.comm, c->stream));
+        }
+        RCCL_OK(c, ncclGroupEnd());
+        MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
+        if (D.rank == 0) {
+            all.resize((size_t)total);
+            std::memcpy(all.data(), mine.data(), mine.size());
+            if (total > my)
+                MPH_HIP_OK(c, hipMemcpy(all.data() + my, drecv.p, (size_t)(total - my), hipMemcpyDeviceToHost));
+        }
+        return MPH_OK;
+    }
+    // host transport: R - 1 rounds along the ring; in round k every rank passes to its left
+    // neighbour what it received in round k - 1 (first its own bytes), so rank 0 receives the
+    // bytes of rank k in round k
+    std::vector<char> carry = D.rank == 0 ? std::vector<char>() : mine;
+    if (D.rank == 0) all = mine;
+    for (int round = 1; round < R; ++round) {
+        long long so = (long long)carry.size(), si = 0;
+        if (D.host_fn(D.host_user, &so, sizeof(so), nullptr, 0, nullptr, 0, &si, sizeof(si)) != 0)
+            return ctx_fail(c, MPH_ERR_TRANSPORT, "host exchange callback failed (output gather sizes)");
+        std::vector<char> in((size_t)si);
+        if (D.host_fn(D.host_user, carry.data(), (size_t)so, nullptr, 0, nullptr, 0, in.data(), (size_t)si) != 0)
+            return ctx_fail(c, MPH_ERR_TRANSPORT, "host exchange callback failed (output gather)");
+        if (D.rank == 0) all.insert(all.end(), in.begin(), in.end());
+        else carry.swap(in);
+    }
+    return MPH_OK;
+}
+
+namespace {
+
+// one owned particle of an output gather (original index, and what the writers print)
+struct OutRec {
+    int id, prop, nc, pad;
+    double pos[3], pos0[3], vel[3], acc[3], force[3];
+};
+// one owned elastic slot: InitialStructureNeighborCount, Stress, Strain
+struct OutSlot {
+    int id, isnc;
+    double S[9], E[9];
+};
+
+template <typename T>
+int fetch(MphCtx* c, const T* d, std::vector<T>& h, size_t count)
+{
+    h.resize(count);
+    if (count) MPH_HIP_OK(c, hipMemcpyAsync(h.data(), d, sizeof(T) * count, hipMemcpyDeviceToHost, c->stream));
+    return MPH_OK;
+}
+
+// the records of the particles (and elastic slots) this rank owns, behind two counts
+int pack_owned(MphCtx* c, std::vector<char>& buf)
+{
+    const int n = c->n;
+    std::vector<int> id, nc;
+    std::vector<double> x, y, z, vx, vy, vz;
+    std::vector<double4> f, a;
+    MPH_CK(fetch(c, (const int*)c->A.id, id, n));
+    MPH_CK(fetch(c, (const int*)c->ncount, nc, n));
+    MPH_CK(fetch(c, (const double*)c->B.x, x, n));
+    MPH_CK(fetch(c, (const double*)c->B.y, y, n));
+    MPH_CK(fetch(c, (const double*)c->B.z, z, n));
+    MPH_CK(fetch(c, (const double*)c->B.vx, vx, n));
+    MPH_CK(fetch(c, (const double*)c->B.vy, vy, n));
+    MPH_CK(fetch(c, (const double*)c->B.vz, vz, n));
+    MPH_CK(fetch(c, (const double4*)c->force, f, n));
+    MPH_CK(fetch(c, (const double4*)c->acc, a, n));
+    const int ns = c->Sd.n_own;
+    std::vector<double> S, E;
+    if (ns) {
+        MPH_CK(fetch(c, (const double*)c->Sd.S, S, 9 * (size_t)ns));
+        MPH_CK(fetch(c, (const double*)c->Sd.E, E, 9 * (size_t)ns));
+    }
+    MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
+    std::vector<OutRec> rec;
+    rec.reserve((size_t)c->dist->n_own);
+    for (int i = 0; i < n; ++i) {
+        if (id[i] < 0) continue;   // a ghost
+        OutRec r{};
+        r.id = id[i];
+        // host index of the static inputs (original order, or the slab-local creation's ids)
+        const size_t k = c->gid.empty() ? (size_t)id[i]
+                                        : (size_t)(std::lower_bound(c->gid.begin(), c->gid.end(), id[i]) - c->gid.begin());
+        if (k >= c->prop.size()) return ctx_fail(c, MPH_ERR_ARG, "slab output: an owned particle without static inputs");
+        r.prop = c->prop[k];
+        r.nc = nc[i];
+        const double p[3] = {x[i], y[i], z[i]}, v[3] = {vx[i], vy[i], vz[i]};
+        const double ac[3] = {a[i].x, a[i].y, a[i].z}, fo[3] = {f[i].x, f[i].y, f[i].z};
+        for (int d = 0; d < 3; ++d) {
+            r.pos[d] = p[d];
+            r.pos0[d] = c->pos0[3 * k + d];
+            r.vel[d] = v[d];
+            r.acc[d] = ac[d];
+            r.force[d] = fo[d];
+        }
+        rec.push_back(r);
+    }
+    std::vector<OutSlot> sl((size_t)ns);
+    for (int s = 0; s < ns; ++s) {
+        sl[s].id = c->sl_orig[s];
+        sl[s].isnc = c->S.count[c->sl_s[s]];
+        std::memcpy(sl[s].S, &S[9 * (size_t)s], sizeof(sl[s].S));
+        std::memcpy(sl[s].E, &E[9 * (size_t)s], sizeof(sl[s].E));
+    }
+    const long long cnt[2] = {(long long)rec.size(), (long long)sl.size()};
+    buf.resize(sizeof(cnt) + sizeof(OutRec) * rec.size() + sizeof(OutSlot) * sl.size());
+    char* o = buf.data();
+    std::memcpy(o, cnt, sizeof(cnt));
+    o += sizeof(cnt);
+    if (!rec.empty()) std::memcpy(o, rec.data(), sizeof(OutRec) * rec.size());
+    o += sizeof(OutRec) * rec.size();
+    if (!sl.empty()) std::memcpy(o, sl.data(), sizeof(OutSlot) * sl.size());
+    return MPH_OK;
+}
+
+// the arrays of the single-context writers, in original order, from every rank's records
+struct OutArrays {
+    std::vector<int> prop, isnc, nc;
+    std::vector<double> pos, pos0, vel, acc, force, stress, strain;
+};
+
+int unpack_all(MphCtx* c, const std::vector<char>& all, int nranks, OutArrays& o)
+{
+    const size_t n = (size_t)c->n_glob;
+    o.prop.assign(n, 0); o.isnc.assign(n, 0); o.nc.assign(n, 0);
+    o.pos.assign(3 * n, 0.0); o.pos0.assign(3 * n, 0.0); o.vel.assign(3 * n, 0.0);
+    o.acc.assign(3 * n, 0.0); o.force.assign(3 * n, 0.0);
+    o.stress.assign(9 * n, 0.0); o.strain.assign(9 * n, 0.0);
+    std::vector<char> seen(n, 0);
+    size_t got = 0;
+    const char* p = all.data();
+    const char* end = p + all.size();
+    for (int r = 0; r < nranks; ++r) {
+        long long cnt[2];
+        if ((size_t)(end - p) < sizeof(cnt)) return ctx_fail(c, MPH_ERR_TRANSPORT, "slab output: truncated gather");
+        std::memcpy(cnt, p, sizeof(cnt));
+        p += sizeof(cnt);
+        if ((size_t)(end - p) < sizeof(OutRec) * cnt[0] + sizeof(OutSlot) * cnt[1])
+            return ctx_fail(c, MPH_ERR_TRANSPORT, "slab output: truncated gather");
+        for (long long k = 0; k < cnt[0]; ++k, p += sizeof(OutRec)) {
+            OutRec q;
+            std::memcpy(&q, p, sizeof(q));
+            if (q.id < 0 || (size_t)q.id >= n || seen[q.id])
+                return ctx_fail(c, MPH_ERR_CAPACITY, "slab output: ownership is not a partition");
+            seen[q.id] = 1;
+            ++got;
+            const size_t i = (size_t)q.id;
+            o.prop[i] = q.prop;
+            o.nc[i] = q.nc;
+            for (int d = 0; d < 3; ++d) {
+                o.pos[3 * i + d] = q.pos[d];
+                o.pos0[3 * i + d] = q.pos0[d];
+                o.vel[3 * i + d] = q.vel[d];
+                o.acc[3 * i + d] = q.acc[d];
+                o.force[3 * i + d] = q.force[d];
+            }
+        }
+        for (long long k = 0; k < cnt[1]; ++k, p += sizeof(OutSlot)) {
+            OutSlot q;
+            std::memcpy(&q, p, sizeof(q));
+            if (q.id < 0 || (size_t)q.id >= n) return ctx_fail(c, MPH_ERR_TRANSPORT, "slab output: bad slot record");
+            const size_t i = (size_t)q.id;
+            o.isnc[i] = q.isnc;
+            std::memcpy(&o.stress[9 * i], q.S, sizeof(q.S));
+            std::memcpy(&o.strain[9 * i], q.E, sizeof(q.E));
+        }
+    }
+    if (got != n) return ctx_fail(c, MPH_ERR_CAPACITY, "slab output: " + std::to_string(n - got) + " particles owned by no rank");
+    return MPH_OK;
+}
+
+}  // namespace
+
+int dist_write_output(MphCtx* c, const char* path, int kind)
+{
+    MphDist& D = *c->dist;
+    std::vector<char> mine, all;
+    MPH_CK(pack_owned(c, mine));
+    MPH_CK(dist_gather_root(c, mine, all));
+    mine.clear();
+    mine.shrink_to_fit();
+    if (D.rank != 0) return MPH_OK;
+    auto o = std::make_shared<OutArrays>();
+    MPH_CK(unpack_all(c, all, D.nranks, *o));
+    all.clear();
+    all.shrink_to_fit();
+    const int n = c->n_glob;
+    if (kind == kOutProf)
+        return mph_write_prof_arrays(path, &c->cfg, c->time, n, o->prop.data(), o->pos.data(), o->pos0.data(),
+                                     o->vel.data());
+    auto write = [o, n](const std::string& pth, bool xml) {
+        auto writer = xml ? mph_write_vtu_arrays : mph_write_vtk_arrays;
+        return writer(pth.c_str(), n, o->prop.data(), o->pos.data(), o->pos0.data(), o->vel.data(), o->acc.data(),
+                      o->force.data(), o->stress.data(), o->strain.data(), o->isnc.data(), o->nc.data());
+    };
+    if (kind == kOutVtkAsync) {
+        const std::string pth = path;
+        c->out_thread = std::thread([c, write, pth] { c->out_rc = write(pth, false); });
+        return MPH_OK;
+    }
+    const int rc = write(path, kind == kOutVtu);
+    return rc ? ctx_fail(c, rc, std::string("writing ") + path) : MPH_OK;
+}
+
+// calculateVirialStressAtParticle (main.cpp:3077-3318) in slab mode: the owned particles' sums need
+// their ghost neighbours' post-step positions and velocities, which the owners computed -- one
+// halo exchange of B (the pass-A values the virial reads are the particle's own)
+int dist_virial(MphCtx* c)
+{
+    HaloFields F{};
+    F.nf = 3;
+    F.f[0] = c->B.x; F.f[1] = c->B.y; F.f[2] = c->B.z;
+    MPH_CK(halo_exchange(c, nullptr, c->stream, &F));
+    F.f[0] = c->B.vx; F.f[1] = c->B.vy; F.f[2] = c->B.vz;
+    MPH_CK(halo_exchange(c, nullptr, c->stream, &F));
+    launch_virial(c->L, c->B, c->vir, c->vpres);
+    MPH_HIP_OK(c, hipGetLastError());
+    MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
+    return MPH_OK;
 }
 
 void dist_free(MphCtx* c)

@@ -82,6 +82,7 @@ struct Launch {
     int2* hdr = nullptr;          // per-wave headers of the column-segmented lists (kSegHdr each)
     int* lhdr = nullptr;          // per-wave headers of the compact 16-bit lists (kLhdr each)
     int* wface = nullptr;         // slab mode: face-wavefront flags written by pass B (early send)
+    bool fused = true;            // search + pass A in one kernel (k_search_pass_a; MPH_FUSED=0: two)
     // pass A products (A order): pressure values, gravity centre (GC, PressureA), sums
     double *pres = nullptr, *gx = nullptr, *gy = nullptr, *gz = nullptr, *pa = nullptr;
     double *dens_a = nullptr, *vstrain = nullptr, *divp = nullptr;
@@ -94,6 +95,8 @@ struct Launch {
 void launch_sort(const Launch& L, int mode);   // mode 0 init, 1 step, 2 step (motion done)
 void launch_neighbors(const Launch& L);
 void launch_pass_a(const Launch& L);
+// launch_neighbors + launch_pass_a, fused into one kernel where the list format allows
+void launch_search_pass_a(const Launch& L);
 void launch_pass_b(const Launch& L, int phase = 0);   // phase: 0 all, 1/2 slab inner/near-face
 void launch_structure(const Launch& L);
 // calculateInitialNeighbor + calculateNormalizer of the ns structure slots (x0 in slot order) on

@@ -8,10 +8,14 @@
 //   k_scan_*         exclusive scan of the cell histogram -> cell start offsets (1711-1728)
 //   k_place          scatter particle ids into their cells (unordered) + Time/WallCenter advance
 //   k_rank_scatter   deterministic in-cell rank (by previous sorted index) and particle reorder
-//   k_neighbors      linked-cell search (1743-1810): 5x5(x5) stencil of cells >= rc/2, the
-//                    reference's exact FP64 acceptance test, ELL neighbour list per wavefront
-//   k_pass_a         DensityA (2141), GravityCenter (2174), DensityP (2314), DivergenceP (2343),
-//                    PhysicalCoefficients (2099), pressure values PressureP (2384) / PressureA (2218)
+//   k_search_pass_a  linked-cell search (1743-1810): 7x7(x5) stencil (2 kReach + 1 columns of cells
+//                    >= rc/3, 2 kContigReach + 1 cells >= rc/2 along the contiguous axis), the
+//                    reference's exact FP64 acceptance test, ELL neighbour list per wavefront; and
+//                    in the same kernel the pass-A sums of every accepted neighbour: DensityA (2141),
+//                    GravityCenter (2174), DensityP (2314), DivergenceP (2343), PhysicalCoefficients
+//                    (2099), pressure values PressureP (2384) / PressureA (2218)
+//   k_neighbors,     the same as two kernels (the compact 16-bit list format, MPH_FUSED=0)
+//   k_pass_a
 //   k_pass_b         PressureP force (2394), PressureA force (2225), DiffuseInterface (2261),
 //                    ViscosityV (2478), InterfaceForce (2427), Gravity (2917), Acceleration (2938),
 //                    Convection (1892)
@@ -707,7 +711,7 @@ __device__ __forceinline__ void pass_a_term(const DevParams& P, const double* s_
             if (!solid) {
                 const double ratio = s_ratio[ti * kTypes + tj];
                 o.da += ratio * (P.ca * t * omt2);
-                const double w = ratio * (P.cg * omt2) * (P.rg / P.r2g);
+                const double w = ratio * (P.cg * omt2) * P.rg_r2g;
                 o.g0 += q0 * w;
                 o.g1 += q1 * w;
                 o.g2 += q2 * w;
@@ -744,7 +748,7 @@ __device__ __forceinline__ void pass_a_term(const DevParams& P, const double* s_
         }
         if (r2 <= P.rg2) {
             const double omt = 1.0 - r * P.inv_rg;
-            const double w = ratio * (P.cg * omt * omt) * (P.rg / P.r2g);
+            const double w = ratio * (P.cg * omt * omt) * P.rg_r2g;
             o.g0 += q0 * w;
             o.g1 += q1 * w;
             o.g2 += q2 * w;
@@ -757,6 +761,80 @@ __device__ __forceinline__ void pass_a_term(const DevParams& P, const double* s_
             o.v2 += c * q2;
         }
     }
+}
+
+// pass_a_term without control flow, for the fused kernel's mask walk: a lane whose slot is empty
+// (valid false) evaluates the same expressions on zeroed inputs, and every contribution is selected
+// by its radius test instead of branched on.  Divergent branches around the twelve accumulators
+// made the compiler copy them at every merge (160 VGPRs); selects need no copies.  Each sum keeps
+// the form  acc += a * b  of pass_a_term with the selected factor inside, so the contraction and the
+// bits are those of pass_a_term.
+template <bool EQR>
+__device__ __forceinline__ void pass_a_term_sel(const DevParams& P, const double* s_ratio, const double* s_mu,
+                                                int ti, int tj, bool solid, bool valid, double q0, double q1,
+                                                double q2, double dvx, double dvy, double dvz, PassA& o)
+{
+    q0 = valid ? q0 : 0.0;
+    q1 = valid ? q1 : 0.0;
+    q2 = valid ? q2 : 0.0;
+    dvx = valid ? dvx : 0.0;
+    dvy = valid ? dvy : 0.0;
+    dvz = valid ? dvz : 0.0;
+    // an empty slot sits just outside every radius (rc2_hi > rc2 >= RadiusX^2), finite throughout
+    const double r2 = valid ? r2_exact(q0, q1, q2) : P.rc2_hi;
+    double r, ir;
+    rsqrt_pair(r2, r, ir);
+    const double dot = dvx * q0 + dvy * q1 + dvz * q2;
+    const bool fluid_i = !solid;
+    const bool sj = !(solid && dev_is_struct(tj));
+    const double ratio = s_ratio[ti * kTypes + tj];
+    const double mu = s_mu[ti * kTypes + tj];   // read unconditionally (no branch around the load)
+    if (EQR) {
+        const bool in = r2 <= P.rp2;
+        const bool strict = r2 < P.rp2;
+        const double t = r * P.inv_rp;
+        const double omt = 1.0 - t;
+        const double omt2 = omt * omt;
+        const double u = P.cdp * omt * ir;
+        o.vs += P.cp * (in ? omt2 : 0.0);
+        o.dv -= dot * (in ? u : 0.0);
+        const double c = (strict && sj) ? u * P.vol : 0.0;
+        o.s0 += c * q0;
+        o.s1 += c * q1;
+        o.s2 += c * q2;
+        const bool fin = in && fluid_i;
+        o.da += ratio * (fin ? P.ca * t * omt2 : 0.0);
+        const double w = fin ? ratio * (P.cg * omt2) * P.rg_r2g : 0.0;
+        o.g0 += q0 * w;
+        o.g1 += q1 * w;
+        o.g2 += q2 * w;
+        const double cv = (strict && fluid_i) ? mu * omt * dot * (ir * ir * ir) : 0.0;
+        o.v0 += cv * q0;
+        o.v1 += cv * q1;
+        o.v2 += cv * q2;
+        return;
+    }
+    const bool inp = r2 <= P.rp2;
+    const double omtp = 1.0 - r * P.inv_rp;
+    const double u = P.cdp * omtp * ir;
+    o.vs += P.cp * (inp ? omtp : 0.0) * omtp;
+    o.dv -= dot * (inp ? u : 0.0);
+    const double c = (r2 < P.rp2 && sj) ? u * P.vol : 0.0;
+    o.s0 += c * q0;
+    o.s1 += c * q1;
+    o.s2 += c * q2;
+    const double ta = r * P.inv_ra;
+    const double omta = 1.0 - ta;
+    o.da += ratio * ((fluid_i && r2 <= P.ra2) ? P.ca * ta * omta * omta : 0.0);
+    const double omtg = 1.0 - r * P.inv_rg;
+    const double w = (fluid_i && r2 <= P.rg2) ? ratio * (P.cg * omtg * omtg) * P.rg_r2g : 0.0;
+    o.g0 += q0 * w;
+    o.g1 += q1 * w;
+    o.g2 += q2 * w;
+    const double cv = (fluid_i && r2 < P.rv2) ? mu * (1.0 - r * P.inv_rv) * dot * (ir * ir * ir) : 0.0;
+    o.v0 += cv * q0;
+    o.v1 += cv * q1;
+    o.v2 += cv * q2;
 }
 
 // Epilogue: PhysicalCoefficients (2099-2137) and the pressure values of calculatePressureP
@@ -849,12 +927,12 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
     // Column trimming: skip the cells of a column (and whole columns) that lie entirely beyond
     // the cutoff.  Conservative (cutoff enlarged by 1e-6 relative, far above the roundoff of the
     // cell geometry), so the accepted set and its order are unchanged.
-    const double rcm2 = P.rc2 * (1.0 + 4e-6);
-    const double cw0 = 1.0 / P.ginv[X::A0], cw1 = 1.0 / P.ginv[X::A1];
+    const double rcm2 = P.rc2_trim;
+    const double cw0 = P.cwid[X::A0], cw1 = P.cwid[X::A1];
     const double uu[3] = {grid_offset(xi, P.corg[0], P.dw[0]), grid_offset(yi, P.corg[1], P.dw[1]),
                           DIM == 3 ? grid_offset(zi, P.corg[2], P.dw[2]) : 0.0};
     const double ua = uu[X::A2];                      // offset along the contiguous axis
-    const double lo2 = P.rc2 * (1.0 - 1e-10), hi2 = P.rc2 * (1.0 + 1e-10);
+    const double lo2 = P.rc2_lo, hi2 = P.rc2_hi;
     const double ginva = P.ginv[X::A2];
     for (int col = 0; col < NCOL; ++col) {
         int base;
@@ -982,15 +1060,15 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     double* sz = sx + 2 * (CAP + SB);
     int* st = reinterpret_cast<int*>(sx + 3 * (CAP + SB));
     const int lane = threadIdx.x & 63;
-    const double lo2 = P.rc2 * (1.0 - 1e-10), hi2 = P.rc2 * (1.0 + 1e-10);
+    const double lo2 = P.rc2_lo, hi2 = P.rc2_hi;
     using X = CellAxes<DIM, PERM>;
     int cnt = 0;
     constexpr int NCOL = DIM == 3 ? kGroups * kGroups : kGroups;
     static_assert(!SEG || NCOL <= kSegCols, "the segmented list header has 25 columns (MPH_R=2)");
     const int cc[3] = {cx, cy, cz};
     const int cca = cc[X::A2];
-    const double rcm2 = P.rc2 * (1.0 + 4e-6);
-    const double cw0 = 1.0 / P.ginv[X::A0], cw1 = 1.0 / P.ginv[X::A1];
+    const double rcm2 = P.rc2_trim;
+    const double cw0 = P.cwid[X::A0], cw1 = P.cwid[X::A1];
     const double uu[3] = {grid_offset(xi, P.corg[0], P.dw[0]), grid_offset(yi, P.corg[1], P.dw[1]),
                           DIM == 3 ? grid_offset(zi, P.corg[2], P.dw[2]) : 0.0};
     const double ua = uu[X::A2];
@@ -1566,6 +1644,281 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
     pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
 }
 
+// ------------------------------------------------------------- fused search + pass A -------
+
+// calculateNeighbor (main.cpp:1743-1810) and the pass-A sums of the same step (DensityA 2141,
+// GravityCenter 2174, DensityP 2314, DivergenceP 2343, PhysicalCoefficients 2099, the pressure
+// values 2384 / 2218, the P_i half of the pressure force 2394 and the viscous force 2478) in one
+// kernel.  The interior search already stages every stencil column's window of the wave in LDS;
+// here it stages the whole {x, y, z, vx, vy, vz, type} of the window, so a neighbour accepted by
+// the exact test is summed at once from LDS -- pass A's list read and its per-lane gathers of the
+// 48-byte records from L1/L2 (its bound) disappear.  The ELL row is still
+// written for pass B.  The lanes of a wave accept in lockstep on lattice-line cells, but not in a
+// disordered flow, so the sums do not run under the acceptance branch: per column every lane
+// collects its accepted candidates in a 64-bit mask over its own candidate range, then the wave
+// walks the set bits (one per lane per iteration), which costs max over lanes of a column's count
+// instead of the column's candidate count.  Same neighbours in the same order, same FP64
+// expressions: every field is bit-identical to the separate k_neighbors + k_pass_a.
+#ifndef MPH_FUSED
+#define MPH_FUSED 1      // default: fused (MPH_FUSED=0 at run time or build: separate kernels)
+#endif
+#ifndef MPH_FCAP
+#define MPH_FCAP 128     // candidates staged per wave and column (6 + 1 arrays, 52 B each)
+#endif
+#ifndef MPH_FU
+#define MPH_FU 1         // accepted neighbours summed per iteration of the mask walk (2: 56 B/lane of spills at 4 waves)
+#endif
+#ifndef MPH_FUSED_DIAG
+#define MPH_FUSED_DIAG 0 // diagnostic builds: 1 = no periodic-face path, 2 = equal-radii sums only
+#endif
+#ifndef MPH_FUSED_WPE
+#define MPH_FUSED_WPE 4  // waves per SIMD (<= 128 VGPRs)
+#endif
+
+struct FusedStage {
+    double x[MPH_FCAP + MPH_SB], y[MPH_FCAP + MPH_SB], z[MPH_FCAP + MPH_SB];
+    double vx[MPH_FCAP + MPH_SB], vy[MPH_FCAP + MPH_SB], vz[MPH_FCAP + MPH_SB];
+    int type[MPH_FCAP + MPH_SB];
+};
+
+// The pass-A sums over the accepted candidates of one lane's chunk: bit b of mask = candidate
+// base + b, read from the staged window (LDS, base = offset in it) or gathered from the 48-byte
+// records (wide window, base = sorted index).  Wave-uniform loop while any lane has bits left.
+template <bool EQR, int U = MPH_FU>
+__device__ __forceinline__ void fused_sum_mask(const DevParams& P, const double* s_ratio, const double* s_mu,
+                                               const Soa& A, const FusedStage& S, bool LDS,
+                                               unsigned long long mask, int base, int ti, bool solid, double xi,
+                                               double yi, double zi, double vxi, double vyi, double vzi, PassA& o)
+{
+    if (MPH_FUSED_DIAG & 4) return;
+    while (__builtin_amdgcn_ballot_w64(mask != 0ull)) {
+        int t[U];
+        bool v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            v[u] = mask != 0ull;
+            const int b = v[u] ? __ffsll((long long)mask) - 1 : 0;
+            mask &= mask - 1ull;   // 0 stays 0
+            t[u] = base + b;
+        }
+        double X[U], Y[U], Z[U], VX[U], VY[U], VZ[U];
+        int TT[U];
+        if (LDS) {   // wave-uniform
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                X[u] = S.x[t[u]]; Y[u] = S.y[t[u]]; Z[u] = S.z[t[u]];
+                VX[u] = S.vx[t[u]]; VY[u] = S.vy[t[u]]; VZ[u] = S.vz[t[u]];
+                TT[u] = S.type[t[u]];
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int j = v[u] ? t[u] : base;
+                const double2* q = A.p6 + 3 * (size_t)j;
+                const double2 a = q[0], b = q[1], c = q[2];
+                X[u] = a.x; Y[u] = a.y; Z[u] = b.x;
+                VX[u] = b.y; VY[u] = c.x; VZ[u] = c.y;
+                TT[u] = A.type[j];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const double q0 = image_exact<true>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
+            const double q1 = image_exact<true>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
+            const double q2 = image_exact<true>(Z[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
+            pass_a_term_sel<EQR>(P, s_ratio, s_mu, ti, v[u] ? TT[u] : 0, solid, v[u], q0, q1, q2, VX[u] - vxi,
+                                 VY[u] - vyi, VZ[u] - vzi, o);
+        }
+    }
+}
+
+// The search of an interior wave (scan_candidates_lds: same column ranges, window, acceptance and
+// list order) with the pass-A sums of every accepted neighbour.  Returns the neighbour count.
+template <int DIM, int PERM, bool EQR, int SB = MPH_SB, int CAP = MPH_FCAP>
+__device__ __forceinline__ int fused_lds(const DevParams& P, const double* s_ratio, const double* s_mu,
+                                         const Soa& A, const int* start, int i, bool act, double xi,
+                                         double yi, double zi, int cx, int cy, int cz, int* out,
+                                         FusedStage& S, int ti, bool solid, double vxi, double vyi,
+                                         double vzi, PassA& o)
+{
+    const int lane = threadIdx.x & 63;
+    const double lo2 = P.rc2_lo, hi2 = P.rc2_hi;
+    using X = CellAxes<DIM, PERM>;
+    int cnt = 0;
+    constexpr int NCOL = DIM == 3 ? kGroups * kGroups : kGroups;
+    const int cc[3] = {cx, cy, cz};
+    const int cca = cc[X::A2];
+    const double rcm2 = P.rc2_trim;
+    const double cw0 = P.cwid[X::A0], cw1 = P.cwid[X::A1];
+    const double uu[3] = {grid_offset(xi, P.corg[0], P.dw[0]), grid_offset(yi, P.corg[1], P.dw[1]),
+                          DIM == 3 ? grid_offset(zi, P.corg[2], P.dw[2]) : 0.0};
+    const double ua = uu[X::A2];
+    const double ginva = P.ginv[X::A2];
+    // per-column candidate range of the lane, as scan_candidates_lds (FP32 bound, rounded outwards)
+    constexpr float kDn = 1.0f - 1.0f / (1 << 20), kUp = 1.0f + 1.0f / (1 << 19);
+    const float rcm2f = (float)rcm2 * kUp;
+    float gx2f = 0.0f;
+    auto col_range = [&](int col, int& jb, int& je) {
+        int base;
+        float d2f;
+        if (DIM == 3) {
+            const int dxc = col / kGroups - kReach, dyc = col % kGroups - kReach;
+            const int c0 = cc[X::A0], c1 = cc[X::A1];
+            if (dyc == -kReach) {
+                const float gx = (float)cell_gap(uu[X::A0], c0, dxc, cw0);
+                gx2f = gx * gx * kDn;
+            }
+            const float gy = (float)cell_gap(uu[X::A1], c1, dyc, cw1);
+            d2f = (gx2f + gy * gy * kDn) * kDn;
+            base = ((c0 + dxc) * P.gc[X::A1] + c1 + dyc) * P.gc[X::A2];
+        } else {
+            const int dxc = col - kReach;
+            const float gx = (float)cell_gap(uu[0], cx, dxc, cw0);
+            d2f = gx * gx * kDn;
+            base = (cx + dxc) * P.gc[1];
+        }
+        jb = 0;
+        je = 0;
+        if (act && d2f <= rcm2f) {
+            const double ra = (double)(__fsqrt_rn(rcm2f - d2f) * kUp);
+            const int lo = (int)fmax(floor((ua - ra) * ginva), (double)(cca - P.sa));
+            const int hi = (int)fmin(floor((ua + ra) * ginva), (double)(cca + P.sa));
+            jb = start[base + lo];
+            je = start[base + hi + 1];
+        }
+    };
+    int nb_jb, nb_je;
+    col_range(0, nb_jb, nb_je);
+    for (int col = 0; col < NCOL; ++col) {
+        const int jb = nb_jb, je = nb_je;
+        if (col + 1 < NCOL) col_range(col + 1, nb_jb, nb_je);
+        const bool any = je > jb;
+        const unsigned long long am = __ballot(any);
+        if (!am) continue;   // wave-uniform: no lane has candidates in this column
+        int mn = __builtin_amdgcn_readlane(jb, __ffsll((long long)am) - 1);
+        int mx = __builtin_amdgcn_readlane(je, 63 - __clzll(am));
+        if (__ballot(any && (jb < mn || je > mx))) {
+            mn = wave_min(any ? jb : 0x7fffffff);
+            mx = wave_max(any ? je : -1);
+        }
+        const int span = mx - mn;
+        const bool staged = span <= CAP;   // wave-uniform
+        if (staged) {
+            for (int t = lane; t < span; t += 64) {
+                const double2* q = A.p6 + 3 * (size_t)(mn + t);
+                const double2 a = q[0], b = q[1], c = q[2];
+                S.x[t] = a.x; S.y[t] = a.y; S.z[t] = b.x;
+                S.vx[t] = b.y; S.vy[t] = c.x; S.vz[t] = c.y;
+                S.type[t] = A.type[mn + t];
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        // the lane's candidates in chunks of 64 (one mask bit each; one chunk unless the lane's
+        // range is longer), each chunk tested, then its accepted candidates summed.  One loop for
+        // staged and wide windows (only the loads differ, under a wave-uniform branch), so the
+        // accumulators flow through a single path
+        for (int c0 = jb; c0 < je; c0 += 64) {
+            const int c1 = min(c0 + 64, je);
+            unsigned long long mask = 0ull;
+            for (int j0 = c0; j0 < c1; j0 += SB) {
+                double xs[SB], ys[SB], zs[SB];
+                if (staged) {
+                    const int k0 = j0 - mn;   // the staging arrays are padded by SB entries
+#pragma unroll
+                    for (int u = 0; u < SB; ++u) {
+                        xs[u] = S.x[k0 + u]; ys[u] = S.y[k0 + u]; zs[u] = S.z[k0 + u];
+                    }
+                } else {
+#pragma unroll
+                    for (int u = 0; u < SB; ++u) {
+                        const int j = j0 + u < c1 ? j0 + u : c1 - 1;
+                        xs[u] = A.x[j]; ys[u] = A.y[j]; zs[u] = A.z[j];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < SB; ++u) {
+                    const int j = j0 + u;
+                    const bool a = accept_interior(P, xs[u] - xi, ys[u] - yi, zs[u] - zi, lo2, hi2) &
+                                   (j < c1) & (j != i);
+                    if (a) {
+                        const int tj = staged ? S.type[j - mn] : A.type[j];
+                        list_store(out + min(cnt, kMaxNeighbor - 1) * kTile, nbr_entry(j, tj));
+                        mask |= 1ull << (j - c0);
+                        ++cnt;
+                    }
+                }
+            }
+            fused_sum_mask<EQR>(P, s_ratio, s_mu, A, S, staged, mask, staged ? c0 - mn : c0, ti, solid, xi, yi, zi,
+                                vxi, vyi, vzi, o);
+        }
+        if (staged) __builtin_amdgcn_wave_barrier();   // every lane done reading before the next staging
+    }
+    return cnt;
+}
+
+template <int DIM, int PERM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MPH_FUSED_WPE))) void k_search_pass_a(
+    DevParams P, const DevTables* __restrict__ T, Soa A, const int* __restrict__ start, int* __restrict__ nbr,
+    int* __restrict__ ncount, DevState* __restrict__ st, PassAOut pout)
+{
+    const int n = dev_n(P);
+    if ((int)blockIdx.x >= live_blocks(n)) return;
+    __shared__ double s_ratio[kTypes * kTypes];
+    __shared__ double s_mu[kTypes * kTypes];
+    __shared__ FusedStage stage[4];
+    if (threadIdx.x < kTypes * kTypes) {
+        s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
+        s_mu[threadIdx.x] = T->mu_ij[threadIdx.x] * (-P.cvis * P.cdv * P.vol);   // pass_a_term's viscous factor
+    }
+    __syncthreads();
+    const int i = xcd_block(blockIdx.x, live_blocks(n)) * blockDim.x + threadIdx.x;
+    const bool live = i < n;
+    const int ii = live ? i : n - 1;
+    const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
+    if (wave_all_ghosts(P, A, live, ii)) {
+        // slab mode: no list, and the ghosts' pass-A values arrive in the halo (which also fills
+        // the .w of the pass-B record; its position part is written here)
+        if (live) {
+            ncount[i] = 0;
+            if (pout.rec) pout.rec[i] = make_double4(xi, yi, zi, 0.0);
+        }
+        return;
+    }
+    const bool ghost = live && P.slab_axis >= 0 && A.id[ii] < 0;
+    if (ghost && pout.rec) pout.rec[i] = make_double4(xi, yi, zi, 0.0);
+    const bool own = live && !ghost;
+    const bool fast = wave_interior(P, own, xi, yi, zi);
+    const int cx = cell_axis(xi, P.corg[0], P.dw[0], P.ginv[0], P.gc[0]);
+    const int cy = cell_axis(yi, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
+    const int cz = DIM == 3 ? cell_axis(zi, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
+    int* out = nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
+    double vxi, vyi, vzi;
+    own_velocity(A, ii, vxi, vyi, vzi);
+    const int ti = A.type[ii];
+    const bool solid = dev_is_struct(ti);
+    PassA o;
+    int cnt = 0;
+    if (fast) {
+        FusedStage& S = stage[threadIdx.x >> 6];
+        cnt = (MPH_FUSED_DIAG & 2) || pass_a_equal_radii(P)
+                  ? fused_lds<DIM, PERM, true>(P, s_ratio, s_mu, A, start, i, own, xi, yi, zi, cx, cy, cz, out, S,
+                                               ti, solid, vxi, vyi, vzi, o)
+                  : fused_lds<DIM, PERM, false>(P, s_ratio, s_mu, A, start, i, own, xi, yi, zi, cx, cy, cz, out, S,
+                                                ti, solid, vxi, vyi, vzi, o);
+    } else if (own && !(MPH_FUSED_DIAG & 1)) {
+        // a wave near a periodic face: the search with per-lane gathers and the general minimum
+        // image, then pass A over the lane's own fresh list row (written by this lane just above)
+        cnt = scan_candidates<DIM, false, PERM>(P, A, start, i, xi, yi, zi, cx, cy, cz, out);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        const NbrList NL = nbr_list(nbr, nullptr, i, nullptr);
+        pass_a_loop<false, false, DIM, false, 2>(P, s_ratio, s_mu, A, NL, min(cnt, kMaxNeighbor), ti, solid, xi, yi,
+                                              zi, vxi, vyi, vzi, o);
+    }
+    if (live) ncount[i] = cnt;
+    if (cnt > kMaxNeighbor) atomicOr(&st->overflow, 1);   // main.cpp:1766-1768
+    if (own) pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
+}
+
 // Displacement u = Mod(x - x0 + W/2, W) - W/2 of calculateElasticDeformationVector (2700-2712),
 // computed once per slot and substep instead of once per pair (same expression, same bits).
 __device__ __forceinline__ double4 struct_disp(const DevParams& P, double4 x, double4 x0)
@@ -1651,7 +2004,7 @@ __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_
                                             double yi, double zi, double gxi, double gyi, double gzi,
                                             double pai, double ai, double& f0, double& f1, double& f2)
 {
-    const double dscale = P.rg / P.r2g * (P.vol / P.dx);
+    const double dscale = P.rg_r2g * (P.vol / P.dx);
     const double cpv = P.cdp * P.vol;
     for (int k0 = 0; k0 < cnt; k0 += U) {
         int jj[U];
@@ -1693,7 +2046,7 @@ __device__ __forceinline__ void pass_b_seg(const DevParams& P, const double* s_r
                                            double& f0, double& f1, double& f2, double4* stage)
 {
     constexpr int NCOL = DIM == 3 ? 25 : 5;
-    const double dscale = P.rg / P.r2g * (P.vol / P.dx);
+    const double dscale = P.rg_r2g * (P.vol / P.dx);
     const double cpv = P.cdp * P.vol;
     const int lane = threadIdx.x & 63;
     int slot = 0;
@@ -1908,14 +2261,15 @@ __global__ __launch_bounds__(256) void k_virial(DevParams P, const DevTables* __
                                                 double* __restrict__ vir, double* __restrict__ vpres)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P.n) return;
+    if (i >= dev_n(P)) return;
+    if (P.slab_axis >= 0 && A.id[i] < 0) return;   // slab mode: a ghost (its owner computes it)
     const int ti = A.type[i];
     const double xi = B.x[i], yi = B.y[i], zi = B.z[i];
     const double vxi = B.vx[i], vyi = B.vy[i], vzi = B.vz[i];
     const double pi = pres[i], pai = pa[i];
     const double gi[3] = {gx[i], gy[i], gz[i]};
     const double a = T->cofa[ti] * P.cofk * P.cofk;
-    const double dscale = P.rg / P.r2g * (P.vol / P.dx);
+    const double dscale = P.rg_r2g * (P.vol / P.dx);
     const double cvis = DIM == 2 ? 8.0 : 10.0;
     double S[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
     const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
@@ -2873,6 +3227,36 @@ void launch_pass_a(const Launch& L)
     else
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T,
                    L.A, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, po);
+}
+
+// calculateNeighbor + the pass-A sums: the fused kernel (k_search_pass_a) when the list is the
+// 32-bit ELL row (not the opt-in compact format) and MPH_FUSED is not 0, else the two kernels
+void launch_search_pass_a(const Launch& L)
+{
+    Profiler* prof = L.prof;
+    const DevParams& P = *L.P;
+    if (P.n == 0) return;
+    if (!L.fused || L.lhdr || MPH_SEG) {
+        launch_neighbors(L);
+        launch_pass_a(L);
+        return;
+    }
+    const PassAOut po = pass_a_out(L);
+#define MPH_FUSED_LAUNCH(D, PERM)                                                                         \
+    MPH_LAUNCH("search_pass_a", L.stream, (k_search_pass_a<D, PERM>), dim3(blocks(P.n, 256)), dim3(256), 0, \
+               L.stream, P, L.T, L.A, L.start, L.nbr, L.ncount, L.st, po)
+    if (P.dim == 3) {
+        switch (P.perm) {
+        case 1: MPH_FUSED_LAUNCH(3, 1); break;
+        case 2: MPH_FUSED_LAUNCH(3, 2); break;
+        case 3: MPH_FUSED_LAUNCH(3, 3); break;
+        case 4: MPH_FUSED_LAUNCH(3, 4); break;
+        default: MPH_FUSED_LAUNCH(3, 0); break;
+        }
+    } else {
+        MPH_FUSED_LAUNCH(2, 0);
+    }
+#undef MPH_FUSED_LAUNCH
 }
 
 static StructHook struct_hook(const Launch& L)

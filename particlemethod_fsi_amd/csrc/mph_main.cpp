@@ -4,10 +4,25 @@
 //     mph_explicit <data> <grid> <prof pattern> <vtk pattern> <log> [nthreads] [device]
 // Same driver semantics as main.cpp:528-700: read files, initialise, write output.vtk, then
 // loop while Time < EndTime + 1e-5*Dt writing the .prof before a step (583-589) and the .vtk
-// after a step (672-683).  Differences: the physics runs on one MI355X through libmph_gpu.so;
+// after a step (672-683).  Differences: the physics runs on MI355X through libmph_gpu.so;
 // the .prof holds the current state (the OpenACC build writes stale host arrays);
 // the timing report is wall time of the step loop, not clock() CPU time.  A <vtk pattern> ending
 // in ".vtu" writes binary VTK XML files instead (mph_write_vtu).
+//
+// Several GPUs: MPH_SLABS=N runs the same case as N slab ranks (include/mph_gpu.h, one process
+// per rank): the process forks N - 1 ranks before any HIP call, rank r takes device
+// (device + r) mod the device count (MPH_SLAB_SHARE_DEVICE=1: all on `device`), the slabs lie
+// along MPH_SLAB_AXIS (default z in 3-D, x in 2-D), the transport is RCCL (rank 0 makes the unique
+// id and hands it to the others through pipes) or, with MPH_SLAB_TRANSPORT=host, neighbour
+// exchanges over socket pairs.  Every output call is collective and rank 0 writes the files the
+// single-GPU run writes, with the same cadence.
+#include <fcntl.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <cerrno>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
@@ -17,12 +32,17 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+
 #include "../../include/mph_gpu.h"
 
 static FILE* g_log = nullptr;
 
+static bool g_quiet = false;   // slab ranks other than 0 report errors only
+
 static void logf(const char* fmt, ...)
 {
+    if (g_quiet) return;
     va_list a, b;
     va_start(a, fmt);
     va_copy(b, a);
@@ -35,8 +55,124 @@ static void logf(const char* fmt, ...)
 
 static void die(MphCtx* c, int rc, const char* what)
 {
+    g_quiet = false;
     logf("error: %s failed (%d): %s\n", what, rc, c ? mph_last_error(c) : "");
     std::exit(1);
+}
+
+// ---- slab ranks: fork, socket-pair ring, RCCL id over pipes ----------------------------------
+
+struct SlabRank {
+    int rank = 0, nranks = 1;
+    int left_fd = -1, right_fd = -1;   // host transport: the ring links to the two neighbours
+    int uid_fd = -1;                   // RCCL: rank > 0 reads the unique id here
+    std::vector<int> uid_out;          // rank 0 writes it to these
+    std::vector<pid_t> children;
+};
+
+static bool write_all(int fd, const void* p, size_t n)
+{
+    const char* c = (const char*)p;
+    while (n) {
+        const ssize_t k = write(fd, c, n);
+        if (k < 0 && errno == EINTR) continue;
+        if (k <= 0) return false;
+        c += k;
+        n -= (size_t)k;
+    }
+    return true;
+}
+
+static bool read_all(int fd, void* p, size_t n)
+{
+    char* c = (char*)p;
+    while (n) {
+        const ssize_t k = read(fd, c, n);
+        if (k < 0 && errno == EINTR) continue;
+        if (k <= 0) return false;
+        c += k;
+        n -= (size_t)k;
+    }
+    return true;
+}
+
+// mph_host_exchange_fn over the two ring sockets: all four transfers progress together (poll), so
+// two neighbours sending large messages to each other cannot block on full socket buffers
+static int socket_exchange(void* user, const void* send_l, size_t bsl, const void* send_r, size_t bsr,
+                           void* recv_l, size_t brl, void* recv_r, size_t brr)
+{
+    const SlabRank& R = *(const SlabRank*)user;
+    const char* so[2] = {(const char*)send_l, (const char*)send_r};
+    char* ri[2] = {(char*)recv_l, (char*)recv_r};
+    size_t sn[2] = {bsl, bsr}, rn[2] = {brl, brr};
+    const int fd[2] = {R.left_fd, R.right_fd};
+    while (sn[0] || sn[1] || rn[0] || rn[1]) {
+        pollfd pf[2];
+        for (int k = 0; k < 2; ++k) {
+            pf[k].fd = fd[k];
+            pf[k].events = (short)((sn[k] ? POLLOUT : 0) | (rn[k] ? POLLIN : 0));
+            pf[k].revents = 0;
+        }
+        if (poll(pf, 2, 600000) <= 0) return 1;   // 10 minutes without progress: a dead peer
+        for (int k = 0; k < 2; ++k) {
+            if (pf[k].revents & (POLLERR | POLLNVAL)) return 1;
+            if (sn[k] && (pf[k].revents & POLLOUT)) {
+                const ssize_t w = send(fd[k], so[k], sn[k], MSG_DONTWAIT | MSG_NOSIGNAL);
+                if (w < 0 && errno != EAGAIN && errno != EINTR) return 1;
+                if (w > 0) { so[k] += w; sn[k] -= (size_t)w; }
+            }
+            if (rn[k] && (pf[k].revents & (POLLIN | POLLHUP))) {
+                const ssize_t r = recv(fd[k], ri[k], rn[k], MSG_DONTWAIT);
+                if (r == 0) return 1;
+                if (r < 0 && errno != EAGAIN && errno != EINTR) return 1;
+                if (r > 0) { ri[k] += r; rn[k] -= (size_t)r; }
+            }
+        }
+    }
+    return 0;
+}
+
+// fork the ranks 1..N-1 (before anything touches the GPU); returns this process's rank
+static int spawn_ranks(SlabRank& R, int n, bool host)
+{
+    R.nranks = n;
+    std::vector<int> link(2 * n, -1);   // ring link k: rank k (right side) <-> rank k+1 (left side)
+    if (host)
+        for (int k = 0; k < n; ++k)
+            if (socketpair(AF_UNIX, SOCK_STREAM, 0, &link[2 * k]) != 0) return -1;
+    std::vector<int> pipes(2 * n, -1);
+    if (!host)
+        for (int r = 1; r < n; ++r)
+            if (pipe(&pipes[2 * r]) != 0) return -1;
+    std::fflush(nullptr);
+    int me = 0;
+    for (int r = 1; r < n; ++r) {
+        const pid_t pid = fork();
+        if (pid < 0) return -1;
+        if (pid == 0) { me = r; R.children.clear(); break; }
+        R.children.push_back(pid);
+    }
+    R.rank = me;
+    if (host) {
+        R.right_fd = link[2 * me];
+        R.left_fd = link[2 * ((me + n - 1) % n) + 1];
+        for (int k = 0; k < 2 * n; ++k)
+            if (link[k] != R.right_fd && link[k] != R.left_fd) close(link[k]);
+    } else {
+        for (int r = 1; r < n; ++r) {
+            if (me == 0) {
+                R.uid_out.push_back(pipes[2 * r + 1]);
+                close(pipes[2 * r]);
+            } else if (r == me) {
+                R.uid_fd = pipes[2 * r];
+                close(pipes[2 * r + 1]);
+            } else {
+                close(pipes[2 * r]);
+                close(pipes[2 * r + 1]);
+            }
+        }
+    }
+    return me;
 }
 
 int main(int argc, char** argv)
@@ -51,7 +187,16 @@ int main(int argc, char** argv)
     if (argc > 5) logname = argv[5];
     // argv[6] is the reference's OpenMP thread count: accepted and ignored
     if (argc > 7) device = std::atoi(argv[7]);
-    g_log = std::fopen(logname.c_str(), "w");
+    SlabRank R;
+    const int nslabs = std::getenv("MPH_SLABS") ? std::atoi(std::getenv("MPH_SLABS")) : 1;
+    const bool host_transport = std::getenv("MPH_SLAB_TRANSPORT") && std::strcmp(std::getenv("MPH_SLAB_TRANSPORT"), "host") == 0;
+    if (nslabs > 1 && spawn_ranks(R, nslabs, host_transport) < 0) {
+        std::fprintf(stderr, "error: could not start %d slab ranks\n", nslabs);
+        return 1;
+    }
+    const bool root = R.rank == 0;
+    g_quiet = !root;
+    if (root) g_log = std::fopen(logname.c_str(), "w");
     {
         time_t t = time(nullptr);
         logf("start reading files at %s\n", ctime(&t));
@@ -80,14 +225,44 @@ int main(int argc, char** argv)
     if (rc) die(nullptr, rc, "reading the grid particles");
     int counts[3] = {0, 0, 0};
     for (int t : prop) counts[t < 2 ? 0 : (t < 4 ? 1 : 2)]++;
-    std::printf("Fluid Particles: %d\nStructure Particles: %d\nWall Particles: %d\n", counts[0], counts[1], counts[2]);
+    if (root)
+        std::printf("Fluid Particles: %d\nStructure Particles: %d\nWall Particles: %d\n", counts[0], counts[1], counts[2]);
     {
         time_t t = time(nullptr);
         logf("start initialization at %s\n", ctime(&t));
     }
     MphCtx* ctx = nullptr;
-    rc = mph_create(&ctx, &cfg, n, prop.data(), pos.data(), pos0.data(), vel.data(), device);
-    if (rc) die(ctx, rc, "mph_create");
+    if (nslabs > 1) {
+        // one slab rank: every rank reads the same files and keeps the particles of its slab
+        MphSlabOptions o{};
+        o.rank = R.rank;
+        o.nranks = nslabs;
+        o.axis = std::getenv("MPH_SLAB_AXIS") ? std::atoi(std::getenv("MPH_SLAB_AXIS")) : (cfg.dim == 3 ? 2 : 0);
+        char uid[128] = {0};
+        if (host_transport) {
+            o.host_fn = socket_exchange;
+            o.host_user = &R;
+        } else {
+            if (root) {
+                rc = mph_dist_unique_id(uid);
+                if (rc) die(nullptr, rc, "mph_dist_unique_id");
+                for (int fd : R.uid_out)
+                    if (!write_all(fd, uid, sizeof(uid))) die(nullptr, MPH_ERR_TRANSPORT, "handing out the RCCL id");
+            } else if (!read_all(R.uid_fd, uid, sizeof(uid))) {
+                die(nullptr, MPH_ERR_TRANSPORT, "receiving the RCCL id");
+            }
+            o.unique_id128 = uid;
+        }
+        if (!(std::getenv("MPH_SLAB_SHARE_DEVICE") && std::atoi(std::getenv("MPH_SLAB_SHARE_DEVICE")))) {
+            int ndev = 0;
+            if (hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0) device = (device + R.rank) % ndev;
+        }
+        rc = mph_create_slab(&ctx, &cfg, n, prop.data(), pos.data(), pos0.data(), vel.data(), device, &o);
+        if (rc) die(ctx, rc, "mph_create_slab");
+    } else {
+        rc = mph_create(&ctx, &cfg, n, prop.data(), pos.data(), pos0.data(), vel.data(), device);
+        if (rc) die(ctx, rc, "mph_create");
+    }
     double sc[36];
     mph_get_scalars(ctx, sc);
     logf("N0a = %e\nN0p = %e\n", sc[0], sc[1]);
@@ -156,5 +331,11 @@ int main(int argc, char** argv)
     if (rc) die(ctx, rc, "writing a .vtk file");
     mph_destroy(ctx);
     if (g_log) std::fclose(g_log);
-    return 0;
+    // rank 0 waits for the other ranks and fails if any did
+    int status = 0;
+    for (pid_t pid : R.children) {
+        int st = 0;
+        if (waitpid(pid, &st, 0) < 0 || !WIFEXITED(st) || WEXITSTATUS(st) != 0) status = 1;
+    }
+    return status;
 }

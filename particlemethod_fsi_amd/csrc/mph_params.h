@@ -47,6 +47,12 @@ constexpr int kHdrFlag = 7;
 #define MPH_LIST_COMPACT (MPH_R == 2)
 #endif
 constexpr bool kListCompact = MPH_LIST_COMPACT;
+// search + pass A fused into one kernel (k_search_pass_a); the compact list
+// format keeps the two kernels
+#ifndef MPH_FUSED_DEFAULT
+#define MPH_FUSED_DEFAULT 1
+#endif
+constexpr bool kFusedDefault = MPH_FUSED_DEFAULT;
 constexpr int kLhdr = 8 + 2 * 64;
 static_assert(kGroups <= kHdrFlag, "group bases overlap the format flag");
 
@@ -121,7 +127,24 @@ struct DevParams {
     double wall_rot[kTypes][3][3];  // initializeWall (main.cpp:1371-1410)
     double wall_omega[kTypes][3];
     double wall_vel[kTypes][3];
+    // Uniform FP64 constants the kernels would otherwise derive per lane (gfx9 has no scalar FP64
+    // ALU: a value computed on the device occupies a VGPR pair for the whole loop it is hoisted
+    // out of; from the kernel arguments it stays in SGPRs).  set_uniforms fills them.
+    double rc2_lo, rc2_hi;   // rc2 (1 - 1e-10), rc2 (1 + 1e-10): the search's exact-test band
+    double rc2_trim;         // rc2 (1 + 4e-6): the column-trimming bound
+    double cwid[3];          // 1 / ginv: GPU cell widths
+    double rg_r2g;           // rg / r2g (GravityCenter, DiffuseInterface)
 };
+
+// Derived uniforms of DevParams (same expressions the kernels used, so the same bits).
+inline void set_uniforms(DevParams& P)
+{
+    P.rc2_lo = P.rc2 * (1.0 - 1e-10);
+    P.rc2_hi = P.rc2 * (1.0 + 1e-10);
+    P.rc2_trim = P.rc2 * (1.0 + 4e-6);
+    for (int d = 0; d < 3; ++d) P.cwid[d] = 1.0 / P.ginv[d];
+    P.rg_r2g = P.rg / P.r2g;
+}
 
 // Mutable per-step device scalars (so a captured hipGraph can replay many steps).
 struct DevState {

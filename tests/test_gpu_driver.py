@@ -144,3 +144,38 @@ def test_driver_matches_reference_executable(tmp_path, case):
     for f in files_ref:
         if f != "output.vtk":
             compare_numeric(os.path.join(dg, f), os.path.join(dr, f))
+
+
+# case -> (MPH_DIM, MPH_MODULE, slab ranks) of the multi-rank driver runs
+SLAB_RUNS = {"dam2d": ("2", "bar", 4), "gate2d_sub": ("2", "dam", 2)}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", sorted(SLAB_RUNS))
+def test_driver_slab_ranks_match_single_gpu(tmp_path, case):
+    """mph_explicit as N slab ranks (MPH_SLABS: forked ranks, host transport over socket pairs,
+    all on the test box's one GPU) writes the files of the single-GPU driver: the same names,
+    output.vtk byte for byte (the initial state), and every .prof / .vtk of the run within the
+    printed precision (compare_numeric) -- the owned records of every rank gathered on rank 0 in
+    original order, the virial over owned particles with the ghosts' post-step state."""
+    dim, module, nslabs = SLAB_RUNS[case]
+    assert os.path.exists(DRIVER), "mph_explicit not built"
+    d1, dn = str(tmp_path / "one"), str(tmp_path / "slabs")
+    os.makedirs(d1)
+    os.makedirs(dn)
+    write_case(d1, case)
+    write_case(dn, case)
+    env = dict(os.environ, MPH_DIM=dim, MPH_MODULE=module)
+    files_one = run(DRIVER, d1, env)
+    files_n = run(DRIVER, dn, dict(env, MPH_SLABS=str(nslabs), MPH_SLAB_TRANSPORT="host", MPH_SLAB_SHARE_DEVICE="1"))
+    assert files_n == files_one and len(files_one) >= 6, files_n
+    identical = 0
+    for f in files_one:
+        a, b = open(os.path.join(dn, f), "rb").read(), open(os.path.join(d1, f), "rb").read()
+        if f == "output.vtk":
+            assert a == b
+        identical += a == b
+        if a != b:
+            compare_numeric(os.path.join(dn, f), os.path.join(d1, f))
+    print("%s: %d of %d files byte-identical" % (case, identical, len(files_one)))
+    assert identical >= 2   # output.vtk and the first .prof at least

@@ -319,3 +319,25 @@ def test_gpu_compact_lists_bitwise_equal_ell(case, monkeypatch):
     for f in fields:
         assert np.array_equal(out["1"][f], out["0"][f]), f
         assert np.array_equal(out["redo"][f], out["0"][f]), f
+
+
+@pytest.mark.parametrize("case,radii", [("box3d", None), ("box3d_st", None), ("gate2d", None), ("dam2d", None),
+                                        ("channel3d", None), ("d1m", None), ("box3d", (2.1, 2.5, 2.3)),
+                                        ("gate3d", (2.5, 2.2, 2.4))])
+def test_gpu_fused_search_pass_a_bitwise(case, radii, monkeypatch):
+    """k_search_pass_a (the default: pass-A sums from the search's LDS-staged window, mask walk,
+    branch-free terms) equals k_neighbors + k_pass_a (MPH_FUSED=0) bit for bit after several steps,
+    in the equal-radii form and, with RadiusRatioA/P/V set apart (radii), in the general form."""
+    cfg, parts = cases.get(case).build()
+    if radii is not None:
+        cfg.radius_ratio_a, cfg.radius_ratio_p, cfg.radius_ratio_v = radii
+    fields = ["Position", "Velocity", "PressureP", "PressureA", "NeighborCount", "Force", "Acceleration",
+              "DensityA", "VolStrainP", "DivergenceP", "GravityCenter"]
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MPH_FUSED", mode)
+        with MphSolver(cfg, parts) as s:
+            s.step(6)
+            out[mode] = {f: s.get(f) for f in fields}
+    for f in fields:
+        assert np.array_equal(out["1"][f], out["0"][f]), (f, float(np.max(np.abs(out["1"][f] - out["0"][f]))))
