@@ -276,6 +276,8 @@ def main():
             units[k] = {"ms": prof[k]["avg_ms"], "bytes": alg_bytes_of(k), "kernels": [k],
                         "per_launch": True, "launches_per_step": prof[k]["launches"] / steps_prof}
     dom = max(units, key=lambda u: units[u]["ms"] * units[u].get("launches_per_step", 1.0))
+    # "gpu_busy" (mph_profile_steps) is the union of the kernel intervals, not a kernel
+    busy_ms = prof.pop("gpu_busy", {}).get("avg_ms")
     step_ms = sum(v["avg_ms"] * v["launches"] for v in prof.values()) / steps_prof
     alg_bytes = units[dom]["bytes"]
     achieved = alg_bytes / (units[dom]["ms"] * 1e-3) / 1e9
@@ -359,6 +361,7 @@ def main():
                  if fp64 else None),
         "kernels_ms": {k: round(v["avg_ms"], 5) for k, v in prof.items()},
         "profiled_step_ms": step_ms,
+        "profiled_gpu_busy_ms": busy_ms,
     }
     if checks is not None:
         out["slab"] = checks

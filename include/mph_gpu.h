@@ -267,7 +267,9 @@ int mph_compute_virial(MphCtx* ctx);
 
 /* Run nsteps with a HIP event pair around every kernel launch (direct launches on the
  * context's stream, no graph) and report per-kernel-kind average duration in milliseconds.
- * names: MPH_PROFILE_MAX slots of 32 chars; returns the number of kernel kinds.              */
+ * names: MPH_PROFILE_MAX slots of 32 chars; returns the number of entries.  The last entry is
+ * "gpu_busy": the union of all kernel intervals per step (launches = nsteps), which is less than
+ * their sum where kernels of two streams overlap (slab mode).                                  */
 #define MPH_PROFILE_MAX 24
 int mph_profile_steps(MphCtx* ctx, int nsteps, double* avg_ms, int* launches, char* names32);
 /* Mean/max neighbour count of the last step (for algorithmic byte/flop accounting).         */

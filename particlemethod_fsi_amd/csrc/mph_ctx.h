@@ -138,7 +138,8 @@ int dist_struct_setup(MphCtx* c, std::vector<int>& lsl, int& n_own);
 int dist_alloc(MphCtx* c);                                               // exchange buffers
 int dist_init(MphCtx* c);                                                // first exchange + init sums
 int dist_step(MphCtx* c, int nsteps, Profiler* prof = nullptr);
-int dist_sync(MphCtx* c);                // host mirror of the layout + error flags after a batch
+// host mirror of the layout + error flags after a batch; grows message capacities past 90 %
+int dist_sync(MphCtx* c, bool grow_ok = true);
 // output in slab mode (collective): every rank's owned records gathered on rank 0, which writes
 // `path` with the single-context writers (kind: kOut*); the virial over the owned particles
 constexpr int kOutProf = 0, kOutVtk = 1, kOutVtu = 2, kOutVtkAsync = 3;

@@ -875,21 +875,37 @@ int mph_profile_steps(MphCtx* c, int nsteps, double* avg_ms, int* launches, char
     }
     std::vector<std::string> order;
     std::map<std::string, std::pair<double, int>> acc;
+    // the kernels' intervals from the first event on, for their union (kernels of the two streams
+    // of a slab step run concurrently, so the sum of their times overstates the GPU time)
+    std::vector<std::pair<float, float>> span;
     for (auto& r : prof.recs) {
-        float ms = 0.0f;
+        float ms = 0.0f, t0 = 0.0f;
         HIP_OK(c, hipEventElapsedTime(&ms, r.a, r.b));
+        HIP_OK(c, hipEventElapsedTime(&t0, prof.recs[0].a, r.a));
+        span.emplace_back(t0, t0 + ms);
         if (!acc.count(r.name)) order.push_back(r.name);
         acc[r.name].first += ms;
         acc[r.name].second += 1;
     }
+    std::sort(span.begin(), span.end());
+    double busy = 0.0, hi = -1e30;
+    for (auto& iv : span) {
+        if (iv.first > hi) { busy += iv.second - iv.first; hi = iv.second; }
+        else if (iv.second > hi) { busy += iv.second - hi; hi = iv.second; }
+    }
     int k = 0;
     for (auto& name : order) {
-        if (k >= MPH_PROFILE_MAX) break;
+        if (k >= MPH_PROFILE_MAX - 1) break;
         avg_ms[k] = acc[name].first / acc[name].second;
         launches[k] = acc[name].second;
         std::snprintf(names32 + 32 * k, 32, "%s", name.c_str());
         ++k;
     }
+    // last entry: "gpu_busy", the union of the kernel intervals per step (launches = steps)
+    avg_ms[k] = busy / nsteps;
+    launches[k] = nsteps;
+    std::snprintf(names32 + 32 * k, 32, "%s", "gpu_busy");
+    ++k;
     DevState hs;
     HIP_OK(c, hipMemcpy(&hs, c->dst, sizeof(DevState), hipMemcpyDeviceToHost));
     CK(ctx_state_status(c, hs));

@@ -216,6 +216,19 @@ int msg_slack()
     }();
     return s;
 }
+int msg_capacity(int c);
+
+// MPH_SLAB_MSG_CAP0_FRAC: the first sizing (mph_create) gives frac x the counts and no slack, so
+// the first capacity check grows them (tests of the growth path)
+int msg_capacity0(int c)
+{
+    static const double frac = [] {
+        const char* e = std::getenv("MPH_SLAB_MSG_CAP0_FRAC");
+        return e ? std::atof(e) : 0.0;
+    }();
+    return frac > 0.0 ? std::max(1, (int)std::ceil(frac * c)) : msg_capacity(c);
+}
+
 int msg_capacity(int c)
 {
     // MPH_SLAB_MSG_CAP: one fixed capacity for every direction (tests of the overflow report)
@@ -269,6 +282,7 @@ int redistribute(MphCtx* c, bool move, bool init, Profiler* prof, bool early_in 
     Launch L = c->L;
     L.prof = prof;
     const int nb = dist_blocks(D.cap);
+    if (early_in) MPH_HIP_OK(c, hipStreamWaitEvent(c->stream, D.ev_s, 0));   // see early_send
     launch_dist_classify(L, D.g, D.cap, D.lay, move ? 1 : 0, D.cls, D.bcnt, early_in ? D.wface : nullptr);
     launch_scan(D.bcnt, kSlabClasses * nb, D.bsum, D.boff, 0, c->stream, prof);
     launch_dist_scatter(L, D.cap, D.lay, D.cls, D.boff, D.C, lay_field<int>(D.lay, offsetof(DistLayout, seg)));
@@ -289,10 +303,10 @@ int redistribute(MphCtx* c, bool move, bool init, Profiler* prof, bool early_in 
         MPH_HIP_OK(c, hipMemcpyAsync(D.hlay, D.lay, sizeof(DistLayout), hipMemcpyDeviceToHost, c->stream));
         MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
         const DistLayout& h = *D.hlay;
-        D.cap_sl = msg_capacity(h.send[0] + h.send[1]);
-        D.cap_sr = msg_capacity(h.send[2] + h.send[3]);
-        D.cap_rl = msg_capacity(h.recv[0] + h.recv[1]);
-        D.cap_rr = msg_capacity(h.recv[2] + h.recv[3]);
+        D.cap_sl = msg_capacity0(h.send[0] + h.send[1]);
+        D.cap_sr = msg_capacity0(h.send[2] + h.send[3]);
+        D.cap_rl = msg_capacity0(h.recv[0] + h.recv[1]);
+        D.cap_rr = msg_capacity0(h.recv[2] + h.recv[3]);
         MPH_CK(msg_alloc(c));
     }
     launch_dist_pack(L, D.C, D.lay, 0, D.cap_sl, D.send_l);
@@ -308,17 +322,20 @@ int redistribute(MphCtx* c, bool move, bool init, Profiler* prof, bool early_in 
 // The next step's redistribution messages, sent from the face wavefronts of this step's pass B
 // on the second stream (joined by the next step's redistribute(early_in)); the same bytes as
 // k_dist_pack would send from C.
-int early_send(MphCtx* c, Profiler* prof)
+int early_send(MphCtx* c, Profiler* prof, hipStream_t stream)
 {
     MphDist& D = *c->dist;
     Launch L = c->L;
     L.prof = prof;
+    L.stream = stream;
     const int nb = dist_blocks(D.cap);
     launch_dist_early_classify(L, D.g, D.cap, D.lay, D.wface, D.cls, D.bcnt);
-    launch_scan(D.bcnt, kSlabClasses * nb, D.bsum, D.boff, 0, c->stream, prof);
+    launch_scan(D.bcnt, kSlabClasses * nb, D.bsum, D.boff, 0, stream, prof);
     launch_dist_early_pack(L, D.cap, D.lay, D.cls, D.boff, D.cap_sl, D.cap_sr, D.send_l, D.send_r);
-    MPH_HIP_OK(c, hipEventRecord(D.ev_s, c->stream));
-    MPH_HIP_OK(c, hipStreamWaitEvent(D.stream2, D.ev_s, 0));
+    // ev_s: the face waves' pass B and these kernels are done (the next step's partition, on the
+    // main stream, waits for it before it reads B and wface); ev_x: the messages have landed
+    MPH_HIP_OK(c, hipEventRecord(D.ev_s, stream));
+    if (stream != D.stream2) MPH_HIP_OK(c, hipStreamWaitEvent(D.stream2, D.ev_s, 0));
     MPH_CK(exchange(c, D.stream2, D.send_l, kMsgHead + kMsgBytes * D.cap_sl, D.send_r,
                     kMsgHead + kMsgBytes * D.cap_sr, D.recv_l, kMsgHead + kMsgBytes * D.cap_rl, D.recv_r,
                     kMsgHead + kMsgBytes * D.cap_rr));
@@ -593,7 +610,7 @@ int dist_alloc(MphCtx* c)
     return MPH_OK;
 }
 
-int dist_sync(MphCtx* c)
+int dist_sync(MphCtx* c, bool grow_ok)
 {
     MphDist& D = *c->dist;
     DevState hs;
@@ -615,7 +632,7 @@ int dist_sync(MphCtx* c)
     // 1.25 c + 4096: every message travels at its capacity (fixed sizes in the graphs)
     int* caps[4] = {&D.cap_sl, &D.cap_sr, &D.cap_rl, &D.cap_rr};
     bool grow = false;
-    for (int k = 0; k < 4; ++k)
+    for (int k = 0; k < 4 && grow_ok; ++k)
         if ((long long)h.hw[k] * 10 > (long long)*caps[k] * 9) {
             *caps[k] = msg_capacity(h.hw[k]);
             grow = true;
@@ -637,11 +654,13 @@ int dist_init(MphCtx* c)
     MPH_CK(redistribute(c, false, true, nullptr));
     sort_local(c, 0, nullptr);
     launch_search_pass_a(c->L);
-    MPH_CK(dist_sync(c));
+    // no capacity growth yet: the first sizing came from these very counts (and a test sizing,
+    // MPH_SLAB_MSG_CAP0_FRAC, is meant to grow at the first check after real steps)
+    MPH_CK(dist_sync(c, false));
     // the integrated-state set B starts as the sorted local set (owned + ghosts, ids signed)
     MPH_CK(copy_soa(c, c->B, c->A, c->n));
     MPH_HIP_OK(c, hipGetLastError());
-    return dist_sync(c);
+    return dist_sync(c, false);
 }
 
 // One slab step on the context's stream (no host synchronisation inside: RCCL transport steps
@@ -658,30 +677,31 @@ int dist_enqueue_step(MphCtx* c, Profiler* prof, bool early_in, bool early_out)
     MPH_CK(redistribute(c, true, false, prof, early_in));
     sort_local(c, 2, prof);
     launch_search_pass_a(L);
-    if (early_out) {
-        // halo first (the face waves need it), the face waves, the messages of the next step on
-        // the second stream, and the interior waves meanwhile
-        MPH_CK(halo_exchange(c, prof, c->stream));
-        launch_pass_b(L, 2);
-        MPH_CK(early_send(c, prof));
-        launch_pass_b(L, 1);
-        return struct_substeps(c, prof);   // none: early sends only without elastic particles
-    }
-    // the pass-A halo travels on stream2 while pass B runs the particles that have no ghost
-    // neighbours; the near-face particles follow once the halo has landed (inner pass B is
-    // enqueued first, so that a host-staged exchange, which blocks the host, also overlaps with it)
     if (!D.overlap) {   // MPH_SLAB_OVERLAP=0: halo first, then one pass B over every particle
         MPH_CK(halo_exchange(c, prof, c->stream));
         launch_pass_b(L, 0);
+        if (early_out) MPH_CK(early_send(c, prof, c->stream));
         return struct_substeps(c, prof);
     }
+    // pass B of the wavefronts without ghost neighbours runs on the main stream while, on the
+    // second stream, the pass-A halo travels and the wavefronts near a face follow as soon as it
+    // has landed: the two pass-B kernels run concurrently, so neither launch's tail idles the GPU
+    // (the interior one is enqueued first, so that a host-staged exchange, which blocks the host,
+    // also overlaps with it).  With the early send the face waves' particles then leave for the
+    // next step's redistribution, still on the second stream.
+    Launch L2 = L;
+    L2.stream = D.stream2;
     MPH_HIP_OK(c, hipEventRecord(D.ev_a, c->stream));
     launch_pass_b(L, 1);
     MPH_HIP_OK(c, hipStreamWaitEvent(D.stream2, D.ev_a, 0));
     MPH_CK(halo_exchange(c, prof, D.stream2));
+    launch_pass_b(L2, 2);
+    if (early_out) {
+        // joined by the next step's redistribute (ev_x); no elastic particles in this mode
+        return early_send(c, prof, D.stream2);
+    }
     MPH_HIP_OK(c, hipEventRecord(D.ev_h, D.stream2));
     MPH_HIP_OK(c, hipStreamWaitEvent(c->stream, D.ev_h, 0));
-    launch_pass_b(L, 2);
     MPH_CK(struct_substeps(c, prof));
     return MPH_OK;
 }

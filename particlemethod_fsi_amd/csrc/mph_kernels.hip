@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -682,15 +683,18 @@ struct PassA {
 
 // One neighbour's contribution to DensityA (2141-2171), GravityCenter (2174-2210), DensityP
 // (2314-2341), DivergenceP (2343-2379), and (FORCE) the P_i half of the pressure force and the
-// viscous force; (dvx, dvy, dvz) = v_j - v_i.
+// viscous force; (dvx, dvy, dvz) = v_j - v_i.  No implicit contraction: every accumulation is an
+// explicit fma, so this branching form and pass_a_term_sel's selecting form (the fused kernel)
+// give the same bits (a deselected fma(a, 0, acc) leaves acc unchanged).
 template <bool FORCE, bool EQR = false>
 __device__ __forceinline__ void pass_a_term(const DevParams& P, const double* s_ratio, const double* s_mu, int ti,
                                             int tj, bool solid, double q0, double q1, double q2, double r2,
                                             double dvx, double dvy, double dvz, PassA& o)
 {
+#pragma clang fp contract(off)
     double r, ir;
     rsqrt_pair(r2, r, ir);
-    const double dot = dvx * q0 + dvy * q1 + dvz * q2;
+    const double dot = fma(dvz, q2, fma(dvy, q1, dvx * q0));
     if (EQR) {
         // RadiusA = RadiusP = RadiusV (pass_a_equal_radii): one cutoff test and one 1 - r/h for
         // all four kernels; same expressions otherwise
@@ -698,28 +702,28 @@ __device__ __forceinline__ void pass_a_term(const DevParams& P, const double* s_
             const double t = r * P.inv_rp;
             const double omt = 1.0 - t;
             const double omt2 = omt * omt;
-            const double u = P.cdp * omt * ir;
-            o.vs += P.cp * omt2;
-            o.dv -= dot * u;
+            const double u = (P.cdp * omt) * ir;
+            o.vs = fma(P.cp, omt2, o.vs);
+            o.dv = fma(-dot, u, o.dv);
             const bool strict = r2 < P.rp2;
             if (FORCE && strict && !(solid && dev_is_struct(tj))) {
                 const double c = u * P.vol;
-                o.s0 += c * q0;
-                o.s1 += c * q1;
-                o.s2 += c * q2;
+                o.s0 = fma(c, q0, o.s0);
+                o.s1 = fma(c, q1, o.s1);
+                o.s2 = fma(c, q2, o.s2);
             }
             if (!solid) {
                 const double ratio = s_ratio[ti * kTypes + tj];
-                o.da += ratio * (P.ca * t * omt2);
-                const double w = ratio * (P.cg * omt2) * P.rg_r2g;
-                o.g0 += q0 * w;
-                o.g1 += q1 * w;
-                o.g2 += q2 * w;
+                o.da = fma(ratio, (P.ca * t) * omt2, o.da);
+                const double w = (ratio * (P.cg * omt2)) * P.rg_r2g;
+                o.g0 = fma(q0, w, o.g0);
+                o.g1 = fma(q1, w, o.g1);
+                o.g2 = fma(q2, w, o.g2);
                 if (FORCE && strict) {
-                    const double c = s_mu[ti * kTypes + tj] * omt * dot * (ir * ir * ir);
-                    o.v0 += c * q0;
-                    o.v1 += c * q1;
-                    o.v2 += c * q2;
+                    const double c = ((s_mu[ti * kTypes + tj] * omt) * dot) * ((ir * ir) * ir);
+                    o.v0 = fma(c, q0, o.v0);
+                    o.v1 = fma(c, q1, o.v1);
+                    o.v2 = fma(c, q2, o.v2);
                 }
             }
         }
@@ -727,16 +731,16 @@ __device__ __forceinline__ void pass_a_term(const DevParams& P, const double* s_
     }
     if (r2 <= P.rp2) {
         const double omt = 1.0 - r * P.inv_rp;
-        const double u = P.cdp * omt * ir;   // dw_p(r) / r
-        o.vs += P.cp * omt * omt;
-        o.dv -= dot * u;
+        const double u = (P.cdp * omt) * ir;   // dw_p(r) / r
+        o.vs = fma(P.cp * omt, omt, o.vs);
+        o.dv = fma(-dot, u, o.dv);
         // strict test of the force loops (2402), and structure i sees only non-structure j
         // (InterfaceForce 2439-2472)
         if (FORCE && r2 < P.rp2 && !(solid && dev_is_struct(tj))) {
             const double c = u * P.vol;
-            o.s0 += c * q0;
-            o.s1 += c * q1;
-            o.s2 += c * q2;
+            o.s0 = fma(c, q0, o.s0);
+            o.s1 = fma(c, q1, o.s1);
+            o.s2 = fma(c, q2, o.s2);
         }
     }
     if (!solid) {
@@ -744,36 +748,36 @@ __device__ __forceinline__ void pass_a_term(const DevParams& P, const double* s_
         if (r2 <= P.ra2) {
             const double t = r * P.inv_ra;
             const double omt = 1.0 - t;
-            o.da += ratio * (P.ca * t * omt * omt);
+            o.da = fma(ratio, ((P.ca * t) * omt) * omt, o.da);
         }
         if (r2 <= P.rg2) {
             const double omt = 1.0 - r * P.inv_rg;
-            const double w = ratio * (P.cg * omt * omt) * P.rg_r2g;
-            o.g0 += q0 * w;
-            o.g1 += q1 * w;
-            o.g2 += q2 * w;
+            const double w = (ratio * ((P.cg * omt) * omt)) * P.rg_r2g;
+            o.g0 = fma(q0, w, o.g0);
+            o.g1 = fma(q1, w, o.g1);
+            o.g2 = fma(q2, w, o.g2);
         }
         if (FORCE && r2 < P.rv2) {
             // s_mu holds -cvis cdv vol mu_ij (k_pass_a): dw_v(r) = -cdv (1 - r / rv)
-            const double c = s_mu[ti * kTypes + tj] * (1.0 - r * P.inv_rv) * dot * (ir * ir * ir);
-            o.v0 += c * q0;
-            o.v1 += c * q1;
-            o.v2 += c * q2;
+            const double c = ((s_mu[ti * kTypes + tj] * (1.0 - r * P.inv_rv)) * dot) * ((ir * ir) * ir);
+            o.v0 = fma(c, q0, o.v0);
+            o.v1 = fma(c, q1, o.v1);
+            o.v2 = fma(c, q2, o.v2);
         }
     }
 }
 
 // pass_a_term without control flow, for the fused kernel's mask walk: a lane whose slot is empty
-// (valid false) evaluates the same expressions on zeroed inputs, and every contribution is selected
-// by its radius test instead of branched on.  Divergent branches around the twelve accumulators
-// made the compiler copy them at every merge (160 VGPRs); selects need no copies.  Each sum keeps
-// the form  acc += a * b  of pass_a_term with the selected factor inside, so the contraction and the
-// bits are those of pass_a_term.
+// (valid false) evaluates the same expressions on zeroed inputs, and every contribution's factor
+// is selected by its radius test instead of branched on.  Divergent branches around the twelve
+// accumulators made the compiler copy them at every merge (160 VGPRs); selects need no copies.
+// Same explicit fmas as pass_a_term, so the same bits.
 template <bool EQR>
 __device__ __forceinline__ void pass_a_term_sel(const DevParams& P, const double* s_ratio, const double* s_mu,
                                                 int ti, int tj, bool solid, bool valid, double q0, double q1,
                                                 double q2, double dvx, double dvy, double dvz, PassA& o)
 {
+#pragma clang fp contract(off)
     q0 = valid ? q0 : 0.0;
     q1 = valid ? q1 : 0.0;
     q2 = valid ? q2 : 0.0;
@@ -784,7 +788,7 @@ __device__ __forceinline__ void pass_a_term_sel(const DevParams& P, const double
     const double r2 = valid ? r2_exact(q0, q1, q2) : P.rc2_hi;
     double r, ir;
     rsqrt_pair(r2, r, ir);
-    const double dot = dvx * q0 + dvy * q1 + dvz * q2;
+    const double dot = fma(dvz, q2, fma(dvy, q1, dvx * q0));
     const bool fluid_i = !solid;
     const bool sj = !(solid && dev_is_struct(tj));
     const double ratio = s_ratio[ti * kTypes + tj];
@@ -795,46 +799,46 @@ __device__ __forceinline__ void pass_a_term_sel(const DevParams& P, const double
         const double t = r * P.inv_rp;
         const double omt = 1.0 - t;
         const double omt2 = omt * omt;
-        const double u = P.cdp * omt * ir;
-        o.vs += P.cp * (in ? omt2 : 0.0);
-        o.dv -= dot * (in ? u : 0.0);
-        const double c = (strict && sj) ? u * P.vol : 0.0;
-        o.s0 += c * q0;
-        o.s1 += c * q1;
-        o.s2 += c * q2;
+        const double u = (P.cdp * omt) * ir;
+        o.vs = fma(P.cp, in ? omt2 : 0.0, o.vs);
+        o.dv = fma(-dot, in ? u : 0.0, o.dv);
+        const double c = (in && strict && sj) ? u * P.vol : 0.0;
+        o.s0 = fma(c, q0, o.s0);
+        o.s1 = fma(c, q1, o.s1);
+        o.s2 = fma(c, q2, o.s2);
         const bool fin = in && fluid_i;
-        o.da += ratio * (fin ? P.ca * t * omt2 : 0.0);
-        const double w = fin ? ratio * (P.cg * omt2) * P.rg_r2g : 0.0;
-        o.g0 += q0 * w;
-        o.g1 += q1 * w;
-        o.g2 += q2 * w;
-        const double cv = (strict && fluid_i) ? mu * omt * dot * (ir * ir * ir) : 0.0;
-        o.v0 += cv * q0;
-        o.v1 += cv * q1;
-        o.v2 += cv * q2;
+        o.da = fma(ratio, fin ? (P.ca * t) * omt2 : 0.0, o.da);
+        const double w = fin ? (ratio * (P.cg * omt2)) * P.rg_r2g : 0.0;
+        o.g0 = fma(q0, w, o.g0);
+        o.g1 = fma(q1, w, o.g1);
+        o.g2 = fma(q2, w, o.g2);
+        const double cv = (fin && strict) ? ((mu * omt) * dot) * ((ir * ir) * ir) : 0.0;
+        o.v0 = fma(cv, q0, o.v0);
+        o.v1 = fma(cv, q1, o.v1);
+        o.v2 = fma(cv, q2, o.v2);
         return;
     }
     const bool inp = r2 <= P.rp2;
     const double omtp = 1.0 - r * P.inv_rp;
-    const double u = P.cdp * omtp * ir;
-    o.vs += P.cp * (inp ? omtp : 0.0) * omtp;
-    o.dv -= dot * (inp ? u : 0.0);
-    const double c = (r2 < P.rp2 && sj) ? u * P.vol : 0.0;
-    o.s0 += c * q0;
-    o.s1 += c * q1;
-    o.s2 += c * q2;
+    const double u = (P.cdp * omtp) * ir;
+    o.vs = fma(P.cp * omtp, inp ? omtp : 0.0, o.vs);
+    o.dv = fma(-dot, inp ? u : 0.0, o.dv);
+    const double c = (inp && r2 < P.rp2 && sj) ? u * P.vol : 0.0;
+    o.s0 = fma(c, q0, o.s0);
+    o.s1 = fma(c, q1, o.s1);
+    o.s2 = fma(c, q2, o.s2);
     const double ta = r * P.inv_ra;
     const double omta = 1.0 - ta;
-    o.da += ratio * ((fluid_i && r2 <= P.ra2) ? P.ca * ta * omta * omta : 0.0);
+    o.da = fma(ratio, (fluid_i && r2 <= P.ra2) ? ((P.ca * ta) * omta) * omta : 0.0, o.da);
     const double omtg = 1.0 - r * P.inv_rg;
-    const double w = (fluid_i && r2 <= P.rg2) ? ratio * (P.cg * omtg * omtg) * P.rg_r2g : 0.0;
-    o.g0 += q0 * w;
-    o.g1 += q1 * w;
-    o.g2 += q2 * w;
-    const double cv = (fluid_i && r2 < P.rv2) ? mu * (1.0 - r * P.inv_rv) * dot * (ir * ir * ir) : 0.0;
-    o.v0 += cv * q0;
-    o.v1 += cv * q1;
-    o.v2 += cv * q2;
+    const double w = (fluid_i && r2 <= P.rg2) ? (ratio * ((P.cg * omtg) * omtg)) * P.rg_r2g : 0.0;
+    o.g0 = fma(q0, w, o.g0);
+    o.g1 = fma(q1, w, o.g1);
+    o.g2 = fma(q2, w, o.g2);
+    const double cv = (fluid_i && r2 < P.rv2) ? ((mu * (1.0 - r * P.inv_rv)) * dot) * ((ir * ir) * ir) : 0.0;
+    o.v0 = fma(cv, q0, o.v0);
+    o.v1 = fma(cv, q1, o.v1);
+    o.v2 = fma(cv, q2, o.v2);
 }
 
 // Epilogue: PhysicalCoefficients (2099-2137) and the pressure values of calculatePressureP
@@ -1421,6 +1425,9 @@ __global__ __launch_bounds__(256) void k_neighbors_redo(DevParams P, Soa A, cons
 
 // List pass: the neighbour loops gather U neighbours' fields
 // before the first use (all loads in flight at once; the loops are memory-latency bound).
+#ifndef MPH_PA_SEL
+#define MPH_PA_SEL 0   // k_pass_a: the branching term (the selecting one: D1M pass A 0.33 -> 0.51 ms)
+#endif
 #ifndef MPH_UA
 #define MPH_UA 5   // pass A (with MPH_PA_WPE 4; coherent gathers at kReach 3: 0.355 ms against 0.376 at U = 8, 3 waves)
 #endif
@@ -1462,8 +1469,13 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
             const double q0 = image_exact<FAST>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
             const double q1 = image_exact<FAST>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
             const double q2 = image_exact<FAST || DIM == 2>(Z[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
-            pass_a_term<true, EQR>(P, s_ratio, s_mu, ti, TT[u], solid, q0, q1, q2, r2_exact(q0, q1, q2), VX[u] - vxi,
-                                   VY[u] - vyi, VZ[u] - vzi, o);
+            // the branching form (MPH_PA_SEL=1: the fused kernel's selecting one; same bits)
+            if (MPH_PA_SEL)
+                pass_a_term_sel<EQR>(P, s_ratio, s_mu, ti, TT[u], solid, true, q0, q1, q2, VX[u] - vxi, VY[u] - vyi,
+                                     VZ[u] - vzi, o);
+            else
+                pass_a_term<true, EQR>(P, s_ratio, s_mu, ti, TT[u], solid, q0, q1, q2, r2_exact(q0, q1, q2),
+                                       VX[u] - vxi, VY[u] - vyi, VZ[u] - vzi, o);
         }
     }
 }
@@ -1668,6 +1680,9 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
 #ifndef MPH_FU
 #define MPH_FU 1         // accepted neighbours summed per iteration of the mask walk (2: 56 B/lane of spills at 4 waves)
 #endif
+#ifndef MPH_FSB
+#define MPH_FSB 3   // candidates per batch in the fused search (125 VGPRs, 4 waves per SIMD)
+#endif
 #ifndef MPH_FUSED_DIAG
 #define MPH_FUSED_DIAG 0 // diagnostic builds: 1 = no periodic-face path, 2 = equal-radii sums only
 #endif
@@ -1675,20 +1690,20 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
 #define MPH_FUSED_WPE 4  // waves per SIMD (<= 128 VGPRs)
 #endif
 
-struct FusedStage {
-    double x[MPH_FCAP + MPH_SB], y[MPH_FCAP + MPH_SB], z[MPH_FCAP + MPH_SB];
-    double vx[MPH_FCAP + MPH_SB], vy[MPH_FCAP + MPH_SB], vz[MPH_FCAP + MPH_SB];
-    int type[MPH_FCAP + MPH_SB];
+struct FusedStage {   // the six arrays consecutive, in this order (fused_lds stages by offset)
+    double x[MPH_FCAP + MPH_FSB], y[MPH_FCAP + MPH_FSB], z[MPH_FCAP + MPH_FSB];
+    double vx[MPH_FCAP + MPH_FSB], vy[MPH_FCAP + MPH_FSB], vz[MPH_FCAP + MPH_FSB];
+    int type[MPH_FCAP + MPH_FSB];
 };
+static_assert(offsetof(FusedStage, vz) == 5 * (MPH_FCAP + MPH_FSB) * sizeof(double), "FusedStage layout");
 
 // The pass-A sums over the accepted candidates of one lane's chunk: bit b of mask = candidate
-// base + b, read from the staged window (LDS, base = offset in it) or gathered from the 48-byte
-// records (wide window, base = sorted index).  Wave-uniform loop while any lane has bits left.
+// base + b of the staged sub-window (LDS).  Wave-uniform loop while any lane has bits left.
 template <bool EQR, int U = MPH_FU>
 __device__ __forceinline__ void fused_sum_mask(const DevParams& P, const double* s_ratio, const double* s_mu,
-                                               const Soa& A, const FusedStage& S, bool LDS,
-                                               unsigned long long mask, int base, int ti, bool solid, double xi,
-                                               double yi, double zi, double vxi, double vyi, double vzi, PassA& o)
+                                               const FusedStage& S, unsigned long long mask, int base, int ti,
+                                               bool solid, double xi, double yi, double zi, double vxi, double vyi,
+                                               double vzi, PassA& o)
 {
     if (MPH_FUSED_DIAG & 4) return;
     while (__builtin_amdgcn_ballot_w64(mask != 0ull)) {
@@ -1703,23 +1718,11 @@ __device__ __forceinline__ void fused_sum_mask(const DevParams& P, const double*
         }
         double X[U], Y[U], Z[U], VX[U], VY[U], VZ[U];
         int TT[U];
-        if (LDS) {   // wave-uniform
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                X[u] = S.x[t[u]]; Y[u] = S.y[t[u]]; Z[u] = S.z[t[u]];
-                VX[u] = S.vx[t[u]]; VY[u] = S.vy[t[u]]; VZ[u] = S.vz[t[u]];
-                TT[u] = S.type[t[u]];
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int j = v[u] ? t[u] : base;
-                const double2* q = A.p6 + 3 * (size_t)j;
-                const double2 a = q[0], b = q[1], c = q[2];
-                X[u] = a.x; Y[u] = a.y; Z[u] = b.x;
-                VX[u] = b.y; VY[u] = c.x; VZ[u] = c.y;
-                TT[u] = A.type[j];
-            }
+        for (int u = 0; u < U; ++u) {
+            X[u] = S.x[t[u]]; Y[u] = S.y[t[u]]; Z[u] = S.z[t[u]];
+            VX[u] = S.vx[t[u]]; VY[u] = S.vy[t[u]]; VZ[u] = S.vz[t[u]];
+            TT[u] = S.type[t[u]];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1734,7 +1737,7 @@ __device__ __forceinline__ void fused_sum_mask(const DevParams& P, const double*
 
 // The search of an interior wave (scan_candidates_lds: same column ranges, window, acceptance and
 // list order) with the pass-A sums of every accepted neighbour.  Returns the neighbour count.
-template <int DIM, int PERM, bool EQR, int SB = MPH_SB, int CAP = MPH_FCAP>
+template <int DIM, int PERM, bool EQR, int SB = MPH_FSB, int CAP = MPH_FCAP>
 __device__ __forceinline__ int fused_lds(const DevParams& P, const double* s_ratio, const double* s_mu,
                                          const Soa& A, const int* start, int i, bool act, double xi,
                                          double yi, double zi, int cx, int cy, int cz, int* out,
@@ -1801,57 +1804,63 @@ __device__ __forceinline__ int fused_lds(const DevParams& P, const double* s_rat
             mn = wave_min(any ? jb : 0x7fffffff);
             mx = wave_max(any ? je : -1);
         }
-        const int span = mx - mn;
-        const bool staged = span <= CAP;   // wave-uniform
-        if (staged) {
-            for (int t = lane; t < span; t += 64) {
-                const double2* q = A.p6 + 3 * (size_t)(mn + t);
-                const double2 a = q[0], b = q[1], c = q[2];
-                S.x[t] = a.x; S.y[t] = a.y; S.z[t] = b.x;
-                S.vx[t] = b.y; S.vy[t] = c.x; S.vz[t] = c.y;
-                S.type[t] = A.type[mn + t];
+        // the window [mn, mx) in sub-windows of at most CAP candidates, each staged in LDS (one
+        // unless the window is wider: a wave whose lanes straddle two distant cell rows); every
+        // candidate is read from LDS, never from global memory here (a global alternative in the
+        // same loop made the compiler merge the two pointers into flat loads, twice as slow)
+        int nxt = jb;   // the lane's next candidate
+        int w0 = mn;
+        for (;;) {
+            const int w1 = min(w0 + CAP, mx);
+            {
+                // the 48-byte records as one flat run of 16-byte pieces: consecutive lanes load
+                // consecutive pieces (8 cache lines per load instead of the 24 of one record per
+                // lane), each scattered into the SoA arrays x y | z vx | vy vz of FusedStage
+                const double2* src = A.p6 + 3 * (size_t)w0;
+                const int n3 = 3 * (w1 - w0);
+                for (int e = lane; e < n3; e += 64) {
+                    const double2 v = src[e];
+                    const int r = e / 3, part = e - 3 * r;
+                    double* lo = S.x + (size_t)(2 * part) * (CAP + SB) + r;
+                    lo[0] = v.x;
+                    lo[CAP + SB] = v.y;
+                }
+                for (int t = lane; t < w1 - w0; t += 64) S.type[t] = A.type[w0 + t];
             }
             __builtin_amdgcn_wave_barrier();
-        }
-        // the lane's candidates in chunks of 64 (one mask bit each; one chunk unless the lane's
-        // range is longer), each chunk tested, then its accepted candidates summed.  One loop for
-        // staged and wide windows (only the loads differ, under a wave-uniform branch), so the
-        // accumulators flow through a single path
-        for (int c0 = jb; c0 < je; c0 += 64) {
-            const int c1 = min(c0 + 64, je);
-            unsigned long long mask = 0ull;
-            for (int j0 = c0; j0 < c1; j0 += SB) {
-                double xs[SB], ys[SB], zs[SB];
-                if (staged) {
-                    const int k0 = j0 - mn;   // the staging arrays are padded by SB entries
+            // the lane's candidates of this sub-window in chunks of 64 (one mask bit each), each
+            // chunk tested, then its accepted candidates summed
+            const int cend = min(je, w1);
+            for (int c0 = nxt; c0 < cend; c0 += 64) {
+                const int c1 = min(c0 + 64, cend);
+                unsigned long long mask = 0ull;
+                for (int j0 = c0; j0 < c1; j0 += SB) {
+                    double xs[SB], ys[SB], zs[SB];
+                    const int k0 = j0 - w0;   // the staging arrays are padded by SB entries
 #pragma unroll
                     for (int u = 0; u < SB; ++u) {
                         xs[u] = S.x[k0 + u]; ys[u] = S.y[k0 + u]; zs[u] = S.z[k0 + u];
                     }
-                } else {
 #pragma unroll
                     for (int u = 0; u < SB; ++u) {
-                        const int j = j0 + u < c1 ? j0 + u : c1 - 1;
-                        xs[u] = A.x[j]; ys[u] = A.y[j]; zs[u] = A.z[j];
+                        const int j = j0 + u;
+                        const bool a = accept_interior(P, xs[u] - xi, ys[u] - yi, zs[u] - zi, lo2, hi2) &
+                                       (j < c1) & (j != i);
+                        if (a) {
+                            list_store(out + min(cnt, kMaxNeighbor - 1) * kTile, nbr_entry(j, S.type[k0 + u]));
+                            mask |= 1ull << (j - c0);
+                            ++cnt;
+                        }
                     }
                 }
-#pragma unroll
-                for (int u = 0; u < SB; ++u) {
-                    const int j = j0 + u;
-                    const bool a = accept_interior(P, xs[u] - xi, ys[u] - yi, zs[u] - zi, lo2, hi2) &
-                                   (j < c1) & (j != i);
-                    if (a) {
-                        const int tj = staged ? S.type[j - mn] : A.type[j];
-                        list_store(out + min(cnt, kMaxNeighbor - 1) * kTile, nbr_entry(j, tj));
-                        mask |= 1ull << (j - c0);
-                        ++cnt;
-                    }
-                }
+                fused_sum_mask<EQR>(P, s_ratio, s_mu, S, mask, c0 - w0, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
             }
-            fused_sum_mask<EQR>(P, s_ratio, s_mu, A, S, staged, mask, staged ? c0 - mn : c0, ti, solid, xi, yi, zi,
-                                vxi, vyi, vzi, o);
+            nxt = max(nxt, cend);
+            __builtin_amdgcn_wave_barrier();   // every lane done reading before the next staging
+            if (w1 >= mx) break;               // wave-uniform
+            w0 = wave_min(nxt < je ? nxt : 0x7fffffff);
+            if (w0 == 0x7fffffff) break;
         }
-        if (staged) __builtin_amdgcn_wave_barrier();   // every lane done reading before the next staging
     }
     return cnt;
 }

@@ -47,10 +47,10 @@ constexpr int kHdrFlag = 7;
 #define MPH_LIST_COMPACT (MPH_R == 2)
 #endif
 constexpr bool kListCompact = MPH_LIST_COMPACT;
-// search + pass A fused into one kernel (k_search_pass_a); the compact list
-// format keeps the two kernels
+// search + pass A fused into one kernel (k_search_pass_a): measured slower
+// (D1M 1.05 ms against 0.39 + 0.32 ms for the two kernels), so opt-in (MPH_FUSED=1); bit-identical
 #ifndef MPH_FUSED_DEFAULT
-#define MPH_FUSED_DEFAULT 1
+#define MPH_FUSED_DEFAULT 0
 #endif
 constexpr bool kFusedDefault = MPH_FUSED_DEFAULT;
 constexpr int kLhdr = 8 + 2 * 64;

@@ -186,10 +186,10 @@ def gpu_capacity_worker(rank, world, port, case, batches, out_dir):
     axis = SLAB_AXIS[case]
     cfg, parts = c.build()
     caps, code, res = [], 0, {}
-    with MphSolver(cfg, parts, device=0, slab=gloo_slab(rank, world, axis)) as s:
-        info = s.dist_info()
-        caps.append([info["cap_send"], info["cap_recv"]])   # as created
-        try:
+    try:
+        with MphSolver(cfg, parts, device=0, slab=gloo_slab(rank, world, axis)) as s:
+            info = s.dist_info()
+            caps.append([info["cap_send"], info["cap_recv"]])   # as created
             for k in batches:
                 s.step(k)
                 info = s.dist_info()
@@ -197,8 +197,8 @@ def gpu_capacity_worker(rank, world, port, case, batches, out_dir):
             ids = s.owned_ids()
             res = {"ids": ids, "Position": s.get("Position")[ids], "Velocity": s.get("Velocity")[ids],
                    "PressureP": s.get("PressureP")[ids], "NeighborCount": s.get("NeighborCount")[ids]}
-        except MphError as e:
-            code = e.code
+    except MphError as e:   # creation included: its first exchange may already overflow
+        code = e.code
     np.savez(os.path.join(out_dir, "rank%d.npz" % rank), caps=np.array(caps, np.int64).reshape(-1, 2),
              code=np.array([code]), **res)
     dist.barrier()
