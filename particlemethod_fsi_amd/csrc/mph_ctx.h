@@ -134,7 +134,7 @@ inline int glob_id(const MphCtx* c, int k) { return c->gid.empty() ? k : c->gid[
 int dist_setup(MphCtx* c, const double* pos, std::vector<int>& owned);   // geometry + owned set
 // elastic slots of this rank: lsl = [owned | ghosts from the left | ghosts from the right] (global
 // slot ids), n_own owned; records the per-substep ghost exchange lists
-int dist_struct_setup(MphCtx* c, std::vector<int>& lsl, int& n_own);
+int dist_struct_setup(MphCtx* c, std::vector<int>& lsl, int& n_own, int& n_inner);
 int dist_alloc(MphCtx* c);                                               // exchange buffers
 int dist_init(MphCtx* c);                                                // first exchange + init sums
 int dist_step(MphCtx* c, int nsteps, Profiler* prof = nullptr);

@@ -125,7 +125,7 @@ void enqueue_step(const Launch& L, bool last)
         Lb.acc = nullptr;
         launch_pass_b(Lb);
     }
-    launch_structure(L);
+    launch_structure(L, last);
 }
 
 int capture(MphCtx* c, int steps, hipGraphExec_t* out)
@@ -215,12 +215,22 @@ int download_struct_m33(MphCtx* c, const double* d, double* out)
     return MPH_OK;
 }
 
+// A launch's start event behind a cross-stream wait reads as early as the wait packet itself (the
+// time the stream went idle), so each launch that follows a join also keeps a floor: an event on
+// the other stream at the joined point; its start is the later of the two.
 struct EventProfiler final : Profiler {
-    struct Rec { std::string name; hipEvent_t a, b; };
+    struct Rec { std::string name; hipEvent_t a, b; int floor; };
     std::vector<Rec> recs;
+    std::vector<hipEvent_t> floors;
+    std::map<hipStream_t, int> pending;
     int begin(const char* name, hipStream_t s) override
     {
-        Rec r{name, nullptr, nullptr};
+        Rec r{name, nullptr, nullptr, -1};
+        const auto it = pending.find(s);
+        if (it != pending.end()) {
+            r.floor = it->second;
+            pending.erase(it);
+        }
         (void)hipEventCreate(&r.a);
         (void)hipEventCreate(&r.b);
         (void)hipEventRecord(r.a, s);
@@ -228,9 +238,18 @@ struct EventProfiler final : Profiler {
         return (int)recs.size() - 1;
     }
     void end(int slot, hipStream_t s) override { (void)hipEventRecord(recs[slot].b, s); }
+    void join(hipStream_t waiting, hipStream_t from) override
+    {
+        hipEvent_t e = nullptr;
+        (void)hipEventCreate(&e);
+        (void)hipEventRecord(e, from);
+        floors.push_back(e);
+        pending[waiting] = (int)floors.size() - 1;
+    }
     ~EventProfiler() override
     {
         for (auto& r : recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+        for (auto e : floors) (void)hipEventDestroy(e);
     }
 };
 
@@ -398,9 +417,9 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         StructDev& D = c->Sd;
         StructureInit& S = c->S;
         std::vector<int> lsl;   // local slot -> global slot
-        int no = ns;
+        int no = ns, ni = ns;
         if (c->dist) {
-            CK(dist_struct_setup(c, lsl, no));
+            CK(dist_struct_setup(c, lsl, no, ni));
         } else {
             lsl.resize(ns);
             for (int s = 0; s < ns; ++s) lsl[s] = s;
@@ -409,6 +428,7 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         std::vector<int> loc(ns, -1);
         for (int k = 0; k < nl; ++k) loc[lsl[k]] = k;
         D.n_own = no;
+        D.n_inner = ni;
         c->sl_orig.resize(nl);
         for (int k = 0; k < nl; ++k) c->sl_orig[k] = glob_id(c, S.orig[lsl[k]]);
         c->sl_s.assign(lsl.begin(), lsl.begin() + no);
@@ -882,6 +902,14 @@ int mph_profile_steps(MphCtx* c, int nsteps, double* avg_ms, int* launches, char
         float ms = 0.0f, t0 = 0.0f;
         HIP_OK(c, hipEventElapsedTime(&ms, r.a, r.b));
         HIP_OK(c, hipEventElapsedTime(&t0, prof.recs[0].a, r.a));
+        if (r.floor >= 0) {
+            float tf = 0.0f;
+            HIP_OK(c, hipEventElapsedTime(&tf, prof.recs[0].a, prof.floors[r.floor]));
+            if (tf > t0) {
+                ms = std::max(0.0f, ms - (tf - t0));
+                t0 = tf;
+            }
+        }
         span.emplace_back(t0, t0 + ms);
         if (!acc.count(r.name)) order.push_back(r.name);
         acc[r.name].first += ms;

@@ -270,6 +270,14 @@ int msg_alloc(MphCtx* c)
     return MPH_OK;
 }
 
+// a cross-stream wait for an event `from` has just recorded (the profiler keeps the point as the
+// earliest start of the next launch on `waiting`, see EventProfiler)
+hipError_t stream_wait(Profiler* prof, hipStream_t waiting, hipEvent_t ev, hipStream_t from)
+{
+    if (prof) prof->join(waiting, from);
+    return hipStreamWaitEvent(waiting, ev, 0);
+}
+
 // Steps 1-3 of the protocol: classify, partition, exchange migrants + ghosts.  Leaves the new
 // local set (owned and ghosts) in D.C and its sizes in D.lay -- on the device: nothing here reads
 // a size on the host, so the step can be captured.  init: first redistribution of mph_create,
@@ -282,13 +290,14 @@ int redistribute(MphCtx* c, bool move, bool init, Profiler* prof, bool early_in 
     Launch L = c->L;
     L.prof = prof;
     const int nb = dist_blocks(D.cap);
-    if (early_in) MPH_HIP_OK(c, hipStreamWaitEvent(c->stream, D.ev_s, 0));   // see early_send
+    // see early_send (no profiler floor: the second stream has moved on to the exchange since)
+    if (early_in) MPH_HIP_OK(c, hipStreamWaitEvent(c->stream, D.ev_s, 0));
     launch_dist_classify(L, D.g, D.cap, D.lay, move ? 1 : 0, D.cls, D.bcnt, early_in ? D.wface : nullptr);
     launch_scan(D.bcnt, kSlabClasses * nb, D.bsum, D.boff, 0, c->stream, prof);
     launch_dist_scatter(L, D.cap, D.lay, D.cls, D.boff, D.C, lay_field<int>(D.lay, offsetof(DistLayout, seg)));
     launch_dist_counts(L, D.lay);
     if (early_in) {
-        MPH_HIP_OK(c, hipStreamWaitEvent(c->stream, D.ev_x, 0));
+        MPH_HIP_OK(c, stream_wait(prof, c->stream, D.ev_x, D.stream2));
         launch_dist_unpack(L, D.recv_l, D.recv_r, D.lay, 0, D.cap_rl, D.cap, D.C);
         launch_dist_unpack(L, D.recv_l, D.recv_r, D.lay, 1, D.cap_rr, D.cap, D.C);
         return MPH_OK;
@@ -335,7 +344,7 @@ int early_send(MphCtx* c, Profiler* prof, hipStream_t stream)
     // ev_s: the face waves' pass B and these kernels are done (the next step's partition, on the
     // main stream, waits for it before it reads B and wface); ev_x: the messages have landed
     MPH_HIP_OK(c, hipEventRecord(D.ev_s, stream));
-    if (stream != D.stream2) MPH_HIP_OK(c, hipStreamWaitEvent(D.stream2, D.ev_s, 0));
+    if (stream != D.stream2) MPH_HIP_OK(c, stream_wait(prof, D.stream2, D.ev_s, stream));
     MPH_CK(exchange(c, D.stream2, D.send_l, kMsgHead + kMsgBytes * D.cap_sl, D.send_r,
                     kMsgHead + kMsgBytes * D.cap_sr, D.recv_l, kMsgHead + kMsgBytes * D.cap_rl, D.recv_r,
                     kMsgHead + kMsgBytes * D.cap_rr));
@@ -390,11 +399,12 @@ int halo_exchange(MphCtx* c, Profiler* prof, hipStream_t stream, const HaloField
 }
 
 // One static ghost exchange of per-slot double4 records (w rows per slot) of the elastic arrays.
-int struct_exchange(MphCtx* c, double4* a, int w, Profiler* prof)
+int struct_exchange(MphCtx* c, double4* a, int w, Profiler* prof, hipStream_t stream)
 {
     MphDist& D = *c->dist;
     Launch L = c->L;
     L.prof = prof;
+    L.stream = stream;
     double4* sl = (double4*)D.send_l;
     double4* sr = (double4*)D.send_r;
     double4* rl = (double4*)D.recv_l;
@@ -402,25 +412,46 @@ int struct_exchange(MphCtx* c, double4* a, int w, Profiler* prof)
     launch_struct_pack(L, a, w, D.ss_l, D.nss_l, sl);
     launch_struct_pack(L, a, w, D.ss_r, D.nss_r, sr);
     const size_t b = sizeof(double4) * w;
-    MPH_CK(exchange(c, c->stream, sl, b * D.nss_l, sr, b * D.nss_r, rl, b * D.nsr_l, rr, b * D.nsr_r));
+    MPH_CK(exchange(c, stream, sl, b * D.nss_l, sr, b * D.nss_r, rl, b * D.nsr_l, rr, b * D.nsr_r));
     launch_struct_unpack(L, rl, w, D.sr_l, D.nsr_l, a);
     launch_struct_unpack(L, rr, w, D.sr_r, D.nsr_r, a);
     return MPH_OK;
 }
 
-// Step 7: the elastic substeps on the owned slots, ghosts refreshed before each half.
+// Step 7: the elastic substeps on the owned slots, ghosts refreshed before each half.  Each ghost
+// exchange (displacements u before DeformationVector/Stress, first Piola-Kirchhoff rows P before
+// StressForce) travels on the second stream while the owned slots whose lists hold no ghost slot
+// ([0, n_inner), dist_struct_setup) run their half on the main stream; the others follow once it
+// has landed.  The slots a neighbour needs are all among the latter (symmetric lists), so a pack
+// never waits for an inner half.
 int struct_substeps(MphCtx* c, Profiler* prof)
 {
     if (c->P.n_struct == 0) return MPH_OK;
+    MphDist& D = *c->dist;
     Launch L = c->L;
     L.prof = prof;
     StructDev& S = c->Sd;
     const int wP = c->P.dim == 2 ? 1 : 3;
+    // launch(s0, s1): the half-substep over owned slots [s0, s1)
+    auto half = [&](double4* a, int w, auto&& launch) -> int {
+        if (!D.overlap) {
+            MPH_CK(struct_exchange(c, a, w, prof, c->stream));
+            launch(0, S.n_own);
+            return MPH_OK;
+        }
+        MPH_HIP_OK(c, hipEventRecord(D.ev_a, c->stream));
+        MPH_HIP_OK(c, stream_wait(prof, D.stream2, D.ev_a, c->stream));
+        launch(0, S.n_inner);   // enqueued before a host-staged exchange blocks the host
+        MPH_CK(struct_exchange(c, a, w, prof, D.stream2));
+        MPH_HIP_OK(c, hipEventRecord(D.ev_h, D.stream2));
+        MPH_HIP_OK(c, stream_wait(prof, c->stream, D.ev_h, D.stream2));
+        launch(S.n_inner, S.n_own);
+        return MPH_OK;
+    };
     for (int sub = 0; sub < c->P.substeps; ++sub) {
-        MPH_CK(struct_exchange(c, S.u, 1, prof));
-        launch_struct_stress(L);
-        MPH_CK(struct_exchange(c, S.P, wP, prof));
-        launch_struct_velocity(L, sub == c->P.substeps - 1);
+        const bool last = sub == c->P.substeps - 1;
+        MPH_CK(half(S.u, 1, [&](int s0, int s1) { launch_struct_stress(L, last, s0, s1); }));
+        MPH_CK(half(S.P, wP, [&](int s0, int s1) { launch_struct_velocity(L, last, s0, s1); }));
     }
     return MPH_OK;
 }
@@ -503,7 +534,7 @@ int dist_setup(MphCtx* c, const double* pos, std::vector<int>& owned)
     return MPH_OK;
 }
 
-int dist_struct_setup(MphCtx* c, std::vector<int>& lsl, int& n_own)
+int dist_struct_setup(MphCtx* c, std::vector<int>& lsl, int& n_own, int& n_inner)
 {
     MphDist& D = *c->dist;
     const HostDerived& h = c->h;
@@ -541,9 +572,20 @@ int dist_struct_setup(MphCtx* c, std::vector<int>& lsl, int& n_own)
     ghosts(D.left, lgl, lgr);
     ghosts(D.right, rgl, rgr);
     if (!err.empty()) return ctx_fail(c, MPH_ERR_DOMAIN, "slab mode: " + err);
+    // the owned slots, those without a ghost slot in their out- or in-list first (the lists are
+    // symmetric, so every slot a neighbour needs is among the others): their substep halves run
+    // while the ghost exchange travels (struct_substeps)
     lsl.clear();
-    for (int s = 0; s < ns; ++s)
-        if (owner[s] == D.rank) lsl.push_back(s);
+    std::vector<int> outer;
+    for (int s = 0; s < ns; ++s) {
+        if (owner[s] != D.rank) continue;
+        bool ghost = false;
+        for (int q = S.offset[s]; q < S.offset[s + 1] && !ghost; ++q) ghost = owner[S.nbr[q]] != D.rank;
+        for (int q = S.in_offset[s]; q < S.in_offset[s + 1] && !ghost; ++q) ghost = owner[S.in_nbr[q]] != D.rank;
+        (ghost ? outer : lsl).push_back(s);
+    }
+    n_inner = (int)lsl.size();
+    lsl.insert(lsl.end(), outer.begin(), outer.end());
     n_own = (int)lsl.size();
     std::vector<int> loc(ns, -1);
     for (int k = 0; k < n_own; ++k) loc[lsl[k]] = k;
@@ -692,17 +734,19 @@ int dist_enqueue_step(MphCtx* c, Profiler* prof, bool early_in, bool early_out)
     Launch L2 = L;
     L2.stream = D.stream2;
     MPH_HIP_OK(c, hipEventRecord(D.ev_a, c->stream));
+    MPH_HIP_OK(c, stream_wait(prof, D.stream2, D.ev_a, c->stream));
     launch_pass_b(L, 1);
-    MPH_HIP_OK(c, hipStreamWaitEvent(D.stream2, D.ev_a, 0));
     MPH_CK(halo_exchange(c, prof, D.stream2));
     launch_pass_b(L2, 2);
-    if (early_out) {
-        // joined by the next step's redistribute (ev_x); no elastic particles in this mode
-        return early_send(c, prof, D.stream2);
-    }
+    // joined by the next step's redistribute (ev_s, ev_x)
+    if (early_out && c->P.n_struct == 0) return early_send(c, prof, D.stream2);
     MPH_HIP_OK(c, hipEventRecord(D.ev_h, D.stream2));
-    MPH_HIP_OK(c, hipStreamWaitEvent(c->stream, D.ev_h, 0));
+    MPH_HIP_OK(c, stream_wait(prof, c->stream, D.ev_h, D.stream2));
     MPH_CK(struct_substeps(c, prof));
+    // elastic particles take their positions from the substeps: their face waves are classified
+    // and packed after them (main stream); the messages still travel on the second stream beside
+    // the next step's partition
+    if (early_out) return early_send(c, prof, c->stream);
     return MPH_OK;
 }
 
@@ -711,7 +755,7 @@ int dist_enqueue_step(MphCtx* c, Profiler* prof, bool early_in, bool early_out)
 bool early_at(const MphCtx* c, int k, int steps, int out)
 {
     const MphDist& D = *c->dist;
-    if (!D.early || !D.overlap || c->P.n_struct > 0) return false;
+    if (!D.early || !D.overlap) return false;
     return out ? k < steps - 1 : k > 0;
 }
 

@@ -15,6 +15,9 @@ struct StructDev {
     int* slot_of = nullptr;       // original particle index -> slot (-1: not structure / not owned)
     int* bidx = nullptr;          // slot -> index of its B entry this step (written by pass B)
     int n_own = 0;                // slots computed here (slab mode: owned, then ghost slots)
+    // slab mode: the owned slots [0, n_inner) have no ghost slot in their out- or in-list (their
+    // substep halves run while the ghost exchange travels); [n_inner, n_own) have one
+    int n_inner = 0;
     int wo = 0, wi = 0;           // ELL widths (max out / in count)
     int* ocnt = nullptr;          // InitialStructureNeighborCount per slot
     int* icnt = nullptr;          // in-degree (how many slots list s)
@@ -39,6 +42,9 @@ struct StructDev {
 struct Profiler {
     virtual int begin(const char* name, hipStream_t s) = 0;
     virtual void end(int slot, hipStream_t s) = 0;
+    // `waiting` is about to wait for an event `from` has just recorded: the next launch on
+    // `waiting` starts no earlier than `from` reaches this point (mph_profile_steps)
+    virtual void join(hipStream_t waiting, hipStream_t from) { (void)waiting; (void)from; }
     virtual ~Profiler() = default;
 };
 
@@ -98,7 +104,7 @@ void launch_pass_a(const Launch& L);
 // launch_neighbors + launch_pass_a, fused into one kernel where the list format allows
 void launch_search_pass_a(const Launch& L);
 void launch_pass_b(const Launch& L, int phase = 0);   // phase: 0 all, 1/2 slab inner/near-face
-void launch_structure(const Launch& L);
+void launch_structure(const Launch& L, bool last);   // last: the batch's last step (output tensors)
 // calculateInitialNeighbor + calculateNormalizer of the ns structure slots (x0 in slot order) on
 // the device: counts (ocnt), ELL out-rows (*eo, width *wo) and their transpose (*ei, *wi), both
 // sorted ascending, Normalizer (Lm [ns][9]) and sum_j w_sj x0_sj (wx0).  The ELL arrays are
@@ -107,8 +113,10 @@ void launch_structure(const Launch& L);
 int launch_struct_init(const Launch& L, int ns, const double4* x0, int* key, int* slot, int* tmp, int* sorted,
                        int* ocnt, int* icnt, int** eo, int* wo, int** ei, int* wi, double* Lm, double4* wx0,
                        void* (*alloc)(void*, size_t), void* actx);
-void launch_struct_stress(const Launch& L);
-void launch_struct_velocity(const Launch& L, bool last);
+// over the slots [s0, s1) (s1 < 0: every computed slot, [0, n_own))
+// store: also write the output-only tensors F, E, S (the last substep of a batch's last step)
+void launch_struct_stress(const Launch& L, bool store, int s0 = 0, int s1 = -1);
+void launch_struct_velocity(const Launch& L, bool last, int s0 = 0, int s1 = -1);
 // slab mode: rows of per-slot double4 records (w per slot) gathered into / scattered from a message
 void launch_struct_pack(const Launch& L, const double4* src, int w, const int* idx, int m, double4* buf);
 void launch_struct_unpack(const Launch& L, const double4* buf, int w, const int* idx, int m, double4* dst);

@@ -639,7 +639,8 @@ __global__ __launch_bounds__(256) void k_place(DevParams P, DevState* __restrict
 __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __restrict__ key,
                                                       const int* __restrict__ start,
                                                       const int* __restrict__ tmp, Soa B, Soa A,
-                                                      int* __restrict__ rank_of, int* __restrict__ dst_of)
+                                                      int* __restrict__ rank_of, int* __restrict__ dst_of,
+                                                      int mode)
 {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= dev_n(P)) return;
@@ -652,9 +653,9 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
     A.y[dst] = B.y[p];
     A.z[dst] = B.z[p];
     // the sorted velocities are read only through the 48-byte records (own_velocity below), unless
-    // the passes gather SoA (MPH_AOS_GATHER=0, or the segmented lists of MPH_SEG), or in slab mode
-    // (dist_init copies the sorted set into B)
-    if (!MPH_AOS_GATHER || MPH_SEG || !A.p6 || dst_of) {
+    // the passes gather SoA (MPH_AOS_GATHER=0, or the segmented lists of MPH_SEG), or at a slab
+    // context's initialisation sort (mode 0: dist_init copies the sorted set into B)
+    if (!MPH_AOS_GATHER || MPH_SEG || !A.p6 || (dst_of && mode == 0)) {
         A.vx[dst] = B.vx[p];
         A.vy[dst] = B.vy[p];
         A.vz[dst] = B.vz[p];
@@ -2398,22 +2399,35 @@ __device__ __forceinline__ size_t sell(int s, int w, int k)
     return ((size_t)(s >> 6) * w + k) * 64 + (s & 63);
 }
 
+// the G lanes of one structure slot (G | 64, adjacent lanes) sum their strided shares of its list
+// in a butterfly: every lane of the group ends with the same total (a + b == b + a exactly)
+template <int G>
+__device__ __forceinline__ double group_sum(double v)
+{
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
 // calculateElasticDeformationVector (2673-2754) + calculateStress (2756-2809) + the first
-// Piola-Kirchhoff tensor P = F S L of calculateStressForce (2837-2852).  One lane per structure
-// slot; the fixed list is read ELL-tiled (coalesced) in batches of MPH_US, and per neighbour only
-// the 32-byte displacement record u_j is gathered.
-template <int DIM, int U = MPH_US>
-__global__ __launch_bounds__(256) void k_struct_stress(DevParams P, int ns, int wo, const int* __restrict__ ocnt,
+// Piola-Kirchhoff tensor P = F S L of calculateStressForce (2837-2852).  G lanes per structure
+// slot (struct_lanes: enough waves to cover the latency of a small structure), each summing every
+// G-th entry of the fixed list, read ELL-tiled in batches of MPH_US; per neighbour only the
+// 32-byte displacement record u_j and the x0 record are gathered.
+template <int DIM, int G, int U = MPH_US>
+__global__ __launch_bounds__(256) void k_struct_stress(DevParams P, int s0, int ns, int wo, const int* __restrict__ ocnt,
                                                        const int* __restrict__ eo_nb,
                                                        const double4* __restrict__ sx0,
                                                        const double4* __restrict__ su,
                                                        const double* __restrict__ L,
                                                        const double2* __restrict__ lame,
                                                        double4* __restrict__ sP, double* __restrict__ sF,
-                                                       double* __restrict__ sE, double* __restrict__ sS)
+                                                       double* __restrict__ sE, double* __restrict__ sS,
+                                                       int store)
 {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= ns) return;
+    const int s = s0 + (int)((blockIdx.x * blockDim.x + threadIdx.x) / G);   // slots [s0, ns)
+    const int g = (int)threadIdx.x & (G - 1);
+    if (s >= ns) return;   // whole groups: G divides the block
     const double4 u4 = su[s];
     const double4 x0s = sx0[s];
     const double ui[3] = {u4.x, u4.y, u4.z};
@@ -2423,11 +2437,11 @@ __global__ __launch_bounds__(256) void k_struct_stress(DevParams P, int ns, int 
 #pragma unroll
         for (int b = 0; b < DIM; ++b) Fr[a][b] = 0.0;
     const int cnt = ocnt[s];
-    for (int k0 = 0; k0 < cnt; k0 += U) {
+    for (int k0 = g; k0 < cnt; k0 += G * U) {
         int t[U];
         double4 pr[U], uj[U], xj[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) t[u] = eo_nb[sell(s, wo, k0 + u < cnt ? k0 + u : cnt - 1)];
+        for (int u = 0; u < U; ++u) t[u] = eo_nb[sell(s, wo, k0 + G * u < cnt ? k0 + G * u : cnt - 1)];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             uj[u] = su[t[u]];
@@ -2437,7 +2451,7 @@ __global__ __launch_bounds__(256) void k_struct_stress(DevParams P, int ns, int 
         for (int u = 0; u < U; ++u) pr[u] = struct_pair<DIM>(P, x0s, xj[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (k0 + u >= cnt) break;
+            if (k0 + G * u >= cnt) break;
             const double x0ij[3] = {pr[u].x, pr[u].y, pr[u].z};
             const double ujv[3] = {uj[u].x, uj[u].y, uj[u].z};
 #pragma unroll
@@ -2447,6 +2461,13 @@ __global__ __launch_bounds__(256) void k_struct_stress(DevParams P, int ns, int 
                 for (int b = 0; b < DIM; ++b) Fr[a][b] += pr[u].w * xa * x0ij[b];
             }
         }
+    }
+    if (G > 1) {
+#pragma unroll
+        for (int a = 0; a < DIM; ++a)
+#pragma unroll
+            for (int b = 0; b < DIM; ++b) Fr[a][b] = group_sum<G>(Fr[a][b]);
+        if (g != 0) return;
     }
     double Lm[DIM][DIM], F[DIM][DIM], E[DIM][DIM], S[DIM][DIM], PK[DIM][DIM];
 #pragma unroll
@@ -2496,6 +2517,7 @@ __global__ __launch_bounds__(256) void k_struct_stress(DevParams P, int ns, int 
 #pragma unroll
         for (int a = 0; a < DIM; ++a) sP[(size_t)s * 3 + a] = make_double4(PK[a][0], PK[a][1], PK[a][DIM - 1], 0.0);
     }
+    if (!store) return;   // F, E, S are outputs only: the last substep of a batch's last step
     double* oF = sF + (size_t)s * 9;
     double* oE = sE + (size_t)s * 9;
     double* oS = sS + (size_t)s * 9;
@@ -2532,8 +2554,8 @@ __device__ __forceinline__ void struct_P(const double4* sP, int s, double (&Pm)[
     }
 }
 
-template <int DIM, int U = MPH_US>
-__global__ __launch_bounds__(256) void k_struct_velocity(DevParams P, int ns, int wi,
+template <int DIM, int G, int U = MPH_US>
+__global__ __launch_bounds__(256) void k_struct_velocity(DevParams P, int s0, int ns, int wi,
                                                          const int* __restrict__ icnt,
                                                          const int* __restrict__ ei_nb,
                                                          const double4* __restrict__ wx0,
@@ -2546,10 +2568,13 @@ __global__ __launch_bounds__(256) void k_struct_velocity(DevParams P, int ns, in
                                                          const int* __restrict__ bidx, Soa B,
                                                          double4* __restrict__ force)
 {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= ns) return;
+    const int s = s0 + (int)((blockIdx.x * blockDim.x + threadIdx.x) / G);   // slots [s0, ns)
+    const int g = (int)threadIdx.x & (G - 1);
+    if (s >= ns) return;   // whole groups: G divides the block
     double dv[DIM];
-    {
+#pragma unroll
+    for (int a = 0; a < DIM; ++a) dv[a] = 0.0;
+    if (g == 0) {   // the receiver's own half, once per slot (G > 1: added to lane 0's share)
         const double4 c = wx0[s];
         const double cv[3] = {c.x, c.y, c.z};
         double Ps[DIM][3];
@@ -2564,12 +2589,12 @@ __global__ __launch_bounds__(256) void k_struct_velocity(DevParams P, int ns, in
     }
     const int cnt = icnt[s];
     const double4 x0me = sx0[s];
-    for (int k0 = 0; k0 < cnt; k0 += U) {
+    for (int k0 = g; k0 < cnt; k0 += G * U) {
         int t[U];
         double4 xi0[U];
         double Pi[U][DIM][3];
 #pragma unroll
-        for (int u = 0; u < U; ++u) t[u] = ei_nb[sell(s, wi, k0 + u < cnt ? k0 + u : cnt - 1)];
+        for (int u = 0; u < U; ++u) t[u] = ei_nb[sell(s, wi, k0 + G * u < cnt ? k0 + G * u : cnt - 1)];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             struct_P<DIM>(sP, t[u], Pi[u]);
@@ -2577,7 +2602,7 @@ __global__ __launch_bounds__(256) void k_struct_velocity(DevParams P, int ns, in
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (k0 + u >= cnt) break;
+            if (k0 + G * u >= cnt) break;
             // the sender i's pair {x0_is, w_is} (main.cpp:2862-2880, from i's side)
             const double4 pr = struct_pair<DIM>(P, xi0[u], x0me);
             const double x0[3] = {pr.x, pr.y, pr.z};
@@ -2589,6 +2614,11 @@ __global__ __launch_bounds__(256) void k_struct_velocity(DevParams P, int ns, in
                 dv[a] -= f * pr.w;
             }
         }
+    }
+    if (G > 1) {
+#pragma unroll
+        for (int a = 0; a < DIM; ++a) dv[a] = group_sum<G>(dv[a]);
+        if (g != 0) return;
     }
     double4 v = sv[s];
     double4 xo = sx[s];
@@ -2874,7 +2904,7 @@ __global__ __launch_bounds__(256) void k_dist_early_classify(DevParams P, DevSta
         double x = B.x[p], y = B.y[p], z = B.z[p];
         move_and_wrap(P, st, B, p, x, y, z);
         const double a = g.axis == 0 ? x : (g.axis == 1 ? y : z);
-        c = slab_class(g, a);   // no elastic particles in early-send mode
+        c = dev_is_struct(B.type[p]) ? slab_class_static(g, a) : slab_class(g, a);   // as k_dist_classify
         if (c == kSlabLost) c = kInner;   // reported by k_dist_classify at the next step
     }
     if (p < n) cls[p] = c;
@@ -3187,7 +3217,7 @@ void launch_sort(const Launch& L, int mode)
     MPH_LAUNCH("place", L.stream, k_place, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.key,
                L.slot, L.start, L.tmp, mode);
     MPH_LAUNCH("rank_scatter", L.stream, k_rank_scatter, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P,
-               L.key, L.start, L.tmp, L.B, L.A, L.rank_of, L.dst_of);
+               L.key, L.start, L.tmp, L.B, L.A, L.rank_of, L.dst_of, mode);
 }
 
 static PassAOut pass_a_out(const Launch& L)
@@ -3319,44 +3349,81 @@ void launch_virial(const Launch& L, const Soa& X, double* vir, double* vpres)
                    L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, vir, vpres);
 }
 
-void launch_struct_stress(const Launch& L)
+// lanes per structure slot: one lane per slot while the launch has >= kStructLanesTarget lanes
+// (eight waves per SIMD), else the smallest power of two up to 4 that reaches it -- a few ten
+// thousand slots (a gate, a rank's share of one) would otherwise run one long serial list loop per
+// lane on a fraction of the SIMDs.  Same box (profiles/r03/struct_lanes/): FSI gate (40 k slots,
+// 3-D) stress + velocity 0.089 ms at 1 lane, 0.052 at 4, 0.055 at 8; Bar (400 k slots, 2-D)
+// 0.094 at 1, 0.091 at 2, 0.102 at 4.  MPH_STRUCT_LANES=1|2|4|8 fixes it (A/B timing, tests).
+constexpr long kStructLanesTarget = 8L * 1024 * 64;
+
+int struct_lanes(int nslots)
+{
+    const char* e = std::getenv("MPH_STRUCT_LANES");   // read per launch (graphs capture once)
+    const int forced = e ? std::atoi(e) : 0;
+    if (forced == 1 || forced == 2 || forced == 4 || forced == 8) return forced;
+    int g = 1;
+    while (g < 4 && (long)nslots * g < kStructLanesTarget) g *= 2;
+    return g;
+}
+
+#define MPH_STRUCT_G(G, D, KERNEL, NAME, ...)                                                     \
+    MPH_LAUNCH(NAME, L.stream, (KERNEL<D, G>), dim3(blocks((s1 - s0) * G, 256)), dim3(256), 0,   \
+               L.stream, __VA_ARGS__)
+#define MPH_STRUCT_DISPATCH(KERNEL, NAME, ...)                                                    \
+    do {                                                                                          \
+        const int lanes = struct_lanes(S.n_own);   /* not the range: the halves sum alike */     \
+        if (P.dim == 3) {                                                                         \
+            switch (lanes) {                                                                      \
+            case 8: MPH_STRUCT_G(8, 3, KERNEL, NAME, __VA_ARGS__); break;                         \
+            case 4: MPH_STRUCT_G(4, 3, KERNEL, NAME, __VA_ARGS__); break;                         \
+            case 2: MPH_STRUCT_G(2, 3, KERNEL, NAME, __VA_ARGS__); break;                         \
+            default: MPH_STRUCT_G(1, 3, KERNEL, NAME, __VA_ARGS__); break;                        \
+            }                                                                                     \
+        } else {                                                                                  \
+            switch (lanes) {                                                                      \
+            case 8: MPH_STRUCT_G(8, 2, KERNEL, NAME, __VA_ARGS__); break;                         \
+            case 4: MPH_STRUCT_G(4, 2, KERNEL, NAME, __VA_ARGS__); break;                         \
+            case 2: MPH_STRUCT_G(2, 2, KERNEL, NAME, __VA_ARGS__); break;                         \
+            default: MPH_STRUCT_G(1, 2, KERNEL, NAME, __VA_ARGS__); break;                        \
+            }                                                                                     \
+        }                                                                                         \
+    } while (0)
+
+void launch_struct_stress(const Launch& L, bool store, int s0, int s1)
 {
     Profiler* prof = L.prof;
     const DevParams& P = *L.P;
     const StructDev& S = *L.S;
-    const int ns = S.n_own;
-    if (ns <= 0) return;
-    if (P.dim == 3)
-        MPH_LAUNCH("struct_stress", L.stream, k_struct_stress<3>, dim3(blocks(ns, 256)), dim3(256), 0, L.stream,
-                   P, ns, S.wo, S.ocnt, S.eo_nb, S.x0, S.u, S.L, S.lame, S.P, S.F, S.E, S.S);
-    else
-        MPH_LAUNCH("struct_stress", L.stream, k_struct_stress<2>, dim3(blocks(ns, 256)), dim3(256), 0, L.stream,
-                   P, ns, S.wo, S.ocnt, S.eo_nb, S.x0, S.u, S.L, S.lame, S.P, S.F, S.E, S.S);
+    if (s1 < 0) s1 = S.n_own;
+    if (s1 <= s0) return;
+#ifdef MPH_STRUCT_STORE_ALL
+    store = true;   // A/B timing of the output stores
+#endif
+    MPH_STRUCT_DISPATCH(k_struct_stress, "struct_stress", P, s0, s1, S.wo, S.ocnt, S.eo_nb, S.x0, S.u, S.L,
+                        S.lame, S.P, S.F, S.E, S.S, store ? 1 : 0);
 }
 
-void launch_struct_velocity(const Launch& L, bool last)
+void launch_struct_velocity(const Launch& L, bool last, int s0, int s1)
 {
     Profiler* prof = L.prof;
     const DevParams& P = *L.P;
     const StructDev& S = *L.S;
-    const int ns = S.n_own;
-    if (ns <= 0) return;
-    if (P.dim == 3)
-        MPH_LAUNCH("struct_velocity", L.stream, k_struct_velocity<3>, dim3(blocks(ns, 256)), dim3(256), 0,
-                   L.stream, P, ns, S.wi, S.icnt, S.ei_nb, S.wx0, S.P, S.inv_rho, S.clamp, S.x0, S.x, S.v, S.u,
-                   last ? 1 : 0, S.bidx, L.B, L.force);
-    else
-        MPH_LAUNCH("struct_velocity", L.stream, k_struct_velocity<2>, dim3(blocks(ns, 256)), dim3(256), 0,
-                   L.stream, P, ns, S.wi, S.icnt, S.ei_nb, S.wx0, S.P, S.inv_rho, S.clamp, S.x0, S.x, S.v, S.u,
-                   last ? 1 : 0, S.bidx, L.B, L.force);
+    if (s1 < 0) s1 = S.n_own;
+    if (s1 <= s0) return;
+    MPH_STRUCT_DISPATCH(k_struct_velocity, "struct_velocity", P, s0, s1, S.wi, S.icnt, S.ei_nb, S.wx0, S.P,
+                        S.inv_rho, S.clamp, S.x0, S.x, S.v, S.u, last ? 1 : 0, S.bidx, L.B, L.force);
 }
+#undef MPH_STRUCT_DISPATCH
+#undef MPH_STRUCT_G
 
-void launch_structure(const Launch& L)
+void launch_structure(const Launch& L, bool last)
 {
     if (L.P->n_struct == 0) return;
     for (int sub = 0; sub < L.P->substeps; ++sub) {
-        launch_struct_stress(L);
-        launch_struct_velocity(L, sub == L.P->substeps - 1);
+        const bool final_sub = sub == L.P->substeps - 1;
+        launch_struct_stress(L, last && final_sub);
+        launch_struct_velocity(L, final_sub);
     }
 }
 

@@ -154,16 +154,31 @@ def test_rccl_exchange_selftest():
     assert rc == 0, (rc, (L.mph_last_error(None) or b"").decode())
 
 
-@pytest.mark.parametrize("case,world", [("channel3d", 3), ("channel2d", 4)])
+@pytest.mark.parametrize("case,world", [("channel3d", 3), ("channel2d", 4), ("bar2d", 3), ("gate2d_sub", 2)])
 def test_slab_early_send_bitwise(tmp_path, case, world, monkeypatch):
     """The early send of the redistribution messages (MPH_SLAB_EARLY, default on: inside a batch,
-    the next step's messages leave from pass B's face wavefronts while the interior ones run)
-    sends exactly the bytes the late pack would, so every field is bit-identical to
-    MPH_SLAB_EARLY=0 -- over batches of 1, 4 and 15 steps."""
+    the next step's messages leave from pass B's face wavefronts while the interior ones run;
+    with elastic particles, after the substeps) sends exactly the bytes the late pack would, so
+    every field is bit-identical to MPH_SLAB_EARLY=0 -- over batches of 1, 4 and 15 steps."""
+    fields = STRUCT_FIELDS if case.startswith(("bar", "gate")) else FIELDS
     out = {}
     for mode in ("1", "0"):
         monkeypatch.setenv("MPH_SLAB_EARLY", mode)
-        out[mode] = run_slab(case, world, [1, 5, 20], str(tmp_path / ("slab%s.npz" % mode)), local=True)
+        out[mode] = run_slab(case, world, [1, 5, 20], str(tmp_path / ("slab%s.npz" % mode)), fields,
+                             local=True)
+    for k in out["1"].files:
+        assert np.array_equal(out["1"][k], out["0"][k]), k
+
+
+@pytest.mark.parametrize("case,world", [("bar2d", 3), ("bar3d", 2)])
+def test_slab_structure_overlap_bitwise(tmp_path, case, world, monkeypatch):
+    """The elastic ghost exchanges beside the inner slots (the u / P messages on the second stream
+    while the slots whose lists hold no ghost run their half-substep) and the split pass B give
+    the bits of the serial order (MPH_SLAB_OVERLAP=0: halo, one pass B, exchange, every slot)."""
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MPH_SLAB_OVERLAP", mode)
+        out[mode] = run_slab(case, world, [1, 7], str(tmp_path / ("slab%s.npz" % mode)), STRUCT_FIELDS)
     for k in out["1"].files:
         assert np.array_equal(out["1"][k], out["0"][k]), k
 

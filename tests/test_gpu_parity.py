@@ -341,3 +341,30 @@ def test_gpu_fused_search_pass_a_bitwise(case, radii, monkeypatch):
             out[mode] = {f: s.get(f) for f in fields}
     for f in fields:
         assert np.array_equal(out["1"][f], out["0"][f]), (f, float(np.max(np.abs(out["1"][f] - out["0"][f]))))
+
+
+@pytest.mark.parametrize("lanes", ["1", "2", "4", "8"])
+@pytest.mark.parametrize("case", ["bar2d", "gate3d_sub"])
+def test_gpu_struct_lanes_match_oracle(case, lanes, monkeypatch):
+    """The elastic kernels with 1, 2, 4 or 8 lanes per structure slot (MPH_STRUCT_LANES; by
+    default the count follows the slot count): each lane sums every G-th list entry, the group adds
+    the shares in a butterfly -- reassociation only, within the solid bounds above.  Two batches of
+    5 steps, so that the output tensors F, E, S (stored on a batch's last step only) are checked
+    after a batch whose earlier steps skipped them."""
+    from oracle_bindings import OracleSolver
+    monkeypatch.setenv("MPH_STRUCT_LANES", lanes)
+    cfg, parts = cases.get(case).build()
+    o = OracleSolver(cfg, parts)
+    o.init()
+    solid = (parts.property >= 2) & (parts.property < 4)
+    with MphSolver(cfg, parts) as s:
+        for k in (5, 10):
+            s.step(5)
+            o.step(5)
+            for f in ["Position", "Velocity"]:
+                t = {"Position": 1e-12, "Velocity": 1e-9}[f]
+                assert float(np.max(np.abs(s.get(f) - o.get(f)))) <= t, (k, f)
+            for f in ["DeformGradient", "Stress", "Strain"]:
+                a, b = s.get(f)[solid], o.get(f)[solid]
+                t = 1e-8 * float(np.max(np.abs(b))) + FLOOR[f]
+                assert float(np.max(np.abs(a - b))) <= t, (k, f, float(np.max(np.abs(a - b))), t)

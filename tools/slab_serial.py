@@ -3,9 +3,10 @@
 The 8-rank rehearsal (tools/gpu_dist_rehearsal.sh) runs eight processes on one card at once, so
 their kernels overlap and the per-kernel times it reports are inflated by the others.  Here the
 N slab contexts live in one process, one thread each, and move their messages through an
-in-process host exchange; a token serialises the GPU phases between exchanges (a context has
-synchronised its stream before it calls the host exchange, and each thread synchronises before
-it gives the token back at the end of a call), so every rank's kernels run alone on the card and
+in-process host exchange; a token serialises the GPU phases between exchanges (the device is
+drained before a rank gives the token back inside the host exchange -- its second stream may
+still run the kernels it enqueued before the exchange -- and each thread synchronises before it
+gives the token back at the end of a call), so every rank's kernels run alone on the card and
 the HIP-event profile of each rank is what that rank would see on its own GPU.
 
 usage: python tools/slab_serial.py [--case d16m] [--ranks 8] [--steps 4] [--warmup 2]
@@ -32,6 +33,19 @@ from particlemethod_fsi_amd.dist import balanced_cuts, build_local  # noqa: E402
 SLAB_AXIS = {2: 0, 3: 2}
 
 
+_HIP = None
+
+
+def _device_sync():
+    global _HIP
+    if _HIP is None:
+        import ctypes
+        _HIP = ctypes.CDLL("libamdhip64.so")
+    rc = _HIP.hipDeviceSynchronize()
+    if rc != 0:
+        raise RuntimeError("hipDeviceSynchronize: %d" % rc)
+
+
 class Token:
     """The GPU: held by one rank thread while it launches work."""
 
@@ -48,6 +62,9 @@ class InProcExchange:
         self.left, self.right = (rank - 1) % nranks, (rank + 1) % nranks
 
     def __call__(self, send_l, send_r, recv_l, recv_r):
+        # the rank's other stream may still run kernels it enqueued before this exchange (the
+        # inner pass B / inner elastic slots): drain the device before another rank takes it
+        _device_sync()
         self.token.lock.release()
         try:
             if len(send_l):
