@@ -68,11 +68,20 @@ def gloo_slab(rank: int, nranks: int, axis: int, group=None, ids=None, n_glob: i
                        cuts=cuts)
 
 
-def balanced_cuts(case, nranks: int, axis: int) -> np.ndarray:
-    """Interior slab boundaries (MphSlabOptions.cuts) that give every rank the same share of the
-    initial particles: count quantiles of the case's lattice planes along `axis`
-    (mphio.plane_counts), each cut halfway between two planes.  Deterministic, so every rank
-    computes the same array."""
+# Relative GPU cost of a ghost particle against an owned one: the per-rank GPU times of D16M in 8
+# slabs, one rank at a time (tools/slab_serial.py, profiles/r03/slab/), fit t = a owned + b ghosts
+# with a ~0.83 and b ~0.6 ms per million (ghosts are sorted, packed, exchanged and unpacked, and
+# their mixed waves run the list loops, but they compute no sums of their own).
+GHOST_WEIGHT = 0.7
+
+
+def balanced_cuts(case, nranks: int, axis: int, ghost_weight: float | None = None) -> np.ndarray:
+    """Interior slab boundaries (MphSlabOptions.cuts) that balance the ranks' GPU work: the largest
+    per-rank cost  owned + ghost_weight x ghosts  is minimised over cuts halfway between the case's
+    lattice planes along `axis` (mphio.plane_counts; ghosts: the planes within one halo of an
+    interior face, periodic).  ghost_weight 0 (or MPH_SLAB_GHOST_WEIGHT=0): equal shares of the
+    initial particles, the count quantiles.  Deterministic, so every rank computes the same array."""
+    import os
     cfg, _ = case._config()
     dmin = cfg.domain_min[axis]
     W = cfg.domain_max[axis] - dmin
@@ -84,7 +93,60 @@ def balanced_cuts(case, nranks: int, axis: int) -> np.ndarray:
         p = int(np.searchsorted(cum, total * k / nranks))   # first plane reaching the quantile
         p = min(p, len(v) - 2)
         cuts.append(0.5 * (v[p] + v[p + 1]))
-    return np.array(cuts, np.float64)
+    cuts = np.array(cuts, np.float64)
+    if ghost_weight is None:
+        ghost_weight = float(os.environ.get("MPH_SLAB_GHOST_WEIGHT", GHOST_WEIGHT))
+    if ghost_weight <= 0.0 or nranks < 2 or len(v) < 2:
+        return cuts
+    halo = solver.slab_bounds(cfg, 0, nranks, axis, cuts)[2]
+    min_width = 2.0 * halo + 2.0 * cfg.particle_spacing   # the slab context's own lower bound
+    csum = np.concatenate([[0], cum])
+
+    def count(a, b):   # particles on the planes in [a, b), periodic, b - a <= W
+        a0 = dmin + (a - dmin) % W
+        b0 = a0 + (b - a)
+        n = csum[np.searchsorted(v, min(b0, dmin + W), "left")] - csum[np.searchsorted(v, a0, "left")]
+        if b0 > dmin + W:
+            n += csum[np.searchsorted(v, b0 - W, "left")]
+        return int(n)
+
+    def cost(lo, hi):
+        return count(lo, hi) + ghost_weight * (count(lo - halo, lo) + count(hi, hi + halo))
+
+    mids = 0.5 * (v[:-1] + v[1:])
+
+    def place(T):   # greedy: each slab as wide as the bound allows (leaving room for the rest)
+        out, lo, k = [], dmin, 0
+        for r in range(nranks - 1):
+            best = None
+            room = dmin + W - (nranks - 1 - r) * min_width
+            while k < len(mids) and mids[k] <= room and cost(lo, mids[k]) <= T:
+                if mids[k] - lo >= min_width:
+                    best = k
+                k += 1
+            if best is None:
+                return None
+            out.append(mids[best])
+            lo = mids[best]
+            k = best + 1
+        if dmin + W - lo < min_width or cost(lo, dmin + W) > T:
+            return None
+        return out
+
+    # bisection below the quantile cuts' largest cost (the greedy's feasibility is monotone near
+    # the optimum, not for bounds so loose that the room left for the last slabs decides)
+    edges = np.concatenate([[dmin], cuts, [dmin + W]])
+    lo_t = 0.0
+    hi_t = max(cost(edges[r], edges[r + 1]) for r in range(nranks))
+    best = None
+    for _ in range(60):
+        mid = 0.5 * (lo_t + hi_t)
+        got = place(mid)
+        if got is None:
+            lo_t = mid
+        else:
+            hi_t, best = mid, got
+    return np.array(best, np.float64) if best is not None else cuts
 
 
 def build_local(case, rank: int, nranks: int, axis: int, cuts=None):

@@ -80,8 +80,9 @@ def test_halo_band_contains_all_neighbours(tmp_path, world):
 @pytest.mark.parametrize("case,nranks", [("d16m", 8), ("d16m", 2), ("d1m", 4), ("dam2d", 3)])
 def test_balanced_cuts_equalise_shares(case, nranks):
     """dist.balanced_cuts (bench.py's slab boundaries): the cuts ascend inside the domain, the
-    library's bounds/owner functions follow them, and the initial particles split into shares
-    within one lattice plane of equal."""
+    library's bounds/owner functions follow them, the initial particles split into shares within
+    two lattice planes of equal, and the largest cost owned + GHOST_WEIGHT x ghosts is no larger
+    than with the count quantiles (ghost_weight=0), which it improves at D16M / 8."""
     from particlemethod_fsi_amd import mphio
     from particlemethod_fsi_amd.dist import balanced_cuts
     c = cases.get(case)
@@ -101,6 +102,20 @@ def test_balanced_cuts_equalise_shares(case, nranks):
     assert share.max() - share.min() <= 2 * n.max(), share
     # equal slabs are the cuts=None default
     assert solver.slab_bounds(cfg, 1, nranks, axis) == solver.slab_bounds(cfg, 1, nranks, axis, None)
+    from particlemethod_fsi_amd.dist import GHOST_WEIGHT
+    halo = b[0][2]
+
+    def max_cost(cs):
+        e = np.concatenate([[dmin], cs, [cfg.domain_max[axis]]])
+        own = [n[(v >= e[r]) & (v < e[r + 1])].sum() for r in range(nranks)]
+        gh = [n[((v >= e[r] - halo) & (v < e[r])) | ((v >= e[r + 1]) & (v < e[r + 1] + halo))].sum()
+              for r in range(nranks)]
+        return max(o + GHOST_WEIGHT * g for o, g in zip(own, gh))
+
+    quant = balanced_cuts(c, nranks, axis, ghost_weight=0.0)
+    assert max_cost(cuts) <= max_cost(quant)
+    if (case, nranks) == ("d16m", 8):
+        assert max_cost(cuts) < 0.98 * max_cost(quant)
 
 
 def test_bad_cuts_rejected():
