@@ -30,6 +30,10 @@ struct MphDist {
     size_t region = 0;            // bytes of each of the four message buffers
     mph::Soa C;                   // redistributed state (pre-sort order)
     int* cls = nullptr;           // class of every B entry
+    // the kept entries of C stay in B (VSrc: C holds the received tail only, vidx[v] = where
+    // entry v lives in B); MPH_SLAB_VIRTUAL_C=0 copies them into C
+    int* vidx = nullptr;
+    bool virt = !(std::getenv("MPH_SLAB_VIRTUAL_C") && std::string(std::getenv("MPH_SLAB_VIRTUAL_C")) == "0");
     int* bcnt = nullptr;          // per (class, block) counts -> offsets
     int* boff = nullptr;
     int* bsum = nullptr;

@@ -278,6 +278,19 @@ hipError_t stream_wait(Profiler* prof, hipStream_t waiting, hipEvent_t ev, hipSt
     return hipStreamWaitEvent(waiting, ev, 0);
 }
 
+// the redistributed set's kept entries: where they live in B (VSrc, D.virt) or nowhere (in C)
+VSrc dist_vsrc(MphCtx* c)
+{
+    MphDist& D = *c->dist;
+    VSrc vs;
+    if (D.virt) {
+        vs.idx = D.vidx;
+        vs.n = lay_field<int>(D.lay, offsetof(DistLayout, seg)) + kSlabDrop;
+        vs.V = c->L.B;
+    }
+    return vs;
+}
+
 // Steps 1-3 of the protocol: classify, partition, exchange migrants + ghosts.  Leaves the new
 // local set (owned and ghosts) in D.C and its sizes in D.lay -- on the device: nothing here reads
 // a size on the host, so the step can be captured.  init: first redistribution of mph_create,
@@ -294,7 +307,8 @@ int redistribute(MphCtx* c, bool move, bool init, Profiler* prof, bool early_in 
     if (early_in) MPH_HIP_OK(c, hipStreamWaitEvent(c->stream, D.ev_s, 0));
     launch_dist_classify(L, D.g, D.cap, D.lay, move ? 1 : 0, D.cls, D.bcnt, early_in ? D.wface : nullptr);
     launch_scan(D.bcnt, kSlabClasses * nb, D.bsum, D.boff, 0, c->stream, prof);
-    launch_dist_scatter(L, D.cap, D.lay, D.cls, D.boff, D.C, lay_field<int>(D.lay, offsetof(DistLayout, seg)));
+    launch_dist_scatter(L, D.cap, D.lay, D.cls, D.boff, D.C, lay_field<int>(D.lay, offsetof(DistLayout, seg)),
+                        D.virt ? D.vidx : nullptr);
     launch_dist_counts(L, D.lay);
     if (early_in) {
         MPH_HIP_OK(c, stream_wait(prof, c->stream, D.ev_x, D.stream2));
@@ -318,8 +332,9 @@ int redistribute(MphCtx* c, bool move, bool init, Profiler* prof, bool early_in 
         D.cap_rr = msg_capacity0(h.recv[2] + h.recv[3]);
         MPH_CK(msg_alloc(c));
     }
-    launch_dist_pack(L, D.C, D.lay, 0, D.cap_sl, D.send_l);
-    launch_dist_pack(L, D.C, D.lay, 1, D.cap_sr, D.send_r);
+    const VSrc vs = dist_vsrc(c);
+    launch_dist_pack(L, D.C, D.lay, 0, D.cap_sl, D.send_l, vs);
+    launch_dist_pack(L, D.C, D.lay, 1, D.cap_sr, D.send_r, vs);
     MPH_CK(exchange(c, c->stream, D.send_l, kMsgHead + kMsgBytes * D.cap_sl, D.send_r,
                     kMsgHead + kMsgBytes * D.cap_sr, D.recv_l, kMsgHead + kMsgBytes * D.cap_rl, D.recv_r,
                     kMsgHead + kMsgBytes * D.cap_rr));
@@ -358,6 +373,7 @@ void sort_local(MphCtx* c, int mode, Profiler* prof)
     Launch L = c->L;
     L.prof = prof;
     L.B = c->dist->C;
+    L.vsrc = dist_vsrc(c);
     L.dst_of = c->rank_of;
     launch_sort(L, mode);
 }
@@ -618,6 +634,7 @@ int dist_alloc(MphCtx* c)
     MPH_CK(ctx_dalloc(c, &C.vx, cap)); MPH_CK(ctx_dalloc(c, &C.vy, cap)); MPH_CK(ctx_dalloc(c, &C.vz, cap));
     MPH_CK(ctx_dalloc(c, &C.type, cap)); MPH_CK(ctx_dalloc(c, &C.id, cap));
     MPH_CK(ctx_dalloc(c, &D.cls, cap));
+    MPH_CK(ctx_dalloc(c, &D.vidx, cap));
     MPH_CK(ctx_dalloc(c, &D.wface, (size_t)cap / 64 + 2));
     MPH_HIP_OK(c, hipMemsetAsync(D.wface, 0, sizeof(int) * ((size_t)cap / 64 + 2), c->stream));
     const size_t nslots = (size_t)kSlabClasses * dist_blocks(cap);

@@ -62,6 +62,15 @@ struct Soa {
     double2* p6 = nullptr;
 };
 
+// Slab mode: the kept part [0, *n) of the redistributed set C is not copied -- entry v lives in
+// the integrated set V at idx[v] (-1 - q: a migrant leaving as a ghost, its id negated on read);
+// only the received tail [*n, ...) is in C itself.  idx null: C holds everything (single context).
+struct VSrc {
+    const int* idx = nullptr;
+    const int* n = nullptr;
+    Soa V;
+};
+
 // Pass B hands the integrated structure particles straight to the slot-ordered elastic arrays
 // (null slot_of: no structure particles) and records where each slot's B entry lives (bidx), so
 // the last substep can write the result back.
@@ -88,6 +97,7 @@ struct Launch {
     int2* hdr = nullptr;          // per-wave headers of the column-segmented lists (kSegHdr each)
     int* lhdr = nullptr;          // per-wave headers of the compact 16-bit lists (kLhdr each)
     int* wface = nullptr;         // slab mode: face-wavefront flags written by pass B (early send)
+    VSrc vsrc;                    // slab mode: where the sort finds the kept entries of its input
     bool fused = true;            // search + pass A in one kernel (k_search_pass_a; MPH_FUSED=0: two)
     // pass A products (A order): pressure values, gravity centre (GC, PressureA), sums
     double *pres = nullptr, *gx = nullptr, *gy = nullptr, *gz = nullptr, *pa = nullptr;
@@ -138,10 +148,12 @@ void launch_dist_early_classify(const Launch& L, const SlabGeom& g, int cap, con
                                 const int* wface, int* cls, int* bcnt);
 void launch_dist_early_pack(const Launch& L, int cap, DistLayout* lay, const int* cls, const int* boff, int cap_l,
                             int cap_r, char* buf_l, char* buf_r);
+// vidx non-null: record the B index of every kept entry (VSrc) instead of copying it into C
 void launch_dist_scatter(const Launch& L, int cap, const DistLayout* lay, const int* cls, const int* boff,
-                         const Soa& C, int* dseg);
+                         const Soa& C, int* dseg, int* vidx = nullptr);
 void launch_dist_counts(const Launch& L, DistLayout* lay);
-void launch_dist_pack(const Launch& L, const Soa& C, DistLayout* lay, int side, int cap_msg, char* buf);
+void launch_dist_pack(const Launch& L, const Soa& C, DistLayout* lay, int side, int cap_msg, char* buf,
+                      const VSrc& vs = VSrc{});
 void launch_dist_unpack(const Launch& L, const char* buf_l, const char* buf_r, DistLayout* lay, int side,
                         int cap_msg, int cap, const Soa& C);
 void launch_halo_pack(const Launch& L, const int* dst_of, const DistLayout* lay, int dir, int cap,

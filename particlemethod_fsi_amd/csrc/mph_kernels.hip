@@ -434,12 +434,30 @@ __device__ __forceinline__ void move_and_wrap(const DevParams& P, const DevState
     B.z[p] = z;
 }
 
-__global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __restrict__ st, Soa B,
+// entry p of a sort input C: its set (C or the VSrc's V) and index there; mig: a kept migrant
+// (its id is read negated)
+__device__ __forceinline__ int vsrc_entry(const VSrc& vs, const Soa& C, int p, Soa& S, bool& mig)
+{
+    S = C;
+    mig = false;
+    if (vs.idx && p < *vs.n) {
+        const int q = vs.idx[p];
+        mig = q < 0;
+        S = vs.V;
+        return mig ? -1 - q : q;
+    }
+    return p;
+}
+
+__global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __restrict__ st, Soa C,
                                               int* __restrict__ key, int* __restrict__ slot,
-                                              int* __restrict__ cnt, int mode)
+                                              int* __restrict__ cnt, int mode, VSrc vs)
 {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     const int n = dev_n(P);
+    Soa B = C;
+    bool mig = false;
+    const int b = p < n ? vsrc_entry(vs, C, p, B, mig) : p;
     if (MPH_PREP_RUNS) {
         // The particles arrive in the previous cell order, so consecutive lanes often share a
         // cell: one histogram atomic per run of equal keys (slot = run base + rank in the run).
@@ -447,8 +465,8 @@ __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __res
         const bool live = p < n;
         int k = -1 - (int)(threadIdx.x & 63);
         if (live) {
-            double x = B.x[p], y = B.y[p], z = B.z[p];
-            if (mode == 1) move_and_wrap(P, st, B, p, x, y, z);
+            double x = B.x[b], y = B.y[b], z = B.z[b];
+            if (mode == 1) move_and_wrap(P, st, B, b, x, y, z);
             if (!isfinite(x + y + z)) atomicOr(const_cast<int*>(&st->overflow), 4);   // MPH_ERR_NONFINITE
             k = cell_id(P, x, y, z);
             key[p] = k;
@@ -468,8 +486,8 @@ __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __res
         return;
     }
     if (p >= n) return;
-    double x = B.x[p], y = B.y[p], z = B.z[p];
-    if (mode == 1) move_and_wrap(P, st, B, p, x, y, z);
+    double x = B.x[b], y = B.y[b], z = B.z[b];
+    if (mode == 1) move_and_wrap(P, st, B, b, x, y, z);
     if (!isfinite(x + y + z)) atomicOr(const_cast<int*>(&st->overflow), 4);   // MPH_ERR_NONFINITE
     const int k = cell_id(P, x, y, z);
     key[p] = k;
@@ -638,9 +656,9 @@ __global__ __launch_bounds__(256) void k_place(DevParams P, DevState* __restrict
 // sorted index.  Reorders the persistent particle state into the new cell order.
 __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __restrict__ key,
                                                       const int* __restrict__ start,
-                                                      const int* __restrict__ tmp, Soa B, Soa A,
+                                                      const int* __restrict__ tmp, Soa C, Soa A,
                                                       int* __restrict__ rank_of, int* __restrict__ dst_of,
-                                                      int mode)
+                                                      int mode, VSrc vs)
 {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= dev_n(P)) return;
@@ -649,25 +667,28 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
     int r = 0;
     for (int q = s; q < e; ++q) r += tmp[q] < p;
     const int dst = s + r;
-    A.x[dst] = B.x[p];
-    A.y[dst] = B.y[p];
-    A.z[dst] = B.z[p];
+    Soa B;
+    bool mig;
+    const int b = vsrc_entry(vs, C, p, B, mig);
+    A.x[dst] = B.x[b];
+    A.y[dst] = B.y[b];
+    A.z[dst] = B.z[b];
     // the sorted velocities are read only through the 48-byte records (own_velocity below), unless
     // the passes gather SoA (MPH_AOS_GATHER=0, or the segmented lists of MPH_SEG), or at a slab
     // context's initialisation sort (mode 0: dist_init copies the sorted set into B)
     if (!MPH_AOS_GATHER || MPH_SEG || !A.p6 || (dst_of && mode == 0)) {
-        A.vx[dst] = B.vx[p];
-        A.vy[dst] = B.vy[p];
-        A.vz[dst] = B.vz[p];
+        A.vx[dst] = B.vx[b];
+        A.vy[dst] = B.vy[b];
+        A.vz[dst] = B.vz[b];
     }
-    A.type[dst] = B.type[p];
-    const int id = B.id[p];
+    A.type[dst] = B.type[b];
+    const int id = mig ? -1 - B.id[b] : B.id[b];
     A.id[dst] = id;
     if (A.p6) {
         double2* q = A.p6 + 3 * (size_t)dst;
-        q[0] = make_double2(B.x[p], B.y[p]);
-        q[1] = make_double2(B.z[p], B.vx[p]);
-        q[2] = make_double2(B.vy[p], B.vz[p]);
+        q[0] = make_double2(B.x[b], B.y[b]);
+        q[1] = make_double2(B.z[b], B.vx[b]);
+        q[2] = make_double2(B.vy[b], B.vz[b]);
     }
     if (dst_of) dst_of[p] = dst;   // slab mode: ids are global (ghosts negative)
     else if (rank_of) rank_of[id] = dst;
@@ -2980,7 +3001,7 @@ __global__ __launch_bounds__(256) void k_dist_early_pack(Soa B, DistLayout* __re
 __global__ __launch_bounds__(256) void k_dist_scatter(Soa B, const DistLayout* __restrict__ lay,
                                                       const int* __restrict__ cls,
                                                       const int* __restrict__ boff, int nb, Soa C,
-                                                      int* __restrict__ dseg)
+                                                      int* __restrict__ dseg, int* __restrict__ vidx)
 {
     __shared__ int wc[4][kSlabClasses];
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2999,6 +3020,10 @@ __global__ __launch_bounds__(256) void k_dist_scatter(Soa B, const DistLayout* _
     if (c < 0 || c == kSlabDrop) return;
     int o = boff[c * nb + blockIdx.x] + rank;
     for (int w = 0; w < wave; ++w) o += wc[w][c];
+    if (vidx) {   // VSrc: only where the entry lives
+        vidx[o] = (c == kMigR || c == kMigL) ? -1 - p : p;
+        return;
+    }
     C.x[o] = B.x[p]; C.y[o] = B.y[p]; C.z[o] = B.z[p];
     C.vx[o] = B.vx[p]; C.vy[o] = B.vy[p]; C.vz[o] = B.vz[p];
     C.type[o] = B.type[p];
@@ -3040,7 +3065,7 @@ __device__ __forceinline__ void dist_recv_range(const DistLayout* lay, const int
 // needed per step), then x[m] y[m] z[m] vx[m] vy[m] vz[m] (double) type[m] id[m] (int), 56 B per
 // particle (kMsgHeader above)
 __global__ __launch_bounds__(256) void k_dist_pack(Soa C, DistLayout* __restrict__ lay, int side, int cap,
-                                                   DevState* __restrict__ st, char* __restrict__ buf)
+                                                   DevState* __restrict__ st, char* __restrict__ buf, VSrc vs)
 {
     int off, m;
     dist_send_range(lay, side, off, m);
@@ -3058,11 +3083,13 @@ __global__ __launch_bounds__(256) void k_dist_pack(Soa C, DistLayout* __restrict
     if (k >= m) return;
     double* d = (double*)(buf + kMsgHeader);
     int* q = (int*)(d + 6 * (size_t)m);
-    const int s = off + k;
-    d[k] = C.x[s]; d[m + k] = C.y[s]; d[2 * m + k] = C.z[s];
-    d[3 * m + k] = C.vx[s]; d[4 * m + k] = C.vy[s]; d[5 * m + k] = C.vz[s];
-    q[k] = C.type[s];
-    q[m + k] = C.id[s];
+    Soa S;
+    bool mig;
+    const int s = vsrc_entry(vs, C, off + k, S, mig);   // the sent classes are all kept entries
+    d[k] = S.x[s]; d[m + k] = S.y[s]; d[2 * m + k] = S.z[s];
+    d[3 * m + k] = S.vx[s]; d[4 * m + k] = S.vy[s]; d[5 * m + k] = S.vz[s];
+    q[k] = S.type[s];
+    q[m + k] = mig ? -1 - S.id[s] : S.id[s];
 }
 
 // received message -> C[off, off+m); ownership flips (their migrants are ours, their band
@@ -3206,7 +3233,7 @@ void launch_sort(const Launch& L, int mode)
     const int n = P.n;
     if (n == 0) return;
     MPH_LAUNCH("prep", L.stream, k_prep, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.B,
-               L.key, L.slot, L.cnt, mode);
+               L.key, L.slot, L.cnt, mode, L.vsrc);
     const int nb = blocks(P.ncell, kScanBlock);
     const int top = nb <= kScanFusedTop;
     MPH_LAUNCH("scan_reduce", L.stream, k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt,
@@ -3217,7 +3244,7 @@ void launch_sort(const Launch& L, int mode)
     MPH_LAUNCH("place", L.stream, k_place, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.key,
                L.slot, L.start, L.tmp, mode);
     MPH_LAUNCH("rank_scatter", L.stream, k_rank_scatter, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P,
-               L.key, L.start, L.tmp, L.B, L.A, L.rank_of, L.dst_of, mode);
+               L.key, L.start, L.tmp, L.B, L.A, L.rank_of, L.dst_of, mode, L.vsrc);
 }
 
 static PassAOut pass_a_out(const Launch& L)
@@ -3548,12 +3575,12 @@ void launch_dist_early_pack(const Launch& L, int cap, DistLayout* lay, const int
 }
 
 void launch_dist_scatter(const Launch& L, int cap, const DistLayout* lay, const int* cls, const int* boff,
-                         const Soa& C, int* dseg)
+                         const Soa& C, int* dseg, int* vidx)
 {
     Profiler* prof = L.prof;
     const int nb = dist_blocks(cap);
     MPH_LAUNCH("dist_scatter", L.stream, k_dist_scatter, dim3(nb), dim3(256), 0, L.stream, L.B, lay, cls, boff,
-               nb, C, dseg);
+               nb, C, dseg, vidx);
 }
 
 void launch_dist_counts(const Launch& L, DistLayout* lay)
@@ -3562,11 +3589,12 @@ void launch_dist_counts(const Launch& L, DistLayout* lay)
     MPH_LAUNCH("dist_counts", L.stream, k_dist_counts, dim3(1), dim3(64), 0, L.stream, lay);
 }
 
-void launch_dist_pack(const Launch& L, const Soa& C, DistLayout* lay, int side, int cap_msg, char* buf)
+void launch_dist_pack(const Launch& L, const Soa& C, DistLayout* lay, int side, int cap_msg, char* buf,
+                      const VSrc& vs)
 {
     Profiler* prof = L.prof;
     MPH_LAUNCH("dist_pack", L.stream, k_dist_pack, dim3(dist_blocks(cap_msg)), dim3(256), 0, L.stream, C, lay,
-               side, cap_msg, L.st, buf);
+               side, cap_msg, L.st, buf, vs);
 }
 
 void launch_dist_unpack(const Launch& L, const char* buf_l, const char* buf_r, DistLayout* lay, int side,

@@ -9,7 +9,14 @@ still run the kernels it enqueued before the exchange -- and each thread synchro
 gives the token back at the end of a call), so every rank's kernels run alone on the card and
 the HIP-event profile of each rank is what that rank would see on its own GPU.
 
-usage: python tools/slab_serial.py [--case d16m] [--ranks 8] [--steps 4] [--warmup 2]
+With --replay (default) the profiled steps run a second time from a fresh start: every rank
+then receives the messages recorded in the first run at once (bit-identical runs), holds the
+token through its whole profile call and does not drain the device in an exchange, so its second
+stream runs beside its main stream as on a rank of its own (the inner pass B / inner elastic
+slots beside the halo, the face pass B and the early send) -- the exchange latency left is the
+host staging's own copies.  The first run's figures are "serialised", the replay's "replay".
+
+usage: python tools/slab_serial.py [--case d16m] [--ranks 8] [--steps 4] [--warmup 2] [--no-replay]
 prints one JSON line: per-rank kernel averages, held/owned counts, their GPU time per step (the
 sum of the kernel times, and gpu_busy: the union of the kernel intervals, less than the sum where
 the kernels of the two streams run concurrently).
@@ -60,8 +67,22 @@ class InProcExchange:
     def __init__(self, rank, nranks, boxes, token):
         self.rank, self.nranks, self.boxes, self.token = rank, nranks, boxes, token
         self.left, self.right = (rank - 1) % nranks, (rank + 1) % nranks
+        self.record = None   # list: the received messages are appended (first run)
+        self.replay = None   # iterator over recorded (recv_l, recv_r): no peers, no token hand-over
 
     def __call__(self, send_l, send_r, recv_l, recv_r):
+        if self.replay is not None:
+            bl, br = next(self.replay)
+            if len(bl) != len(recv_l) or len(br) != len(recv_r):
+                raise RuntimeError("replayed exchange differs from the recorded one")
+            recv_l[:] = bl
+            recv_r[:] = br
+            return
+        self._live(send_l, send_r, recv_l, recv_r)
+        if self.record is not None:
+            self.record.append((bytes(recv_l), bytes(recv_r)))
+
+    def _live(self, send_l, send_r, recv_l, recv_r):
         # the rank's other stream may still run kernels it enqueued before this exchange (the
         # inner pass B / inner elastic slots): drain the device before another rank takes it
         _device_sync()
@@ -87,17 +108,39 @@ def main():
     ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-replay", dest="replay", action="store_false")
     args = ap.parse_args()
     case = cases.get(args.case)
     axis = SLAB_AXIS[case.dim]
     R = args.ranks
+    cuts = None if os.environ.get("MPH_SLAB_EQUAL") == "1" else balanced_cuts(case, R, axis)
+    locals_ = [build_local(case, r, R, axis, cuts) for r in range(R)]
+    records = [[] for _ in range(R)]
+    serial = run_ranks(args, R, axis, cuts, locals_, records=records)
+    result = {"case": args.case, "ranks": R, "perm": os.environ.get("MPH_SLAB_PERM", "default"),
+              "cuts": [float(c) for c in cuts] if cuts is not None else None}
+    result.update(summary(serial))
+    result["per_rank"] = serial
+    if args.replay:
+        rep = run_ranks(args, R, axis, cuts, locals_, replay=records)
+        result["replay"] = dict(summary(rep), per_rank=rep)
+    print(json.dumps(result))
+
+
+def summary(out):
+    return {"max_rank_gpu_ms_per_step": max(o["gpu_ms_per_step"] for o in out),
+            "max_rank_gpu_busy_ms_per_step": max(o["gpu_busy_ms_per_step"] or 0.0 for o in out)}
+
+
+def run_ranks(args, R, axis, cuts, locals_, records=None, replay=None):
+    """One run of the R rank threads: create, warm up, profile.  records: per-rank lists that
+    collect the profiled steps' received messages; replay: such lists, handed to the profiled
+    steps instead of the peers' messages."""
     token = Token()
     boxes = {}
     for r in range(R):
         for d, peer in (("L", (r - 1) % R), ("R", (r + 1) % R)):
             boxes[(r, peer, d)] = queue.Queue()
-    cuts = None if os.environ.get("MPH_SLAB_EQUAL") == "1" else balanced_cuts(case, R, axis)
-    locals_ = [build_local(case, r, R, axis, cuts) for r in range(R)]
     out = [None] * R
     errs = []
 
@@ -112,11 +155,16 @@ def main():
             with token.lock:
                 s.step(args.warmup)
                 s.synchronize()
+            if records is not None:
+                ex.record = records[r]
+            if replay is not None:
+                ex.replay = iter(replay[r])
             with token.lock:
                 t0 = time.perf_counter()
                 prof = s.profile(args.steps)
                 s.synchronize()
                 wall = time.perf_counter() - t0
+            ex.record = ex.replay = None
             info = s.dist_info()
             busy = prof.pop("gpu_busy", {}).get("avg_ms")   # union of the kernel intervals per step
             out[r] = {"rank": r, "owned": len(s.owned_ids()), "held": info["held"],
@@ -139,11 +187,7 @@ def main():
     if errs:
         print(json.dumps({"errors": errs}))
         sys.exit(1)
-    worst = max(o["gpu_ms_per_step"] for o in out)
-    busy = max(o["gpu_busy_ms_per_step"] or 0.0 for o in out)
-    print(json.dumps({"case": args.case, "ranks": R, "perm": os.environ.get("MPH_SLAB_PERM", "default"),
-                      "max_rank_gpu_ms_per_step": worst, "max_rank_gpu_busy_ms_per_step": busy,
-                      "per_rank": out}))
+    return out
 
 
 if __name__ == "__main__":
