@@ -67,8 +67,15 @@
 #ifndef MPH_SEARCH_LDS
 #define MPH_SEARCH_LDS 1
 #endif
+#ifndef MPH_COLRANGE32
+#define MPH_COLRANGE32 1   // the search's per-column candidate ranges in FP32 (outward margins)
+#endif
 #ifndef MPH_SEARCH_PREFETCH
-#define MPH_SEARCH_PREFETCH 1   // pipeline the per-column start[] loads of the LDS search
+// pipeline the per-column start[] loads of the LDS search, 1 or 2 columns ahead (same box, D1M
+// search: 0.405 ms at 1 with FP64 ranges, 0.396 with FP32 ranges, 0.389 at 2; D16M 4.41 / 4.45 / 4.37;
+// profiles/r03/search/).  A search that only sets the columns up (MPH_DIAG_SEARCH=2) takes 0.21 ms
+// of the 0.39: the per-column chain start[] -> window -> staging is latency-bound.
+#define MPH_SEARCH_PREFETCH 2
 #endif
 #ifndef MPH_PREP_RUNS
 #define MPH_PREP_RUNS 1   // k_prep: one cell-histogram atomic per run of equal keys in a wave
@@ -263,6 +270,8 @@ constexpr int kSpan16 = (1 << kOff16) - 1;  // longest group range a compact wav
 #ifndef MPH_GB_LDS
 #define MPH_GB_LDS 1   // group base of an entry read from LDS (else a select tree)
 #endif
+static_assert(kTile == 64, "list rows are addressed as (k << 8) | (lane << 2) bytes");
+
 struct NbrList {
     const int* tile;                // the wave's list tile (wave-uniform)
     int lane;
@@ -327,7 +336,12 @@ __device__ __forceinline__ void nbr_at(const NbrList& L, int k, int& j, int& t)
         j = b + (int)(e & kSpan16);
         t = (int)(e >> kOff16);
     } else {
-        const int e = list_load(L.tile + k * kTile + L.lane);
+        // row k of the wave's tile by a 32-bit byte offset from its (SGPR) base: one shift-or per
+        // entry instead of 64-bit address arithmetic
+        using gcchar = const __attribute__((address_space(1))) char;
+        using gcint = const __attribute__((address_space(1))) int;
+        gcint* p = (gcint*)((gcchar*)L.tile + (((unsigned)k << 8) | ((unsigned)L.lane << 2)));
+        const int e = MPH_LIST_NT ? __builtin_nontemporal_load(p) : *p;
         j = e & kIndexMask;
         t = e >> kTypeShift;
     }
@@ -1107,6 +1121,55 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     constexpr float kDn = 1.0f - 1.0f / (1 << 20), kUp = 1.0f + 1.0f / (1 << 19);
     const float rcm2f = (float)rcm2 * kUp;
     float gx2f = 0.0f;
+#if MPH_COLRANGE32
+    // FP32 column ranges from per-lane values computed once (the offsets inside the own cell, the
+    // cell coordinate along the contiguous axis, the row base): every rounding goes outwards by an
+    // absolute margin (gaps down by 2^-20 cell widths, the range ends out by 1e-3 cells), so each
+    // range holds the FP64 one of col_range below -- a superset, the exact test decides.
+    const int c0l = cc[X::A0], c1l = DIM == 3 ? cc[X::A1] : 0;
+    const float cw0f = (float)cw0, cw1f = (float)cw1;
+    const float f0 = (float)(uu[X::A0] - c0l * cw0), f1 = DIM == 3 ? (float)(uu[X::A1] - c1l * cw1) : 0.0f;
+    const float g0p = f0, g0m = cw0f - f0, g1p = f1, g1m = cw1f - f1;   // subtracted for d > 0 / d < 0
+    const float mu0 = cw0f * (1.0f / (1 << 20)), mu1 = cw1f * (1.0f / (1 << 20));
+    const float ginvaf = (float)ginva;
+    const float caf = (float)(ua * ginva);   // cell coordinate along the contiguous axis
+    const int rowbase = DIM == 3 ? (c0l * P.gc[X::A1] + c1l) * P.gc[X::A2] : c0l * P.gc[1];
+    const int clo = cca - P.sa, chi = cca + P.sa;
+    auto gap32 = [](int d, float cwf, float gp, float gm, float mu) {
+        if (d == 0) return 0.0f;
+        const float v = (float)(d > 0 ? d : -d) * cwf - (d > 0 ? gp : gm) - mu;
+        return v > 0.0f ? v : 0.0f;
+    };
+    auto col_range = [&](int col, int& jb, int& je) {
+        int cofs;
+        float d2f;
+        if (DIM == 3) {
+            const int dxc = col / kGroups - kReach, dyc = col % kGroups - kReach;
+            if (dyc == -kReach) {
+                const float gx = gap32(dxc, cw0f, g0p, g0m, mu0);
+                gx2f = gx * gx * kDn;
+            }
+            const float gy = gap32(dyc, cw1f, g1p, g1m, mu1);
+            d2f = (gx2f + gy * gy * kDn) * kDn;
+            cofs = (dxc * P.gc[X::A1] + dyc) * P.gc[X::A2];
+        } else {
+            const int dxc = col - kReach;
+            const float gx = gap32(dxc, cw0f, g0p, g0m, mu0);
+            d2f = gx * gx * kDn;
+            cofs = dxc * P.gc[1];
+        }
+        jb = 0;
+        je = 0;
+        if (act && d2f <= rcm2f) {
+            const float rc = __builtin_amdgcn_sqrtf(rcm2f - d2f) * kUp * ginvaf;   // half range, cells
+            const int lo = max((int)floorf(caf - rc - 1e-3f), clo);
+            const int hi = min((int)floorf(caf + rc + 1e-3f), chi);
+            const int b = rowbase + cofs;
+            jb = start[b + lo];
+            je = start[b + hi + 1];
+        }
+    };
+#else
     auto col_range = [&](int col, int& jb, int& je) {
         int base;
         float d2f;
@@ -1136,6 +1199,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             je = start[base + hi + 1];
         }
     };
+#endif
     // compact list (nbr_list): the wave-wide index range of every column group, from the cell
     // ranges of its first and last column (no column wraps: the wave is interior)
     const bool want16 = MPH_LIST16 && !SEG && lh != nullptr;
@@ -1171,8 +1235,9 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     }
     // software pipeline: the start[] loads of column col + 1 are in flight while column col is
     // staged and tested (the per-column chain start[] -> window -> staging loads is latency bound)
-    int nb_jb, nb_je;
+    int nb_jb, nb_je, n2_jb = 0, n2_je = 0;   // columns col + 1 and (MPH_SEARCH_PREFETCH=2) col + 2
     col_range(0, nb_jb, nb_je);
+    if (MPH_SEARCH_PREFETCH == 2 && NCOL > 1) col_range(1, n2_jb, n2_je);
     int slot = 0;   // SEG: first slot of this column's segment
     for (int col = 0; col < NCOL; ++col) {
         if (c16) {
@@ -1187,7 +1252,13 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             }
         }
         const int jb = nb_jb, je = nb_je;
-        if (MPH_SEARCH_PREFETCH && col + 1 < NCOL) col_range(col + 1, nb_jb, nb_je);
+        if (MPH_SEARCH_PREFETCH == 2) {   // two columns ahead
+            nb_jb = n2_jb;
+            nb_je = n2_je;
+            if (col + 2 < NCOL) col_range(col + 2, n2_jb, n2_je);
+        } else if (MPH_SEARCH_PREFETCH && col + 1 < NCOL) {
+            col_range(col + 1, nb_jb, nb_je);
+        }
         const bool any = je > jb;
         // the wave's window [mn, mx): the lanes are in cell order, so the first lane with candidates
         // normally has the lowest jb and the last the highest je -- read those two lanes, and take
@@ -1212,7 +1283,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
         }
         const int span = mx - mn;
         const int cnt0 = cnt;   // SEG: this lane's entries before the column
-        if (MPH_DIAG_SEARCH & 2) { cnt += span & 1; continue; }
+        if (MPH_DIAG_SEARCH & 2) { cnt += span == 0x7fffffff; continue; }   // never true: empty lists
         if (span <= CAP) {
             for (int t = lane; t < span; t += 64) {
                 sx[t] = A.x[mn + t];
@@ -1221,7 +1292,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                 st[t] = A.type[mn + t];
             }
             __builtin_amdgcn_wave_barrier();
-            if (MPH_DIAG_SEARCH & 1) { cnt += sx[lane] > 0.0; continue; }
+            if (MPH_DIAG_SEARCH & 1) { cnt += sx[lane] == -1.25e300; continue; }   // (never true)
             // the staging arrays are padded by SB entries, so a batch may read past je (masked)
             for (int j0 = jb; j0 < je; j0 += SB) {
                 double xs[SB], ys[SB], zs[SB];
@@ -1331,6 +1402,22 @@ __device__ __forceinline__ bool wave_all_ghosts(const DevParams& P, const Soa& A
     return __all(!live || A.id[ii] < 0);
 }
 
+// Slab mode: wface[w] = 1 when wave w holds an owned particle within slab_h of a slab face (pass B
+// runs it after the halo, phase 2, and the early send takes its particles), else 0 (interior
+// waves and waves of ghosts only, phase 1).  Written by the search, so that each pass-B launch
+// drops the other's waves with one load; the redistribution of the next step reads it too.
+__device__ __forceinline__ void slab_wave_flag(const DevParams& P, const Soa& A, int i, int n, int* wface)
+{
+    if (P.slab_axis < 0 || !wface) return;
+    const bool live = i < n;
+    const int ii = live ? i : n - 1;
+    const bool own = live && A.id[ii] >= 0;
+    const double c = P.slab_axis == 0 ? A.x[ii] : (P.slab_axis == 1 ? A.y[ii] : A.z[ii]);
+    const bool inner = c - P.slab_lo > P.slab_h && P.slab_hi - c > P.slab_h;
+    const bool face = !__all(!own || inner);
+    if ((threadIdx.x & 63) == 0) wface[i >> 6] = face ? 1 : 0;
+}
+
 template <int DIM, int PERM, int REDO>
 __device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A, const int* start, int* nbr,
                                                int* ncount, int2* hdr, int* lhdr, DevState* st, double* stage,
@@ -1406,12 +1493,13 @@ template <int DIM, int PERM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MPH_NB_WPE))) void k_neighbors(DevParams P, Soa A, const int* __restrict__ start,
                                                    int* __restrict__ nbr, int* __restrict__ ncount,
                                                    int2* __restrict__ hdr, int* __restrict__ lhdr,
-                                                   DevState* __restrict__ st)
+                                                   DevState* __restrict__ st, int* __restrict__ wface)
 {
     const int n = dev_n(P);
     if ((int)blockIdx.x >= live_blocks(n)) return;
     __shared__ double stage[4][3 * (MPH_LDS_CAP + MPH_SB) + (MPH_LDS_CAP + MPH_SB + 1) / 2];
     const int i = xcd_block(blockIdx.x, live_blocks(n)) * blockDim.x + threadIdx.x;
+    slab_wave_flag(P, A, i, n, wface);
     neighbors_body<DIM, PERM, 0>(P, A, start, nbr, ncount, hdr, lhdr, st, stage[threadIdx.x >> 6], i);
 }
 
@@ -1812,8 +1900,9 @@ __device__ __forceinline__ int fused_lds(const DevParams& P, const double* s_rat
             je = start[base + hi + 1];
         }
     };
-    int nb_jb, nb_je;
+    int nb_jb, nb_je, n2_jb = 0, n2_je = 0;   // columns col + 1 and (MPH_SEARCH_PREFETCH=2) col + 2
     col_range(0, nb_jb, nb_je);
+    if (MPH_SEARCH_PREFETCH == 2 && NCOL > 1) col_range(1, n2_jb, n2_je);
     for (int col = 0; col < NCOL; ++col) {
         const int jb = nb_jb, je = nb_je;
         if (col + 1 < NCOL) col_range(col + 1, nb_jb, nb_je);
@@ -1890,7 +1979,7 @@ __device__ __forceinline__ int fused_lds(const DevParams& P, const double* s_rat
 template <int DIM, int PERM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MPH_FUSED_WPE))) void k_search_pass_a(
     DevParams P, const DevTables* __restrict__ T, Soa A, const int* __restrict__ start, int* __restrict__ nbr,
-    int* __restrict__ ncount, DevState* __restrict__ st, PassAOut pout)
+    int* __restrict__ ncount, DevState* __restrict__ st, PassAOut pout, int* __restrict__ wface)
 {
     const int n = dev_n(P);
     if ((int)blockIdx.x >= live_blocks(n)) return;
@@ -1903,6 +1992,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MPH_FUSED_W
     }
     __syncthreads();
     const int i = xcd_block(blockIdx.x, live_blocks(n)) * blockDim.x + threadIdx.x;
+    slab_wave_flag(P, A, i, n, wface);
     const bool live = i < n;
     const int ii = live ? i : n - 1;
     const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
@@ -2175,9 +2265,16 @@ __global__ __launch_bounds__(256) MPH_PB_ATTR void k_pass_b(DevParams P, const D
     const int ii = i < n ? i : n - 1;
     const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
     bool live = i < n;
+    if (phase) {
+        // slab mode: phase 1 = the waves without a particle near a face (run while the halo of
+        // pass-A values is in flight; also the waves of ghosts only), phase 2 = the rest, after the
+        // halo arrived -- split by whole waves (wface, written by the search), so that no wave runs
+        // its list loop twice
+        const int f = wface[__builtin_amdgcn_readfirstlane(i >> 6)];
+        if (phase == 1 ? f != 0 : f == 0) return;
+    }
     if (wave_all_ghosts(P, A, live, ii)) {
         if (live) B.id[i] = A.id[i];
-        if (phase == 2 && wface && (threadIdx.x & 63) == 0) wface[i >> 6] = 0;
         return;
     }
     if (live && P.slab_axis >= 0 && A.id[ii] < 0) {   // a ghost lane of a mixed wave
@@ -2185,17 +2282,17 @@ __global__ __launch_bounds__(256) MPH_PB_ATTR void k_pass_b(DevParams P, const D
         live = false;
     }
     if (phase) {
-        // slab mode: phase 1 = the wavefronts whose particles have no ghost neighbour (run while
-        // the halo of pass-A values is in flight), phase 2 = the rest, after the halo arrived --
-        // split by whole waves, so that no wave runs its list loop twice
-        const double c = P.slab_axis == 0 ? xi : (P.slab_axis == 1 ? yi : zi);
-        const bool inner = c - P.slab_lo > P.slab_h && P.slab_hi - c > P.slab_h;
-        const bool wave_inner = __all(!live || inner);
-        // the face waves of this step, for the early send of the redistribution (mph_dist.hip)
-        if (phase == 2 && wface && (threadIdx.x & 63) == 0) wface[i >> 6] = wave_inner ? 0 : 1;
-        if (phase == 1 ? !wave_inner : wave_inner) return;
+        // slab mode: phase 1 = the waves without a particle near a face (run while the halo of
+        // pass-A values is in flight; also the waves of ghosts only), phase 2 = the rest, after the
+        // halo arrived -- split by whole waves (wface, written by the search), so that no wave runs
+        // its list loop twice
+        const int f = wface[__builtin_amdgcn_readfirstlane(i >> 6)];
+        if (phase == 1 ? f != 0 : f == 0) return;
     }
-    const int2* h = hdr ? hdr + (size_t)(i >> 6) * kSegHdr : nullptr;
+    if (wave_all_ghosts(P, A, live, ii)) {
+        if (live) B.id[i] = A.id[i];
+        return;
+    }    const int2* h = hdr ? hdr + (size_t)(i >> 6) * kSegHdr : nullptr;
     const bool segmented = MPH_SEG && h && h[kSegCols].x == 1;   // wave-uniform
     const bool fast = segmented || wave_interior(P, live, xi, yi, zi);
     if (!segmented && !live) return;
@@ -3262,7 +3359,8 @@ void launch_neighbors(const Launch& L)
 #define MPH_NEIGHBORS(D, PERM)                                                                               \
     do {                                                                                                     \
         MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM>), dim3(blocks(P.n, 256)), dim3(256), 0,     \
-                   L.stream, P, L.A, L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, L.st);   \
+                   L.stream, P, L.A, L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, L.st,    \
+                   L.wface);                                                                                \
         if (L.lhdr)                                                                                          \
             MPH_LAUNCH("neighbors_redo", L.stream, (k_neighbors_redo<D, PERM>), dim3(1),                  \
                        dim3(256), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.lhdr, L.st);            \
@@ -3310,7 +3408,7 @@ void launch_search_pass_a(const Launch& L)
     const PassAOut po = pass_a_out(L);
 #define MPH_FUSED_LAUNCH(D, PERM)                                                                         \
     MPH_LAUNCH("search_pass_a", L.stream, (k_search_pass_a<D, PERM>), dim3(blocks(P.n, 256)), dim3(256), 0, \
-               L.stream, P, L.T, L.A, L.start, L.nbr, L.ncount, L.st, po)
+               L.stream, P, L.T, L.A, L.start, L.nbr, L.ncount, L.st, po, L.wface)
     if (P.dim == 3) {
         switch (P.perm) {
         case 1: MPH_FUSED_LAUNCH(3, 1); break;

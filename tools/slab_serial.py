@@ -9,14 +9,17 @@ still run the kernels it enqueued before the exchange -- and each thread synchro
 gives the token back at the end of a call), so every rank's kernels run alone on the card and
 the HIP-event profile of each rank is what that rank would see on its own GPU.
 
-With --replay (default) the profiled steps run a second time from a fresh start: every rank
+With --replay the profiled steps run a second time from a fresh start: every rank
 then receives the messages recorded in the first run at once (bit-identical runs), holds the
 token through its whole profile call and does not drain the device in an exchange, so its second
 stream runs beside its main stream as on a rank of its own (the inner pass B / inner elastic
 slots beside the halo, the face pass B and the early send) -- the exchange latency left is the
-host staging's own copies.  The first run's figures are "serialised", the replay's "replay".
+host staging's own copies.  The first run's figures are "serialised", the replay's "replay"
+("consistent": every rank ended with the recorded run's held and owned counts; runs where a
+rank's replayed state diverged -- seen on one GPU box, a rank then searching ~all particles --
+are not measurements).
 
-usage: python tools/slab_serial.py [--case d16m] [--ranks 8] [--steps 4] [--warmup 2] [--no-replay]
+usage: python tools/slab_serial.py [--case d16m] [--ranks 8] [--steps 4] [--warmup 2] [--replay]
 prints one JSON line: per-rank kernel averages, held/owned counts, their GPU time per step (the
 sum of the kernel times, and gpu_busy: the union of the kernel intervals, less than the sum where
 the kernels of the two streams run concurrently).
@@ -108,7 +111,7 @@ def main():
     ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--no-replay", dest="replay", action="store_false")
+    ap.add_argument("--replay", action="store_true")
     args = ap.parse_args()
     case = cases.get(args.case)
     axis = SLAB_AXIS[case.dim]
@@ -123,7 +126,9 @@ def main():
     result["per_rank"] = serial
     if args.replay:
         rep = run_ranks(args, R, axis, cuts, locals_, replay=records)
-        result["replay"] = dict(summary(rep), per_rank=rep)
+        # the replay is only meaningful while every rank ends where the recorded run did
+        same = all(a["held"] == b["held"] and a["owned"] == b["owned"] for a, b in zip(serial, rep))
+        result["replay"] = dict(summary(rep), consistent=same, per_rank=rep)
     print(json.dumps(result))
 
 
