@@ -222,6 +222,7 @@ int mph_create(MphCtx** ctx, const MphConfig* cfg, int n, const int* property,
  * replayed batch, so after a successful mph_step they hold that step's values; after an error
  * they are undefined (the state itself -- Position, Velocity -- is the failing step's).        */
 int mph_step(MphCtx* ctx, int nsteps);
+/* Wait for all work the context enqueued (slab mode: both of its streams). */
 int mph_synchronize(MphCtx* ctx);
 /* Copy a field to host, AoS, original particle order.                                      */
 int mph_get(MphCtx* ctx, int field, void* host_out);

@@ -56,6 +56,10 @@ struct MphDist {
     mph_host_exchange_fn host_fn = nullptr;
     void* host_user = nullptr;
     char* host_stage = nullptr;   // pinned staging for the host transport (4 messages)
+    // the last host-staged exchange's copies into the device (they read host_stage): the next
+    // exchange, possibly on the other stream, waits for them before the callback refills it
+    hipEvent_t ev_stage = nullptr;
+    bool stage_busy = false;
     // elastic ghost slots (static): local slot indices sent to / received from each neighbour
     int *ss_l = nullptr, *ss_r = nullptr, *sr_l = nullptr, *sr_r = nullptr;
     int nss_l = 0, nss_r = 0, nsr_l = 0, nsr_r = 0;

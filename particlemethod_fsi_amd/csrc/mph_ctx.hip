@@ -633,6 +633,8 @@ int mph_synchronize(MphCtx* c)
 {
     if (!c) return MPH_ERR_ARG;
     HIP_OK(c, hipStreamSynchronize(c->stream));
+    // slab mode: the second stream too (halo, face pass B, early send, elastic ghost exchanges)
+    if (c->dist && c->dist->stream2) HIP_OK(c, hipStreamSynchronize(c->dist->stream2));
     return MPH_OK;
 }
 

@@ -191,6 +191,9 @@ int exchange(MphCtx* c, hipStream_t stream, const void* send_l, size_t bsl, cons
     char* hs_r = D.host_stage + region;
     char* hr_l = D.host_stage + 2 * region;
     char* hr_r = D.host_stage + 3 * region;
+    // the previous exchange's host-to-device copies may still read the receive halves (when it ran
+    // on the other stream, this stream's synchronisation below does not cover them)
+    if (D.stage_busy) MPH_HIP_OK(c, hipEventSynchronize(D.ev_stage));
     if (bsl) MPH_HIP_OK(c, hipMemcpyAsync(hs_l, send_l, bsl, hipMemcpyDeviceToHost, stream));
     if (bsr) MPH_HIP_OK(c, hipMemcpyAsync(hs_r, send_r, bsr, hipMemcpyDeviceToHost, stream));
     MPH_HIP_OK(c, hipStreamSynchronize(stream));
@@ -198,6 +201,9 @@ int exchange(MphCtx* c, hipStream_t stream, const void* send_l, size_t bsl, cons
         return ctx_fail(c, MPH_ERR_TRANSPORT, "host exchange callback failed");
     if (brl) MPH_HIP_OK(c, hipMemcpyAsync(recv_l, hr_l, brl, hipMemcpyHostToDevice, stream));
     if (brr) MPH_HIP_OK(c, hipMemcpyAsync(recv_r, hr_r, brr, hipMemcpyHostToDevice, stream));
+    if (!D.ev_stage) MPH_HIP_OK(c, hipEventCreateWithFlags(&D.ev_stage, hipEventDisableTiming));
+    MPH_HIP_OK(c, hipEventRecord(D.ev_stage, stream));
+    D.stage_busy = true;
     return MPH_OK;
 }
 
@@ -262,6 +268,8 @@ int msg_alloc(MphCtx* c)
         MPH_HIP_OK(c, hipMalloc((void**)b, region));
     }
     if (!D.rccl) {
+        if (D.stage_busy) MPH_HIP_OK(c, hipEventSynchronize(D.ev_stage));   // no copy still reads it
+        D.stage_busy = false;
         if (D.host_stage) (void)hipHostFree(D.host_stage);
         D.host_stage = nullptr;
         MPH_HIP_OK(c, hipHostMalloc((void**)&D.host_stage, 4 * region, hipHostMallocDefault));
@@ -1117,6 +1125,7 @@ void dist_free(MphCtx* c)
     if (D->ev_h) (void)hipEventDestroy(D->ev_h);
     if (D->ev_s) (void)hipEventDestroy(D->ev_s);
     if (D->ev_x) (void)hipEventDestroy(D->ev_x);
+    if (D->ev_stage) (void)hipEventDestroy(D->ev_stage);
     if (D->stream2) (void)hipStreamDestroy(D->stream2);
     if (D->hlay) (void)hipHostFree(D->hlay);
     for (char* b : {D->send_l, D->send_r, D->recv_l, D->recv_r})

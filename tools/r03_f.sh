@@ -14,10 +14,10 @@ case $rc in 0|1) ;; *) exit 12;; esac
 # fsi3d is 0.12 deep along z: 4 slabs (8 would be thinner than two halo widths)
 for cr in ${CASES:-fsi3d:4 bar2d_400k:8 d16m:8}; do
   c=${cr%:*}; r=${cr#*:}
-  timeout -k 10 400 python tools/slab_serial.py --case $c --ranks $r --steps 6 --warmup 2 > $OUT/serial_${c}_$r.json 2>> $OUT/serial.err || exit 13
-  MPH_SLAB_OVERLAP=0 timeout -k 10 400 python tools/slab_serial.py --case $c --ranks $r --steps 6 --warmup 2 > $OUT/serial_${c}_${r}_nooverlap.json 2>> $OUT/serial.err || exit 14
+  timeout -k 10 400 python tools/slab_serial.py --case $c --ranks $r --steps 6 --warmup 2 ${REPLAY:+--replay} > $OUT/serial_${c}_$r.json 2>> $OUT/serial.err || exit 13
+  MPH_SLAB_OVERLAP=0 timeout -k 10 400 python tools/slab_serial.py --case $c --ranks $r --steps 6 --warmup 2 ${REPLAY:+--replay} > $OUT/serial_${c}_${r}_nooverlap.json 2>> $OUT/serial.err || exit 14
 done
 # A/B switches on the D16M slabs (VARS: space-separated VAR=VALUE, one run each)
 for v in ${VARS}; do
-  env $v timeout -k 10 400 python tools/slab_serial.py --case d16m --ranks 8 --steps 6 --warmup 2 > $OUT/serial_d16m_8_${v}.json 2>> $OUT/serial.err || exit 15
+  env $v timeout -k 10 400 python tools/slab_serial.py --case d16m --ranks 8 --steps 6 --warmup 2 ${REPLAY:+--replay} > $OUT/serial_d16m_8_${v}.json 2>> $OUT/serial.err || exit 15
 done

@@ -15,9 +15,10 @@ token through its whole profile call and does not drain the device in an exchang
 stream runs beside its main stream as on a rank of its own (the inner pass B / inner elastic
 slots beside the halo, the face pass B and the early send) -- the exchange latency left is the
 host staging's own copies.  The first run's figures are "serialised", the replay's "replay"
-("consistent": every rank ended with the recorded run's held and owned counts; runs where a
-rank's replayed state diverged -- seen on one GPU box, a rank then searching ~all particles --
-are not measurements).
+("consistent": every rank ended with the recorded run's held and owned counts).  The replay
+exposed a race of the host transport (an exchange on one stream refilled the pinned staging
+buffers while the previous exchange's copies on the other stream still read them; a rank then
+diverged): each host-staged exchange now waits for the previous one's copies (mph_dist.hip).
 
 usage: python tools/slab_serial.py [--case d16m] [--ranks 8] [--steps 4] [--warmup 2] [--replay]
 prints one JSON line: per-rank kernel averages, held/owned counts, their GPU time per step (the
