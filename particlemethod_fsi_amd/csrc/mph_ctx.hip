@@ -375,6 +375,10 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     CK(dalloc(c, &c->cnt, c->P.ncell)); CK(dalloc(c, &c->start, (size_t)c->P.ncell + 1));
     CK(dalloc(c, &c->bsum, (size_t)c->P.ncell / 4096 + 2));
     CK(dalloc(c, &c->nbr, ntile * kTile * kMaxNeighbor)); CK(dalloc(c, &c->ncount, cap));
+#if defined(MPH_DIAG_NOSTORE) && MPH_DIAG_NOSTORE
+    // diagnostic build: the search stores no list, so the passes read index 0 (never garbage)
+    if (hipMemset(c->nbr, 0, sizeof(int) * ntile * kTile * kMaxNeighbor) != hipSuccess) return MPH_ERR_HIP;
+#endif
     CK(dalloc(c, &c->seg_hdr, ntile * kSegHdr));
     CK(dalloc(c, &c->list_hdr, ntile * kLhdr));
     CK(dalloc(c, &c->pres, cap)); CK(dalloc(c, &c->gx, cap)); CK(dalloc(c, &c->gy, cap)); CK(dalloc(c, &c->gz, cap));

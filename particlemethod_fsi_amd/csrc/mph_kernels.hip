@@ -8,14 +8,14 @@
 //   k_scan_*         exclusive scan of the cell histogram -> cell start offsets (1711-1728)
 //   k_place          scatter particle ids into their cells (unordered) + Time/WallCenter advance
 //   k_rank_scatter   deterministic in-cell rank (by previous sorted index) and particle reorder
-//   k_search_pass_a  linked-cell search (1743-1810): 7x7(x5) stencil (2 kReach + 1 columns of cells
+//   k_neighbors      linked-cell search (1743-1810): 7x7(x5) stencil (2 kReach + 1 columns of cells
 //                    >= rc/3, 2 kContigReach + 1 cells >= rc/2 along the contiguous axis), the
-//                    reference's exact FP64 acceptance test, ELL neighbour list per wavefront; and
-//                    in the same kernel the pass-A sums of every accepted neighbour: DensityA (2141),
-//                    GravityCenter (2174), DensityP (2314), DivergenceP (2343), PhysicalCoefficients
-//                    (2099), pressure values PressureP (2384) / PressureA (2218)
-//   k_neighbors,     the same as two kernels (the compact 16-bit list format, MPH_FUSED=0)
-//   k_pass_a
+//                    reference's exact FP64 acceptance test, ELL neighbour list per wavefront
+//   k_pass_a         the pass-A sums over the list: DensityA (2141), GravityCenter (2174), DensityP
+//                    (2314), DivergenceP (2343), PhysicalCoefficients (2099), pressure values
+//                    PressureP (2384) / PressureA (2218)
+//   k_search_pass_a  the two above in one kernel (opt-in, MPH_FUSED=1 at run time; measured slower,
+//                    DESIGN.md section 4), bit-identical
 //   k_pass_b         PressureP force (2394), PressureA force (2225), DiffuseInterface (2261),
 //                    ViscosityV (2478), InterfaceForce (2427), Gravity (2917), Acceleration (2938),
 //                    Convection (1892)
@@ -83,8 +83,21 @@
 #ifndef MPH_LDS_CAP
 #define MPH_LDS_CAP 192   // candidates staged per wave and stencil column
 #endif
+#ifndef MPH_GLDS
+// the search stages a column's window with global_load_lds (16 bytes per lane straight into LDS:
+// no VGPRs, no ds_write, and the pieces of a window in flight together) instead of register loads
+// + ds_write per 64 candidates (each piece waited for before the next)
+#define MPH_GLDS 1
+#endif
 
 namespace mph {
+
+// LDS staging of one wavefront in the search: x, y, z (stage_d doubles each, 16-byte aligned and
+// large enough for a 16-byte-aligned window of CAP candidates plus the SB-entry batch over-read),
+// then the types (stage_t ints, 4-aligned window).  Doubles per wave: stage_words.
+__host__ __device__ constexpr int stage_d(int cap, int sb) { return (cap + sb + 2 + 1) & ~1; }
+__host__ __device__ constexpr int stage_t(int cap, int sb) { return (cap + sb + 8 + 3) & ~3; }
+__host__ __device__ constexpr int stage_words(int cap, int sb) { return 3 * stage_d(cap, sb) + stage_t(cap, sb) / 2; }
 
 
 // ------------------------------------------------------------------------------ helpers ------
@@ -1096,9 +1109,10 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                                                    unsigned short* seg, int2* hdr, int* seg_overflow,
                                                    int* lh = nullptr, unsigned short* o16 = nullptr)
 {
-    double* sy = sx + (CAP + SB);
-    double* sz = sx + 2 * (CAP + SB);
-    int* st = reinterpret_cast<int*>(sx + 3 * (CAP + SB));
+    constexpr int SD = stage_d(CAP, SB);
+    double* sy = sx + SD;
+    double* sz = sx + 2 * SD;
+    int* st = reinterpret_cast<int*>(sx + 3 * SD);
     const int lane = threadIdx.x & 63;
     const double lo2 = P.rc2_lo, hi2 = P.rc2_hi;
     using X = CellAxes<DIM, PERM>;
@@ -1285,18 +1299,39 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
         const int cnt0 = cnt;   // SEG: this lane's entries before the column
         if (MPH_DIAG_SEARCH & 2) { cnt += span == 0x7fffffff; continue; }   // never true: empty lists
         if (span <= CAP) {
+#if MPH_GLDS
+            // the window from a 16-byte-aligned start: candidate j sits at j - mn + da in x, y, z
+            // and at j - mn + ta in the types; pieces of 128 doubles / 256 ints per instruction,
+            // lanes past the window masked (the arrays hold kPad elements beyond any window)
+            const int da = mn & 1, ta = mn & 3;
+            const int n2 = span + da, n4 = span + ta;
+            for (int p = 0; p * 128 < n2; ++p) {   // wave-uniform
+                const int e = p * 128 + 2 * lane;
+                if (e < n2) {
+                    __builtin_amdgcn_global_load_lds(A.x + (mn - da) + e, sx + p * 128, 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds(A.y + (mn - da) + e, sy + p * 128, 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds(A.z + (mn - da) + e, sz + p * 128, 16, 0, 0);
+                }
+            }
+            static_assert(CAP + 3 <= 256, "one 256-int piece holds the types of a window");
+            if (4 * lane < n4) __builtin_amdgcn_global_load_lds(A.type + (mn - ta) + 4 * lane, st, 16, 0, 0);
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the pieces have landed in LDS
+            const int kofs = da, tofs = ta - da;
+#else
             for (int t = lane; t < span; t += 64) {
                 sx[t] = A.x[mn + t];
                 sy[t] = A.y[mn + t];
                 sz[t] = A.z[mn + t];
                 st[t] = A.type[mn + t];
             }
+            const int kofs = 0, tofs = 0;
+#endif
             __builtin_amdgcn_wave_barrier();
             if (MPH_DIAG_SEARCH & 1) { cnt += sx[lane] == -1.25e300; continue; }   // (never true)
             // the staging arrays are padded by SB entries, so a batch may read past je (masked)
             for (int j0 = jb; j0 < je; j0 += SB) {
                 double xs[SB], ys[SB], zs[SB];
-                const int k0 = j0 - mn;
+                const int k0 = j0 - mn + kofs;
 #pragma unroll
                 for (int u = 0; u < SB; ++u) {
                     xs[u] = sx[k0 + u];
@@ -1315,13 +1350,13 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                         if (SEG) {
                             const int sl = slot + (cnt - cnt0);
                             if (sl < kSegCap)
-                                seg[(size_t)sl * kTile + lane] = (unsigned short)((j - mn) | (st[k0 + u] << 8));
+                                seg[(size_t)sl * kTile + lane] = (unsigned short)((j - mn) | (st[k0 + u + tofs] << 8));
                         } else if (c16) {
                             const int k = min(cnt, kMaxNeighbor - 1);
                             o16[(((k >> 1) * kTile + lane) << 1) + (k & 1)] =
-                                (unsigned short)((j - gbase) | (st[k0 + u] << kOff16));
+                                (unsigned short)((j - gbase) | (st[k0 + u + tofs] << kOff16));
                         } else if (!MPH_DIAG_NOSTORE) {
-                            list_store(out + min(cnt, kMaxNeighbor - 1) * kTile, nbr_entry(j, st[k0 + u]));
+                            list_store(out + min(cnt, kMaxNeighbor - 1) * kTile, nbr_entry(j, st[k0 + u + tofs]));
                         }
                         ++cnt;
                     }
@@ -1497,7 +1532,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MPH_NB_WPE)
 {
     const int n = dev_n(P);
     if ((int)blockIdx.x >= live_blocks(n)) return;
-    __shared__ double stage[4][3 * (MPH_LDS_CAP + MPH_SB) + (MPH_LDS_CAP + MPH_SB + 1) / 2];
+    __shared__ __attribute__((aligned(16))) double stage[4][stage_words(MPH_LDS_CAP, MPH_SB)];
     const int i = xcd_block(blockIdx.x, live_blocks(n)) * blockDim.x + threadIdx.x;
     slab_wave_flag(P, A, i, n, wface);
     neighbors_body<DIM, PERM, 0>(P, A, start, nbr, ncount, hdr, lhdr, st, stage[threadIdx.x >> 6], i);
@@ -1515,7 +1550,7 @@ __global__ __launch_bounds__(256) void k_neighbors_redo(DevParams P, Soa A, cons
     if (st->list_redo == 0) return;
     const int n = dev_n(P);
     const int ntile = (n + kTile - 1) / kTile;
-    __shared__ double stage[4][3 * (MPH_LDS_CAP + MPH_SB) + (MPH_LDS_CAP + MPH_SB + 1) / 2];
+    __shared__ __attribute__((aligned(16))) double stage[4][stage_words(MPH_LDS_CAP, MPH_SB)];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int t0 = wave * 64; t0 < ntile; t0 += 4 * 64) {
         const int t = t0 + lane;   // the wave header this lane checks
@@ -1782,7 +1817,8 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
 // instead of the column's candidate count.  Same neighbours in the same order, same FP64
 // expressions: every field is bit-identical to the separate k_neighbors + k_pass_a.
 #ifndef MPH_FUSED
-#define MPH_FUSED 1      // default: fused (MPH_FUSED=0 at run time or build: separate kernels)
+#define MPH_FUSED 1      // 1: the fused kernel is compiled (selected at run time: MPH_FUSED=1 or
+                         // kFusedDefault, which is off); 0: not built at all
 #endif
 #ifndef MPH_FCAP
 #define MPH_FCAP 128     // candidates staged per wave and column (6 + 1 arrays, 52 B each)
