@@ -375,9 +375,11 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     CK(dalloc(c, &c->cnt, c->P.ncell)); CK(dalloc(c, &c->start, (size_t)c->P.ncell + 1));
     CK(dalloc(c, &c->bsum, (size_t)c->P.ncell / 4096 + 2));
     CK(dalloc(c, &c->nbr, ntile * kTile * kMaxNeighbor)); CK(dalloc(c, &c->ncount, cap));
-#if defined(MPH_DIAG_NOSTORE) && MPH_DIAG_NOSTORE
-    // diagnostic build: the search stores no list, so the passes read index 0 (never garbage)
+#if (defined(MPH_DIAG_NOSTORE) && MPH_DIAG_NOSTORE) || (defined(MPH_DIAG_SEARCH) && (MPH_DIAG_SEARCH & 4))
+    // diagnostic builds: the search stores no list (or skips the waves near a periodic face, whose
+    // counts then stay 0), so the passes read index 0 (never garbage)
     if (hipMemset(c->nbr, 0, sizeof(int) * ntile * kTile * kMaxNeighbor) != hipSuccess) return MPH_ERR_HIP;
+    if (hipMemset(c->ncount, 0, sizeof(int) * cap) != hipSuccess) return MPH_ERR_HIP;
 #endif
     CK(dalloc(c, &c->seg_hdr, ntile * kSegHdr));
     CK(dalloc(c, &c->list_hdr, ntile * kLhdr));

@@ -317,11 +317,9 @@ int redistribute(MphCtx* c, bool move, bool init, Profiler* prof, bool early_in 
     launch_scan(D.bcnt, kSlabClasses * nb, D.bsum, D.boff, 0, c->stream, prof);
     launch_dist_scatter(L, D.cap, D.lay, D.cls, D.boff, D.C, lay_field<int>(D.lay, offsetof(DistLayout, seg)),
                         D.virt ? D.vidx : nullptr);
-    launch_dist_counts(L, D.lay);
     if (early_in) {
         MPH_HIP_OK(c, stream_wait(prof, c->stream, D.ev_x, D.stream2));
-        launch_dist_unpack(L, D.recv_l, D.recv_r, D.lay, 0, D.cap_rl, D.cap, D.C);
-        launch_dist_unpack(L, D.recv_l, D.recv_r, D.lay, 1, D.cap_rr, D.cap, D.C);
+        launch_dist_unpack(L, D.recv_l, D.recv_r, D.lay, D.cap_rl, D.cap_rr, D.cap, D.C);
         return MPH_OK;
     }
     if (init) {
@@ -341,13 +339,11 @@ int redistribute(MphCtx* c, bool move, bool init, Profiler* prof, bool early_in 
         MPH_CK(msg_alloc(c));
     }
     const VSrc vs = dist_vsrc(c);
-    launch_dist_pack(L, D.C, D.lay, 0, D.cap_sl, D.send_l, vs);
-    launch_dist_pack(L, D.C, D.lay, 1, D.cap_sr, D.send_r, vs);
+    launch_dist_pack(L, D.C, D.lay, D.cap_sl, D.cap_sr, D.send_l, D.send_r, vs);
     MPH_CK(exchange(c, c->stream, D.send_l, kMsgHead + kMsgBytes * D.cap_sl, D.send_r,
                     kMsgHead + kMsgBytes * D.cap_sr, D.recv_l, kMsgHead + kMsgBytes * D.cap_rl, D.recv_r,
                     kMsgHead + kMsgBytes * D.cap_rr));
-    launch_dist_unpack(L, D.recv_l, D.recv_r, D.lay, 0, D.cap_rl, D.cap, D.C);
-    launch_dist_unpack(L, D.recv_l, D.recv_r, D.lay, 1, D.cap_rr, D.cap, D.C);
+    launch_dist_unpack(L, D.recv_l, D.recv_r, D.lay, D.cap_rl, D.cap_rr, D.cap, D.C);
     return MPH_OK;
 }
 
@@ -413,12 +409,10 @@ int halo_exchange(MphCtx* c, Profiler* prof, hipStream_t stream, const HaloField
     double* sr = (double*)D.send_r;
     double* rl = (double*)D.recv_l;
     double* rr = (double*)D.recv_r;
-    launch_halo_pack(L, c->rank_of, D.lay, 0, capl, F, sl);
-    launch_halo_pack(L, c->rank_of, D.lay, 1, capr, F, sr);
+    launch_halo_pack(L, c->rank_of, D.lay, capl, capr, F, sl, sr);
     const size_t b = sizeof(double) * F.nf;
     MPH_CK(exchange(c, stream, sl, b * capl, sr, b * capr, rl, b * capl, rr, b * capr));
-    launch_halo_unpack(L, rl, c->rank_of, D.lay, 2, capl, F);
-    launch_halo_unpack(L, rr, c->rank_of, D.lay, 3, capr, F);
+    launch_halo_unpack(L, rl, rr, c->rank_of, D.lay, capl, capr, F);
     return MPH_OK;
 }
 

@@ -149,16 +149,16 @@ void launch_dist_early_classify(const Launch& L, const SlabGeom& g, int cap, con
 void launch_dist_early_pack(const Launch& L, int cap, DistLayout* lay, const int* cls, const int* boff, int cap_l,
                             int cap_r, char* buf_l, char* buf_r);
 // vidx non-null: record the B index of every kept entry (VSrc) instead of copying it into C
-void launch_dist_scatter(const Launch& L, int cap, const DistLayout* lay, const int* cls, const int* boff,
+void launch_dist_scatter(const Launch& L, int cap, DistLayout* lay, const int* cls, const int* boff,
                          const Soa& C, int* dseg, int* vidx = nullptr);
-void launch_dist_counts(const Launch& L, DistLayout* lay);
-void launch_dist_pack(const Launch& L, const Soa& C, DistLayout* lay, int side, int cap_msg, char* buf,
-                      const VSrc& vs = VSrc{});
-void launch_dist_unpack(const Launch& L, const char* buf_l, const char* buf_r, DistLayout* lay, int side,
-                        int cap_msg, int cap, const Soa& C);
-void launch_halo_pack(const Launch& L, const int* dst_of, const DistLayout* lay, int dir, int cap,
-                      const HaloFields& F, double* buf);
-void launch_halo_unpack(const Launch& L, const double* buf, const int* dst_of, const DistLayout* lay, int dir,
-                        int cap, const HaloFields& F);
+// both sides / directions in one launch each (blockIdx.y)
+void launch_dist_pack(const Launch& L, const Soa& C, DistLayout* lay, int cap_l, int cap_r, char* buf_l,
+                      char* buf_r, const VSrc& vs = VSrc{});
+void launch_dist_unpack(const Launch& L, const char* buf_l, const char* buf_r, DistLayout* lay, int cap_l,
+                        int cap_r, int cap, const Soa& C);
+void launch_halo_pack(const Launch& L, const int* dst_of, const DistLayout* lay, int cap_l, int cap_r,
+                      const HaloFields& F, double* buf_l, double* buf_r);
+void launch_halo_unpack(const Launch& L, const double* buf_l, const double* buf_r, const int* dst_of,
+                        const DistLayout* lay, int cap_l, int cap_r, const HaloFields& F);
 
 }  // namespace mph

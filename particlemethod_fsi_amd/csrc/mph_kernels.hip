@@ -3131,7 +3131,9 @@ __global__ __launch_bounds__(256) void k_dist_early_pack(Soa B, DistLayout* __re
     q[m + j] = (c == kMigR || c == kMigL) ? -1 - id : id;
 }
 
-__global__ __launch_bounds__(256) void k_dist_scatter(Soa B, const DistLayout* __restrict__ lay,
+// also writes the layout's send counts (left-going {bandL, migL}, right-going {migR, bandR}) from
+// the class starts (block 0), which the pack kernels and the count exchange of mph_create read
+__global__ __launch_bounds__(256) void k_dist_scatter(Soa B, DistLayout* __restrict__ lay,
                                                       const int* __restrict__ cls,
                                                       const int* __restrict__ boff, int nb, Soa C,
                                                       int* __restrict__ dseg, int* __restrict__ vidx)
@@ -3150,6 +3152,13 @@ __global__ __launch_bounds__(256) void k_dist_scatter(Soa B, const DistLayout* _
     }
     __syncthreads();
     if (blockIdx.x == 0 && threadIdx.x <= kSlabClasses) dseg[threadIdx.x] = boff[threadIdx.x * nb];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        auto len = [&](int k) { return boff[(k + 1) * nb] - boff[k * nb]; };
+        lay->send[0] = len(kBandL);
+        lay->send[1] = len(kMigL);
+        lay->send[2] = len(kMigR);
+        lay->send[3] = len(kBandR);
+    }
     if (c < 0 || c == kSlabDrop) return;
     int o = boff[c * nb + blockIdx.x] + rank;
     for (int w = 0; w < wave; ++w) o += wc[w][c];
@@ -3162,17 +3171,6 @@ __global__ __launch_bounds__(256) void k_dist_scatter(Soa B, const DistLayout* _
     C.type[o] = B.type[p];
     const int id = B.id[p];
     C.id[o] = (c == kMigR || c == kMigL) ? -1 - id : id;
-}
-
-// count messages from the segment starts: left-going {bandL, migL}, right-going {migR, bandR}
-__global__ void k_dist_counts(DistLayout* __restrict__ lay)
-{
-    if (threadIdx.x != 0) return;
-    const int* seg = lay->seg;
-    lay->send[0] = seg[kBandL + 1] - seg[kBandL];
-    lay->send[1] = seg[kMigL + 1] - seg[kMigL];
-    lay->send[2] = seg[kMigR + 1] - seg[kMigR];
-    lay->send[3] = seg[kBandR + 1] - seg[kBandR];
 }
 
 // Messages of a redistribution travel with a fixed capacity (so the exchange has host-known
@@ -3197,9 +3195,14 @@ __device__ __forceinline__ void dist_recv_range(const DistLayout* lay, const int
 // message layout: a 16-byte header with the two class counts (so no separate count message is
 // needed per step), then x[m] y[m] z[m] vx[m] vy[m] vz[m] (double) type[m] id[m] (int), 56 B per
 // particle (kMsgHeader above)
-__global__ __launch_bounds__(256) void k_dist_pack(Soa C, DistLayout* __restrict__ lay, int side, int cap,
-                                                   DevState* __restrict__ st, char* __restrict__ buf, VSrc vs)
+// both messages in one launch: blockIdx.y = side
+__global__ __launch_bounds__(256) void k_dist_pack(Soa C, DistLayout* __restrict__ lay, int cap_l, int cap_r,
+                                                   DevState* __restrict__ st, char* __restrict__ buf_l,
+                                                   char* __restrict__ buf_r, VSrc vs)
 {
+    const int side = blockIdx.y;
+    const int cap = side ? cap_r : cap_l;
+    char* buf = side ? buf_r : buf_l;
     int off, m;
     dist_send_range(lay, side, off, m);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -3228,10 +3231,13 @@ __global__ __launch_bounds__(256) void k_dist_pack(Soa C, DistLayout* __restrict
 // received message -> C[off, off+m); ownership flips (their migrants are ours, their band
 // particles are our ghosts): id -> -1-id for every entry.  The right-hand message completes the
 // layout: n = kept + received, n_own = the kept owned classes + the received migrants.
+// both messages in one launch: blockIdx.y = side (0 from the left with capacity cap_l, 1 from the right)
 __global__ __launch_bounds__(256) void k_dist_unpack(const char* __restrict__ buf_l, const char* __restrict__ buf_r,
-                                                     DistLayout* __restrict__ lay, int side, int cap_msg, int cap,
+                                                     DistLayout* __restrict__ lay, int cap_l, int cap_r, int cap,
                                                      DevState* __restrict__ st, Soa C)
 {
+    const int side = blockIdx.y;
+    const int cap_msg = side ? cap_r : cap_l;
     // the received counts, from the two message headers (from the left: {migR, bandR} of the left
     // neighbour, from the right: {bandL, migL} of the right neighbour)
     const int* hl = (const int*)buf_l;
@@ -3309,9 +3315,15 @@ __device__ __forceinline__ void halo_ranges(const DistLayout* L, int dir, int& o
 
 // pass-A values of two C-index ranges, read at their sorted position dst_of[c]; cap bounds the
 // message (the counts are within it once the redistribution's capacity checks passed)
+// both directions in one launch: dir = blockIdx.y (0 to the left into buf_a with capacity cap_a,
+// 1 to the right into buf_b)
 __global__ __launch_bounds__(256) void k_halo_pack(const int* __restrict__ dst_of, const DistLayout* __restrict__ lay,
-                                                   int dir, int cap, HaloFields F, double* __restrict__ buf)
+                                                   int cap_a, int cap_b, HaloFields F, double* __restrict__ buf_a,
+                                                   double* __restrict__ buf_b)
 {
+    const int dir = blockIdx.y;
+    const int cap = dir ? cap_b : cap_a;
+    double* buf = dir ? buf_b : buf_a;
     int o1, n1, o2, n2;
     halo_ranges(lay, dir, o1, n1, o2, n2);
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -3321,10 +3333,14 @@ __global__ __launch_bounds__(256) void k_halo_pack(const int* __restrict__ dst_o
     for (int f = 0; f < F.nf; ++f) buf[(size_t)f * m + k] = F.f[f][a];
 }
 
-__global__ __launch_bounds__(256) void k_halo_unpack(const double* __restrict__ buf, const int* __restrict__ dst_of,
-                                                     const DistLayout* __restrict__ lay, int dir, int cap,
-                                                     HaloFields F)
+// both directions in one launch: dir = 2 + blockIdx.y (2 from the left out of buf_a, 3 from the right)
+__global__ __launch_bounds__(256) void k_halo_unpack(const double* __restrict__ buf_a, const double* __restrict__ buf_b,
+                                                     const int* __restrict__ dst_of, const DistLayout* __restrict__ lay,
+                                                     int cap_a, int cap_b, HaloFields F)
 {
+    const int dir = 2 + blockIdx.y;
+    const int cap = blockIdx.y ? cap_b : cap_a;
+    const double* buf = blockIdx.y ? buf_b : buf_a;
     int o1, n1, o2, n2;
     halo_ranges(lay, dir, o1, n1, o2, n2);
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -3708,7 +3724,7 @@ void launch_dist_early_pack(const Launch& L, int cap, DistLayout* lay, const int
                boff, nb, cap_l, cap_r, L.st, buf_l, buf_r);
 }
 
-void launch_dist_scatter(const Launch& L, int cap, const DistLayout* lay, const int* cls, const int* boff,
+void launch_dist_scatter(const Launch& L, int cap, DistLayout* lay, const int* cls, const int* boff,
                          const Soa& C, int* dseg, int* vidx)
 {
     Profiler* prof = L.prof;
@@ -3717,42 +3733,36 @@ void launch_dist_scatter(const Launch& L, int cap, const DistLayout* lay, const 
                nb, C, dseg, vidx);
 }
 
-void launch_dist_counts(const Launch& L, DistLayout* lay)
+void launch_dist_pack(const Launch& L, const Soa& C, DistLayout* lay, int cap_l, int cap_r, char* buf_l,
+                      char* buf_r, const VSrc& vs)
 {
     Profiler* prof = L.prof;
-    MPH_LAUNCH("dist_counts", L.stream, k_dist_counts, dim3(1), dim3(64), 0, L.stream, lay);
+    MPH_LAUNCH("dist_pack", L.stream, k_dist_pack, dim3(dist_blocks(std::max(cap_l, cap_r)), 2), dim3(256), 0,
+               L.stream, C, lay, cap_l, cap_r, L.st, buf_l, buf_r, vs);
 }
 
-void launch_dist_pack(const Launch& L, const Soa& C, DistLayout* lay, int side, int cap_msg, char* buf,
-                      const VSrc& vs)
+void launch_dist_unpack(const Launch& L, const char* buf_l, const char* buf_r, DistLayout* lay, int cap_l,
+                        int cap_r, int cap, const Soa& C)
 {
     Profiler* prof = L.prof;
-    MPH_LAUNCH("dist_pack", L.stream, k_dist_pack, dim3(dist_blocks(cap_msg)), dim3(256), 0, L.stream, C, lay,
-               side, cap_msg, L.st, buf, vs);
+    MPH_LAUNCH("dist_unpack", L.stream, k_dist_unpack, dim3(dist_blocks(std::max(cap_l, cap_r)), 2), dim3(256), 0,
+               L.stream, buf_l, buf_r, lay, cap_l, cap_r, cap, L.st, C);
 }
 
-void launch_dist_unpack(const Launch& L, const char* buf_l, const char* buf_r, DistLayout* lay, int side,
-                        int cap_msg, int cap, const Soa& C)
+void launch_halo_pack(const Launch& L, const int* dst_of, const DistLayout* lay, int cap_l, int cap_r,
+                      const HaloFields& F, double* buf_l, double* buf_r)
 {
     Profiler* prof = L.prof;
-    MPH_LAUNCH("dist_unpack", L.stream, k_dist_unpack, dim3(dist_blocks(cap_msg)), dim3(256), 0, L.stream, buf_l,
-               buf_r, lay, side, cap_msg, cap, L.st, C);
+    MPH_LAUNCH("halo_pack", L.stream, k_halo_pack, dim3(dist_blocks(std::max(cap_l, cap_r)), 2), dim3(256), 0,
+               L.stream, dst_of, lay, cap_l, cap_r, F, buf_l, buf_r);
 }
 
-void launch_halo_pack(const Launch& L, const int* dst_of, const DistLayout* lay, int dir, int cap,
-                      const HaloFields& F, double* buf)
+void launch_halo_unpack(const Launch& L, const double* buf_l, const double* buf_r, const int* dst_of,
+                        const DistLayout* lay, int cap_l, int cap_r, const HaloFields& F)
 {
     Profiler* prof = L.prof;
-    MPH_LAUNCH("halo_pack", L.stream, k_halo_pack, dim3(dist_blocks(cap)), dim3(256), 0, L.stream, dst_of, lay,
-               dir, cap, F, buf);
-}
-
-void launch_halo_unpack(const Launch& L, const double* buf, const int* dst_of, const DistLayout* lay, int dir,
-                        int cap, const HaloFields& F)
-{
-    Profiler* prof = L.prof;
-    MPH_LAUNCH("halo_unpack", L.stream, k_halo_unpack, dim3(dist_blocks(cap)), dim3(256), 0, L.stream, buf,
-               dst_of, lay, dir, cap, F);
+    MPH_LAUNCH("halo_unpack", L.stream, k_halo_unpack, dim3(dist_blocks(std::max(cap_l, cap_r)), 2), dim3(256), 0,
+               L.stream, buf_l, buf_r, dst_of, lay, cap_l, cap_r, F);
 }
 
 }  // namespace mph
