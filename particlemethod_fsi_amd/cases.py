@@ -307,6 +307,13 @@ _reg(Case("channel2d", 2, "dam", 0.001, (0.0, 0.0, 0.0), (0.04, 0.03, 0.001), [
     Cuboid(1, (0.0, 0.003, 0.0), (0.04, 0.015, 0.001), 0.001, (_U, 0.0, 0.0)),
     Cuboid(4, (0.0, 0.0, 0.0), (0.04, 0.003, 0.001), 0.001),
 ], note="periodic 2-D channel flow (slab tests)"))
+# fluid on both sides of the periodic y face with empty space between: the GPU grid's origin
+# moves into the gap (choose_grid_origin), so the y face lies inside the grid and the pairs across
+# it need the search's face rule (DevState.seam_occ) -- parity test of that rule
+_reg(Case("seam3d", 3, "dam", 0.001, (0.0, 0.0, 0.0), (0.03, 0.04, 0.02), [
+    Cuboid(1, (0.0, 0.0, 0.0), (0.03, 0.006, 0.02), 0.001, (0.0, -_U, 0.0)),
+    Cuboid(1, (0.0, 0.034, 0.0), (0.03, 0.04, 0.02), 0.001, (_U, 0.0, 0.0)),
+], note="fluid across the periodic y face, empty band between (grid origin / face rule)"))
 _reg(Case("channel3d_st", 3, "dam", 0.001, CASES["channel3d"].lower, CASES["channel3d"].upper,
           CASES["channel3d"].cuboids, data_changes=_ST, note="channel3d with surface tension"))
 

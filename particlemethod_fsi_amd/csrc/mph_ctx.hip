@@ -326,13 +326,26 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     // below a quarter of the domain width, which needs > 4 x that many cells on every axis)
     c->P.sa = kContigReach;
     c->P.fast_ok = 1;
+    c->P.seam_always = 0;
+    // the grid's origin in an empty band of the initial particles (choose_grid_origin;
+    // MPH_GRID_SHIFT=0 keeps dmin): the search's interior box is then in grid offsets
+    const char* gsh = std::getenv("MPH_GRID_SHIFT");
+    const bool shift = !(gsh && gsh[0] == '0');
     for (int d = 0; d < 3; ++d) {
-        if (d == 2 && cfg->dim == 2) { c->P.inner_lo[d] = -1e300; c->P.inner_hi[d] = 1e300; continue; }
+        if (d == 2 && cfg->dim == 2) {
+            c->P.inner_lo[d] = c->P.sinner_lo[d] = -1e300;
+            c->P.inner_hi[d] = c->P.sinner_hi[d] = 1e300;
+            continue;
+        }
         const int m = stencil_margin(c->P, d);
         if (c->P.gc[d] <= 4 * m) c->P.fast_ok = 0;
         const double cw = c->h.dw[d] / c->P.gc[d];
         c->P.inner_lo[d] = c->h.dmin[d] + m * cw * (1.0 + 1e-9);
         c->P.inner_hi[d] = c->h.dmax[d] - m * cw * (1.0 + 1e-9);
+        const int s0 = shift && c->P.fast_ok ? choose_grid_origin(c->h, n, pos, d, c->P.gc[d], m) : 0;
+        c->P.corg[d] = c->h.dmin[d] + s0 * cw;
+        c->P.sinner_lo[d] = m * cw * (1.0 + 1e-9);
+        c->P.sinner_hi[d] = c->h.dw[d] - m * cw * (1.0 + 1e-9);
     }
     // slab mode: owned subset, local window grid along the slab axis, array capacity
     std::vector<int> owned;

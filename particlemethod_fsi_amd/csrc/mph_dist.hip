@@ -523,6 +523,10 @@ int dist_setup(MphCtx* c, const double* pos, std::vector<int>& owned)
     // fast-path interior: >= 3 cells inside both the window and the periodic domain
     c->P.inner_lo[axis] = std::max(wlo, h.dmin[axis]) + m * cw * (1.0 + 1e-9);
     c->P.inner_hi[axis] = std::min(whi, h.dmax[axis]) - m * cw * (1.0 + 1e-9);
+    // the search's box in offsets from the window's edge; the face box always applies on this axis
+    c->P.sinner_lo[axis] = std::max(wlo, h.dmin[axis]) - wlo + m * cw * (1.0 + 1e-9);
+    c->P.sinner_hi[axis] = std::min(whi, h.dmax[axis]) - wlo - m * cw * (1.0 + 1e-9);
+    c->P.seam_always |= 1 << axis;
     // initial owned set and a capacity for owned + ghosts (+ headroom for migration imbalance)
     owned.clear();
     size_t near = 0;

@@ -649,6 +649,46 @@ int choose_cell_order(const HostDerived& h, int n, const double* pos, double rc)
     return (hi[0] - lo[0]) >= (hi[1] - lo[1]) ? 3 : 4;
 }
 
+// Origin of the GPU cell grid along axis d, in whole cells from dmin: the middle of the longest
+// circular run of cells that hold none of the initial particles, when that run is at least
+// 2 m + 2 cells (m = the stencil margin); else 0 (the grid starts at dmin).  A grid whose faces lie
+// in empty space keeps the waves at a wall on a periodic face of the domain (the dam's bottom
+// wall at y = 0) off the wrapped slow path of the search (DevParams.sinner_lo, seam_occ).
+int choose_grid_origin(const HostDerived& h, int n, const double* pos, int d, int gc, int m)
+{
+    if (gc <= 0 || n <= 0) return 0;
+    std::vector<char> occ((size_t)gc, 0);
+    const double ginv = gc / h.dw[d];
+    for (int i = 0; i < n; ++i) {
+        double u = pos[3 * (size_t)i + d] - h.dmin[d];
+        u -= h.dw[d] * std::floor(u / h.dw[d]);
+        const int c = std::min(gc - 1, std::max(0, (int)std::floor(u * ginv)));
+        occ[(size_t)c] = 1;
+    }
+    int first = -1;
+    for (int c = 0; c < gc && first < 0; ++c)
+        if (occ[(size_t)c]) first = c;
+    if (first < 0) return 0;
+    // only worth it when particles lie within the margin of a face of the domain (the waves there
+    // take the wrapped search otherwise); a grid that already starts in empty space stays at dmin
+    bool at_face = false;
+    for (int c = 0; c < m && !at_face; ++c) at_face = occ[(size_t)c] || occ[(size_t)(gc - 1 - c)];
+    if (!at_face) return 0;
+    int best = 0, best_start = 0, run = 0, run_start = 0;
+    for (int k = 1; k <= gc; ++k) {   // one lap from the first occupied cell
+        const int c = (first + k) % gc;
+        if (!occ[(size_t)c]) {
+            if (run == 0) run_start = c;
+            ++run;
+        } else {
+            if (run > best) { best = run; best_start = run_start; }
+            run = 0;
+        }
+    }
+    if (best < 2 * m + 2) return 0;
+    return (best_start + best / 2) % gc;
+}
+
 // GPU linked-cell grid: cells of width >= rc/kReach along the two outer axes (a +-kReach stencil
 // covers the acceptance sphere) and >= rc/sa along the contiguous axis (z in 3-D, y in 2-D;
 // a +-sa stencil, scanned as one contiguous index range per column, so thinner cells there

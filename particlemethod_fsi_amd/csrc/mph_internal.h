@@ -24,6 +24,7 @@ void derive_constants(const MphConfig& c, HostDerived& h);
 void fill_scalars(const HostDerived& h, const MphConfig& c, double* out36);
 // z-slab cell order (DevParams.perm 3 or 4) from the particle positions
 int choose_cell_order(const HostDerived& h, int n, const double* pos, double rc);
+int choose_grid_origin(const HostDerived& h, int n, const double* pos, int d, int gc, int m);
 int choose_grid(const HostDerived& h, int dim, double rc, int sa, int gc[3], double ginv[3], std::string& err,
                 int perm = 0);
 void make_dev_params(const MphConfig& c, const HostDerived& h, int n, int n_struct, DevParams& P);

@@ -205,6 +205,46 @@ __device__ __forceinline__ bool wave_interior(const DevParams& P, bool live, dou
     return P.fast_ok && __all(in);
 }
 
+// Particles of this lane within the face box margin of a periodic face: bit 2k low face, 2k + 1
+// high face of axis k (k_prep gathers them per step into DevState.seam_occ).
+__device__ __forceinline__ int seam_bits(const DevParams& P, double x, double y, double z)
+{
+    const double v[3] = {x, y, z};
+    int b = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (k == 2 && P.dim == 2) break;
+        if ((P.seam_always >> k) & 1) continue;   // (the slab axis: the face box always applies)
+        b |= (v[k] < P.inner_lo[k] ? 1 : 0) << (2 * k);
+        b |= (v[k] > P.inner_hi[k] ? 2 : 0) << (2 * k);
+    }
+    return b;
+}
+
+// wave-uniform, for the search: every live lane is >= 3 cells inside the cell grid's faces (so no
+// stencil row wraps) and, on every axis with particles near BOTH periodic faces (this step's
+// seam_occ) or on the slab axis, also >= 3 cells from the domain's faces (so no candidate pair
+// straddles the periodic seam and the raw differences are the minimum image).  With the grid
+// origin at dmin this is wave_interior; with the origin in an empty band it also admits the waves
+// at a wall on a periodic face whose far side is empty (the dam's bottom wall).
+__device__ __forceinline__ bool wave_search_interior(const DevParams& P, const DevState* st, bool live,
+                                                     double x, double y, double z)
+{
+    const int occ = st->seam_occ[(st->seam_step - 1) & 1];
+    const double v[3] = {x, y, z};
+    bool in = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (k == 2 && P.dim == 2) break;
+        double u = v[k] - P.corg[k];
+        u = u < 0.0 ? u + P.dw[k] : (u >= P.dw[k] ? u - P.dw[k] : u);
+        in = in && u >= P.sinner_lo[k] && u <= P.sinner_hi[k];
+        const bool seam = ((P.seam_always >> k) & 1) || ((occ >> (2 * k)) & 3) == 3;
+        if (seam) in = in && v[k] >= P.inner_lo[k] && v[k] <= P.inner_hi[k];
+    }
+    return P.fast_ok && __all(!live || in);
+}
+
 // XCD-aware block order: hardware deals consecutive blocks round-robin over the 8 XCDs; remap so
 // that each XCD sweeps one contiguous 1/8 of the (cell-sorted) particles and neighbour gathers
 // hit its own L2 (cdna_hip_programming.md T1, bijective form).
@@ -491,12 +531,14 @@ __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __res
         // Every lane of the wave takes part in the shuffles; lanes past n form runs of their own.
         const bool live = p < n;
         int k = -1 - (int)(threadIdx.x & 63);
+        int occ = 0;
         if (live) {
             double x = B.x[b], y = B.y[b], z = B.z[b];
             if (mode == 1) move_and_wrap(P, st, B, b, x, y, z);
             if (!isfinite(x + y + z)) atomicOr(const_cast<int*>(&st->overflow), 4);   // MPH_ERR_NONFINITE
             k = cell_id(P, x, y, z);
             key[p] = k;
+            occ = seam_bits(P, x, y, z);
         }
         const int lane = threadIdx.x & 63;
         const int kprev = __shfl_up(k, 1, 64);
@@ -510,6 +552,22 @@ __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __res
         if (live && head) base = atomicAdd(&cnt[k], next - lane);
         base = __shfl(base, hl, 64);
         if (live) slot[p] = base + (lane - hl);
+        // the block's face bits: OR-ed in LDS, then one device atomic per block, only for bits the
+        // step's word does not hold yet (few blocks: the particles near a periodic face)
+        __shared__ int s_occ;
+        if (threadIdx.x == 0) s_occ = 0;
+        __syncthreads();
+        if (__ballot(occ != 0)) {
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) occ |= __shfl_xor(occ, o, 64);
+            if (lane == 0) atomicOr(&s_occ, occ);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0 && s_occ) {
+            int* w = const_cast<int*>(&st->seam_occ[st->seam_step & 1]);
+            const int cur = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (s_occ & ~cur) atomicOr(w, s_occ);
+        }
         return;
     }
     if (p >= n) return;
@@ -519,6 +577,11 @@ __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __res
     const int k = cell_id(P, x, y, z);
     key[p] = k;
     slot[p] = atomicAdd(&cnt[k], 1);
+    const int occ = seam_bits(P, x, y, z);
+    if (occ) {
+        int* w = const_cast<int*>(&st->seam_occ[st->seam_step & 1]);
+        if (occ & ~__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicOr(w, occ);
+    }
 }
 
 // Exclusive scan of the cell histogram: 3 launches (block reduce, top-level scan, down-sweep).
@@ -668,6 +731,10 @@ __global__ __launch_bounds__(256) void k_place(DevParams P, DevState* __restrict
 {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // this step's face bits are complete (k_prep): the searches read them; the next step's
+        // k_prep gathers into the other word
+        st->seam_occ[(st->seam_step + 1) & 1] = 0;
+        st->seam_step += 1;
         if (mode) {
 #pragma clang fp contract(off)
             for (int t = 4; t < 6; ++t)
@@ -1473,7 +1540,7 @@ __device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A,
     // the ghost lanes of a mixed wave take no part either (empty list)
     const bool own = live && !(P.slab_axis >= 0 && A.id[ii] < 0);
     const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
-    const bool fast = wave_interior(P, own, xi, yi, zi);
+    const bool fast = wave_search_interior(P, st, own, xi, yi, zi);
     int cnt = 0;
     const int cx = cell_axis(xi, P.corg[0], P.dw[0], P.ginv[0], P.gc[0]);
     const int cy = cell_axis(yi, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
@@ -1737,7 +1804,8 @@ template <int DIM>
 __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const DevTables* __restrict__ T, Soa A,
                                                 const int* __restrict__ nbr,
                                                 const int* __restrict__ ncount, const int2* __restrict__ hdr,
-                                                const int* __restrict__ lhdr, PassAOut pout)
+                                                const int* __restrict__ lhdr, PassAOut pout,
+                                                const DevState* __restrict__ st)
 {
     const int n = dev_n(P);
     if ((int)blockIdx.x >= live_blocks(n)) return;
@@ -1775,7 +1843,8 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
         if (own) pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
         return;
     }
-    const bool fast = wave_interior(P, own, xi, yi, zi);
+    // the search's rule (its list order and the fast minimum image go together)
+    const bool fast = wave_search_interior(P, st, own, xi, yi, zi);
     if (!own) return;
     double vxi, vyi, vzi;
     own_velocity(A, i, vxi, vyi, vzi);
@@ -2044,7 +2113,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MPH_FUSED_W
     const bool ghost = live && P.slab_axis >= 0 && A.id[ii] < 0;
     if (ghost && pout.rec) pout.rec[i] = make_double4(xi, yi, zi, 0.0);
     const bool own = live && !ghost;
-    const bool fast = wave_interior(P, own, xi, yi, zi);
+    const bool fast = wave_search_interior(P, st, own, xi, yi, zi);
     const int cx = cell_axis(xi, P.corg[0], P.dw[0], P.ginv[0], P.gc[0]);
     const int cy = cell_axis(yi, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
     const int cz = DIM == 3 ? cell_axis(zi, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
@@ -2288,7 +2357,8 @@ __global__ __launch_bounds__(256) MPH_PB_ATTR void k_pass_b(DevParams P, const D
                                                 const int* __restrict__ ncount, const int2* __restrict__ hdr,
                                                 const int* __restrict__ lhdr,
                                                 double4* __restrict__ force, double4* __restrict__ acc,
-                                                Soa B, int phase, int* __restrict__ wface, StructHook H)
+                                                Soa B, int phase, int* __restrict__ wface, StructHook H,
+                                                const DevState* __restrict__ st)
 {
     const int n = dev_n(P);
     if ((int)blockIdx.x >= live_blocks(n)) return;
@@ -2330,7 +2400,7 @@ __global__ __launch_bounds__(256) MPH_PB_ATTR void k_pass_b(DevParams P, const D
         return;
     }    const int2* h = hdr ? hdr + (size_t)(i >> 6) * kSegHdr : nullptr;
     const bool segmented = MPH_SEG && h && h[kSegCols].x == 1;   // wave-uniform
-    const bool fast = segmented || wave_interior(P, live, xi, yi, zi);
+    const bool fast = segmented || wave_search_interior(P, st, live, xi, yi, zi);
     if (!segmented && !live) return;
     const int ti = A.type[ii];
     const bool solid = dev_is_struct(ti);
@@ -3439,10 +3509,10 @@ void launch_pass_a(const Launch& L)
     const PassAOut po = pass_a_out(L);
     if (P.dim == 3)
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, po);
+                   L.A, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, po, L.st);
     else
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, po);
+                   L.A, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, po, L.st);
 }
 
 // calculateNeighbor + the pass-A sums: the fused kernel (k_search_pass_a) when the list is the
@@ -3504,7 +3574,7 @@ void launch_pass_b(const Launch& L, int phase)
     MPH_LAUNCH(phase == 2 ? "pass_b_face" : "pass_b", L.stream, (k_pass_b<S, D>), dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, \
                L.T, L.A, L.rec, L.fpart, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, L.force, L.acc, L.B, \
                phase, L.wface, \
-               struct_hook(L))
+               struct_hook(L), L.st)
     if (P.surface) {
         if (P.dim == 3) MPH_PASS_B(true, 3); else MPH_PASS_B(true, 2);
     } else {

@@ -101,6 +101,13 @@ struct DevParams {
     int fast_ok;       // every active axis has > 12 GPU cells: interior waves may skip the
                        // periodic branch of the minimum image (see k_neighbors)
     double inner_lo[3], inner_hi[3];   // interior box: >= 3 GPU cells from every periodic face
+    // the search's interior box in grid offsets (position - corg, wrapped into [0, dw)): >= 3
+    // cells from the grid's faces.  The grid origin corg may sit inside an empty band of the
+    // domain (choose_grid_origin), so particles at a periodic face of the domain can be interior
+    // to the grid; their waves then need the face box above only while particles lie within it at
+    // both ends of that axis (DevState.seam_occ) or on the slab axis (seam_always bit)
+    double sinner_lo[3], sinner_hi[3];
+    int seam_always;
     double dmin[3], dw[3], hw[3], w075[3];   // domain min / width / half width / 0.75 width
     double corg[3];    // origin of the GPU cell grid (dmin, or the slab window's lower edge)
     double ginv[3];    // 1 / GPU cell width per axis
@@ -156,6 +163,12 @@ struct DevState {
     int overflow;                // error bits: 1 neighbour overflow (> MAX_NEIGHBOR_COUNT),
                                  // 2 slab jump (mph_dist), 4 non-finite position
     int list_redo;               // waves of this step's search left for k_neighbors_redo
+    // particles within the face box margin of a periodic face, per axis (bit 2k: low face, 2k+1:
+    // high face), gathered by k_prep into seam_occ[seam_step & 1]; k_place clears the other word
+    // and advances seam_step, so the search reads seam_occ[(seam_step - 1) & 1]
+    int seam_occ[2];
+    int seam_step;
+    int seam_pad;
 };
 
 #if defined(__HIPCC__)

@@ -12,7 +12,7 @@ for case in ${CASES:-${CASE:-d1m}}; do
     envset=()
     if [[ "$name" == *@* ]]; then   # <build>@VAR=VALUE: an alternative build with a run-time setting
       lib=$PWD/particlemethod_fsi_amd/lib_${name%%@*}/libmph_gpu.so; envset=("${name#*@}")
-    elif [[ "$name" == *=* ]]; then envset=("$name")
+    elif [[ "$name" == *=* ]]; then IFS=, read -ra envset <<< "$name"   # VAR=VALUE[,VAR2=VALUE2]
     elif [ "$name" != base ]; then lib=$PWD/particlemethod_fsi_amd/lib_$name/libmph_gpu.so; fi
     env "${envset[@]}" MPH_GPU_LIB=$lib timeout -k 10 300 python bench.py --case $case --steps ${STEPS:-20} \
         --warmup 4 --no-cpu-baseline > "gpurun_out/ab_${case}_${name}.log" 2>&1 || exit 40
