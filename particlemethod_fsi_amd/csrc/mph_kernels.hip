@@ -263,6 +263,13 @@ __device__ __forceinline__ int dev_n(const DevParams& P) { return P.n_dev ? *P.n
 // XCD remap runs over the live blocks only, so the work stays spread over all 8 XCDs.
 __device__ __forceinline__ int live_blocks(int n) { return (n + 255) >> 8; }
 
+// Threads per block of the three list kernels (search, pass A, pass B): MPH_LB / 64 wavefronts
+#ifndef MPH_LB
+#define MPH_LB 256
+#endif
+constexpr int kWB = MPH_LB / 64;
+__device__ __forceinline__ int list_blocks(int n) { return (n + MPH_LB - 1) / MPH_LB; }
+
 __device__ __forceinline__ int nbr_entry(int j, int type) { return j | (type << kTypeShift); }
 
 // Velocity of sorted particle i for the list passes: from its 48-byte gather record {x, y, z, vx,
@@ -1592,15 +1599,15 @@ __device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A,
 #define MPH_NB_WPE 6
 #endif
 template <int DIM, int PERM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MPH_NB_WPE))) void k_neighbors(DevParams P, Soa A, const int* __restrict__ start,
+__global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_WPE))) void k_neighbors(DevParams P, Soa A, const int* __restrict__ start,
                                                    int* __restrict__ nbr, int* __restrict__ ncount,
                                                    int2* __restrict__ hdr, int* __restrict__ lhdr,
                                                    DevState* __restrict__ st, int* __restrict__ wface)
 {
     const int n = dev_n(P);
-    if ((int)blockIdx.x >= live_blocks(n)) return;
-    __shared__ __attribute__((aligned(16))) double stage[4][stage_words(MPH_LDS_CAP, MPH_SB)];
-    const int i = xcd_block(blockIdx.x, live_blocks(n)) * blockDim.x + threadIdx.x;
+    if ((int)blockIdx.x >= list_blocks(n)) return;
+    __shared__ __attribute__((aligned(16))) double stage[kWB][stage_words(MPH_LDS_CAP, MPH_SB)];
+    const int i = xcd_block(blockIdx.x, list_blocks(n)) * blockDim.x + threadIdx.x;
     slab_wave_flag(P, A, i, n, wface);
     neighbors_body<DIM, PERM, 0>(P, A, start, nbr, ncount, hdr, lhdr, st, stage[threadIdx.x >> 6], i);
 }
@@ -1801,14 +1808,14 @@ __device__ __forceinline__ void pass_a_seg(const DevParams& P, const double* s_r
 #define MPH_PA_ATTR
 #endif
 template <int DIM>
-__global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const DevTables* __restrict__ T, Soa A,
+__global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, const DevTables* __restrict__ T, Soa A,
                                                 const int* __restrict__ nbr,
                                                 const int* __restrict__ ncount, const int2* __restrict__ hdr,
                                                 const int* __restrict__ lhdr, PassAOut pout,
                                                 const DevState* __restrict__ st)
 {
     const int n = dev_n(P);
-    if ((int)blockIdx.x >= live_blocks(n)) return;
+    if ((int)blockIdx.x >= list_blocks(n)) return;
     __shared__ double s_ratio[kTypes * kTypes];
     __shared__ double s_mu[kTypes * kTypes];
     if (threadIdx.x < kTypes * kTypes) {
@@ -1816,7 +1823,7 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
         s_mu[threadIdx.x] = T->mu_ij[threadIdx.x] * (-P.cvis * P.cdv * P.vol);   // pass_a_term's viscous factor
     }
     __syncthreads();
-    const int i = xcd_block(blockIdx.x, live_blocks(n)) * blockDim.x + threadIdx.x;
+    const int i = xcd_block(blockIdx.x, list_blocks(n)) * blockDim.x + threadIdx.x;
     const bool live = i < n;
     const int ii = live ? i : n - 1;
     const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
@@ -1832,7 +1839,7 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
     const bool own = live && !ghost;
     const int2* h = hdr ? hdr + (size_t)(i >> 6) * kSegHdr : nullptr;
     if (MPH_SEG && h && h[kSegCols].x == 1) {   // wave-uniform: this wave's list is column-segmented
-        __shared__ double2 stage[4][3 * MPH_LDS_CAP];
+        __shared__ double2 stage[kWB][3 * MPH_LDS_CAP];
         double vxi, vyi, vzi;
         own_velocity(A, ii, vxi, vyi, vzi);
         const int ti = A.type[ii];
@@ -1851,7 +1858,7 @@ __global__ __launch_bounds__(256) MPH_PA_ATTR void k_pass_a(DevParams P, const D
     const int ti = A.type[i];
     const bool solid = dev_is_struct(ti);
     const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
-    __shared__ int s_gb[4][8];
+    __shared__ int s_gb[kWB][8];
     const NbrList NL = nbr_list(nbr, lhdr, i, s_gb[threadIdx.x >> 6]);
     PassA o;
     // wave-uniform: equal radii (every BASELINE config) take the single-cutoff form of the sums
@@ -2345,7 +2352,7 @@ template <bool SURF, int DIM>
 #else
 #define MPH_PB_ATTR
 #endif
-__global__ __launch_bounds__(256) MPH_PB_ATTR void k_pass_b(DevParams P, const DevTables* __restrict__ T, Soa A,
+__global__ __launch_bounds__(MPH_LB) MPH_PB_ATTR void k_pass_b(DevParams P, const DevTables* __restrict__ T, Soa A,
                                                 const double4* __restrict__ rec,
                                                 const double4* __restrict__ fpart,
                                                 const double* __restrict__ pres,
@@ -2361,13 +2368,13 @@ __global__ __launch_bounds__(256) MPH_PB_ATTR void k_pass_b(DevParams P, const D
                                                 const DevState* __restrict__ st)
 {
     const int n = dev_n(P);
-    if ((int)blockIdx.x >= live_blocks(n)) return;
+    if ((int)blockIdx.x >= list_blocks(n)) return;
     __shared__ double s_ratio[kTypes * kTypes];
     if (SURF) {
         if (threadIdx.x < kTypes * kTypes) s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
         __syncthreads();
     }
-    const int i = xcd_block(blockIdx.x, live_blocks(n)) * blockDim.x + threadIdx.x;
+    const int i = xcd_block(blockIdx.x, list_blocks(n)) * blockDim.x + threadIdx.x;
     const int ii = i < n ? i : n - 1;
     const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
     bool live = i < n;
@@ -2413,13 +2420,13 @@ __global__ __launch_bounds__(256) MPH_PB_ATTR void k_pass_b(DevParams P, const D
     }
     if (segmented) {
         // every lane of the wave stages; the lanes without a particle of this phase only help
-        __shared__ double4 stage[4][MPH_LDS_CAP];
+        __shared__ double4 stage[kWB][MPH_LDS_CAP];
         pass_b_seg<SURF, DIM>(P, s_ratio, rec, gx, gy, gz, pa, seg_tile(nbr, i), h, live, ti, solid, xi, yi, zi,
                               gxi, gyi, gzi, pai, ai, f0, f1, f2, stage[threadIdx.x >> 6]);
         if (!live) return;
     } else {
         const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
-        __shared__ int s_gb[4][8];
+        __shared__ int s_gb[kWB][8];
         const NbrList NL = nbr_list(nbr, lhdr, i, s_gb[threadIdx.x >> 6]);
         if (NL.c16)   // compact lists come from interior searches only
             pass_b_loop<true, true, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, NL, cnt, ti, solid, xi,
@@ -3480,7 +3487,7 @@ void launch_neighbors(const Launch& L)
     // first marked them
 #define MPH_NEIGHBORS(D, PERM)                                                                               \
     do {                                                                                                     \
-        MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM>), dim3(blocks(P.n, 256)), dim3(256), 0,     \
+        MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM>), dim3(blocks(P.n, MPH_LB)), dim3(MPH_LB), 0,     \
                    L.stream, P, L.A, L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, L.st,    \
                    L.wface);                                                                                \
         if (L.lhdr)                                                                                          \
@@ -3508,10 +3515,10 @@ void launch_pass_a(const Launch& L)
     if (P.n == 0) return;
     const PassAOut po = pass_a_out(L);
     if (P.dim == 3)
-        MPH_LAUNCH("pass_a", L.stream, k_pass_a<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T,
+        MPH_LAUNCH("pass_a", L.stream, k_pass_a<3>, dim3(blocks(P.n, MPH_LB)), dim3(MPH_LB), 0, L.stream, P, L.T,
                    L.A, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, po, L.st);
     else
-        MPH_LAUNCH("pass_a", L.stream, k_pass_a<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T,
+        MPH_LAUNCH("pass_a", L.stream, k_pass_a<2>, dim3(blocks(P.n, MPH_LB)), dim3(MPH_LB), 0, L.stream, P, L.T,
                    L.A, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, po, L.st);
 }
 
@@ -3571,7 +3578,7 @@ void launch_pass_b(const Launch& L, int phase)
         std::abort();
     }
 #define MPH_PASS_B(S, D)                                                                            \
-    MPH_LAUNCH(phase == 2 ? "pass_b_face" : "pass_b", L.stream, (k_pass_b<S, D>), dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, \
+    MPH_LAUNCH(phase == 2 ? "pass_b_face" : "pass_b", L.stream, (k_pass_b<S, D>), dim3(blocks(P.n, MPH_LB)), dim3(MPH_LB), 0, L.stream, P, \
                L.T, L.A, L.rec, L.fpart, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, L.force, L.acc, L.B, \
                phase, L.wface, \
                struct_hook(L), L.st)

@@ -16,6 +16,10 @@ if [ -z "$NO_SERIAL" ]; then
   timeout -k 10 400 python tools/slab_serial.py --case d16m --ranks 8 --steps 6 --warmup 2 > $OUT/serial_d16m_8.json 2>> $OUT/serial.err || exit 13
   MPH_SLAB_OVERLAP=0 timeout -k 10 400 python tools/slab_serial.py --case d16m --ranks 8 --steps 6 --warmup 2 > $OUT/serial_d16m_8_nooverlap.json 2>> $OUT/serial.err || exit 14
 fi
+for v in $SERIAL_VARIANTS; do   # alternative builds (lib_<name>), one rank at a time without the overlap
+  MPH_GPU_LIB=$PWD/particlemethod_fsi_amd/lib_$v/libmph_gpu.so MPH_SLAB_OVERLAP=0 timeout -k 10 400 python tools/slab_serial.py \
+      --case d16m --ranks 8 --steps 6 --warmup 2 > $OUT/serial_d16m_8_nooverlap_$v.json 2>> $OUT/serial.err || exit 17
+done
 if [ -n "$PMC_VARIANTS" ]; then
   VARIANTS="$PMC_VARIANTS" bash tools/pmc_ab.sh || exit 15
   for v in $PMC_VARIANTS; do cp gpurun_out/pmc_$v.txt $OUT/; done
