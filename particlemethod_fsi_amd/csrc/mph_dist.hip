@@ -2,8 +2,8 @@
 //
 // The reference has no domain decomposition (one OpenMP/OpenACC process, main.cpp:597-686).  The
 // update of a particle depends only on neighbours within the cutoff rc = MaxRadius + MARGIN
-// (main.cpp:1765), so the periodic domain is cut into `nranks` equal slabs along one axis
-// (SURVEY 8e).  Each rank holds
+// (main.cpp:1765), so the periodic domain is cut into `nranks` slabs along one axis (equal widths,
+// or the cuts of MphSlabOptions).  Each rank holds
 //
 //   owned   particles inside its slab [lo, hi)                (computed, returned by mph_get)
 //   ghosts  copies of the neighbours' particles within h >= rc of a face, and of its own
