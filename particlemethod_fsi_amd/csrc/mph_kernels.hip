@@ -55,7 +55,8 @@
                             // 4 = waves near a periodic face do nothing
 #endif
 #ifndef MPH_DIAG_NOSTORE
-#define MPH_DIAG_NOSTORE 0   // diagnostic builds only: the search counts but stores no list
+#define MPH_DIAG_NOSTORE 0   // diagnostic builds only: 1 = the search counts but stores no list,
+                             // 2 = every store goes to the lane's row 0 (same instructions, no list traffic)
 #endif
 #ifndef MPH_DIAG_GATHER
 #define MPH_DIAG_GATHER 0   // diagnostic builds only: 1 = list passes gather a coalesced dummy
@@ -1429,6 +1430,8 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                             const int k = min(cnt, kMaxNeighbor - 1);
                             o16[(((k >> 1) * kTile + lane) << 1) + (k & 1)] =
                                 (unsigned short)((j - gbase) | (st[k0 + u + tofs] << kOff16));
+                        } else if (MPH_DIAG_NOSTORE == 2) {   // diagnostic: same stores, one row (no list traffic)
+                            list_store(out + (min(cnt, kMaxNeighbor - 1) & 0) * kTile, nbr_entry(j, st[k0 + u + tofs]));
                         } else if (!MPH_DIAG_NOSTORE) {
                             list_store(out + min(cnt, kMaxNeighbor - 1) * kTile, nbr_entry(j, st[k0 + u + tofs]));
                         }
