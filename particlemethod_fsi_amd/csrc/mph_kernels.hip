@@ -84,6 +84,14 @@
 #ifndef MPH_LDS_CAP
 #define MPH_LDS_CAP 192   // candidates staged per wave and stencil column
 #endif
+#ifndef MPH_TYPE_BATCH
+// the search reads the candidates' types with each batch of SB (no LDS wait per accepted entry;
+// D1M search -1.6 %, D16M -3.2 %, profiles/r03/search/type_batch/)
+#define MPH_TYPE_BATCH 1
+#endif
+#ifndef MPH_BUF_STORE
+#define MPH_BUF_STORE 1   // ELL list stores of the staged search through a buffer descriptor (A/B)
+#endif
 #ifndef MPH_GLDS
 // the search stages a column's window with global_load_lds (16 bytes per lane straight into LDS:
 // no VGPRs, no ds_write, and the pieces of a window in flight together) instead of register loads
@@ -1189,6 +1197,14 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     double* sz = sx + 2 * SD;
     int* st = reinterpret_cast<int*>(sx + 3 * SD);
     const int lane = threadIdx.x & 63;
+    // buffer descriptor of the wave's ELL tile (out - lane, wave-uniform): list stores take a 32-bit
+    // lane offset instead of a 64-bit address; a store past the tile is dropped by the hardware
+    const unsigned long long tb = (unsigned long long)(out - lane);
+    const unsigned tlo = __builtin_amdgcn_readfirstlane((unsigned)tb);
+    const unsigned thi = __builtin_amdgcn_readfirstlane((unsigned)(tb >> 32));
+    const __amdgpu_buffer_rsrc_t tile_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((unsigned long long)thi << 32) | tlo), 0, kTile * kMaxNeighbor * (int)sizeof(int),
+        0x00020000);
     const double lo2 = P.rc2_lo, hi2 = P.rc2_hi;
     using X = CellAxes<DIM, PERM>;
     int cnt = 0;
@@ -1406,12 +1422,15 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             // the staging arrays are padded by SB entries, so a batch may read past je (masked)
             for (int j0 = jb; j0 < je; j0 += SB) {
                 double xs[SB], ys[SB], zs[SB];
+                int ts[SB];
                 const int k0 = j0 - mn + kofs;
 #pragma unroll
                 for (int u = 0; u < SB; ++u) {
                     xs[u] = sx[k0 + u];
                     ys[u] = sy[k0 + u];
                     zs[u] = sz[k0 + u];
+                    // MPH_TYPE_BATCH: the types with the batch (no LDS wait per accepted entry)
+                    if (MPH_TYPE_BATCH) ts[u] = st[k0 + u + tofs];
                 }
 #pragma unroll
                 for (int u = 0; u < SB; ++u) {
@@ -1433,7 +1452,12 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                         } else if (MPH_DIAG_NOSTORE == 2) {   // diagnostic: same stores, one row (no list traffic)
                             list_store(out + (min(cnt, kMaxNeighbor - 1) & 0) * kTile, nbr_entry(j, st[k0 + u + tofs]));
                         } else if (!MPH_DIAG_NOSTORE) {
-                            list_store(out + min(cnt, kMaxNeighbor - 1) * kTile, nbr_entry(j, st[k0 + u + tofs]));
+                            const int e = nbr_entry(j, MPH_TYPE_BATCH ? ts[u] : st[k0 + u + tofs]);
+                            if (MPH_BUF_STORE)   // 32-bit offset into the wave's tile (SGPR descriptor)
+                                __builtin_amdgcn_raw_buffer_store_b32(
+                                    e, tile_rsrc, (min(cnt, kMaxNeighbor - 1) << 8) + (lane << 2), 0, 0);
+                            else
+                                list_store(out + min(cnt, kMaxNeighbor - 1) * kTile, e);
                         }
                         ++cnt;
                     }
