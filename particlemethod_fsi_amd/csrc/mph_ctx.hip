@@ -359,7 +359,14 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     if (cap > kIndexMask)
         return fail(c, MPH_ERR_UNSUPPORTED, "more than 2^28 particles in one context (neighbour-list entries "
                                             "carry the type in their top bits)");
-    c->P.ncell = c->P.gc[0] * c->P.gc[1] * c->P.gc[2];
+    {
+        // the search addresses the cell table with 32-bit byte offsets (buffer descriptors)
+        const long long nc = (long long)c->P.gc[0] * c->P.gc[1] * c->P.gc[2];
+        if (nc + 1 > (1LL << 30))
+            return fail(c, MPH_ERR_UNSUPPORTED, "cell grid of " + std::to_string(nc) +
+                                                    " cells: more than 2^30 (4 GiB of cell starts)");
+        c->P.ncell = (int)nc;
+    }
     // tables
     for (int t = 0; t < kTypes; ++t) {
         for (int u = 0; u < kTypes; ++u) {

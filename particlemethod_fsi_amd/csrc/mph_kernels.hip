@@ -89,6 +89,11 @@
 // D1M search -1.6 %, D16M -3.2 %, profiles/r03/search/type_batch/)
 #define MPH_TYPE_BATCH 1
 #endif
+#ifndef MPH_GLDS_BUF
+// the search's staging and start[] loads through buffer descriptors (32-bit offsets): measured
+// neutral at D1M and +1.9 % at D16M (profiles/r03/search/buf_staging/), so off
+#define MPH_GLDS_BUF 0
+#endif
 #ifndef MPH_BUF_STORE
 #define MPH_BUF_STORE 1   // ELL list stores of the staged search through a buffer descriptor (A/B)
 #endif
@@ -100,6 +105,18 @@
 #endif
 
 namespace mph {
+
+// Buffer descriptor of a device array (gfx9 raw-buffer format word, 4 GiB of records): loads through
+// it take a 32-bit unsigned byte offset from a VGPR instead of a 64-bit address.  The cell table
+// (ncell + 1 ints, checked at creation) and the particle arrays (< 2^28 entries) stay below 4 GiB.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t arr_rsrc(const void* p)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, -1, 0x00020000);
+}
+__device__ __forceinline__ __attribute__((address_space(3))) void* lds_ptr(void* p)
+{
+    return (__attribute__((address_space(3))) void*)p;
+}
 
 // LDS staging of one wavefront in the search: x, y, z (stage_d doubles each, 16-byte aligned and
 // large enough for a 16-byte-aligned window of CAP candidates plus the SB-entry batch over-read),
@@ -1270,8 +1287,13 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             const int lo = max((int)floorf(caf - rc - 1e-3f), clo);
             const int hi = min((int)floorf(caf + rc + 1e-3f), chi);
             const int b = rowbase + cofs;
-            jb = start[b + lo];
-            je = start[b + hi + 1];
+            if (MPH_GLDS_BUF) {
+                jb = __builtin_amdgcn_raw_buffer_load_b32(arr_rsrc(start), (unsigned)(b + lo) * 4u, 0, 0);
+                je = __builtin_amdgcn_raw_buffer_load_b32(arr_rsrc(start), (unsigned)(b + hi + 1) * 4u, 0, 0);
+            } else {
+                jb = start[b + lo];
+                je = start[b + hi + 1];
+            }
         }
     };
 #else
@@ -1396,6 +1418,22 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             // lanes past the window masked (the arrays hold kPad elements beyond any window)
             const int da = mn & 1, ta = mn & 3;
             const int n2 = span + da, n4 = span + ta;
+#if MPH_GLDS_BUF
+            // buffer form: one 32-bit lane offset for x, y and z (SGPR descriptors of the arrays)
+            for (int p = 0; p * 128 < n2; ++p) {   // wave-uniform
+                const int e = p * 128 + 2 * lane;
+                if (e < n2) {
+                    const unsigned vo = (unsigned)(mn - da + e) * 8u;
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(arr_rsrc(A.x), lds_ptr(sx + p * 128), 16, vo, 0, 0, 0);
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(arr_rsrc(A.y), lds_ptr(sy + p * 128), 16, vo, 0, 0, 0);
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(arr_rsrc(A.z), lds_ptr(sz + p * 128), 16, vo, 0, 0, 0);
+                }
+            }
+            static_assert(CAP + 3 <= 256, "one 256-int piece holds the types of a window");
+            if (4 * lane < n4)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(arr_rsrc(A.type), lds_ptr(st), 16,
+                                                         (unsigned)(mn - ta + 4 * lane) * 4u, 0, 0, 0);
+#else
             for (int p = 0; p * 128 < n2; ++p) {   // wave-uniform
                 const int e = p * 128 + 2 * lane;
                 if (e < n2) {
@@ -1406,6 +1444,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             }
             static_assert(CAP + 3 <= 256, "one 256-int piece holds the types of a window");
             if (4 * lane < n4) __builtin_amdgcn_global_load_lds(A.type + (mn - ta) + 4 * lane, st, 16, 0, 0);
+#endif
             __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the pieces have landed in LDS
             const int kofs = da, tofs = ta - da;
 #else
