@@ -63,7 +63,10 @@
                             // neighbour (j = lane id ^ 1) instead of the listed one, 2 = gathers only
 #endif
 #ifndef MPH_SB
-#define MPH_SB 3   // candidates per batch in the search (3: 72 VGPRs, 7 waves per SIMD; D1M 0.395 ms against 0.433 at 4)
+// candidates per batch in the search: 2 (64 VGPRs) with the LDS capacity below gives 8 waves per
+// SIMD (round 3: D1M 0.355 -> 0.347 ms, D16M 4.11 -> 3.86, profiles/r03/search/sb2/); 3 took
+// 72 VGPRs and 7 waves (round 2: 0.395 ms against 0.433 at 4)
+#define MPH_SB 2
 #endif
 #ifndef MPH_SEARCH_LDS
 #define MPH_SEARCH_LDS 1
@@ -82,7 +85,9 @@
 #define MPH_PREP_RUNS 1   // k_prep: one cell-histogram atomic per run of equal keys in a wave
 #endif
 #ifndef MPH_LDS_CAP
-#define MPH_LDS_CAP 192   // candidates staged per wave and stencil column
+// candidates staged per wave and stencil column: 176 keeps a wave's staging at 5,072 B, so 32
+// waves (8 per SIMD) fit the 160 KB of LDS; wider windows take the global-gather loop
+#define MPH_LDS_CAP 176
 #endif
 #ifndef MPH_TYPE_BATCH
 // the search reads the candidates' types with each batch of SB (no LDS wait per accepted entry;
@@ -1659,10 +1664,10 @@ __device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A,
     if (cnt > kMaxNeighbor) atomicOr(&st->overflow, 1);
 }
 
-// one kernel per cell order (DevParams.perm), so each keeps its own register budget; held to 80
-// VGPRs (at least 6 waves per SIMD: the search waits on its start[] and staging loads)
+// one kernel per cell order (DevParams.perm), so each keeps its own register budget; held to 64
+// VGPRs (8 waves per SIMD: the search waits on its start[] and staging loads)
 #ifndef MPH_NB_WPE
-#define MPH_NB_WPE 6
+#define MPH_NB_WPE 8
 #endif
 template <int DIM, int PERM>
 __global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_WPE))) void k_neighbors(DevParams P, Soa A, const int* __restrict__ start,
