@@ -75,11 +75,11 @@
 #define MPH_COLRANGE32 1   // the search's per-column candidate ranges in FP32 (outward margins)
 #endif
 #ifndef MPH_SEARCH_PREFETCH
-// pipeline the per-column start[] loads of the LDS search, 1 or 2 columns ahead (same box, D1M
-// search: 0.405 ms at 1 with FP64 ranges, 0.396 with FP32 ranges, 0.389 at 2; D16M 4.41 / 4.45 / 4.37;
-// profiles/r03/search/).  A search that only sets the columns up (MPH_DIAG_SEARCH=2) takes 0.21 ms
-// of the 0.39: the per-column chain start[] -> window -> staging is latency-bound.
-#define MPH_SEARCH_PREFETCH 2
+// pipeline the per-column start[] loads of the LDS search, 1 or 2 columns ahead.  At 7 waves per
+// SIMD two columns ahead won (D1M search 0.405 ms at 1 with FP64 ranges, 0.396 with FP32 ranges,
+// 0.389 at 2; profiles/r03/search/); at 8 waves (SB = 2) one column ahead is better, the second
+// stage only costs registers (D1M 0.341 -> 0.322 ms, D16M 4.16 -> 3.74, profiles/r03/search/prefetch1/)
+#define MPH_SEARCH_PREFETCH 1
 #endif
 #ifndef MPH_PREP_RUNS
 #define MPH_PREP_RUNS 1   // k_prep: one cell-histogram atomic per run of equal keys in a wave
