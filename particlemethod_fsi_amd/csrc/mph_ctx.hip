@@ -592,7 +592,7 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     HIP_OK(c, hipStreamSynchronize(c->stream));
     {
         DevState hs;
-        HIP_OK(c, hipMemcpy(&hs, c->dst, sizeof(DevState), hipMemcpyDeviceToHost));
+        HIP_OK(c, hipMemcpy(&hs, c->dst, kStateHead, hipMemcpyDeviceToHost));
         CK(ctx_state_status(c, hs));
     }
     return MPH_OK;
@@ -649,7 +649,7 @@ int mph_step(MphCtx* c, int nsteps)
     for (int k = 0; k < nsteps; ++k) c->time += c->cfg.dt;
     c->stepped = true;
     DevState hs;
-    HIP_OK(c, hipMemcpyAsync(&hs, c->dst, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipMemcpyAsync(&hs, c->dst, kStateHead, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipStreamSynchronize(c->stream));
     CK(ctx_state_status(c, hs));
     return MPH_OK;
@@ -963,7 +963,7 @@ int mph_profile_steps(MphCtx* c, int nsteps, double* avg_ms, int* launches, char
     std::snprintf(names32 + 32 * k, 32, "%s", "gpu_busy");
     ++k;
     DevState hs;
-    HIP_OK(c, hipMemcpy(&hs, c->dst, sizeof(DevState), hipMemcpyDeviceToHost));
+    HIP_OK(c, hipMemcpy(&hs, c->dst, kStateHead, hipMemcpyDeviceToHost));
     CK(ctx_state_status(c, hs));
     return k;
 }
@@ -998,6 +998,27 @@ int mph_list_formats(MphCtx* c, int* out2)
     out2[1] = nt;
     return MPH_OK;
 }
+
+#if MPH_DIAG_XCD
+// Diagnostic builds only (not in include/mph_gpu.h): copies DevState.xcd_diag (3 x 4 x 8 words,
+// see XcdProbe in mph_kernels.hip) to out after draining the device; reset != 0 then restarts it.
+__attribute__((visibility("default"))) int mph_diag_xcd(MphCtx* c, unsigned long long* out, int reset)
+{
+    if (!c) return MPH_ERR_ARG;
+    HIP_OK(c, hipSetDevice(c->device));
+    HIP_OK(c, hipDeviceSynchronize());
+    constexpr size_t kBytes = sizeof(DevState::xcd_diag);
+    char* dev = reinterpret_cast<char*>(c->dst) + offsetof(DevState, xcd_diag);
+    if (out) HIP_OK(c, hipMemcpy(out, dev, kBytes, hipMemcpyDeviceToHost));
+    if (reset) {
+        unsigned long long h[3][4][8] = {};
+        for (auto& k : h)
+            for (auto& v : k[0]) v = ~0ull;
+        HIP_OK(c, hipMemcpy(dev, h, kBytes, hipMemcpyHostToDevice));
+    }
+    return MPH_OK;
+}
+#endif
 
 void mph_destroy(MphCtx* c)
 {

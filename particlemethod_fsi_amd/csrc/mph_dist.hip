@@ -679,7 +679,7 @@ int dist_sync(MphCtx* c, bool grow_ok)
 {
     MphDist& D = *c->dist;
     DevState hs;
-    MPH_HIP_OK(c, hipMemcpyAsync(&hs, c->dst, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
+    MPH_HIP_OK(c, hipMemcpyAsync(&hs, c->dst, kStateHead, hipMemcpyDeviceToHost, c->stream));
     MPH_HIP_OK(c, hipMemcpyAsync(D.hlay, D.lay, sizeof(DistLayout), hipMemcpyDeviceToHost, c->stream));
     MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
     if (hs.overflow & 8)

@@ -286,6 +286,31 @@ __device__ __forceinline__ int xcd_block(int b, int nb)
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
 }
 
+#if MPH_DIAG_XCD
+// Diagnostic build: each wave of a list kernel records, from lane 0 at whichever return it takes,
+// its start and end (wall_clock64, 100 MHz) into DevState.xcd_diag[kernel][.][XCC_ID].
+struct XcdProbe {
+    unsigned long long* d;
+    unsigned long long t0;
+    __device__ XcdProbe(const DevState* st, int k)
+        : d(st ? &const_cast<DevState*>(st)->xcd_diag[k][0][0] : nullptr), t0(wall_clock64()) {}
+    __device__ ~XcdProbe()
+    {
+        if (d && __lane_id() == 0) {
+            const unsigned long long t1 = wall_clock64();
+            const int x = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7;   // HW_REG_XCC_ID[3:0]
+            atomicMin(d + x, t0);
+            atomicMax(d + 8 + x, t1);
+            atomicAdd(d + 16 + x, t1 - t0);
+            atomicAdd(d + 24 + x, 1ull);
+        }
+    }
+};
+#define XCD_PROBE(st, k) XcdProbe xcd_probe_((st), (k))
+#else
+#define XCD_PROBE(st, k)
+#endif
+
 // Particles held by this context: exact on a single GPU; in slab mode the device-resident count
 // of the last redistribution (P.n is then only the capacity the grids are sized for).
 __device__ __forceinline__ int dev_n(const DevParams& P) { return P.n_dev ? *P.n_dev : P.n; }
@@ -300,6 +325,61 @@ __device__ __forceinline__ int live_blocks(int n) { return (n + 255) >> 8; }
 #endif
 constexpr int kWB = MPH_LB / 64;
 __device__ __forceinline__ int list_blocks(int n) { return (n + MPH_LB - 1) / MPH_LB; }
+
+// Work-balanced XCD map of the two list passes.  The waves' work is not uniform along the sorted
+// order (walls, the free surface, a slab's ghost waves), so equal block counts per XCD leave some
+// XCDs idle while the last one finishes (tools/xcd_diag.py: the XCDs' end times spread 8-29 %).
+// The launch has list_grid() blocks (a multiple of 8 with 25 % slack); logical XCD j = b & 7 (the
+// hardware deals blocks round-robin) takes the contiguous range [lo_j, lo_j+1) of the nb live
+// blocks, lo_j = xcd_frac[j] * nb / 2^16 from DevState (k_xcd_split, from this step's search:
+// a wave's work = its longest list + kWaveCost), and its blocks past the range exit.  Any range
+// past the grid's share, or no split yet, falls back to the equal ranges of xcd_block: each live
+// block is taken exactly once either way.  Returns the block's index among the live blocks, or -1.
+// The search itself keeps the equal ranges: its cost follows the candidates it scans, not the
+// lists it writes (balanced by list length it ran 8 % slower at D1M; by the previous step's wave
+// durations all three kernels oscillated, profiles/r03/xcd_balance/).
+#ifndef MPH_XCD_BAL
+#define MPH_XCD_BAL 1
+#endif
+constexpr int kWaveCost = 16;   // a wave's fixed cost, in list entries, for the work histogram
+
+__device__ __forceinline__ int list_block(const DevState* st, int n)
+{
+    const int nb = list_blocks(n);
+    const int b = blockIdx.x;
+    if (MPH_XCD_BAL && st) {
+        const int* fr = st->xcd_frac;
+        const int cap = gridDim.x >> 3;
+        const int j = b & 7;
+        bool ok = fr[0] == 0 && fr[8] == 65536;
+        int lo = 0, mine_lo = 0, mine_c = 0;
+        for (int x = 0; x < 8; ++x) {
+            const int hi = (int)(((long long)fr[x + 1] * nb) >> 16);
+            const int c = hi - lo;
+            ok = ok && c >= 0 && c <= cap;
+            if (x == j) { mine_lo = lo; mine_c = c; }
+            lo = hi;
+        }
+        if (ok) {
+            const int q = b >> 3;
+            return q < mine_c ? mine_lo + q : -1;
+        }
+    }
+    return b < nb ? xcd_block(b, nb) : -1;
+}
+
+// The search's contribution to the work histogram: its wave's longest list (all lanes converged;
+// one atomic per wave, spread over the 512 runs).
+__device__ __forceinline__ void add_wave_work(DevState* st, int cnt, int i, int n)
+{
+    if (!MPH_XCD_BAL || !st) return;
+    int m = cnt;
+    for (int o = 32; o; o >>= 1) m = max(m, __shfl_xor(m, o));
+    const int tile = __builtin_amdgcn_readfirstlane(i >> 6);
+    const int ntile = (n + 63) >> 6;
+    if ((threadIdx.x & 63) == 0 && tile < ntile)
+        atomicAdd(&st->seg_work[(int)(((long long)tile * kXcdSegs) / ntile)], m + kWaveCost);
+}
 
 __device__ __forceinline__ int nbr_entry(int j, int type) { return j | (type << kTypeShift); }
 
@@ -1599,7 +1679,7 @@ __device__ __forceinline__ void slab_wave_flag(const DevParams& P, const Soa& A,
 }
 
 template <int DIM, int PERM, int REDO>
-__device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A, const int* start, int* nbr,
+__device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, const int* start, int* nbr,
                                                int* ncount, int2* hdr, int* lhdr, DevState* st, double* stage,
                                                int i)
 {
@@ -1613,7 +1693,7 @@ __device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A,
     if (lhdr && (threadIdx.x & 63) == 0) lhdr[(size_t)tile * kLhdr + kHdrFlag] = 0;
     if (wave_all_ghosts(P, A, live, ii)) {
         if (live) ncount[i] = 0;
-        return;
+        return 0;
     }
     // the ghost lanes of a mixed wave take no part either (empty list)
     const bool own = live && !(P.slab_axis >= 0 && A.id[ii] < 0);
@@ -1662,6 +1742,7 @@ __device__ __forceinline__ void neighbors_body(const DevParams& P, const Soa& A,
     // one same-address device atomic per wave serialises at ~11 ns each (21.8k waves at D1M took
     // 0.5 ms); mph_neighbor_stats reduces ncount on demand.
     if (cnt > kMaxNeighbor) atomicOr(&st->overflow, 1);
+    return cnt;
 }
 
 // one kernel per cell order (DevParams.perm), so each keeps its own register budget; held to 64
@@ -1677,10 +1758,59 @@ __global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_W
 {
     const int n = dev_n(P);
     if ((int)blockIdx.x >= list_blocks(n)) return;
+    XCD_PROBE(st, 0);
     __shared__ __attribute__((aligned(16))) double stage[kWB][stage_words(MPH_LDS_CAP, MPH_SB)];
     const int i = xcd_block(blockIdx.x, list_blocks(n)) * blockDim.x + threadIdx.x;
     slab_wave_flag(P, A, i, n, wface);
-    neighbors_body<DIM, PERM, 0>(P, A, start, nbr, ncount, hdr, lhdr, st, stage[threadIdx.x >> 6], i);
+    const int cnt = neighbors_body<DIM, PERM, 0>(P, A, start, nbr, ncount, hdr, lhdr, st, stage[threadIdx.x >> 6], i);
+    add_wave_work(st, cnt, i, n);
+}
+
+// The XCD ranges of the list passes from the search's work histogram (see list_block): one block,
+// an inclusive scan of the runs' work (4 consecutive runs per thread), the 7 inner cut points at
+// equal shares of the total (interpolated inside their run), then the histogram cleared.
+__global__ __launch_bounds__(kXcdSplitThreads) void k_xcd_split(DevState* __restrict__ st)
+{
+    constexpr int R = kXcdSegs / kXcdSplitThreads;
+    __shared__ long long s[kXcdSplitThreads];
+    const int t = threadIdx.x;
+    int w[R];
+    long long sum = 0;
+    for (int r = 0; r < R; ++r) {
+        w[r] = max(st->seg_work[t * R + r], 0);
+        st->seg_work[t * R + r] = 0;
+        sum += w[r];
+    }
+    s[t] = sum;
+    __syncthreads();
+    for (int o = 1; o < kXcdSplitThreads; o <<= 1) {
+        const long long v = t >= o ? s[t - o] : 0;
+        __syncthreads();
+        s[t] += v;
+        __syncthreads();
+    }
+    const long long tot = s[kXcdSplitThreads - 1];
+    int* fr = st->xcd_frac;
+    if (tot < 8) {
+        if (t < 9) fr[t] = 8192 * t;
+        return;
+    }
+    for (int x = 1; x < 8; ++x) {
+        const long long tgt = tot * x / 8;
+        long long prev = t ? s[t - 1] : 0;
+        if (!(prev < tgt && s[t] >= tgt)) continue;
+        for (int r = 0; r < R; ++r) {
+            if (w[r] > 0 && prev < tgt && prev + w[r] >= tgt) {
+                const double f = (t * R + r + (double)(tgt - prev) / (double)w[r]) / kXcdSegs;
+                fr[x] = min(65536, max(0, (int)(f * 65536.0 + 0.5)));
+            }
+            prev += w[r];
+        }
+    }
+    if (t == 0) {
+        fr[0] = 0;
+        fr[8] = 65536;
+    }
 }
 
 // The second launch, over the waves whose compact list did not fit (scan_candidates_lds marks
@@ -1886,7 +2016,9 @@ __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, cons
                                                 const DevState* __restrict__ st)
 {
     const int n = dev_n(P);
-    if ((int)blockIdx.x >= list_blocks(n)) return;
+    const int lb = list_block(st, n);
+    if (lb < 0) return;
+    XCD_PROBE(st, 1);
     __shared__ double s_ratio[kTypes * kTypes];
     __shared__ double s_mu[kTypes * kTypes];
     if (threadIdx.x < kTypes * kTypes) {
@@ -1894,7 +2026,7 @@ __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, cons
         s_mu[threadIdx.x] = T->mu_ij[threadIdx.x] * (-P.cvis * P.cdv * P.vol);   // pass_a_term's viscous factor
     }
     __syncthreads();
-    const int i = xcd_block(blockIdx.x, list_blocks(n)) * blockDim.x + threadIdx.x;
+    const int i = lb * blockDim.x + threadIdx.x;
     const bool live = i < n;
     const int ii = live ? i : n - 1;
     const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
@@ -2439,13 +2571,15 @@ __global__ __launch_bounds__(MPH_LB) MPH_PB_ATTR void k_pass_b(DevParams P, cons
                                                 const DevState* __restrict__ st)
 {
     const int n = dev_n(P);
-    if ((int)blockIdx.x >= list_blocks(n)) return;
+    const int lb = list_block(st, n);
+    if (lb < 0) return;
+    XCD_PROBE(st, 2);
     __shared__ double s_ratio[kTypes * kTypes];
     if (SURF) {
         if (threadIdx.x < kTypes * kTypes) s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
         __syncthreads();
     }
-    const int i = xcd_block(blockIdx.x, list_blocks(n)) * blockDim.x + threadIdx.x;
+    const int i = lb * blockDim.x + threadIdx.x;
     const int ii = i < n ? i : n - 1;
     const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
     bool live = i < n;
@@ -3503,6 +3637,14 @@ __global__ __launch_bounds__(256) void k_halo_unpack(const double* __restrict__ 
 
 static inline int blocks(int n, int t) { return (n + t - 1) / t; }
 
+// Grid of the two list passes: the XCD map (list_block) needs a multiple of 8 blocks, with 25 %
+// slack for its unequal ranges
+static inline int list_grid(int n)
+{
+    const int nb = blocks(n, MPH_LB);
+    return MPH_XCD_BAL ? (nb + nb / 4 + 15) / 8 * 8 : nb;
+}
+
 struct ProfScope {
     Profiler* p;
     int slot;
@@ -3558,9 +3700,11 @@ void launch_neighbors(const Launch& L)
     // first marked them
 #define MPH_NEIGHBORS(D, PERM)                                                                               \
     do {                                                                                                     \
-        MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM>), dim3(blocks(P.n, MPH_LB)), dim3(MPH_LB), 0,     \
+        MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM>), dim3(blocks(P.n, MPH_LB)), dim3(MPH_LB), 0, \
                    L.stream, P, L.A, L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, L.st,    \
                    L.wface);                                                                                \
+        if (MPH_XCD_BAL)                                                                                     \
+            MPH_LAUNCH("xcd_split", L.stream, k_xcd_split, dim3(1), dim3(kXcdSplitThreads), 0, L.stream, L.st);     \
         if (L.lhdr)                                                                                          \
             MPH_LAUNCH("neighbors_redo", L.stream, (k_neighbors_redo<D, PERM>), dim3(1),                  \
                        dim3(256), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.lhdr, L.st);            \
@@ -3586,10 +3730,10 @@ void launch_pass_a(const Launch& L)
     if (P.n == 0) return;
     const PassAOut po = pass_a_out(L);
     if (P.dim == 3)
-        MPH_LAUNCH("pass_a", L.stream, k_pass_a<3>, dim3(blocks(P.n, MPH_LB)), dim3(MPH_LB), 0, L.stream, P, L.T,
+        MPH_LAUNCH("pass_a", L.stream, k_pass_a<3>, dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P, L.T,
                    L.A, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, po, L.st);
     else
-        MPH_LAUNCH("pass_a", L.stream, k_pass_a<2>, dim3(blocks(P.n, MPH_LB)), dim3(MPH_LB), 0, L.stream, P, L.T,
+        MPH_LAUNCH("pass_a", L.stream, k_pass_a<2>, dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P, L.T,
                    L.A, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, po, L.st);
 }
 
@@ -3649,7 +3793,7 @@ void launch_pass_b(const Launch& L, int phase)
         std::abort();
     }
 #define MPH_PASS_B(S, D)                                                                            \
-    MPH_LAUNCH(phase == 2 ? "pass_b_face" : "pass_b", L.stream, (k_pass_b<S, D>), dim3(blocks(P.n, MPH_LB)), dim3(MPH_LB), 0, L.stream, P, \
+    MPH_LAUNCH(phase == 2 ? "pass_b_face" : "pass_b", L.stream, (k_pass_b<S, D>), dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P, \
                L.T, L.A, L.rec, L.fpart, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, L.force, L.acc, L.B, \
                phase, L.wface, \
                struct_hook(L), L.st)

@@ -2,9 +2,14 @@
 // HIP kernels (mph_kernels.hip).  No HIP types here, so the host files build with g++/hipcc alike.
 #pragma once
 
+#include <cstddef>
 #include <cstdint>
 
 #include "../../include/mph_gpu.h"
+
+#ifndef MPH_DIAG_XCD
+#define MPH_DIAG_XCD 0   // 1: per-XCD wave timing of the list kernels (diagnostic builds only)
+#endif
 
 namespace mph {
 
@@ -153,6 +158,11 @@ inline void set_uniforms(DevParams& P)
     P.rg_r2g = P.rg / P.r2g;
 }
 
+// work histogram of the XCD map: waves in 4096 equal runs (D16M: ~60 waves per run, so the
+// search's per-wave atomics spread over ~100 addresses at a time; 512 runs cost its search 7 %)
+constexpr int kXcdSegs = 4096;
+constexpr int kXcdSplitThreads = 1024;   // k_xcd_split: 4 runs per thread
+
 // Mutable per-step device scalars (so a captured hipGraph can replay many steps).
 struct DevState {
     double time;                 // Time
@@ -169,7 +179,21 @@ struct DevState {
     int seam_occ[2];
     int seam_step;
     int seam_pad;
+    // work-balanced XCD map of the two list passes (mph_kernels.hip, list_block): the search adds
+    // each wave's work (its longest list + a fixed cost) into seg_work[its 1/kXcdSegs of the waves];
+    // k_xcd_split turns that into the XCDs' contiguous block ranges (xcd_frac: fractions of 2^16,
+    // 0 ... 65536) for this step's passes and clears seg_work
+    int seg_work[kXcdSegs];
+    int xcd_frac[9];
+    int xcd_pad[3];
+#if MPH_DIAG_XCD
+    // diagnostic build only (tools/xcd_diag.py): per list kernel (search, pass A, pass B) and XCD,
+    // the first wave's start, the last wave's end (wall_clock64), the summed wave time, the waves
+    unsigned long long xcd_diag[3][4][8];
+#endif
 };
+// the part of DevState the host reads back after steps (the error bits and the step scalars)
+constexpr size_t kStateHead = offsetof(DevState, seg_work);
 
 #if defined(__HIPCC__)
 #define MPH_HD __host__ __device__

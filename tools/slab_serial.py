@@ -171,6 +171,16 @@ def run_ranks(args, R, axis, cuts, locals_, records=None, replay=None):
                 s.synchronize()
                 wall = time.perf_counter() - t0
             ex.record = ex.replay = None
+            xcd = None
+            if os.environ.get("MPH_XCD_DIAG") == "1":   # diagnostic build: tools/xcd_diag.py
+                from xcd_diag import xcd_read
+                with token.lock:
+                    xcd_read(s, reset=True)
+                # one more step (all ranks take it: it exchanges); each context's words are its own
+                with token.lock:
+                    s.step(1)
+                    s.synchronize()
+                    xcd = xcd_read(s, reset=True)
             info = s.dist_info()
             busy = prof.pop("gpu_busy", {}).get("avg_ms")   # union of the kernel intervals per step
             out[r] = {"rank": r, "owned": len(s.owned_ids()), "held": info["held"],
@@ -180,6 +190,8 @@ def run_ranks(args, R, axis, cuts, locals_, records=None, replay=None):
                                       for k, v in prof.items()},
                       "gpu_ms_per_step": sum(v["avg_ms"] * v["launches"] for v in prof.values()) / args.steps,
                       "wall_s": wall}
+            if xcd is not None:
+                out[r]["xcd"] = xcd
             with token.lock:
                 s.close()
         except Exception as e:  # noqa: BLE001 -- reported below
