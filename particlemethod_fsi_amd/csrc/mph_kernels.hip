@@ -341,6 +341,9 @@ __device__ __forceinline__ int list_blocks(int n) { return (n + MPH_LB - 1) / MP
 #ifndef MPH_XCD_BAL
 #define MPH_XCD_BAL 1
 #endif
+#ifndef MPH_XCD_SAMPLE
+#define MPH_XCD_SAMPLE 1   // 1 of this many waves adds to the histogram (weighted)
+#endif
 constexpr int kWaveCost = 16;   // a wave's fixed cost, in list entries, for the work histogram
 
 __device__ __forceinline__ int list_block(const DevState* st, int n)
@@ -377,8 +380,8 @@ __device__ __forceinline__ void add_wave_work(DevState* st, int cnt, int i, int 
     for (int o = 32; o; o >>= 1) m = max(m, __shfl_xor(m, o));
     const int tile = __builtin_amdgcn_readfirstlane(i >> 6);
     const int ntile = (n + 63) >> 6;
-    if ((threadIdx.x & 63) == 0 && tile < ntile)
-        atomicAdd(&st->seg_work[(int)(((long long)tile * kXcdSegs) / ntile)], m + kWaveCost);
+    if ((threadIdx.x & 63) == 0 && tile < ntile && tile % MPH_XCD_SAMPLE == 0)
+        atomicAdd(&st->seg_work[(int)(((long long)tile * kXcdSegs) / ntile)], (m + kWaveCost) * MPH_XCD_SAMPLE);
 }
 
 __device__ __forceinline__ int nbr_entry(int j, int type) { return j | (type << kTypeShift); }
@@ -3639,6 +3642,11 @@ static inline int blocks(int n, int t) { return (n + t - 1) / t; }
 
 // Grid of the two list passes: the XCD map (list_block) needs a multiple of 8 blocks, with 25 %
 // slack for its unequal ranges
+// below this many particles the split kernel's ~7 us costs more than the balance gains (Bar 400k,
+// 0.23 ms per step: 1.76e9 p-steps/s with it, 1.80e9 without); the passes then keep the equal
+// ranges.  The full-size parity tests (D1M, FSI, the D16M slabs) run the balanced map
+constexpr int kXcdBalMin = 1 << 20;
+
 static inline int list_grid(int n)
 {
     const int nb = blocks(n, MPH_LB);
@@ -3703,7 +3711,7 @@ void launch_neighbors(const Launch& L)
         MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM>), dim3(blocks(P.n, MPH_LB)), dim3(MPH_LB), 0, \
                    L.stream, P, L.A, L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, L.st,    \
                    L.wface);                                                                                \
-        if (MPH_XCD_BAL)                                                                                     \
+        if (MPH_XCD_BAL && P.n >= kXcdBalMin)                                                                \
             MPH_LAUNCH("xcd_split", L.stream, k_xcd_split, dim3(1), dim3(kXcdSplitThreads), 0, L.stream, L.st);     \
         if (L.lhdr)                                                                                          \
             MPH_LAUNCH("neighbors_redo", L.stream, (k_neighbors_redo<D, PERM>), dim3(1),                  \
