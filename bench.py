@@ -244,6 +244,20 @@ def main():
         elapsed = float(t.item())
     value = n_total * args.steps / elapsed   # every particle of the whole job, once per step
 
+    # the drop-in binding's own call pattern: one mph_step(ctx, 1) per
+    # time-loop iteration (1-step graph, every output-only field stored, one readback of the step's
+    # error flags per call) over the same number of steps
+    step1 = None
+    if world == 1:
+        barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            solver.step(1)
+        barrier()
+        e1 = time.perf_counter() - t1
+        step1 = {"value": n_total * args.steps / e1, "ms_per_step": e1 * 1e3 / args.steps,
+                 "gap": 1.0 - (n_total * args.steps / e1) / value}
+
     mean_nb, max_nb = solver.neighbor_stats()
     prof = solver.profile(args.profile_steps)
     checks = None
@@ -362,6 +376,8 @@ def main():
         "kernels_ms": {k: round(v["avg_ms"], 5) for k, v in prof.items()},
         "profiled_step_ms": step_ms,
         "profiled_gpu_busy_ms": busy_ms,
+        "value_step1": step1["value"] if step1 else None,
+        "step1": step1,
     }
     if checks is not None:
         out["slab"] = checks

@@ -273,6 +273,17 @@ int mph_compute_virial(MphCtx* ctx);
  * their sum where kernels of two streams overlap (slab mode).                                  */
 #define MPH_PROFILE_MAX 24
 int mph_profile_steps(MphCtx* ctx, int nsteps, double* avg_ms, int* launches, char* names32);
+/* Phase timing: the reference's clock() buckets of its step loop (main.cpp:695-700) from HIP
+ * events.  With on != 0 mph_step launches the kernels of its step batches directly instead of
+ * replaying the captured graphs (HIP does not time events recorded inside a graph), with three
+ * events per step -- before the cell sort, after the neighbour search, after the elastic
+ * substeps -- read after every batch (mph_step returns after its steps have run anyway);
+ * mph_compute_virial is bracketed too.  mph_phase_times adds up, in milliseconds of GPU time since the context was
+ * created: [0] neighbour search (calculateNeighbor with its cell sort: k_prep .. k_neighbors),
+ * [1] explicit calculation (the pass-A/pass-B sums, integration and elastic substeps), [2] the
+ * virial.  Single contexts only (slab mode: MPH_ERR_ARG for on != 0).                          */
+int mph_phase_timing(MphCtx* ctx, int on);
+int mph_phase_times(const MphCtx* ctx, double* out3);
 /* Mean/max neighbour count of the last step (for algorithmic byte/flop accounting).         */
 int mph_neighbor_stats(MphCtx* ctx, double* mean, int* max);
 

@@ -25,7 +25,13 @@
 #endif
 
 #define NT MPH_TYPE_COUNT
+/* MAXN: the reference's list capacity; MPH_ORACLE_MAXN shrinks the row stride for memory (the
+ * D16M fixture build, tools/make_d16m_ncount.py: 128 >= the case's 80; overflow still detected) */
+#ifdef MPH_ORACLE_MAXN
+#define MAXN MPH_ORACLE_MAXN
+#else
 #define MAXN MPH_MAX_NEIGHBOR_COUNT
+#endif
 /* type classes, main.cpp:68-74 */
 #define IS_FLUID(t) ((t) >= 0 && (t) < 2)
 #define IS_STRUCT(t) ((t) >= 2 && (t) < 4)

@@ -80,6 +80,12 @@ struct MphCtx {
     bool stepped = false;
     hipStream_t stream = nullptr;
     hipGraphExec_t graph1 = nullptr, graph8 = nullptr;
+    // phase timing (mph_phase_timing): steps launched directly (no graph) with events at every
+    // step's phase boundaries -- before the sort, after the search, after the elastic substeps --
+    // three per step of a batch of up to 8 (ev8), and around the virial (ev_vir)
+    bool phase_timing = false;
+    std::vector<hipEvent_t> ev8, ev_vir;
+    double phase_ms[3] = {0.0, 0.0, 0.0};   // neighbour search, explicit calculation, virial
     // host copies of the static inputs: original order, or -- slab-local creation -- the
     // particles this rank was created with, whose original indices are gid (ascending)
     std::vector<int> prop;
@@ -96,7 +102,6 @@ struct MphCtx {
     int *key = nullptr, *slot = nullptr, *tmp = nullptr, *cnt = nullptr, *start = nullptr, *bsum = nullptr;
     double *vir = nullptr, *vpres = nullptr;   // VirialStress [cap][9] / VirialPressure (A order), lazy
     int *nbr = nullptr, *ncount = nullptr;
-    int2* seg_hdr = nullptr;     // per-wave list headers (column-segmented lists)
     int* list_hdr = nullptr;     // per-wave headers of the compact 16-bit lists (kLhdr ints each)
     double *pres = nullptr, *gx = nullptr, *gy = nullptr, *gz = nullptr, *pa = nullptr;
     double4 *force = nullptr, *acc = nullptr, *fpart = nullptr, *rec = nullptr;

@@ -53,6 +53,8 @@ int ctx_state_status(MphCtx* c, const DevState& hs)
     if (hs.overflow & 1)
         return ctx_fail(c, MPH_ERR_NEIGHBOR_OVERFLOW, "a particle has more than 512 neighbours");
     if (hs.overflow & 2) return ctx_fail(c, MPH_ERR_CAPACITY, "a particle moved past a neighbouring slab");
+    if (hs.overflow & 8)   // MPH_DIAG_BOUNDS builds only
+        return ctx_fail(c, MPH_ERR_HIP, "diagnostic: a search window out of range (MPH_DIAG_BOUNDS)");
     return MPH_OK;
 }
 
@@ -69,15 +71,16 @@ void ctx_fill_launch(MphCtx* c)
     // returned through A.id), so k_rank_scatter skips that scatter; slab mode uses dst_of.
     L.A = c->A; L.B = c->B; L.rank_of = nullptr; L.dst_of = nullptr;
     L.key = c->key; L.slot = c->slot; L.tmp = c->tmp; L.cnt = c->cnt; L.start = c->start; L.bsum = c->bsum;
-    L.nbr = c->nbr; L.ncount = c->ncount; L.hdr = c->seg_hdr;
+    L.nbr = c->nbr; L.ncount = c->ncount;
     // compact 16-bit lists of interior wavefronts (MPH_LIST16=1), or 32-bit ELL rows everywhere
     // (MPH_LIST16=0); unset: kListCompact
     const char* l16 = std::getenv("MPH_LIST16");
     const bool compact = l16 && *l16 ? std::string(l16) != "0" : kListCompact;
     L.lhdr = compact && pass_a_equal_radii(c->P) ? c->list_hdr : nullptr;
-    // the fused search + pass A (k_search_pass_a) unless MPH_FUSED=0 at creation (A/B, tests)
-    const char* fu = std::getenv("MPH_FUSED");
-    L.fused = fu && *fu ? fu[0] != '0' : kFusedDefault;
+    // work-balanced XCD map of the passes from this many particles (MPH_XCD_BAL_MIN: tests force it
+    // on small cases, the default keeps it off below 2^20 where the split kernel costs more)
+    const char* bm = std::getenv("MPH_XCD_BAL_MIN");
+    L.xcd_bal_min = bm && *bm ? std::atoi(bm) : (1 << 20);
     L.pres = c->pres; L.gx = c->gx; L.gy = c->gy; L.gz = c->gz; L.pa = c->pa;
     L.force = c->force; L.acc = c->acc; L.fpart = c->fpart; L.rec = c->rec;
     L.dens_a = c->dens_a; L.vstrain = c->vstrain; L.divp = c->divp;
@@ -106,17 +109,21 @@ void fill_launch(MphCtx* c) { ctx_fill_launch(c); }
 // (pass B -6 % at D1M); mph_get after any mph_step sees the last step's values as before.  The
 // same holds in pass A for DensityA, VolStrainP, DivergenceP and, without surface tension (pass B
 // then reads neither), GravityCenter and PressureA.  The virial (k_virial) runs after a batch.
-void enqueue_step(const Launch& L, bool last)
+// ev (phase timing, else null): three events recorded on the stream at the step's phase
+// boundaries -- before the sort, after the search (neighbour search = sort + search, as the
+// reference's calculateNeighbor holds its own cell sort), after the elastic substeps.
+void enqueue_step(const Launch& L, bool last, hipEvent_t* ev = nullptr)
 {
+    if (ev) (void)hipEventRecord(ev[0], L.stream);
     launch_sort(L, 1);
-    if (last) {
-        launch_search_pass_a(L);
-    } else {
-        Launch La = L;
+    Launch La = L;
+    if (!last) {
         La.dens_a = La.vstrain = La.divp = nullptr;
         if (!L.P->surface) La.gx = La.gy = La.gz = La.pa = nullptr;
-        launch_search_pass_a(La);
     }
+    launch_neighbors(La);
+    if (ev) (void)hipEventRecord(ev[1], L.stream);
+    launch_pass_a(La);
     if (last) {
         launch_pass_b(L);
     } else {
@@ -126,6 +133,7 @@ void enqueue_step(const Launch& L, bool last)
         launch_pass_b(Lb);
     }
     launch_structure(L, last);
+    if (ev) (void)hipEventRecord(ev[2], L.stream);
 }
 
 int capture(MphCtx* c, int steps, hipGraphExec_t* out)
@@ -136,6 +144,21 @@ int capture(MphCtx* c, int steps, hipGraphExec_t* out)
     HIP_OK(c, hipStreamEndCapture(c->stream, &g));
     HIP_OK(c, hipGraphInstantiate(out, g, nullptr, nullptr, 0));
     HIP_OK(c, hipGraphDestroy(g));
+    return MPH_OK;
+}
+
+// phase timing: the events of a batch of `steps` steps (three per step) into the neighbour /
+// explicit sums
+int accumulate_phases(MphCtx* c, const std::vector<hipEvent_t>& ev, int steps)
+{
+    HIP_OK(c, hipEventSynchronize(ev[3 * (size_t)steps - 1]));
+    for (size_t k = 0; k + 2 < 3 * (size_t)steps; k += 3) {
+        float a = 0.0f, b = 0.0f;
+        HIP_OK(c, hipEventElapsedTime(&a, ev[k], ev[k + 1]));
+        HIP_OK(c, hipEventElapsedTime(&b, ev[k + 1], ev[k + 2]));
+        c->phase_ms[0] += a;
+        c->phase_ms[1] += b;
+    }
     return MPH_OK;
 }
 
@@ -401,7 +424,6 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     if (hipMemset(c->nbr, 0, sizeof(int) * ntile * kTile * kMaxNeighbor) != hipSuccess) return MPH_ERR_HIP;
     if (hipMemset(c->ncount, 0, sizeof(int) * cap) != hipSuccess) return MPH_ERR_HIP;
 #endif
-    CK(dalloc(c, &c->seg_hdr, ntile * kSegHdr));
     CK(dalloc(c, &c->list_hdr, ntile * kLhdr));
     CK(dalloc(c, &c->pres, cap)); CK(dalloc(c, &c->gx, cap)); CK(dalloc(c, &c->gy, cap)); CK(dalloc(c, &c->gz, cap));
     CK(dalloc(c, &c->pa, cap)); CK(dalloc(c, &c->force, cap)); CK(dalloc(c, &c->acc, cap));
@@ -641,11 +663,24 @@ int mph_step(MphCtx* c, int nsteps)
         for (int k = 0; k < nsteps; ++k) c->time += c->cfg.dt;
         return MPH_OK;
     }
-    if (!c->graph1) CK(capture(c, 1, &c->graph1));
-    if (!c->graph8 && nsteps >= 8) CK(capture(c, 8, &c->graph8));
     int left = nsteps;
-    while (left >= 8) { HIP_OK(c, hipGraphLaunch(c->graph8, c->stream)); left -= 8; }
-    while (left > 0) { HIP_OK(c, hipGraphLaunch(c->graph1, c->stream)); left -= 1; }
+    if (c->phase_timing) {
+        // the graphs' batches (8 steps, then single steps; the output-only stores on each batch's
+        // last step) as direct launches with the phase events (HIP cannot time events recorded
+        // inside a captured graph), read after every batch
+        while (left > 0) {
+            const int b = left >= 8 ? 8 : 1;
+            for (int k = 0; k < b; ++k) enqueue_step(c->L, k == b - 1, c->ev8.data() + 3 * k);
+            HIP_OK(c, hipGetLastError());
+            CK(accumulate_phases(c, c->ev8, b));
+            left -= b;
+        }
+    } else {
+        if (!c->graph1) CK(capture(c, 1, &c->graph1));
+        if (!c->graph8 && nsteps >= 8) CK(capture(c, 8, &c->graph8));
+        while (left >= 8) { HIP_OK(c, hipGraphLaunch(c->graph8, c->stream)); left -= 8; }
+        while (left > 0) { HIP_OK(c, hipGraphLaunch(c->graph1, c->stream)); left -= 1; }
+    }
     for (int k = 0; k < nsteps; ++k) c->time += c->cfg.dt;
     c->stepped = true;
     DevState hs;
@@ -775,9 +810,16 @@ int mph_compute_virial(MphCtx* c)
     }
     if (c->dist) return dist_virial(c);
     // after a step the integrated state B is in A (list) order; before the first step A is current
+    if (c->phase_timing) HIP_OK(c, hipEventRecord(c->ev_vir[0], c->stream));
     launch_virial(c->L, c->stepped ? c->B : c->A, c->vir, c->vpres);
     HIP_OK(c, hipGetLastError());
+    if (c->phase_timing) HIP_OK(c, hipEventRecord(c->ev_vir[1], c->stream));
     HIP_OK(c, hipStreamSynchronize(c->stream));
+    if (c->phase_timing) {
+        float ms = 0.0f;
+        HIP_OK(c, hipEventElapsedTime(&ms, c->ev_vir[0], c->ev_vir[1]));
+        c->phase_ms[2] += ms;
+    }
     return MPH_OK;
 }
 
@@ -905,6 +947,31 @@ int mph_write_vtk_async(MphCtx* c, const char* path)
     return MPH_OK;
 }
 
+int mph_phase_timing(MphCtx* c, int on)
+{
+    if (!c) return MPH_ERR_ARG;
+    if (c->dist) return on ? fail(c, MPH_ERR_ARG, "phase timing is not available in slab mode") : MPH_OK;
+    HIP_OK(c, hipSetDevice(c->device));
+    const bool want = on != 0;
+    if (want == c->phase_timing) return MPH_OK;
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    c->phase_timing = want;   // (mph_step then launches directly; the graphs stay for later)
+    if (want && c->ev_vir.empty()) {
+        c->ev_vir.assign(2, nullptr);
+        for (auto& e : c->ev_vir) HIP_OK(c, hipEventCreate(&e));
+        c->ev8.assign(3 * 8, nullptr);
+        for (auto& e : c->ev8) HIP_OK(c, hipEventCreate(&e));
+    }
+    return MPH_OK;
+}
+
+int mph_phase_times(const MphCtx* c, double* out3)
+{
+    if (!c || !out3) return MPH_ERR_ARG;
+    for (int k = 0; k < 3; ++k) out3[k] = c->phase_ms[k];
+    return MPH_OK;
+}
+
 int mph_profile_steps(MphCtx* c, int nsteps, double* avg_ms, int* launches, char* names32)
 {
     if (!c || nsteps <= 0 || !avg_ms || !launches || !names32) return MPH_ERR_ARG;
@@ -1028,6 +1095,8 @@ void mph_destroy(MphCtx* c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->graph1) (void)hipGraphExecDestroy(c->graph1);
     if (c->graph8) (void)hipGraphExecDestroy(c->graph8);
+    for (auto* v : {&c->ev8, &c->ev_vir})
+        for (hipEvent_t e : *v) (void)hipEventDestroy(e);
     if (c->dist) dist_free(c);
     for (void* p : c->allocs) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);

@@ -94,11 +94,12 @@ struct Launch {
     int* dst_of = nullptr;        // slab mode: pre-sort index -> sorted index (else rank_of[id])
     int *key = nullptr, *slot = nullptr, *tmp = nullptr, *cnt = nullptr, *start = nullptr, *bsum = nullptr;
     int *nbr = nullptr, *ncount = nullptr;
-    int2* hdr = nullptr;          // per-wave headers of the column-segmented lists (kSegHdr each)
     int* lhdr = nullptr;          // per-wave headers of the compact 16-bit lists (kLhdr each)
     int* wface = nullptr;         // slab mode: face-wavefront flags written by pass B (early send)
     VSrc vsrc;                    // slab mode: where the sort finds the kept entries of its input
-    bool fused = true;            // search + pass A in one kernel (k_search_pass_a; MPH_FUSED=0: two)
+    // fewest particles for the work-balanced XCD map of the passes (k_xcd_split each step);
+    // MPH_XCD_BAL_MIN overrides it at creation (tests force the map on small cases)
+    int xcd_bal_min = 1 << 20;
     // pass A products (A order): pressure values, gravity centre (GC, PressureA), sums
     double *pres = nullptr, *gx = nullptr, *gy = nullptr, *gz = nullptr, *pa = nullptr;
     double *dens_a = nullptr, *vstrain = nullptr, *divp = nullptr;
@@ -111,7 +112,7 @@ struct Launch {
 void launch_sort(const Launch& L, int mode);   // mode 0 init, 1 step, 2 step (motion done)
 void launch_neighbors(const Launch& L);
 void launch_pass_a(const Launch& L);
-// launch_neighbors + launch_pass_a, fused into one kernel where the list format allows
+// launch_neighbors + launch_pass_a
 void launch_search_pass_a(const Launch& L);
 void launch_pass_b(const Launch& L, int phase = 0);   // phase: 0 all, 1/2 slab inner/near-face
 void launch_structure(const Launch& L, bool last);   // last: the batch's last step (output tensors)

@@ -14,8 +14,6 @@
 //   k_pass_a         the pass-A sums over the list: DensityA (2141), GravityCenter (2174), DensityP
 //                    (2314), DivergenceP (2343), PhysicalCoefficients (2099), pressure values
 //                    PressureP (2384) / PressureA (2218)
-//   k_search_pass_a  the two above in one kernel (opt-in, MPH_FUSED=1 at run time; measured slower,
-//                    DESIGN.md section 4), bit-identical
 //   k_pass_b         PressureP force (2394), PressureA force (2225), DiffuseInterface (2261),
 //                    ViscosityV (2478), InterfaceForce (2427), Gravity (2917), Acceleration (2938),
 //                    Convection (1892)
@@ -37,6 +35,7 @@
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 #include "mph_kernels.h"
@@ -71,16 +70,6 @@
 #ifndef MPH_SEARCH_LDS
 #define MPH_SEARCH_LDS 1
 #endif
-#ifndef MPH_COLRANGE32
-#define MPH_COLRANGE32 1   // the search's per-column candidate ranges in FP32 (outward margins)
-#endif
-#ifndef MPH_SEARCH_PREFETCH
-// pipeline the per-column start[] loads of the LDS search, 1 or 2 columns ahead.  At 7 waves per
-// SIMD two columns ahead won (D1M search 0.405 ms at 1 with FP64 ranges, 0.396 with FP32 ranges,
-// 0.389 at 2; profiles/r03/search/); at 8 waves (SB = 2) one column ahead is better, the second
-// stage only costs registers (D1M 0.341 -> 0.322 ms, D16M 4.16 -> 3.74, profiles/r03/search/prefetch1/)
-#define MPH_SEARCH_PREFETCH 1
-#endif
 #ifndef MPH_PREP_RUNS
 #define MPH_PREP_RUNS 1   // k_prep: one cell-histogram atomic per run of equal keys in a wave
 #endif
@@ -88,25 +77,6 @@
 // candidates staged per wave and stencil column: 176 keeps a wave's staging at 5,072 B, so 32
 // waves (8 per SIMD) fit the 160 KB of LDS; wider windows take the global-gather loop
 #define MPH_LDS_CAP 176
-#endif
-#ifndef MPH_TYPE_BATCH
-// the search reads the candidates' types with each batch of SB (no LDS wait per accepted entry;
-// D1M search -1.6 %, D16M -3.2 %, profiles/r03/search/type_batch/)
-#define MPH_TYPE_BATCH 1
-#endif
-#ifndef MPH_GLDS_BUF
-// the search's staging and start[] loads through buffer descriptors (32-bit offsets): measured
-// neutral at D1M and +1.9 % at D16M (profiles/r03/search/buf_staging/), so off
-#define MPH_GLDS_BUF 0
-#endif
-#ifndef MPH_BUF_STORE
-#define MPH_BUF_STORE 1   // ELL list stores of the staged search through a buffer descriptor (A/B)
-#endif
-#ifndef MPH_GLDS
-// the search stages a column's window with global_load_lds (16 bytes per lane straight into LDS:
-// no VGPRs, no ds_write, and the pieces of a window in flight together) instead of register loads
-// + ds_write per 64 candidates (each piece waited for before the next)
-#define MPH_GLDS 1
 #endif
 
 namespace mph {
@@ -122,6 +92,31 @@ __device__ __forceinline__ __attribute__((address_space(3))) void* lds_ptr(void*
 {
     return (__attribute__((address_space(3))) void*)p;
 }
+
+// A 4-byte load through a buffer descriptor that hipcc does not count (the search's start[]
+// loads, scan_candidates_lds): no s_waitcnt is emitted for it, so the caller waits for it with an
+// explicit vmcnt(0) on every path before start_landed() and the first use of the value.
+#ifndef MPH_START_ASM
+#define MPH_START_ASM 1   // 0: plain buffer loads hipcc counts (it then waits for them early)
+#endif
+#ifndef MPH_DIAG_BOUNDS
+#define MPH_DIAG_BOUNDS 0   // diagnostic builds: the search checks its column windows (DevState.overflow 8)
+#endif
+// Both bounds of a column range in one statement: the descriptor may come from SGPRs that a VALU
+// instruction (v_readlane of an SGPR spill) has just written, which a VMEM instruction may read only
+// 5 wait states later (hipcc pads only what it sees: s_nop 4 opens the string).
+__device__ __forceinline__ void start_load2(__amdgpu_buffer_rsrc_t r, unsigned ob, unsigned oe, int& b, int& e)
+{
+    if (MPH_START_ASM) {
+        asm volatile("s_nop 4\n\tbuffer_load_dword %0, %2, %4, 0 offen\n\tbuffer_load_dword %1, %3, %4, 0 offen"
+                     : "=&v"(b), "=&v"(e) : "v"(ob), "v"(oe), "s"(r) : "memory");
+    } else {
+        b = __builtin_amdgcn_raw_buffer_load_b32(r, ob, 0, 0);
+        e = __builtin_amdgcn_raw_buffer_load_b32(r, oe, 0, 0);
+    }
+}
+// marks the start_load2 results as landed: no consumer is scheduled above this point
+__device__ __forceinline__ void start_landed(int& a, int& b) { asm volatile("" : "+v"(a), "+v"(b)); }
 
 // LDS staging of one wavefront in the search: x, y, z (stage_d doubles each, 16-byte aligned and
 // large enough for a 16-byte-aligned window of CAP candidates plus the SB-entry batch over-read),
@@ -521,32 +516,6 @@ __device__ __forceinline__ void nbr_at(const NbrList& L, int k, int& j, int& t)
     }
 }
 
-// Column-segmented neighbour list of an interior wavefront (MPH_SEG).  The search visits the
-// stencil columns in order; per column the wave's candidates form one window [mn, mn + span) of
-// the cell-sorted arrays.  Each column gets a segment of W slots (W = the most any lane accepted
-// there), slot k of lane l at seg[k][l] (uint16): the offset of the neighbour in the window (8 bits)
-// and its type (bits 8-10), or kSegNone in the padding.  A column whose window exceeds the staging
-// capacity is "wide": two slots per entry, the low and high halves of the sorted index (type in
-// bits 12-14 of the high half).  Per wave the header holds, per column, {mn, span | W << 16 |
-// wide << 31}, and in entry kSegCols the list format (1 = segmented, 0 = the ELL rows).  The
-// entries of a lane come in the same order as in its ELL row (column order, ascending index), so
-// both formats give bit-identical sums.  The segments reuse the wave's ELL tile (128 KB).
-#ifndef MPH_SEG
-#define MPH_SEG 0   // measured slower: pass A 0.44 -> 0.92 ms at D1M
-#endif
-constexpr int kSegCols = kSegHdr - 1;              // stencil columns (3-D; 2-D uses 5)
-constexpr int kSegCap = kTile * kMaxNeighbor * 4 / (2 * kTile);   // 1024 slots of 64 x uint16
-constexpr unsigned short kSegNone = 0xFFFF;
-
-__device__ __forceinline__ unsigned short* seg_tile(int* nbr, int i)
-{
-    return reinterpret_cast<unsigned short*>(nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor));
-}
-__device__ __forceinline__ const unsigned short* seg_tile(const int* nbr, int i)
-{
-    return reinterpret_cast<const unsigned short*>(nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor));
-}
-
 // ------------------------------------------------------------------------- sort phase -------
 
 // calculateWall (main.cpp:3031-3060) + calculatePeriodicBoundary (3322-3333) + cell histogram.
@@ -889,9 +858,9 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
     A.y[dst] = B.y[b];
     A.z[dst] = B.z[b];
     // the sorted velocities are read only through the 48-byte records (own_velocity below), unless
-    // the passes gather SoA (MPH_AOS_GATHER=0, or the segmented lists of MPH_SEG), or at a slab
-    // context's initialisation sort (mode 0: dist_init copies the sorted set into B)
-    if (!MPH_AOS_GATHER || MPH_SEG || !A.p6 || (dst_of && mode == 0)) {
+    // the passes gather SoA (MPH_AOS_GATHER=0), or at a slab context's initialisation sort (mode 0:
+    // dist_init copies the sorted set into B)
+    if (!MPH_AOS_GATHER || !A.p6 || (dst_of && mode == 0)) {
         A.vx[dst] = B.vx[b];
         A.vy[dst] = B.vy[b];
         A.vz[dst] = B.vz[b];
@@ -921,7 +890,7 @@ struct PassA {
 // One neighbour's contribution to DensityA (2141-2171), GravityCenter (2174-2210), DensityP
 // (2314-2341), DivergenceP (2343-2379), and (FORCE) the P_i half of the pressure force and the
 // viscous force; (dvx, dvy, dvz) = v_j - v_i.  No implicit contraction: every accumulation is an
-// explicit fma, so this branching form and pass_a_term_sel's selecting form (the fused kernel)
+// explicit fma, so this branching form and the selecting form of the round-3 fused kernel
 // give the same bits (a deselected fma(a, 0, acc) leaves acc unchanged).
 template <bool FORCE, bool EQR = false>
 __device__ __forceinline__ void pass_a_term(const DevParams& P, const double* s_ratio, const double* s_mu, int ti,
@@ -1004,80 +973,6 @@ __device__ __forceinline__ void pass_a_term(const DevParams& P, const double* s_
     }
 }
 
-// pass_a_term without control flow, for the fused kernel's mask walk: a lane whose slot is empty
-// (valid false) evaluates the same expressions on zeroed inputs, and every contribution's factor
-// is selected by its radius test instead of branched on.  Divergent branches around the twelve
-// accumulators made the compiler copy them at every merge (160 VGPRs); selects need no copies.
-// Same explicit fmas as pass_a_term, so the same bits.
-template <bool EQR>
-__device__ __forceinline__ void pass_a_term_sel(const DevParams& P, const double* s_ratio, const double* s_mu,
-                                                int ti, int tj, bool solid, bool valid, double q0, double q1,
-                                                double q2, double dvx, double dvy, double dvz, PassA& o)
-{
-#pragma clang fp contract(off)
-    q0 = valid ? q0 : 0.0;
-    q1 = valid ? q1 : 0.0;
-    q2 = valid ? q2 : 0.0;
-    dvx = valid ? dvx : 0.0;
-    dvy = valid ? dvy : 0.0;
-    dvz = valid ? dvz : 0.0;
-    // an empty slot sits just outside every radius (rc2_hi > rc2 >= RadiusX^2), finite throughout
-    const double r2 = valid ? r2_exact(q0, q1, q2) : P.rc2_hi;
-    double r, ir;
-    rsqrt_pair(r2, r, ir);
-    const double dot = fma(dvz, q2, fma(dvy, q1, dvx * q0));
-    const bool fluid_i = !solid;
-    const bool sj = !(solid && dev_is_struct(tj));
-    const double ratio = s_ratio[ti * kTypes + tj];
-    const double mu = s_mu[ti * kTypes + tj];   // read unconditionally (no branch around the load)
-    if (EQR) {
-        const bool in = r2 <= P.rp2;
-        const bool strict = r2 < P.rp2;
-        const double t = r * P.inv_rp;
-        const double omt = 1.0 - t;
-        const double omt2 = omt * omt;
-        const double u = (P.cdp * omt) * ir;
-        o.vs = fma(P.cp, in ? omt2 : 0.0, o.vs);
-        o.dv = fma(-dot, in ? u : 0.0, o.dv);
-        const double c = (in && strict && sj) ? u * P.vol : 0.0;
-        o.s0 = fma(c, q0, o.s0);
-        o.s1 = fma(c, q1, o.s1);
-        o.s2 = fma(c, q2, o.s2);
-        const bool fin = in && fluid_i;
-        o.da = fma(ratio, fin ? (P.ca * t) * omt2 : 0.0, o.da);
-        const double w = fin ? (ratio * (P.cg * omt2)) * P.rg_r2g : 0.0;
-        o.g0 = fma(q0, w, o.g0);
-        o.g1 = fma(q1, w, o.g1);
-        o.g2 = fma(q2, w, o.g2);
-        const double cv = (fin && strict) ? ((mu * omt) * dot) * ((ir * ir) * ir) : 0.0;
-        o.v0 = fma(cv, q0, o.v0);
-        o.v1 = fma(cv, q1, o.v1);
-        o.v2 = fma(cv, q2, o.v2);
-        return;
-    }
-    const bool inp = r2 <= P.rp2;
-    const double omtp = 1.0 - r * P.inv_rp;
-    const double u = (P.cdp * omtp) * ir;
-    o.vs = fma(P.cp * omtp, inp ? omtp : 0.0, o.vs);
-    o.dv = fma(-dot, inp ? u : 0.0, o.dv);
-    const double c = (inp && r2 < P.rp2 && sj) ? u * P.vol : 0.0;
-    o.s0 = fma(c, q0, o.s0);
-    o.s1 = fma(c, q1, o.s1);
-    o.s2 = fma(c, q2, o.s2);
-    const double ta = r * P.inv_ra;
-    const double omta = 1.0 - ta;
-    o.da = fma(ratio, (fluid_i && r2 <= P.ra2) ? ((P.ca * ta) * omta) * omta : 0.0, o.da);
-    const double omtg = 1.0 - r * P.inv_rg;
-    const double w = (fluid_i && r2 <= P.rg2) ? (ratio * ((P.cg * omtg) * omtg)) * P.rg_r2g : 0.0;
-    o.g0 = fma(q0, w, o.g0);
-    o.g1 = fma(q1, w, o.g1);
-    o.g2 = fma(q2, w, o.g2);
-    const double cv = (fluid_i && r2 < P.rv2) ? ((mu * (1.0 - r * P.inv_rv)) * dot) * ((ir * ir) * ir) : 0.0;
-    o.v0 = fma(cv, q0, o.v0);
-    o.v1 = fma(cv, q1, o.v1);
-    o.v2 = fma(cv, q2, o.v2);
-}
-
 // Epilogue: PhysicalCoefficients (2099-2137) and the pressure values of calculatePressureP
 // (2384-2392) and calculatePressureA (2218-2223); with fpart, the neighbour-independent part of
 // the force P_i S_i + viscous force, and the pass-B gather record {x, y, z, P}.
@@ -1152,6 +1047,15 @@ __device__ __forceinline__ bool accept_interior(const DevParams& P, double dx, d
         a = r2_exact(q0, q1, q2) <= P.rc2;
     }
     return a;
+}
+
+// the reference's own acceptance expression (as accept_interior inside its band)
+__device__ __forceinline__ bool accept_band(const DevParams& P, double dx, double dy, double dz)
+{
+    const double q0 = image_exact<true>(dx, P.dw[0], P.hw[0], P.w075[0]);
+    const double q1 = image_exact<true>(dy, P.dw[1], P.hw[1], P.w075[1]);
+    const double q2 = image_exact<true>(dz, P.dw[2], P.hw[2], P.w075[2]);
+    return r2_exact(q0, q1, q2) <= P.rc2;
 }
 
 template <int DIM, bool FAST, int PERM, int SB = MPH_SB>
@@ -1241,9 +1145,6 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
     return cnt;
 }
 
-#ifndef MPH_WIN_BALLOT
-#define MPH_WIN_BALLOT 1   // search window bounds from the first/last active lanes (verified)
-#endif
 #ifndef MPH_DPP_REDUCE
 #define MPH_DPP_REDUCE 1   // wave min/max by DPP row shifts + row broadcasts (else ds_bpermute)
 #endif
@@ -1289,13 +1190,21 @@ __device__ __forceinline__ int wave_max(int v)
 // per-lane loop cost ~19 L1 tag lookups per load instruction (PMC, profiles/r01) and the
 // texture-address unit was the bound; a staged column costs 4.  Same candidates, same order,
 // same FP64 test as scan_candidates, so the list is identical.  Every lane of the wave must call
-// this (act = live particle); the column loop and the staging are wave-uniform.
-template <int DIM, bool SEG, int PERM, int SB = MPH_SB, int CAP = MPH_LDS_CAP>
+// this (act = live particle); the column loop and the staging are wave-uniform.  C16: the compact
+// 16-bit list format (opt-in, lh / o16 non-null).
+//
+// Per column the wave waits for memory once: the start[] loads of column col + 1 are issued before
+// column col's staging loads, so the one wait for the staging also covers them and the next
+// column's window is ready at once.  hipcc would wait for them at their first use instead (round 3:
+// predicated loads, a register copy at the loop latch, a merge with the list stores pending on
+// the same counter -- each made it emit vmcnt(0) right after issuing them: two round trips per
+// column), so they are issued in asm (start_load), which hipcc does not count, and every path of a
+// column ends in an explicit vmcnt(0) before the next column reads them (start_landed).
+template <int DIM, int PERM, bool C16, int SB = MPH_SB, int CAP = MPH_LDS_CAP>
 __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa& A, const int* start,
                                                    int i, bool act, double xi, double yi, double zi,
                                                    int cx, int cy, int cz, int* out, double* sx,
-                                                   unsigned short* seg, int2* hdr, int* seg_overflow,
-                                                   int* lh = nullptr, unsigned short* o16 = nullptr)
+                                                   int* lh, unsigned short* o16, DevState* dst)
 {
     constexpr int SD = stage_d(CAP, SB);
     double* sy = sx + SD;
@@ -1314,37 +1223,35 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     using X = CellAxes<DIM, PERM>;
     int cnt = 0;
     constexpr int NCOL = DIM == 3 ? kGroups * kGroups : kGroups;
-    static_assert(!SEG || NCOL <= kSegCols, "the segmented list header has 25 columns (MPH_R=2)");
     const int cc[3] = {cx, cy, cz};
     const int cca = cc[X::A2];
-    const double rcm2 = P.rc2_trim;
     const double cw0 = P.cwid[X::A0], cw1 = P.cwid[X::A1];
     const double uu[3] = {grid_offset(xi, P.corg[0], P.dw[0]), grid_offset(yi, P.corg[1], P.dw[1]),
                           DIM == 3 ? grid_offset(zi, P.corg[2], P.dw[2]) : 0.0};
     const double ua = uu[X::A2];
     const double ginva = P.ginv[X::A2];
-    // candidate range of this lane in stencil column col (cell ranges -> start[] loads).  The
-    // trimming is only a bound (the exact test decides), so it runs in FP32, rounded outwards: the
-    // squared cell gaps down, the cutoff and the half range up, so every range holds the one of the
-    // FP64 bound (same candidates, same list).  The gap along the slowest axis changes once per
-    // group of columns (the columns are visited in order).
+    // Candidate range of this lane in stencil column col (cell ranges -> start[] loads).  The
+    // trimming is only a bound (the exact test decides), so it runs in FP32 from per-lane values
+    // computed once (the offsets inside the own cell across the columns and along the contiguous
+    // axis, the row base), every rounding outwards by an absolute margin: the squared cell gaps
+    // down (2^-20 cell widths), the cutoff and the half range up, the range ends out by 1e-3
+    // cells.  Each range therefore holds the FP64 one (a superset: same candidates, same list).
+    // The contiguous-axis offset is taken relative to the own cell in FP64 before the conversion
+    // (ua ginv - c lies in [0, 1) for an interior lane), so the margin holds on any grid size.
+    // The gap along the slowest axis changes once per group of columns (visited in order).
     constexpr float kDn = 1.0f - 1.0f / (1 << 20), kUp = 1.0f + 1.0f / (1 << 19);
-    const float rcm2f = (float)rcm2 * kUp;
+    const float rcm2f = (float)P.rc2_trim * kUp;
     float gx2f = 0.0f;
-#if MPH_COLRANGE32
-    // FP32 column ranges from per-lane values computed once (the offsets inside the own cell, the
-    // cell coordinate along the contiguous axis, the row base): every rounding goes outwards by an
-    // absolute margin (gaps down by 2^-20 cell widths, the range ends out by 1e-3 cells), so each
-    // range holds the FP64 one of col_range below -- a superset, the exact test decides.
     const int c0l = cc[X::A0], c1l = DIM == 3 ? cc[X::A1] : 0;
     const float cw0f = (float)cw0, cw1f = (float)cw1;
     const float f0 = (float)(uu[X::A0] - c0l * cw0), f1 = DIM == 3 ? (float)(uu[X::A1] - c1l * cw1) : 0.0f;
     const float g0p = f0, g0m = cw0f - f0, g1p = f1, g1m = cw1f - f1;   // subtracted for d > 0 / d < 0
     const float mu0 = cw0f * (1.0f / (1 << 20)), mu1 = cw1f * (1.0f / (1 << 20));
     const float ginvaf = (float)ginva;
-    const float caf = (float)(ua * ginva);   // cell coordinate along the contiguous axis
-    const int rowbase = DIM == 3 ? (c0l * P.gc[X::A1] + c1l) * P.gc[X::A2] : c0l * P.gc[1];
-    const int clo = cca - P.sa, chi = cca + P.sa;
+    const float caf = (float)(ua * ginva - (double)cca);   // offset inside the own cell, cells
+    const int rowbase = (DIM == 3 ? (c0l * P.gc[X::A1] + c1l) * P.gc[X::A2] : c0l * P.gc[1]) + cca;
+    const int sa = P.sa;
+    const __amdgpu_buffer_rsrc_t srs = arr_rsrc(start);
     auto gap32 = [](int d, float cwf, float gp, float gm, float mu) {
         if (d == 0) return 0.0f;
         const float v = (float)(d > 0 ? d : -d) * cwf - (d > 0 ? gp : gm) - mu;
@@ -1368,78 +1275,38 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             d2f = gx * gx * kDn;
             cofs = dxc * P.gc[1];
         }
-        jb = 0;
-        je = 0;
-        if (act && d2f <= rcm2f) {
-            const float rc = __builtin_amdgcn_sqrtf(rcm2f - d2f) * kUp * ginvaf;   // half range, cells
-            const int lo = max((int)floorf(caf - rc - 1e-3f), clo);
-            const int hi = min((int)floorf(caf + rc + 1e-3f), chi);
-            const int b = rowbase + cofs;
-            if (MPH_GLDS_BUF) {
-                jb = __builtin_amdgcn_raw_buffer_load_b32(arr_rsrc(start), (unsigned)(b + lo) * 4u, 0, 0);
-                je = __builtin_amdgcn_raw_buffer_load_b32(arr_rsrc(start), (unsigned)(b + hi + 1) * 4u, 0, 0);
-            } else {
-                jb = start[b + lo];
-                je = start[b + hi + 1];
-            }
-        }
+        const bool ok = act && d2f <= rcm2f;
+        const float rc = __builtin_amdgcn_sqrtf(fmaxf(rcm2f - d2f, 0.0f)) * kUp * ginvaf;   // half range, cells
+        const int lo = max((int)floorf(caf - rc - 1e-3f), -sa);
+        const int hi = min((int)floorf(caf + rc + 1e-3f), sa);
+        const int b = rowbase + cofs;
+        // a lane without candidates reads start[0] twice (empty range)
+        start_load2(srs, ok ? (unsigned)(b + lo) * 4u : 0u, ok ? (unsigned)(b + hi + 1) * 4u : 0u, jb, je);
     };
-#else
-    auto col_range = [&](int col, int& jb, int& je) {
-        int base;
-        float d2f;
-        if (DIM == 3) {
-            const int dxc = col / kGroups - kReach, dyc = col % kGroups - kReach;
-            const int c0 = cc[X::A0], c1 = cc[X::A1];
-            if (dyc == -kReach) {
-                const float gx = (float)cell_gap(uu[X::A0], c0, dxc, cw0);
-                gx2f = gx * gx * kDn;
-            }
-            const float gy = (float)cell_gap(uu[X::A1], c1, dyc, cw1);
-            d2f = (gx2f + gy * gy * kDn) * kDn;
-            base = ((c0 + dxc) * P.gc[X::A1] + c1 + dyc) * P.gc[X::A2];
-        } else {
-            const int dxc = col - kReach;
-            const float gx = (float)cell_gap(uu[0], cx, dxc, cw0);
-            d2f = gx * gx * kDn;
-            base = (cx + dxc) * P.gc[1];
-        }
-        jb = 0;
-        je = 0;
-        if (act && d2f <= rcm2f) {
-            const double ra = (double)(__fsqrt_rn(rcm2f - d2f) * kUp);
-            const int lo = (int)fmax(floor((ua - ra) * ginva), (double)(cca - P.sa));
-            const int hi = (int)fmin(floor((ua + ra) * ginva), (double)(cca + P.sa));
-            jb = start[base + lo];
-            je = start[base + hi + 1];
-        }
-    };
-#endif
     // compact list (nbr_list): the wave-wide index range of every column group, from the cell
     // ranges of its first and last column (no column wraps: the wave is interior)
-    const bool want16 = MPH_LIST16 && !SEG && lh != nullptr;
-    bool c16 = false;
     int gb[kGroups], gbase = 0;   // wave-uniform group bases
-    if (want16) {
-        bool ok = true;
+    bool c16 = false;
+    if (C16) {
+        bool okg = true;
 #pragma unroll
         for (int g = 0; g < kGroups; ++g) {
             int lo = 0x7fffffff, hi = -1;
             if (act) {
                 if (DIM == 3) {
                     const int a0 = cc[X::A0] + g - kReach, c1 = cc[X::A1];
-                    lo = start[((a0 * P.gc[X::A1] + c1 - kReach) * P.gc[X::A2]) + cca - P.sa];
-                    hi = start[((a0 * P.gc[X::A1] + c1 + kReach) * P.gc[X::A2]) + cca + P.sa + 1];
+                    lo = start[((a0 * P.gc[X::A1] + c1 - kReach) * P.gc[X::A2]) + cca - sa];
+                    hi = start[((a0 * P.gc[X::A1] + c1 + kReach) * P.gc[X::A2]) + cca + sa + 1];
                 } else {
-                    lo = start[(cx + g - kReach) * P.gc[1] + cca - P.sa];
-                    hi = start[(cx + g - kReach) * P.gc[1] + cca + P.sa + 1];
+                    lo = start[(cx + g - kReach) * P.gc[1] + cca - sa];
+                    hi = start[(cx + g - kReach) * P.gc[1] + cca + sa + 1];
                 }
             }
             const int mn = wave_min(lo), mx = wave_max(hi);
-            ok = ok && (mx <= mn || mx - mn <= kSpan16 + 1);
+            okg = okg && (mx <= mn || mx - mn <= kSpan16 + 1);
             gb[g] = mx > mn ? mn : 0;
         }
-        c16 = ok;
+        c16 = okg;
     }
     // the lane's group ends go straight to the header (byte g - 1: the count at the end of group
     // g - 1; unused bytes 127, nbr_at), so they hold no registers during the column loop
@@ -1448,14 +1315,15 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
         lh[8 + lane] = 0x7F7F7F7F;
         if (kGroups > 5) lh[8 + 64 + lane] = 0x7F7F7F7F;
     }
-    // software pipeline: the start[] loads of column col + 1 are in flight while column col is
-    // staged and tested (the per-column chain start[] -> window -> staging loads is latency bound)
-    int nb_jb, nb_je, n2_jb = 0, n2_je = 0;   // columns col + 1 and (MPH_SEARCH_PREFETCH=2) col + 2
-    col_range(0, nb_jb, nb_je);
-    if (MPH_SEARCH_PREFETCH == 2 && NCOL > 1) col_range(1, n2_jb, n2_je);
-    int slot = 0;   // SEG: first slot of this column's segment
-    for (int col = 0; col < NCOL; ++col) {
-        if (c16) {
+    // the lane's next list slot: C16 counts entries (cnt); the ELL rows keep the slot's byte offset
+    // in the wave's tile, soff = cnt * 256 + lane * 4 (one add per entry, no address arithmetic)
+    int soff = lane << 2;
+    constexpr int kSelfCol = DIM == 3 ? kReach * kGroups + kReach : kReach;   // the lane's own column
+    // one stencil column: its range [jb, je) was loaded one column ahead; (nb_jb, nb_je) receive
+    // column col + 1's.  The loop below is unrolled by two with the roles of the two register pairs
+    // swapped, so no copy at the loop latch waits for the loads in flight.
+    auto column = [&](int col, int jb, int je, int& nb_jb, int& nb_je) {
+        if (C16 && c16) {
             // entering group g: the count so far ends group g - 1
             const bool first = DIM == 3 ? col % kGroups == 0 : true;
             const int g = DIM == 3 ? col / kGroups : col;
@@ -1466,62 +1334,43 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                     if (q == g) gbase = gb[q];
             }
         }
-        const int jb = nb_jb, je = nb_je;
-        if (MPH_SEARCH_PREFETCH == 2) {   // two columns ahead
-            nb_jb = n2_jb;
-            nb_je = n2_je;
-            if (col + 2 < NCOL) col_range(col + 2, n2_jb, n2_je);
-        } else if (MPH_SEARCH_PREFETCH && col + 1 < NCOL) {
-            col_range(col + 1, nb_jb, nb_je);
-        }
+        start_landed(jb, je);   // loaded one column ahead; every path below ended in vmcnt(0)
+        if (col + 1 < NCOL) col_range(col + 1, nb_jb, nb_je);
         const bool any = je > jb;
         // the wave's window [mn, mx): the lanes are in cell order, so the first lane with candidates
         // normally has the lowest jb and the last the highest je -- read those two lanes, and take
         // the DPP reductions only when a lane says otherwise (wave-uniform check)
         const unsigned long long am = __ballot(any);
-        int mn = 0x7fffffff, mx = -1;
-        if (am && !MPH_WIN_BALLOT) {
+        if (!am) {   // wave-uniform: no lane has candidates in this column
+            // wait here for column col + 1's start[] loads, so that every path into the next column
+            // has them landed and its first use needs no wait (which would also wait for this
+            // column's list stores: loads and stores share vmcnt)
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+            return;
+        }
+        int mn = __builtin_amdgcn_readlane(jb, __ffsll((long long)am) - 1);
+        int mx = __builtin_amdgcn_readlane(je, 63 - __clzll(am));
+        if (__ballot(any && (jb < mn || je > mx))) {
             mn = wave_min(any ? jb : 0x7fffffff);
             mx = wave_max(any ? je : -1);
-        } else if (am) {
-            mn = __builtin_amdgcn_readlane(jb, __ffsll((long long)am) - 1);
-            mx = __builtin_amdgcn_readlane(je, 63 - __clzll(am));
-            if (__ballot(any && (jb < mn || je > mx))) {
-                mn = wave_min(any ? jb : 0x7fffffff);
-                mx = wave_max(any ? je : -1);
-            }
         }
-        if (!MPH_SEARCH_PREFETCH && col + 1 < NCOL) col_range(col + 1, nb_jb, nb_je);
-        if (mx <= mn) {   // wave-uniform: no lane has candidates in this column
-            if (SEG && lane == 0) hdr[col] = make_int2(0, 0);
-            continue;
+        if (MPH_DIAG_BOUNDS && (mn < 0 || mx > dev_n(P) || mx < mn)) {   // diagnostic builds only
+            if (lane == 0) atomicOr(&dst->overflow, 8);
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+            return;
         }
         const int span = mx - mn;
-        const int cnt0 = cnt;   // SEG: this lane's entries before the column
-        if (MPH_DIAG_SEARCH & 2) { cnt += span == 0x7fffffff; continue; }   // never true: empty lists
+        if (MPH_DIAG_SEARCH & 2) {   // never true: empty lists
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+            soff += span == 0x7fffffff ? 256 : 0;
+            return;
+        }
         if (span <= CAP) {
-#if MPH_GLDS
             // the window from a 16-byte-aligned start: candidate j sits at j - mn + da in x, y, z
             // and at j - mn + ta in the types; pieces of 128 doubles / 256 ints per instruction,
             // lanes past the window masked (the arrays hold kPad elements beyond any window)
             const int da = mn & 1, ta = mn & 3;
             const int n2 = span + da, n4 = span + ta;
-#if MPH_GLDS_BUF
-            // buffer form: one 32-bit lane offset for x, y and z (SGPR descriptors of the arrays)
-            for (int p = 0; p * 128 < n2; ++p) {   // wave-uniform
-                const int e = p * 128 + 2 * lane;
-                if (e < n2) {
-                    const unsigned vo = (unsigned)(mn - da + e) * 8u;
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(arr_rsrc(A.x), lds_ptr(sx + p * 128), 16, vo, 0, 0, 0);
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(arr_rsrc(A.y), lds_ptr(sy + p * 128), 16, vo, 0, 0, 0);
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(arr_rsrc(A.z), lds_ptr(sz + p * 128), 16, vo, 0, 0, 0);
-                }
-            }
-            static_assert(CAP + 3 <= 256, "one 256-int piece holds the types of a window");
-            if (4 * lane < n4)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(arr_rsrc(A.type), lds_ptr(st), 16,
-                                                         (unsigned)(mn - ta + 4 * lane) * 4u, 0, 0, 0);
-#else
             for (int p = 0; p * 128 < n2; ++p) {   // wave-uniform
                 const int e = p * 128 + 2 * lane;
                 if (e < n2) {
@@ -1532,64 +1381,70 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             }
             static_assert(CAP + 3 <= 256, "one 256-int piece holds the types of a window");
             if (4 * lane < n4) __builtin_amdgcn_global_load_lds(A.type + (mn - ta) + 4 * lane, st, 16, 0, 0);
-#endif
-            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the pieces have landed in LDS
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the pieces (and column col + 1's start[]) landed
             const int kofs = da, tofs = ta - da;
-#else
-            for (int t = lane; t < span; t += 64) {
-                sx[t] = A.x[mn + t];
-                sy[t] = A.y[mn + t];
-                sz[t] = A.z[mn + t];
-                st[t] = A.type[mn + t];
-            }
-            const int kofs = 0, tofs = 0;
-#endif
             __builtin_amdgcn_wave_barrier();
-            if (MPH_DIAG_SEARCH & 1) { cnt += sx[lane] == -1.25e300; continue; }   // (never true)
-            // the staging arrays are padded by SB entries, so a batch may read past je (masked)
-            for (int j0 = jb; j0 < je; j0 += SB) {
-                double xs[SB], ys[SB], zs[SB];
-                int ts[SB];
-                const int k0 = j0 - mn + kofs;
+            if (MPH_DIAG_SEARCH & 1) { soff += sx[lane] == -1.25e300 ? 256 : 0; return; }   // (never true)
+            // this lane's candidates [jb, je) sit at staged position k = j - jd (types at k + tofs);
+            // the staging arrays are padded by SB entries, so a batch may read past je (masked).
+            // Per candidate: the FP64 distance (6), two compares -- the decision r2 <= rc2 (1 -
+            // 1e-10) and, XOR-ed with it, r2 <= rc2 (1 + 1e-10), which flags the rare band where the
+            // reference's own expression decides -- and, when accepted, the entry and one add.  The
+            // self test runs only in the lane's own column (SELF), the range test only past the
+            // batch's first candidate (the loop condition covers it).
+            const int jd = mn - kofs;
+            auto test = [&](auto self_tag) {
+                constexpr bool SELF = decltype(self_tag)::value;
+                for (int j0 = jb; j0 < je; j0 += SB) {
+                    double xs[SB], ys[SB], zs[SB];
+                    int ts[SB];
+                    const int k0 = j0 - jd;
 #pragma unroll
-                for (int u = 0; u < SB; ++u) {
-                    xs[u] = sx[k0 + u];
-                    ys[u] = sy[k0 + u];
-                    zs[u] = sz[k0 + u];
-                    // MPH_TYPE_BATCH: the types with the batch (no LDS wait per accepted entry)
-                    if (MPH_TYPE_BATCH) ts[u] = st[k0 + u + tofs];
-                }
+                    for (int u = 0; u < SB; ++u) {
+                        xs[u] = sx[k0 + u];
+                        ys[u] = sy[k0 + u];
+                        zs[u] = sz[k0 + u];
+                        ts[u] = st[k0 + u + tofs];   // the types with the batch (no LDS wait per accepted entry)
+                    }
 #pragma unroll
-                for (int u = 0; u < SB; ++u) {
-                    const int j = j0 + u;
-                    // non-short-circuit conditions (one exec mask), and no branch on the list
-                    // capacity: past kMaxNeighbor the last slot is overwritten and the overflow
-                    // flag ends the run (MPH_ERR_NEIGHBOR_OVERFLOW)
-                    const bool a = accept_interior(P, xs[u] - xi, ys[u] - yi, zs[u] - zi, lo2, hi2) &
-                                   (j < je) & (j != i);
-                    if (a) {
-                        if (SEG) {
-                            const int sl = slot + (cnt - cnt0);
-                            if (sl < kSegCap)
-                                seg[(size_t)sl * kTile + lane] = (unsigned short)((j - mn) | (st[k0 + u + tofs] << 8));
-                        } else if (c16) {
-                            const int k = min(cnt, kMaxNeighbor - 1);
-                            o16[(((k >> 1) * kTile + lane) << 1) + (k & 1)] =
-                                (unsigned short)((j - gbase) | (st[k0 + u + tofs] << kOff16));
-                        } else if (MPH_DIAG_NOSTORE == 2) {   // diagnostic: same stores, one row (no list traffic)
-                            list_store(out + (min(cnt, kMaxNeighbor - 1) & 0) * kTile, nbr_entry(j, st[k0 + u + tofs]));
-                        } else if (!MPH_DIAG_NOSTORE) {
-                            const int e = nbr_entry(j, MPH_TYPE_BATCH ? ts[u] : st[k0 + u + tofs]);
-                            if (MPH_BUF_STORE)   // 32-bit offset into the wave's tile (SGPR descriptor)
-                                __builtin_amdgcn_raw_buffer_store_b32(
-                                    e, tile_rsrc, (min(cnt, kMaxNeighbor - 1) << 8) + (lane << 2), 0, 0);
-                            else
-                                list_store(out + min(cnt, kMaxNeighbor - 1) * kTile, e);
+                    for (int u = 0; u < SB; ++u) {
+                        const int j = j0 + u;
+                        const double dx = xs[u] - xi, dy = ys[u] - yi, dz = zs[u] - zi;
+                        const double r2a = fma(dx, dx, fma(dy, dy, dz * dz));
+                        const bool in = r2a <= lo2;
+                        bool a = in;
+                        if ((r2a <= hi2) != in) a = accept_band(P, dx, dy, dz);
+                        if (u > 0) a = a & (j < je);
+                        if (SELF) a = a & (j != i);
+                        if (a) {
+                            if (C16 && c16) {
+                                const int k = min(cnt, kMaxNeighbor - 1);
+                                o16[(((k >> 1) * kTile + lane) << 1) + (k & 1)] =
+                                    (unsigned short)((j - gbase) | (ts[u] << kOff16));
+                                ++cnt;
+                            } else if (MPH_DIAG_NOSTORE == 2) {   // diagnostic: same stores, one row
+                                list_store(out, nbr_entry(j, ts[u]));
+                                soff += 256;
+                            } else if (MPH_DIAG_NOSTORE) {
+                                soff += 256;
+                            } else if (!C16) {
+                                // byte offset into the wave's tile (SGPR descriptor); past kMaxNeighbor
+                                // entries the store falls outside the descriptor's range and is
+                                // dropped, and the overflow flag ends the run (MPH_ERR_NEIGHBOR_OVERFLOW)
+                                __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, ts[u]), tile_rsrc, soff, 0, 0);
+                                soff += 256;
+                            } else {
+                                __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, ts[u]), tile_rsrc,
+                                                                      (min(cnt, kMaxNeighbor - 1) << 8) + (lane << 2),
+                                                                      0, 0);
+                                ++cnt;
+                            }
                         }
-                        ++cnt;
                     }
                 }
-            }
+            };
+            if (col == kSelfCol) test(std::true_type{});
+            else test(std::false_type{});
             __builtin_amdgcn_wave_barrier();   // every lane done reading before the next staging
         } else {
             for (int j0 = jb; j0 < je; j0 += SB) {
@@ -1605,38 +1460,35 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                 for (int u = 0; u < SB; ++u) {
                     const int j = j0 + u;
                     if (accept_interior(P, xs[u] - xi, ys[u] - yi, zs[u] - zi, lo2, hi2) && j < je && j != i) {
-                        if (SEG) {
-                            const int sl = slot + 2 * (cnt - cnt0);
-                            if (sl + 1 < kSegCap) {
-                                seg[(size_t)sl * kTile + lane] = (unsigned short)(j & 0xFFFF);
-                                seg[(size_t)(sl + 1) * kTile + lane] = (unsigned short)((j >> 16) | (A.type[j] << 12));
+                        if (C16) {
+                            if (cnt < kMaxNeighbor) {
+                                if (c16)
+                                    o16[(((cnt >> 1) * kTile + lane) << 1) + (cnt & 1)] =
+                                        (unsigned short)((j - gbase) | (A.type[j] << kOff16));
+                                else
+                                    list_store(out + cnt * kTile, nbr_entry(j, A.type[j]));
                             }
-                        } else if (c16) {
-                            if (cnt < kMaxNeighbor)
-                                o16[(((cnt >> 1) * kTile + lane) << 1) + (cnt & 1)] =
-                                    (unsigned short)((j - gbase) | (A.type[j] << kOff16));
-                        } else if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) {
-                            list_store(out + cnt * kTile, nbr_entry(j, A.type[j]));
+                            ++cnt;
+                        } else {
+                            if (!MPH_DIAG_NOSTORE && soff < kMaxNeighbor * 256)
+                                list_store(out + (soff >> 8) * kTile, nbr_entry(j, A.type[j]));
+                            soff += 256;
                         }
-                        ++cnt;
                     }
                 }
             }
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // column col + 1's start[] loads (wide windows are rare)
         }
-        if (SEG) {
-            // close the column's segment: W = the most entries any lane has in it; the others pad
-            const bool wide = span > CAP;
-            const int mine = cnt - cnt0;
-            const int w = wave_max(mine);
-            const int per = wide ? 2 : 1;
-            for (int k = mine * per; k < w * per; ++k)
-                if (slot + k < kSegCap) seg[(size_t)(slot + k) * kTile + lane] = kSegNone;
-            if (lane == 0) hdr[col] = make_int2(mn, (span & 0xFFFF) | (w << 16) | (wide ? (int)0x80000000 : 0));
-            slot += w * per;
-        }
+    };
+    int ra_b, ra_e, rb_b = 0, rb_e = 0;   // the two register pairs of the column ranges
+    col_range(0, ra_b, ra_e);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    for (int col = 0; col < NCOL; col += 2) {
+        column(col, ra_b, ra_e, rb_b, rb_e);
+        if (col + 1 < NCOL) column(col + 1, rb_b, rb_e, ra_b, ra_e);
     }
-    if (SEG && slot > kSegCap) *seg_overflow = 1;
-    if (c16) {
+    if (!C16) cnt = soff >> 8;
+    if (C16 && c16) {
         // the group ends are bytes below 128 (nbr_at): a wave with a lane past 127 neighbours (the
         // reference allows 511) is marked for the ELL search of launch_neighbors' second launch
         // (k_neighbors REDO)
@@ -1681,19 +1533,17 @@ __device__ __forceinline__ void slab_wave_flag(const DevParams& P, const Soa& A,
     if ((threadIdx.x & 63) == 0) wface[i >> 6] = face ? 1 : 0;
 }
 
-template <int DIM, int PERM, int REDO>
+template <int DIM, int PERM, bool C16, int REDO>
 __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, const int* start, int* nbr,
-                                               int* ncount, int2* hdr, int* lhdr, DevState* st, double* stage,
-                                               int i)
+                                               int* ncount, int* lhdr, DevState* st, double* stage, int i)
 {
     const int n = dev_n(P);
     const bool live = i < n;
     const int ii = live ? i : n - 1;
     // list format of the wave: the 32-bit ELL row unless the interior search below goes compact
     const int tile = __builtin_amdgcn_readfirstlane(i >> 6);
-    int* lh = lhdr ? lhdr + (size_t)tile * kLhdr : nullptr;
-    if (REDO) lh = nullptr;   // a wave the first launch marked: now into ELL rows
-    if (lhdr && (threadIdx.x & 63) == 0) lhdr[(size_t)tile * kLhdr + kHdrFlag] = 0;
+    int* lh = C16 && !REDO ? lhdr + (size_t)tile * kLhdr : nullptr;   // REDO: a marked wave, now into ELL rows
+    if (C16 && (threadIdx.x & 63) == 0) lhdr[(size_t)tile * kLhdr + kHdrFlag] = 0;
     if (wave_all_ghosts(P, A, live, ii)) {
         if (live) ncount[i] = 0;
         return 0;
@@ -1707,24 +1557,15 @@ __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, 
     const int cy = cell_axis(yi, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
     const int cz = DIM == 3 ? cell_axis(zi, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
     int* out = nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
-#if MPH_SEG
-    int2* h = hdr ? hdr + (size_t)(i >> 6) * kSegHdr : nullptr;
-    int seg_over = 0;
-#endif
     if (MPH_SEARCH_LDS && fast) {
-#if MPH_SEG
-        if (h) {
-            cnt = scan_candidates_lds<DIM, true, PERM>(P, A, start, i, own, xi, yi, zi, cx, cy, cz, out,
-                                                       stage, seg_tile(nbr, i), h, &seg_over);
-            if ((threadIdx.x & 63) == 0) h[kSegCols] = make_int2(1, 0);
-        } else
-#endif
-        {
-            cnt = scan_candidates_lds<DIM, false, PERM>(P, A, start, i, own, xi, yi, zi, cx, cy, cz, out,
-                                                        stage, nullptr, nullptr, nullptr, lh,
-                                                        reinterpret_cast<unsigned short*>(
-                                                            nbr + (size_t)tile * (kTile * kMaxNeighbor)));
-            if (lh && (threadIdx.x & 63) == 0 && lh[kHdrFlag] == 2) atomicAdd(&st->list_redo, 1);
+        if (C16 && !REDO) {
+            cnt = scan_candidates_lds<DIM, PERM, true>(P, A, start, i, own, xi, yi, zi, cx, cy, cz, out, stage, lh,
+                                                       reinterpret_cast<unsigned short*>(
+                                                           nbr + (size_t)tile * (kTile * kMaxNeighbor)), st);
+            if ((threadIdx.x & 63) == 0 && lh[kHdrFlag] == 2) atomicAdd(&st->list_redo, 1);
+        } else {
+            cnt = scan_candidates_lds<DIM, PERM, false>(P, A, start, i, own, xi, yi, zi, cx, cy, cz, out, stage,
+                                                        nullptr, nullptr, st);
         }
         if (live) ncount[i] = cnt;
     } else {
@@ -1732,15 +1573,7 @@ __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, 
             cnt = fast ? scan_candidates<DIM, true, PERM>(P, A, start, i, xi, yi, zi, cx, cy, cz, out)
                        : scan_candidates<DIM, false, PERM>(P, A, start, i, xi, yi, zi, cx, cy, cz, out);
         if (live && !(MPH_DIAG_SEARCH & 4)) ncount[i] = cnt;
-#if MPH_SEG
-        if (h && (threadIdx.x & 63) == 0) h[kSegCols] = make_int2(0, 0);
-#endif
     }
-#if MPH_SEG
-    // a segmented list past the tile's 1024 slots (far beyond any physical state: ~100 used at
-    // D1M) is reported like a neighbour overflow
-    if (seg_over) atomicOr(&st->overflow, 1);
-#endif
     // overflow flag (main.cpp:1766-1768 is the reference's limit).  No per-step statistics here:
     // one same-address device atomic per wave serialises at ~11 ns each (21.8k waves at D1M took
     // 0.5 ms); mph_neighbor_stats reduces ncount on demand.
@@ -1748,16 +1581,16 @@ __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, 
     return cnt;
 }
 
-// one kernel per cell order (DevParams.perm), so each keeps its own register budget; held to 64
-// VGPRs (8 waves per SIMD: the search waits on its start[] and staging loads)
+// one kernel per cell order (DevParams.perm) and list format, so each keeps its own register
+// budget; held to 64 VGPRs (8 waves per SIMD: the search waits on its start[] and staging loads).
+// bal: the passes' XCD split runs this step (launch_neighbors), so the waves feed its histogram.
 #ifndef MPH_NB_WPE
 #define MPH_NB_WPE 8
 #endif
-template <int DIM, int PERM>
-__global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_WPE))) void k_neighbors(DevParams P, Soa A, const int* __restrict__ start,
-                                                   int* __restrict__ nbr, int* __restrict__ ncount,
-                                                   int2* __restrict__ hdr, int* __restrict__ lhdr,
-                                                   DevState* __restrict__ st, int* __restrict__ wface)
+template <int DIM, int PERM, bool C16>
+__global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_WPE))) void k_neighbors(
+    DevParams P, Soa A, const int* __restrict__ start, int* __restrict__ nbr, int* __restrict__ ncount,
+    int* __restrict__ lhdr, DevState* __restrict__ st, int* __restrict__ wface, int bal)
 {
     const int n = dev_n(P);
     if ((int)blockIdx.x >= list_blocks(n)) return;
@@ -1765,8 +1598,8 @@ __global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_W
     __shared__ __attribute__((aligned(16))) double stage[kWB][stage_words(MPH_LDS_CAP, MPH_SB)];
     const int i = xcd_block(blockIdx.x, list_blocks(n)) * blockDim.x + threadIdx.x;
     slab_wave_flag(P, A, i, n, wface);
-    const int cnt = neighbors_body<DIM, PERM, 0>(P, A, start, nbr, ncount, hdr, lhdr, st, stage[threadIdx.x >> 6], i);
-    add_wave_work(st, cnt, i, n);
+    const int cnt = neighbors_body<DIM, PERM, C16, 0>(P, A, start, nbr, ncount, lhdr, st, stage[threadIdx.x >> 6], i);
+    if (bal) add_wave_work(st, cnt, i, n);
 }
 
 // The XCD ranges of the list passes from the search's work histogram (see list_block): one block,
@@ -1836,8 +1669,7 @@ __global__ __launch_bounds__(256) void k_neighbors_redo(DevParams P, Soa A, cons
         while (m) {
             const int b = __ffsll((long long)m) - 1;
             m &= m - 1;
-            neighbors_body<DIM, PERM, 1>(P, A, start, nbr, ncount, nullptr, lhdr, st, stage[wave],
-                                         (t0 + b) * kTile + lane);
+            neighbors_body<DIM, PERM, true, 1>(P, A, start, nbr, ncount, lhdr, st, stage[wave], (t0 + b) * kTile + lane);
         }
     }
     __syncthreads();
@@ -1848,9 +1680,6 @@ __global__ __launch_bounds__(256) void k_neighbors_redo(DevParams P, Soa A, cons
 
 // List pass: the neighbour loops gather U neighbours' fields
 // before the first use (all loads in flight at once; the loops are memory-latency bound).
-#ifndef MPH_PA_SEL
-#define MPH_PA_SEL 0   // k_pass_a: the branching term (the selecting one: D1M pass A 0.33 -> 0.51 ms)
-#endif
 #ifndef MPH_UA
 #define MPH_UA 5   // pass A (with MPH_PA_WPE 4; coherent gathers at kReach 3: 0.355 ms against 0.376 at U = 8, 3 waves)
 #endif
@@ -1892,113 +1721,8 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
             const double q0 = image_exact<FAST>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
             const double q1 = image_exact<FAST>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
             const double q2 = image_exact<FAST || DIM == 2>(Z[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
-            // the branching form (MPH_PA_SEL=1: the fused kernel's selecting one; same bits)
-            if (MPH_PA_SEL)
-                pass_a_term_sel<EQR>(P, s_ratio, s_mu, ti, TT[u], solid, true, q0, q1, q2, VX[u] - vxi, VY[u] - vyi,
-                                     VZ[u] - vzi, o);
-            else
-                pass_a_term<true, EQR>(P, s_ratio, s_mu, ti, TT[u], solid, q0, q1, q2, r2_exact(q0, q1, q2),
-                                       VX[u] - vxi, VY[u] - vyi, VZ[u] - vzi, o);
-        }
-    }
-}
-
-// MPH_SEG_GATHER: how the segmented passes read a column's records -- 0 staged in LDS, 1 AoS
-// gathers from global memory, 2 SoA gathers (the lanes' k-th entries of a column are aligned,
-// so the 64 lanes touch a few consecutive lines per 8-byte load)
-#ifndef MPH_SEG_GATHER
-#define MPH_SEG_GATHER 0
-#endif
-// Pass A over a column-segmented list (interior waves): per stencil column the wave stages its
-// window of 48-byte records in LDS with coalesced loads and every lane reads its neighbours from
-// there -- instead of per-lane gathers whose 64 lanes touch ~41 cache lines per 16-byte load (the
-// per-CU L1 tag rate bound pass A).  Wide columns (window beyond the staging capacity) gather
-// from global memory.  Every lane of the wave takes part (live = it has a particle).
-template <int DIM, int U = MPH_UA, int CAP = MPH_LDS_CAP>
-__device__ __forceinline__ void pass_a_seg(const DevParams& P, const double* s_ratio, const double* s_mu,
-                                           const Soa& A, const unsigned short* seg, const int2* hdr, bool live,
-                                           int ti, bool solid, double xi, double yi, double zi, double vxi,
-                                           double vyi, double vzi, PassA& o, double2* stage)
-{
-    constexpr int NCOL = DIM == 3 ? 25 : 5;
-    const int lane = threadIdx.x & 63;
-    int slot = 0;
-    for (int col = 0; col < NCOL; ++col) {
-        const int2 h = hdr[col];
-        const int w = (h.y >> 16) & 0x7FFF;
-        if (w == 0) continue;
-        const int mn = h.x;
-        if (h.y >= 0) {
-            const int span = h.y & 0xFFFF;
-            const double2* src = A.p6 + 3 * (size_t)mn;
-            if (MPH_SEG_GATHER == 0) {
-                for (int t = lane; t < 3 * span; t += 64) stage[t] = src[t];
-                __builtin_amdgcn_wave_barrier();
-            }
-            for (int k0 = 0; k0 < w; k0 += U) {
-                unsigned e[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    e[u] = k0 + u < w ? seg[(size_t)min(slot + k0 + u, kSegCap - 1) * kTile + lane] : kSegNone;
-                double X[U], Y[U], Z[U], VX[U], VY[U], VZ[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int q = e[u] == kSegNone ? 0 : (int)(e[u] & 0xFF);
-                    if (MPH_SEG_GATHER == 2) {   // column-aligned lanes: coherent 8-byte SoA gathers
-                        const int j = mn + q;
-                        X[u] = A.x[j]; Y[u] = A.y[j]; Z[u] = A.z[j];
-                        VX[u] = A.vx[j]; VY[u] = A.vy[j]; VZ[u] = A.vz[j];
-                        continue;
-                    }
-                    const double2* r = MPH_SEG_GATHER == 1 ? src : stage;
-                    const double2 a = r[3 * q], b = r[3 * q + 1], c = r[3 * q + 2];
-                    X[u] = a.x; Y[u] = a.y; Z[u] = b.x;
-                    VX[u] = b.y; VY[u] = c.x; VZ[u] = c.y;
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    if (!live || e[u] == kSegNone) continue;
-                    const double q0 = image_exact<true>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
-                    const double q1 = image_exact<true>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
-                    const double q2 = image_exact<true>(Z[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
-                    pass_a_term<true>(P, s_ratio, s_mu, ti, (int)((e[u] >> 8) & 7), solid, q0, q1, q2,
-                                      r2_exact(q0, q1, q2), VX[u] - vxi, VY[u] - vyi, VZ[u] - vzi, o);
-                }
-            }
-            if (MPH_SEG_GATHER == 0) __builtin_amdgcn_wave_barrier();   // reads done before the next staging
-            slot += w;
-        } else {
-            for (int k0 = 0; k0 < w; k0 += U) {
-                int jj[U], TT[U];
-                bool ok[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int sl = min(slot + 2 * (k0 + u), kSegCap - 2);
-                    const unsigned lo = k0 + u < w ? seg[(size_t)sl * kTile + lane] : 0u;
-                    const unsigned hi = k0 + u < w ? seg[(size_t)(sl + 1) * kTile + lane] : kSegNone;
-                    ok[u] = hi != kSegNone;
-                    jj[u] = ok[u] ? (int)(lo | ((hi & 0xFFF) << 16)) : mn;
-                    TT[u] = (int)(hi >> 12) & 7;
-                }
-                double X[U], Y[U], Z[U], VX[U], VY[U], VZ[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const double2* q = A.p6 + 3 * (size_t)jj[u];
-                    const double2 a = q[0], b = q[1], c = q[2];
-                    X[u] = a.x; Y[u] = a.y; Z[u] = b.x;
-                    VX[u] = b.y; VY[u] = c.x; VZ[u] = c.y;
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    if (!live || !ok[u]) continue;
-                    const double q0 = image_exact<true>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
-                    const double q1 = image_exact<true>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
-                    const double q2 = image_exact<true>(Z[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
-                    pass_a_term<true>(P, s_ratio, s_mu, ti, TT[u], solid, q0, q1, q2, r2_exact(q0, q1, q2),
-                                      VX[u] - vxi, VY[u] - vyi, VZ[u] - vzi, o);
-                }
-            }
-            slot += 2 * w;
+            pass_a_term<true, EQR>(P, s_ratio, s_mu, ti, TT[u], solid, q0, q1, q2, r2_exact(q0, q1, q2),
+                                   VX[u] - vxi, VY[u] - vyi, VZ[u] - vzi, o);
         }
     }
 }
@@ -2014,7 +1738,7 @@ __device__ __forceinline__ void pass_a_seg(const DevParams& P, const double* s_r
 template <int DIM>
 __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, const DevTables* __restrict__ T, Soa A,
                                                 const int* __restrict__ nbr,
-                                                const int* __restrict__ ncount, const int2* __restrict__ hdr,
+                                                const int* __restrict__ ncount,
                                                 const int* __restrict__ lhdr, PassAOut pout,
                                                 const DevState* __restrict__ st)
 {
@@ -2043,19 +1767,6 @@ __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, cons
     const bool ghost = live && P.slab_axis >= 0 && A.id[ii] < 0;
     if (ghost && pout.rec) pout.rec[i] = make_double4(xi, yi, zi, 0.0);
     const bool own = live && !ghost;
-    const int2* h = hdr ? hdr + (size_t)(i >> 6) * kSegHdr : nullptr;
-    if (MPH_SEG && h && h[kSegCols].x == 1) {   // wave-uniform: this wave's list is column-segmented
-        __shared__ double2 stage[kWB][3 * MPH_LDS_CAP];
-        double vxi, vyi, vzi;
-        own_velocity(A, ii, vxi, vyi, vzi);
-        const int ti = A.type[ii];
-        const bool solid = dev_is_struct(ti);
-        PassA o;
-        pass_a_seg<DIM>(P, s_ratio, s_mu, A, seg_tile(nbr, i), h, own, ti, solid, xi, yi, zi, vxi, vyi,
-                        vzi, o, stage[threadIdx.x >> 6]);
-        if (own) pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
-        return;
-    }
     // the search's rule (its list order and the fast minimum image go together)
     const bool fast = wave_search_interior(P, st, own, xi, yi, zi);
     if (!own) return;
@@ -2081,281 +1792,6 @@ __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, cons
     else
         pass_a_loop<false, false, DIM, false>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
     pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
-}
-
-// ------------------------------------------------------------- fused search + pass A -------
-
-// calculateNeighbor (main.cpp:1743-1810) and the pass-A sums of the same step (DensityA 2141,
-// GravityCenter 2174, DensityP 2314, DivergenceP 2343, PhysicalCoefficients 2099, the pressure
-// values 2384 / 2218, the P_i half of the pressure force 2394 and the viscous force 2478) in one
-// kernel.  The interior search already stages every stencil column's window of the wave in LDS;
-// here it stages the whole {x, y, z, vx, vy, vz, type} of the window, so a neighbour accepted by
-// the exact test is summed at once from LDS -- pass A's list read and its per-lane gathers of the
-// 48-byte records from L1/L2 (its bound) disappear.  The ELL row is still
-// written for pass B.  The lanes of a wave accept in lockstep on lattice-line cells, but not in a
-// disordered flow, so the sums do not run under the acceptance branch: per column every lane
-// collects its accepted candidates in a 64-bit mask over its own candidate range, then the wave
-// walks the set bits (one per lane per iteration), which costs max over lanes of a column's count
-// instead of the column's candidate count.  Same neighbours in the same order, same FP64
-// expressions: every field is bit-identical to the separate k_neighbors + k_pass_a.
-#ifndef MPH_FUSED
-#define MPH_FUSED 1      // 1: the fused kernel is compiled (selected at run time: MPH_FUSED=1 or
-                         // kFusedDefault, which is off); 0: not built at all
-#endif
-#ifndef MPH_FCAP
-#define MPH_FCAP 128     // candidates staged per wave and column (6 + 1 arrays, 52 B each)
-#endif
-#ifndef MPH_FU
-#define MPH_FU 1         // accepted neighbours summed per iteration of the mask walk (2: 56 B/lane of spills at 4 waves)
-#endif
-#ifndef MPH_FSB
-#define MPH_FSB 3   // candidates per batch in the fused search (125 VGPRs, 4 waves per SIMD)
-#endif
-#ifndef MPH_FUSED_DIAG
-#define MPH_FUSED_DIAG 0 // diagnostic builds: 1 = no periodic-face path, 2 = equal-radii sums only
-#endif
-#ifndef MPH_FUSED_WPE
-#define MPH_FUSED_WPE 4  // waves per SIMD (<= 128 VGPRs)
-#endif
-
-struct FusedStage {   // the six arrays consecutive, in this order (fused_lds stages by offset)
-    double x[MPH_FCAP + MPH_FSB], y[MPH_FCAP + MPH_FSB], z[MPH_FCAP + MPH_FSB];
-    double vx[MPH_FCAP + MPH_FSB], vy[MPH_FCAP + MPH_FSB], vz[MPH_FCAP + MPH_FSB];
-    int type[MPH_FCAP + MPH_FSB];
-};
-static_assert(offsetof(FusedStage, vz) == 5 * (MPH_FCAP + MPH_FSB) * sizeof(double), "FusedStage layout");
-
-// The pass-A sums over the accepted candidates of one lane's chunk: bit b of mask = candidate
-// base + b of the staged sub-window (LDS).  Wave-uniform loop while any lane has bits left.
-template <bool EQR, int U = MPH_FU>
-__device__ __forceinline__ void fused_sum_mask(const DevParams& P, const double* s_ratio, const double* s_mu,
-                                               const FusedStage& S, unsigned long long mask, int base, int ti,
-                                               bool solid, double xi, double yi, double zi, double vxi, double vyi,
-                                               double vzi, PassA& o)
-{
-    if (MPH_FUSED_DIAG & 4) return;
-    while (__builtin_amdgcn_ballot_w64(mask != 0ull)) {
-        int t[U];
-        bool v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            v[u] = mask != 0ull;
-            const int b = v[u] ? __ffsll((long long)mask) - 1 : 0;
-            mask &= mask - 1ull;   // 0 stays 0
-            t[u] = base + b;
-        }
-        double X[U], Y[U], Z[U], VX[U], VY[U], VZ[U];
-        int TT[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            X[u] = S.x[t[u]]; Y[u] = S.y[t[u]]; Z[u] = S.z[t[u]];
-            VX[u] = S.vx[t[u]]; VY[u] = S.vy[t[u]]; VZ[u] = S.vz[t[u]];
-            TT[u] = S.type[t[u]];
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const double q0 = image_exact<true>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
-            const double q1 = image_exact<true>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
-            const double q2 = image_exact<true>(Z[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
-            pass_a_term_sel<EQR>(P, s_ratio, s_mu, ti, v[u] ? TT[u] : 0, solid, v[u], q0, q1, q2, VX[u] - vxi,
-                                 VY[u] - vyi, VZ[u] - vzi, o);
-        }
-    }
-}
-
-// The search of an interior wave (scan_candidates_lds: same column ranges, window, acceptance and
-// list order) with the pass-A sums of every accepted neighbour.  Returns the neighbour count.
-template <int DIM, int PERM, bool EQR, int SB = MPH_FSB, int CAP = MPH_FCAP>
-__device__ __forceinline__ int fused_lds(const DevParams& P, const double* s_ratio, const double* s_mu,
-                                         const Soa& A, const int* start, int i, bool act, double xi,
-                                         double yi, double zi, int cx, int cy, int cz, int* out,
-                                         FusedStage& S, int ti, bool solid, double vxi, double vyi,
-                                         double vzi, PassA& o)
-{
-    const int lane = threadIdx.x & 63;
-    const double lo2 = P.rc2_lo, hi2 = P.rc2_hi;
-    using X = CellAxes<DIM, PERM>;
-    int cnt = 0;
-    constexpr int NCOL = DIM == 3 ? kGroups * kGroups : kGroups;
-    const int cc[3] = {cx, cy, cz};
-    const int cca = cc[X::A2];
-    const double rcm2 = P.rc2_trim;
-    const double cw0 = P.cwid[X::A0], cw1 = P.cwid[X::A1];
-    const double uu[3] = {grid_offset(xi, P.corg[0], P.dw[0]), grid_offset(yi, P.corg[1], P.dw[1]),
-                          DIM == 3 ? grid_offset(zi, P.corg[2], P.dw[2]) : 0.0};
-    const double ua = uu[X::A2];
-    const double ginva = P.ginv[X::A2];
-    // per-column candidate range of the lane, as scan_candidates_lds (FP32 bound, rounded outwards)
-    constexpr float kDn = 1.0f - 1.0f / (1 << 20), kUp = 1.0f + 1.0f / (1 << 19);
-    const float rcm2f = (float)rcm2 * kUp;
-    float gx2f = 0.0f;
-    auto col_range = [&](int col, int& jb, int& je) {
-        int base;
-        float d2f;
-        if (DIM == 3) {
-            const int dxc = col / kGroups - kReach, dyc = col % kGroups - kReach;
-            const int c0 = cc[X::A0], c1 = cc[X::A1];
-            if (dyc == -kReach) {
-                const float gx = (float)cell_gap(uu[X::A0], c0, dxc, cw0);
-                gx2f = gx * gx * kDn;
-            }
-            const float gy = (float)cell_gap(uu[X::A1], c1, dyc, cw1);
-            d2f = (gx2f + gy * gy * kDn) * kDn;
-            base = ((c0 + dxc) * P.gc[X::A1] + c1 + dyc) * P.gc[X::A2];
-        } else {
-            const int dxc = col - kReach;
-            const float gx = (float)cell_gap(uu[0], cx, dxc, cw0);
-            d2f = gx * gx * kDn;
-            base = (cx + dxc) * P.gc[1];
-        }
-        jb = 0;
-        je = 0;
-        if (act && d2f <= rcm2f) {
-            const double ra = (double)(__fsqrt_rn(rcm2f - d2f) * kUp);
-            const int lo = (int)fmax(floor((ua - ra) * ginva), (double)(cca - P.sa));
-            const int hi = (int)fmin(floor((ua + ra) * ginva), (double)(cca + P.sa));
-            jb = start[base + lo];
-            je = start[base + hi + 1];
-        }
-    };
-    int nb_jb, nb_je, n2_jb = 0, n2_je = 0;   // columns col + 1 and (MPH_SEARCH_PREFETCH=2) col + 2
-    col_range(0, nb_jb, nb_je);
-    if (MPH_SEARCH_PREFETCH == 2 && NCOL > 1) col_range(1, n2_jb, n2_je);
-    for (int col = 0; col < NCOL; ++col) {
-        const int jb = nb_jb, je = nb_je;
-        if (col + 1 < NCOL) col_range(col + 1, nb_jb, nb_je);
-        const bool any = je > jb;
-        const unsigned long long am = __ballot(any);
-        if (!am) continue;   // wave-uniform: no lane has candidates in this column
-        int mn = __builtin_amdgcn_readlane(jb, __ffsll((long long)am) - 1);
-        int mx = __builtin_amdgcn_readlane(je, 63 - __clzll(am));
-        if (__ballot(any && (jb < mn || je > mx))) {
-            mn = wave_min(any ? jb : 0x7fffffff);
-            mx = wave_max(any ? je : -1);
-        }
-        // the window [mn, mx) in sub-windows of at most CAP candidates, each staged in LDS (one
-        // unless the window is wider: a wave whose lanes straddle two distant cell rows); every
-        // candidate is read from LDS, never from global memory here (a global alternative in the
-        // same loop made the compiler merge the two pointers into flat loads, twice as slow)
-        int nxt = jb;   // the lane's next candidate
-        int w0 = mn;
-        for (;;) {
-            const int w1 = min(w0 + CAP, mx);
-            {
-                // the 48-byte records as one flat run of 16-byte pieces: consecutive lanes load
-                // consecutive pieces (8 cache lines per load instead of the 24 of one record per
-                // lane), each scattered into the SoA arrays x y | z vx | vy vz of FusedStage
-                const double2* src = A.p6 + 3 * (size_t)w0;
-                const int n3 = 3 * (w1 - w0);
-                for (int e = lane; e < n3; e += 64) {
-                    const double2 v = src[e];
-                    const int r = e / 3, part = e - 3 * r;
-                    double* lo = S.x + (size_t)(2 * part) * (CAP + SB) + r;
-                    lo[0] = v.x;
-                    lo[CAP + SB] = v.y;
-                }
-                for (int t = lane; t < w1 - w0; t += 64) S.type[t] = A.type[w0 + t];
-            }
-            __builtin_amdgcn_wave_barrier();
-            // the lane's candidates of this sub-window in chunks of 64 (one mask bit each), each
-            // chunk tested, then its accepted candidates summed
-            const int cend = min(je, w1);
-            for (int c0 = nxt; c0 < cend; c0 += 64) {
-                const int c1 = min(c0 + 64, cend);
-                unsigned long long mask = 0ull;
-                for (int j0 = c0; j0 < c1; j0 += SB) {
-                    double xs[SB], ys[SB], zs[SB];
-                    const int k0 = j0 - w0;   // the staging arrays are padded by SB entries
-#pragma unroll
-                    for (int u = 0; u < SB; ++u) {
-                        xs[u] = S.x[k0 + u]; ys[u] = S.y[k0 + u]; zs[u] = S.z[k0 + u];
-                    }
-#pragma unroll
-                    for (int u = 0; u < SB; ++u) {
-                        const int j = j0 + u;
-                        const bool a = accept_interior(P, xs[u] - xi, ys[u] - yi, zs[u] - zi, lo2, hi2) &
-                                       (j < c1) & (j != i);
-                        if (a) {
-                            list_store(out + min(cnt, kMaxNeighbor - 1) * kTile, nbr_entry(j, S.type[k0 + u]));
-                            mask |= 1ull << (j - c0);
-                            ++cnt;
-                        }
-                    }
-                }
-                fused_sum_mask<EQR>(P, s_ratio, s_mu, S, mask, c0 - w0, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
-            }
-            nxt = max(nxt, cend);
-            __builtin_amdgcn_wave_barrier();   // every lane done reading before the next staging
-            if (w1 >= mx) break;               // wave-uniform
-            w0 = wave_min(nxt < je ? nxt : 0x7fffffff);
-            if (w0 == 0x7fffffff) break;
-        }
-    }
-    return cnt;
-}
-
-template <int DIM, int PERM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MPH_FUSED_WPE))) void k_search_pass_a(
-    DevParams P, const DevTables* __restrict__ T, Soa A, const int* __restrict__ start, int* __restrict__ nbr,
-    int* __restrict__ ncount, DevState* __restrict__ st, PassAOut pout, int* __restrict__ wface)
-{
-    const int n = dev_n(P);
-    if ((int)blockIdx.x >= live_blocks(n)) return;
-    __shared__ double s_ratio[kTypes * kTypes];
-    __shared__ double s_mu[kTypes * kTypes];
-    __shared__ FusedStage stage[4];
-    if (threadIdx.x < kTypes * kTypes) {
-        s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
-        s_mu[threadIdx.x] = T->mu_ij[threadIdx.x] * (-P.cvis * P.cdv * P.vol);   // pass_a_term's viscous factor
-    }
-    __syncthreads();
-    const int i = xcd_block(blockIdx.x, live_blocks(n)) * blockDim.x + threadIdx.x;
-    slab_wave_flag(P, A, i, n, wface);
-    const bool live = i < n;
-    const int ii = live ? i : n - 1;
-    const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
-    if (wave_all_ghosts(P, A, live, ii)) {
-        // slab mode: no list, and the ghosts' pass-A values arrive in the halo (which also fills
-        // the .w of the pass-B record; its position part is written here)
-        if (live) {
-            ncount[i] = 0;
-            if (pout.rec) pout.rec[i] = make_double4(xi, yi, zi, 0.0);
-        }
-        return;
-    }
-    const bool ghost = live && P.slab_axis >= 0 && A.id[ii] < 0;
-    if (ghost && pout.rec) pout.rec[i] = make_double4(xi, yi, zi, 0.0);
-    const bool own = live && !ghost;
-    const bool fast = wave_search_interior(P, st, own, xi, yi, zi);
-    const int cx = cell_axis(xi, P.corg[0], P.dw[0], P.ginv[0], P.gc[0]);
-    const int cy = cell_axis(yi, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
-    const int cz = DIM == 3 ? cell_axis(zi, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
-    int* out = nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
-    double vxi, vyi, vzi;
-    own_velocity(A, ii, vxi, vyi, vzi);
-    const int ti = A.type[ii];
-    const bool solid = dev_is_struct(ti);
-    PassA o;
-    int cnt = 0;
-    if (fast) {
-        FusedStage& S = stage[threadIdx.x >> 6];
-        cnt = (MPH_FUSED_DIAG & 2) || pass_a_equal_radii(P)
-                  ? fused_lds<DIM, PERM, true>(P, s_ratio, s_mu, A, start, i, own, xi, yi, zi, cx, cy, cz, out, S,
-                                               ti, solid, vxi, vyi, vzi, o)
-                  : fused_lds<DIM, PERM, false>(P, s_ratio, s_mu, A, start, i, own, xi, yi, zi, cx, cy, cz, out, S,
-                                                ti, solid, vxi, vyi, vzi, o);
-    } else if (own && !(MPH_FUSED_DIAG & 1)) {
-        // a wave near a periodic face: the search with per-lane gathers and the general minimum
-        // image, then pass A over the lane's own fresh list row (written by this lane just above)
-        cnt = scan_candidates<DIM, false, PERM>(P, A, start, i, xi, yi, zi, cx, cy, cz, out);
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-        const NbrList NL = nbr_list(nbr, nullptr, i, nullptr);
-        pass_a_loop<false, false, DIM, false, 2>(P, s_ratio, s_mu, A, NL, min(cnt, kMaxNeighbor), ti, solid, xi, yi,
-                                              zi, vxi, vyi, vzi, o);
-    }
-    if (live) ncount[i] = cnt;
-    if (cnt > kMaxNeighbor) atomicOr(&st->overflow, 1);   // main.cpp:1766-1768
-    if (own) pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
 }
 
 // Displacement u = Mod(x - x0 + W/2, W) - W/2 of calculateElasticDeformationVector (2700-2712),
@@ -2474,77 +1910,6 @@ __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_
     }
 }
 
-// Pass B over a column-segmented list (interior waves): the 32-byte records {x, y, z, P} of each
-// column window staged in LDS (pass_a_seg); wide columns gather from global memory.
-template <bool SURF, int DIM, int U = MPH_UB, int CAP = MPH_LDS_CAP>
-__device__ __forceinline__ void pass_b_seg(const DevParams& P, const double* s_ratio, const double4* rec,
-                                           const double* gx, const double* gy, const double* gz,
-                                           const double* pa, const unsigned short* seg, const int2* hdr,
-                                           bool live, int ti, bool solid, double xi, double yi, double zi,
-                                           double gxi, double gyi, double gzi, double pai, double ai,
-                                           double& f0, double& f1, double& f2, double4* stage)
-{
-    constexpr int NCOL = DIM == 3 ? 25 : 5;
-    const double dscale = P.rg_r2g * (P.vol / P.dx);
-    const double cpv = P.cdp * P.vol;
-    const int lane = threadIdx.x & 63;
-    int slot = 0;
-    for (int col = 0; col < NCOL; ++col) {
-        const int2 h = hdr[col];
-        const int w = (h.y >> 16) & 0x7FFF;
-        if (w == 0) continue;
-        const int mn = h.x;
-        if (h.y >= 0) {
-            const int span = h.y & 0xFFFF;
-            for (int t = lane; t < span; t += 64) stage[t] = rec[mn + t];
-            __builtin_amdgcn_wave_barrier();
-            for (int k0 = 0; k0 < w; k0 += U) {
-                unsigned e[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    e[u] = k0 + u < w ? seg[(size_t)min(slot + k0 + u, kSegCap - 1) * kTile + lane] : kSegNone;
-                double4 R[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) R[u] = stage[e[u] == kSegNone ? 0 : (int)(e[u] & 0xFF)];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    if (!live || e[u] == kSegNone) continue;
-                    pass_b_term<true, SURF, DIM>(P, s_ratio, gx, gy, gz, pa, mn + (int)(e[u] & 0xFF),
-                                                 (int)((e[u] >> 8) & 7), R[u].x, R[u].y, R[u].z, R[u].w, ti, solid,
-                                                 xi, yi, zi, gxi, gyi, gzi, pai, ai, dscale, cpv, f0, f1, f2);
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            slot += w;
-        } else {
-            for (int k0 = 0; k0 < w; k0 += U) {
-                int jj[U], TT[U];
-                bool ok[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int sl = min(slot + 2 * (k0 + u), kSegCap - 2);
-                    const unsigned lo = k0 + u < w ? seg[(size_t)sl * kTile + lane] : 0u;
-                    const unsigned hi = k0 + u < w ? seg[(size_t)(sl + 1) * kTile + lane] : kSegNone;
-                    ok[u] = hi != kSegNone;
-                    jj[u] = ok[u] ? (int)(lo | ((hi & 0xFFF) << 16)) : mn;
-                    TT[u] = (int)(hi >> 12) & 7;
-                }
-                double4 R[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) R[u] = rec[jj[u]];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    if (!live || !ok[u]) continue;
-                    pass_b_term<true, SURF, DIM>(P, s_ratio, gx, gy, gz, pa, jj[u], TT[u], R[u].x, R[u].y, R[u].z,
-                                                 R[u].w, ti, solid, xi, yi, zi, gxi, gyi, gzi, pai, ai, dscale, cpv,
-                                                 f0, f1, f2);
-                }
-            }
-            slot += 2 * w;
-        }
-    }
-}
-
 // Pair forces of PressureP (2394-2424), PressureA (2225-2258), DiffuseInterface (2261-2312),
 // ViscosityV (2478-2522) for non-structure i; InterfaceForce (2439-2472) for structure i; then
 // Gravity (2917-2936), Acceleration/kick (2938-2956) and Convection/drift (1892-1907).  The sums
@@ -2567,7 +1932,7 @@ __global__ __launch_bounds__(MPH_LB) MPH_PB_ATTR void k_pass_b(DevParams P, cons
                                                 const double* __restrict__ gz,
                                                 const double* __restrict__ pa,
                                                 const int* __restrict__ nbr,
-                                                const int* __restrict__ ncount, const int2* __restrict__ hdr,
+                                                const int* __restrict__ ncount,
                                                 const int* __restrict__ lhdr,
                                                 double4* __restrict__ force, double4* __restrict__ acc,
                                                 Soa B, int phase, int* __restrict__ wface, StructHook H,
@@ -2602,21 +1967,8 @@ __global__ __launch_bounds__(MPH_LB) MPH_PB_ATTR void k_pass_b(DevParams P, cons
         B.id[i] = A.id[i];
         live = false;
     }
-    if (phase) {
-        // slab mode: phase 1 = the waves without a particle near a face (run while the halo of
-        // pass-A values is in flight; also the waves of ghosts only), phase 2 = the rest, after the
-        // halo arrived -- split by whole waves (wface, written by the search), so that no wave runs
-        // its list loop twice
-        const int f = wface[__builtin_amdgcn_readfirstlane(i >> 6)];
-        if (phase == 1 ? f != 0 : f == 0) return;
-    }
-    if (wave_all_ghosts(P, A, live, ii)) {
-        if (live) B.id[i] = A.id[i];
-        return;
-    }    const int2* h = hdr ? hdr + (size_t)(i >> 6) * kSegHdr : nullptr;
-    const bool segmented = MPH_SEG && h && h[kSegCols].x == 1;   // wave-uniform
-    const bool fast = segmented || wave_search_interior(P, st, live, xi, yi, zi);
-    if (!segmented && !live) return;
+    const bool fast = wave_search_interior(P, st, live, xi, yi, zi);
+    if (!live) return;
     const int ti = A.type[ii];
     const bool solid = dev_is_struct(ti);
     const double4 fp = fpart[ii];
@@ -2626,26 +1978,18 @@ __global__ __launch_bounds__(MPH_LB) MPH_PB_ATTR void k_pass_b(DevParams P, cons
         gxi = gx[ii]; gyi = gy[ii]; gzi = gz[ii]; pai = pa[ii];
         ai = T->cofa[ti] * P.cofk * P.cofk;
     }
-    if (segmented) {
-        // every lane of the wave stages; the lanes without a particle of this phase only help
-        __shared__ double4 stage[kWB][MPH_LDS_CAP];
-        pass_b_seg<SURF, DIM>(P, s_ratio, rec, gx, gy, gz, pa, seg_tile(nbr, i), h, live, ti, solid, xi, yi, zi,
-                              gxi, gyi, gzi, pai, ai, f0, f1, f2, stage[threadIdx.x >> 6]);
-        if (!live) return;
-    } else {
-        const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
-        __shared__ int s_gb[kWB][8];
-        const NbrList NL = nbr_list(nbr, lhdr, i, s_gb[threadIdx.x >> 6]);
-        if (NL.c16)   // compact lists come from interior searches only
-            pass_b_loop<true, true, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, NL, cnt, ti, solid, xi,
-                                               yi, zi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
-        else if (fast)
-            pass_b_loop<true, false, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, NL, cnt, ti, solid, xi,
-                                                yi, zi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
-        else
-            pass_b_loop<false, false, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, NL, cnt, ti, solid, xi,
-                                                 yi, zi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
-    }
+    const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
+    __shared__ int s_gb[kWB][8];
+    const NbrList NL = nbr_list(nbr, lhdr, i, s_gb[threadIdx.x >> 6]);
+    if (NL.c16)   // compact lists come from interior searches only
+        pass_b_loop<true, true, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, NL, cnt, ti, solid, xi, yi,
+                                           zi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
+    else if (fast)
+        pass_b_loop<true, false, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, NL, cnt, ti, solid, xi, yi,
+                                            zi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
+    else
+        pass_b_loop<false, false, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, NL, cnt, ti, solid, xi, yi,
+                                             zi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
     double vxi, vyi, vzi;
     own_velocity(A, i, vxi, vyi, vzi);
     double vo0 = vxi, vo1 = vyi, vo2 = vzi;
@@ -2705,7 +2049,7 @@ __global__ __launch_bounds__(256) void k_virial(DevParams P, const DevTables* __
                                                 const double* __restrict__ pres, const double* __restrict__ pa,
                                                 const double* __restrict__ gx, const double* __restrict__ gy,
                                                 const double* __restrict__ gz, const int* __restrict__ nbr,
-                                                const int* __restrict__ ncount, const int2* __restrict__ hdr,
+                                                const int* __restrict__ ncount,
                                                 const int* __restrict__ lhdr,
                                                 double* __restrict__ vir, double* __restrict__ vpres)
 {
@@ -2723,46 +2067,17 @@ __global__ __launch_bounds__(256) void k_virial(DevParams P, const DevTables* __
     double S[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
     const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
     const int* row = ell_row(nbr, i);
-    // either list format (the neighbours come in the same order): ELL row, or the lane's column
-    // segments decoded per entry
-    const int2* h = hdr ? hdr + (size_t)(i >> 6) * kSegHdr : nullptr;
-    const bool segmented = MPH_SEG && h && h[kSegCols].x == 1;
-    const unsigned short* seg = seg_tile(nbr, i);
-    const int lane = i & 63;
+    // either list format (the neighbours come in the same order): ELL row or compact entries
     __shared__ int s_gb[4][8];
     const NbrList NL = nbr_list(nbr, lhdr, i, s_gb[threadIdx.x >> 6]);
-    int col = 0, slot = 0, used = 0;
     for (int k = 0; k < cnt; ++k) {
         int j, tj;
         if (NL.c16) {
             nbr_at<true>(NL, k, j, tj);
-        } else if (!segmented) {
+        } else {
             const int e = row[k * kTile];
             j = e & kIndexMask;
             tj = e >> kTypeShift;
-        } else {
-            // next real entry of this lane: walk the segments (padding skipped)
-            for (;;) {
-                const int2 hc = h[col];
-                const int w = (hc.y >> 16) & 0x7FFF;
-                const bool wide = hc.y < 0;
-                if (used >= w) { slot += wide ? 2 * w : w; used = 0; ++col; continue; }
-                if (wide) {
-                    const unsigned lo = seg[(size_t)(slot + 2 * used) * kTile + lane];
-                    const unsigned hi = seg[(size_t)(slot + 2 * used + 1) * kTile + lane];
-                    ++used;
-                    if (hi == kSegNone) continue;
-                    j = (int)(lo | ((hi & 0xFFF) << 16));
-                    tj = (int)(hi >> 12) & 7;
-                } else {
-                    const unsigned e = seg[(size_t)(slot + used) * kTile + lane];
-                    ++used;
-                    if (e == kSegNone) continue;
-                    j = hc.x + (int)(e & 0xFF);
-                    tj = (int)(e >> 8) & 7;
-                }
-                break;
-            }
         }
         double q[3];
         q[0] = image_exact<false>(B.x[j] - xi, P.dw[0], P.hw[0], P.w075[0]);
@@ -3641,12 +2956,9 @@ __global__ __launch_bounds__(256) void k_halo_unpack(const double* __restrict__ 
 static inline int blocks(int n, int t) { return (n + t - 1) / t; }
 
 // Grid of the two list passes: the XCD map (list_block) needs a multiple of 8 blocks, with 25 %
-// slack for its unequal ranges
-// below this many particles the split kernel's ~7 us costs more than the balance gains (Bar 400k,
-// 0.23 ms per step: 1.76e9 p-steps/s with it, 1.80e9 without); the passes then keep the equal
-// ranges.  The full-size parity tests (D1M, FSI, the D16M slabs) run the balanced map
-constexpr int kXcdBalMin = 1 << 20;
-
+// slack for its unequal ranges.  Below Launch.xcd_bal_min particles (default 2^20) the split
+// kernel's ~7 us costs more than the balance gains (Bar 400k, 0.23 ms per step: 1.76e9 p-steps/s
+// with it, 1.80e9 without), so the passes keep the equal ranges and the search feeds no histogram.
 static inline int list_grid(int n)
 {
     const int nb = blocks(n, MPH_LB);
@@ -3706,16 +3018,20 @@ void launch_neighbors(const Launch& L)
     if (P.n == 0) return;
     // the second launch (REDO) only when compact lists are on; its waves exit at once unless the
     // first marked them
+    const int bal = MPH_XCD_BAL && P.n >= L.xcd_bal_min;
 #define MPH_NEIGHBORS(D, PERM)                                                                               \
     do {                                                                                                     \
-        MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM>), dim3(blocks(P.n, MPH_LB)), dim3(MPH_LB), 0, \
-                   L.stream, P, L.A, L.start, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, L.st,    \
-                   L.wface);                                                                                \
-        if (MPH_XCD_BAL && P.n >= kXcdBalMin)                                                                \
-            MPH_LAUNCH("xcd_split", L.stream, k_xcd_split, dim3(1), dim3(kXcdSplitThreads), 0, L.stream, L.st);     \
         if (L.lhdr)                                                                                          \
-            MPH_LAUNCH("neighbors_redo", L.stream, (k_neighbors_redo<D, PERM>), dim3(1),                  \
-                       dim3(256), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.lhdr, L.st);            \
+            MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM, true>), dim3(blocks(P.n, MPH_LB)),        \
+                       dim3(MPH_LB), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.lhdr, L.st, L.wface, bal); \
+        else                                                                                                 \
+            MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM, false>), dim3(blocks(P.n, MPH_LB)),       \
+                       dim3(MPH_LB), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.lhdr, L.st, L.wface, bal); \
+        if (bal)                                                                                             \
+            MPH_LAUNCH("xcd_split", L.stream, k_xcd_split, dim3(1), dim3(kXcdSplitThreads), 0, L.stream, L.st); \
+        if (L.lhdr)                                                                                          \
+            MPH_LAUNCH("neighbors_redo", L.stream, (k_neighbors_redo<D, PERM>), dim3(1),                     \
+                       dim3(256), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.lhdr, L.st);               \
     } while (0)
     if (P.dim == 3) {
         switch (P.perm) {
@@ -3739,40 +3055,17 @@ void launch_pass_a(const Launch& L)
     const PassAOut po = pass_a_out(L);
     if (P.dim == 3)
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<3>, dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, po, L.st);
+                   L.A, L.nbr, L.ncount, L.lhdr, po, L.st);
     else
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<2>, dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, po, L.st);
+                   L.A, L.nbr, L.ncount, L.lhdr, po, L.st);
 }
 
-// calculateNeighbor + the pass-A sums: the fused kernel (k_search_pass_a) when the list is the
-// 32-bit ELL row (not the opt-in compact format) and MPH_FUSED is not 0, else the two kernels
+// calculateNeighbor + the pass-A sums (the search, the XCD split of the passes, pass A)
 void launch_search_pass_a(const Launch& L)
 {
-    Profiler* prof = L.prof;
-    const DevParams& P = *L.P;
-    if (P.n == 0) return;
-    if (!L.fused || L.lhdr || MPH_SEG) {
-        launch_neighbors(L);
-        launch_pass_a(L);
-        return;
-    }
-    const PassAOut po = pass_a_out(L);
-#define MPH_FUSED_LAUNCH(D, PERM)                                                                         \
-    MPH_LAUNCH("search_pass_a", L.stream, (k_search_pass_a<D, PERM>), dim3(blocks(P.n, 256)), dim3(256), 0, \
-               L.stream, P, L.T, L.A, L.start, L.nbr, L.ncount, L.st, po, L.wface)
-    if (P.dim == 3) {
-        switch (P.perm) {
-        case 1: MPH_FUSED_LAUNCH(3, 1); break;
-        case 2: MPH_FUSED_LAUNCH(3, 2); break;
-        case 3: MPH_FUSED_LAUNCH(3, 3); break;
-        case 4: MPH_FUSED_LAUNCH(3, 4); break;
-        default: MPH_FUSED_LAUNCH(3, 0); break;
-        }
-    } else {
-        MPH_FUSED_LAUNCH(2, 0);
-    }
-#undef MPH_FUSED_LAUNCH
+    launch_neighbors(L);
+    launch_pass_a(L);
 }
 
 static StructHook struct_hook(const Launch& L)
@@ -3802,7 +3095,7 @@ void launch_pass_b(const Launch& L, int phase)
     }
 #define MPH_PASS_B(S, D)                                                                            \
     MPH_LAUNCH(phase == 2 ? "pass_b_face" : "pass_b", L.stream, (k_pass_b<S, D>), dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P, \
-               L.T, L.A, L.rec, L.fpart, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, L.force, L.acc, L.B, \
+               L.T, L.A, L.rec, L.fpart, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, L.lhdr, L.force, L.acc, L.B, \
                phase, L.wface, \
                struct_hook(L), L.st)
     if (P.surface) {
@@ -3820,10 +3113,10 @@ void launch_virial(const Launch& L, const Soa& X, double* vir, double* vpres)
     if (P.n == 0) return;
     if (P.dim == 3)
         MPH_LAUNCH("virial", L.stream, k_virial<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T, L.A, X,
-                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, vir, vpres);
+                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, L.lhdr, vir, vpres);
     else
         MPH_LAUNCH("virial", L.stream, k_virial<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T, L.A, X,
-                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, MPH_SEG ? L.hdr : nullptr, L.lhdr, vir, vpres);
+                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, L.lhdr, vir, vpres);
 }
 
 // lanes per structure slot: one lane per slot while the launch has >= kStructLanesTarget lanes

@@ -18,6 +18,8 @@
 // single-GPU run writes, with the same cadence.
 #include <fcntl.h>
 #include <poll.h>
+#include <signal.h>
+#include <sys/prctl.h>
 #include <sys/socket.h>
 #include <sys/wait.h>
 #include <unistd.h>
@@ -33,6 +35,7 @@
 #include <vector>
 
 #include <hip/hip_runtime_api.h>
+#include <roctracer/roctx.h>
 
 #include "../../include/mph_gpu.h"
 
@@ -53,10 +56,47 @@ static void logf(const char* fmt, ...)
     if (g_log) fflush(g_log);
 }
 
+// ---- slab ranks: failure propagation ---------------------------------------------------------
+// A rank that fails must not leave the others blocked in RCCL (no timeout there) or orphaned on
+// their GPUs.  Children die with rank 0 (PR_SET_PDEATHSIG); rank 0 reaps children from a SIGCHLD
+// handler and, on any non-zero or abnormal exit, kills the remaining ranks and exits 1 itself --
+// from the handler, since rank 0 may be blocked inside a collective with the dead rank.
+static constexpr int kMaxRanks = 64;
+static pid_t g_child_pid[kMaxRanks];
+static volatile sig_atomic_t g_child_done[kMaxRanks];   // 0 running, 1 exited 0, 2 failed
+static volatile sig_atomic_t g_nchildren = 0;
+
+static void kill_children()
+{
+    for (int k = 0; k < g_nchildren; ++k)
+        if (g_child_done[k] == 0 && g_child_pid[k] > 0) kill(g_child_pid[k], SIGKILL);
+}
+
+static void on_sigchld(int)
+{
+    const int saved = errno;
+    for (;;) {
+        int st = 0;
+        const pid_t pid = waitpid(-1, &st, WNOHANG);
+        if (pid <= 0) break;
+        const bool ok = WIFEXITED(st) && WEXITSTATUS(st) == 0;
+        for (int k = 0; k < g_nchildren; ++k)
+            if (g_child_pid[k] == pid) g_child_done[k] = ok ? 1 : 2;
+        if (!ok) {
+            static const char msg[] = "error: a slab rank failed; stopping the other ranks\n";
+            (void)!write(2, msg, sizeof(msg) - 1);
+            kill_children();
+            _exit(1);
+        }
+    }
+    errno = saved;
+}
+
 static void die(MphCtx* c, int rc, const char* what)
 {
     g_quiet = false;
     logf("error: %s failed (%d): %s\n", what, rc, c ? mph_last_error(c) : "");
+    kill_children();   // rank 0: the other ranks would wait for it forever (children: none)
     std::exit(1);
 }
 
@@ -145,13 +185,37 @@ static int spawn_ranks(SlabRank& R, int n, bool host)
         for (int r = 1; r < n; ++r)
             if (pipe(&pipes[2 * r]) != 0) return -1;
     std::fflush(nullptr);
+    if (n > kMaxRanks) return -1;
+    struct sigaction sa {};
+    sa.sa_handler = on_sigchld;
+    sigemptyset(&sa.sa_mask);
+    sa.sa_flags = SA_RESTART | SA_NOCLDSTOP;
+    if (sigaction(SIGCHLD, &sa, nullptr) != 0) return -1;
+    // children are registered with SIGCHLD blocked, so the handler never sees a pid it cannot match
+    sigset_t blk, old;
+    sigemptyset(&blk);
+    sigaddset(&blk, SIGCHLD);
+    sigprocmask(SIG_BLOCK, &blk, &old);
+    const pid_t parent = getpid();
     int me = 0;
     for (int r = 1; r < n; ++r) {
         const pid_t pid = fork();
-        if (pid < 0) return -1;
-        if (pid == 0) { me = r; R.children.clear(); break; }
+        if (pid < 0) { sigprocmask(SIG_SETMASK, &old, nullptr); kill_children(); return -1; }
+        if (pid == 0) {
+            me = r;
+            R.children.clear();
+            g_nchildren = 0;
+            signal(SIGCHLD, SIG_DFL);
+            prctl(PR_SET_PDEATHSIG, SIGKILL);   // rank 0 gone: this rank goes too
+            if (getppid() != parent) _exit(1);  // (it died before the line above)
+            break;
+        }
         R.children.push_back(pid);
+        g_child_pid[g_nchildren] = pid;
+        g_child_done[g_nchildren] = 0;
+        g_nchildren = g_nchildren + 1;
     }
+    sigprocmask(SIG_SETMASK, &old, nullptr);
     R.rank = me;
     if (host) {
         R.right_fd = link[2 * me];
@@ -272,6 +336,14 @@ int main(int argc, char** argv)
         time_t t = time(nullptr);
         logf("start main roop at %s\n", ctime(&t));
     }
+    // the reference's timing buckets (main.cpp:695-700) from HIP events in the step graphs
+    // (single GPU; MPH_PHASE_TIMING=0 turns them off)
+    const bool phases = nslabs == 1 && !(std::getenv("MPH_PHASE_TIMING") && std::atoi(std::getenv("MPH_PHASE_TIMING")) == 0);
+    if (phases) {
+        rc = mph_phase_timing(ctx, 1);
+        if (rc) die(ctx, rc, "mph_phase_timing");
+    }
+    const auto loop_t0 = std::chrono::steady_clock::now();
     double time_now = cfg.time;
     const double dt = cfg.dt;
     int istep = (int)(time_now / dt);
@@ -283,7 +355,9 @@ int main(int argc, char** argv)
     while (time_now < cfg.end_time + 1.0e-5 * dt) {
         if (time_now + 1.0e-5 * dt >= out_next) {
             std::snprintf(name, sizeof(name), prof.c_str(), istep);
+            roctxRangePushA("write_prof");
             rc = mph_write_prof(ctx, name);
+            roctxRangePop();
             if (rc) die(ctx, rc, "writing a .prof file");
             logf("@ Prof Output Time : %e\n", time_now);
             out_next += cfg.output_interval;
@@ -299,15 +373,23 @@ int main(int argc, char** argv)
             if (t + 1.0e-5 * dt >= out_next || !(t < cfg.end_time + 1.0e-5 * dt)) break;
         }
         const auto t0 = std::chrono::steady_clock::now();
+        roctxRangePushA("mph_step");
         rc = mph_step(ctx, k);
         if (rc) die(ctx, rc, "mph_step");
         mph_synchronize(ctx);
+        roctxRangePop();
+        // fault injection for the failure-propagation test (tests/test_gpu_driver.py): this rank
+        // fails after its first batch
+        if (const char* f = std::getenv("MPH_FAIL_RANK"))
+            if (nslabs > 1 && std::atoi(f) == R.rank) die(ctx, MPH_ERR_ARG, "MPH_FAIL_RANK fault injection");
         loop_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         steps_run += k;
         for (int s = 0; s < k; ++s) {
             if (vtk_after && s == k - 1) {
                 // main.cpp:672-673: the virial diagnostic runs before every VTK write
+                roctxRangePushA("virial");
                 rc = mph_compute_virial(ctx);
+                roctxRangePop();
                 if (rc) die(ctx, rc, "mph_compute_virial");
                 std::snprintf(name, sizeof(name), vtk.c_str(), istep);
                 // formatted and written by a background thread while the next steps run
@@ -321,8 +403,23 @@ int main(int argc, char** argv)
         }
     }
     {
+        const double total_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - loop_t0).count();
         time_t t = time(nullptr);
         logf("end main roop at %s\n", ctime(&t));
+        if (phases) {
+            // main.cpp:695-700, in GPU seconds from HIP events; "other" is the rest of the loop's
+            // wall time (file output, host work, launch gaps)
+            double ph[3] = {0.0, 0.0, 0.0};
+            mph_phase_times(ctx, ph);
+            const double nb = ph[0] * 1e-3, ex = ph[1] * 1e-3, vi = ph[2] * 1e-3;
+            const double other = total_s - nb - ex - vi;
+            logf("neighbor search:         %lf [GPU sec]\n", nb);
+            logf("explicit calculation:    %lf [GPU sec]\n", ex);
+            logf("virial calculation:      %lf [GPU sec]\n", vi);
+            logf("other calculation:       %lf [sec]\n", other);
+            logf("total:                   %lf [sec]\n", nb + ex + vi + other);
+            logf("total (check):           %lf [sec]\n", total_s);
+        }
         logf("step loop (wall):        %lf [sec] for %lld steps\n", loop_s, steps_run);
         if (loop_s > 0)
             logf("throughput:              %e [particle-steps/sec]\n", (double)n * steps_run / loop_s);
@@ -331,11 +428,12 @@ int main(int argc, char** argv)
     if (rc) die(ctx, rc, "writing a .vtk file");
     mph_destroy(ctx);
     if (g_log) std::fclose(g_log);
-    // rank 0 waits for the other ranks and fails if any did
-    int status = 0;
-    for (pid_t pid : R.children) {
-        int st = 0;
-        if (waitpid(pid, &st, 0) < 0 || !WIFEXITED(st) || WEXITSTATUS(st) != 0) status = 1;
+    // rank 0 waits for the other ranks (the SIGCHLD handler reaps them and ends the run if one failed)
+    for (;;) {
+        bool running = false;
+        for (int k = 0; k < g_nchildren; ++k) running = running || g_child_done[k] == 0;
+        if (!running) break;
+        usleep(1000);
     }
-    return status;
+    return 0;
 }

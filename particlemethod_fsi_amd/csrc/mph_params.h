@@ -38,9 +38,6 @@ constexpr int kGroups = 2 * kReach + 1;   // compact-list groups: one per slowes
 constexpr int kTypeShift = 28;
 constexpr int kIndexMask = (1 << kTypeShift) - 1;
 constexpr int kPad = 8;         // extra elements behind every per-particle array (vector over-reads)
-// per-wave header of the column-segmented neighbour list (mph_kernels.hip, MPH_SEG): one entry per
-// stencil column (25 in 3-D) plus the list format
-constexpr int kSegHdr = 26;
 // Compact neighbour list of a wavefront (mph_kernels.hip, MPH_LIST16): ints per wave header --
 // kGroups (<= 7) group bases, the format flag at kHdrFlag, then the 64 lanes' group ends: the
 // ends of groups 0-3 (4 bytes) at [8 + lane], of groups 4-5 at [8 + 64 + lane]
@@ -52,12 +49,6 @@ constexpr int kHdrFlag = 7;
 #define MPH_LIST_COMPACT (MPH_R == 2)
 #endif
 constexpr bool kListCompact = MPH_LIST_COMPACT;
-// search + pass A fused into one kernel (k_search_pass_a): measured slower
-// (D1M 1.05 ms against 0.39 + 0.32 ms for the two kernels), so opt-in (MPH_FUSED=1); bit-identical
-#ifndef MPH_FUSED_DEFAULT
-#define MPH_FUSED_DEFAULT 0
-#endif
-constexpr bool kFusedDefault = MPH_FUSED_DEFAULT;
 constexpr int kLhdr = 8 + 2 * 64;
 static_assert(kGroups <= kHdrFlag, "group bases overlap the format flag");
 

@@ -56,7 +56,7 @@ EXPORTED_SYMBOLS = [
     "mph_config_sizeof", "mph_write_vtk_async", "mph_output_wait", "mph_write_grid_binary",
     "mph_write_vtu_arrays", "mph_write_vtu", "mph_velocity_profile_arrays",
     "mph_set_initial_velocity_profile", "mph_dist_info", "mph_create_slab", "mph_slab_window",
-    "mph_list_formats", "mph_abi_version",
+    "mph_list_formats", "mph_abi_version", "mph_phase_timing", "mph_phase_times",
 ]
 
 ABI_VERSION = 3   # MPH_ABI_VERSION of include/mph_gpu.h that these bindings follow
@@ -150,6 +150,8 @@ def load_library() -> ctypes.CDLL:
         "mph_list_formats": (ip, [vp, vp]),
         "mph_create_slab": (ip, [ctypes.POINTER(vp), cfgp, ip, vp, vp, vp, vp, ip, ctypes.POINTER(MphSlabOptions)]),
         "mph_slab_window": (ip, [cfgp, ip, ip, ip, vp, vp]),
+        "mph_phase_timing": (ip, [vp, ip]),
+        "mph_phase_times": (ip, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -414,6 +416,18 @@ class MphSolver:
             nm = raw[32 * i:32 * (i + 1)].split(b"\0", 1)[0].decode()
             out[nm] = {"avg_ms": float(avg[i]), "launches": int(cnt[i])}
         return out
+
+    def phase_timing(self, on: bool = True):
+        """Record HIP events at every step's phase boundaries inside the step graphs (the
+        reference's clock() buckets, main.cpp:695-700); read the sums with phase_times()."""
+        _check(self._L.mph_phase_timing(self._h, 1 if on else 0), self._h)
+
+    def phase_times(self) -> dict:
+        """Accumulated GPU milliseconds: neighbour search (sort + search), explicit calculation
+        (sums, integration, elastic substeps), virial."""
+        a = np.zeros(3)
+        _check(self._L.mph_phase_times(self._h, a.ctypes.data), self._h)
+        return {"neighbor_ms": float(a[0]), "explicit_ms": float(a[1]), "virial_ms": float(a[2])}
 
     def owned_ids(self) -> np.ndarray:
         """Original indices of the particles this context owns (all of them without a slab)."""

@@ -21,7 +21,8 @@ from particlemethod_fsi_amd import mphio
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
-ORACLE_LIB = os.path.join(ORACLE_DIR, "_build", "libmph_oracle.so")
+# MPH_ORACLE_LIB: an alternative build of the same source (the 128-entry rows of oracle128)
+ORACLE_LIB = os.environ.get("MPH_ORACLE_LIB") or os.path.join(ORACLE_DIR, "_build", "libmph_oracle.so")
 REF_DIR = os.path.join(ORACLE_DIR, "_ref")
 
 VEC3 = {"Position", "InitialPosition", "Velocity", "Force", "Acceleration", "GravityCenter"}

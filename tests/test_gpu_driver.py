@@ -144,6 +144,16 @@ def test_driver_matches_reference_executable(tmp_path, case):
     for f in files_ref:
         if f != "output.vtk":
             compare_numeric(os.path.join(dg, f), os.path.join(dr, f))
+    # the reference's timing report (main.cpp:695-700): the same four buckets and two totals, from
+    # HIP events in the step graphs (GPU seconds) and the loop's wall time
+    log = open(os.path.join(dg, "dam.log")).read()
+    vals = {}
+    for key in ("neighbor search:", "explicit calculation:", "virial calculation:", "other calculation:",
+                "total:", "total (check):"):
+        line = next(ln for ln in log.splitlines() if ln.startswith(key))
+        vals[key] = float(line[len(key):].split()[0])
+    assert vals["neighbor search:"] > 0 and vals["explicit calculation:"] > 0 and vals["virial calculation:"] > 0
+    assert abs(vals["total:"] - vals["total (check):"]) < 1e-3, vals
 
 
 # case -> (MPH_DIM, MPH_MODULE, slab ranks) of the multi-rank driver runs
@@ -179,3 +189,23 @@ def test_driver_slab_ranks_match_single_gpu(tmp_path, case):
             compare_numeric(os.path.join(dn, f), os.path.join(d1, f))
     print("%s: %d of %d files byte-identical" % (case, identical, len(files_one)))
     assert identical >= 2   # output.vtk and the first .prof at least
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fail_rank", ["1", "0"])
+def test_driver_slab_rank_failure_ends_the_run(tmp_path, fail_rank):
+    """A slab rank that fails mid-run ends the whole run with a non-zero status instead of leaving
+    the others blocked in their exchange: rank 1 failing makes rank 0 kill the other
+    ranks and exit 1 (SIGCHLD); rank 0 failing takes the other ranks down with it
+    (PR_SET_PDEATHSIG).  Either way every process holding the output pipes is gone within the
+    timeout (subprocess.run waits for the pipes' EOF)."""
+    assert os.path.exists(DRIVER), "mph_explicit not built"
+    d = str(tmp_path / "fail")
+    os.makedirs(d)
+    write_case(d, "dam2d")
+    env = dict(os.environ, MPH_DIM="2", MPH_MODULE="bar", MPH_SLABS="3", MPH_SLAB_TRANSPORT="host",
+               MPH_SLAB_SHARE_DEVICE="1", MPH_FAIL_RANK=fail_rank)
+    cmd = [DRIVER, "dam.data", "dam.grid", "dam%03d.prof", "dam%03d.vtk", "dam.log", "4"]
+    r = subprocess.run(cmd, cwd=d, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0, (r.stdout[-500:], r.stderr[-500:])
+    assert "fault injection" in r.stderr or "slab rank failed" in r.stderr, r.stderr[-1000:]

@@ -322,26 +322,27 @@ def test_gpu_compact_lists_bitwise_equal_ell(case, monkeypatch):
         assert np.array_equal(out["redo"][f], out["0"][f]), f
 
 
-@pytest.mark.parametrize("case,radii", [("box3d", None), ("box3d_st", None), ("gate2d", None), ("dam2d", None),
-                                        ("channel3d", None), ("d1m", None), ("box3d", (2.1, 2.5, 2.3)),
-                                        ("gate3d", (2.5, 2.2, 2.4))])
-def test_gpu_fused_search_pass_a_bitwise(case, radii, monkeypatch):
-    """k_search_pass_a (the default: pass-A sums from the search's LDS-staged window, mask walk,
-    branch-free terms) equals k_neighbors + k_pass_a (MPH_FUSED=0) bit for bit after several steps,
-    in the equal-radii form and, with RadiusRatioA/P/V set apart (radii), in the general form."""
+@pytest.mark.parametrize("case", ["box3d", "box3d_st", "gate2d", "dam2d", "seam3d", "gate3d_sub"])
+def test_gpu_xcd_balanced_map_bitwise(case, monkeypatch):
+    """The work-balanced XCD block map of passes A and B (k_xcd_split + list_block), which by default
+    runs only from 2^20 particles, forced on small cases (MPH_XCD_BAL_MIN=0; their few blocks also
+    trip the map's fallback to equal ranges when a range exceeds its slack): it only changes which
+    block handles which wave, so every field equals the default run bit for bit."""
     cfg, parts = cases.get(case).build()
-    if radii is not None:
-        cfg.radius_ratio_a, cfg.radius_ratio_p, cfg.radius_ratio_v = radii
     fields = ["Position", "Velocity", "PressureP", "PressureA", "NeighborCount", "Force", "Acceleration",
               "DensityA", "VolStrainP", "DivergenceP", "GravityCenter"]
     out = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("MPH_FUSED", mode)
+    for mode in ("0", None):
+        if mode is None:
+            monkeypatch.delenv("MPH_XCD_BAL_MIN", raising=False)
+        else:
+            monkeypatch.setenv("MPH_XCD_BAL_MIN", mode)
         with MphSolver(cfg, parts) as s:
-            s.step(6)
+            s.step(3)
+            s.step(4)
             out[mode] = {f: s.get(f) for f in fields}
     for f in fields:
-        assert np.array_equal(out["1"][f], out["0"][f]), (f, float(np.max(np.abs(out["1"][f] - out["0"][f]))))
+        assert np.array_equal(out["0"][f], out[None][f]), (f, float(np.max(np.abs(out["0"][f] - out[None][f]))))
 
 
 @pytest.mark.parametrize("lanes", ["1", "2", "4", "8"])
