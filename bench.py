@@ -310,7 +310,7 @@ def main():
         list_info = {"entries_per_particle": mean_nb, "alg_bytes_written": list_alg,
                      "alg_bytes_read_by_passes": 2.0 * list_alg,
                      "search_write_bytes_measured": wr * 1024.0 if wr else None,
-                     "write_amplification": (wr * 1024.0 / list_alg) if wr else None}
+                     "write_amplification": (wr * 1024.0 / list_alg) if wr and list_alg else None}
     # measured HBM traffic of a whole step: rocprofv3 FETCH_SIZE/WRITE_SIZE per kernel in the timed
     # region's store pattern (tools/profile.sh + tools/pmc_traffic.py, calibration
     # profiles/pmc_calib.json), over this run's own step time
@@ -321,6 +321,36 @@ def main():
         if d.get("case") == case_name and world == 1:
             step_bytes = d.get("hbm_bytes_per_step")
     except (OSError, ValueError):
+        pass
+    # what binds the dominant stage's kernels (the HBM roofline does not): the
+    # larger of VALU issue and the L1 (TCP) tag-lookup rate, each as a fraction of its ceiling, from
+    # the committed PMC summary of this case (tools/pmc_ab.sh + tools/pmc_issue.py)
+    binding = None
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_issue.json")) as fh:
+            iss = json.load(fh)
+        if iss.get("case") == case_name and world == 1:
+            per = {}
+            for k in units[dom]["kernels"]:
+                v = iss.get(k)
+                if not v:
+                    continue
+                # the measured verdict when the summary records one (e.g. the search: latency, since
+                # fewer VALU per wave did not shorten it), else the larger of the two rates
+                res = v.get("binding") or ("valu_issue" if v["valu_busy"] >= v["l1_lookups_per_clk"]
+                                           else "l1_tag_lookups")
+                per[k] = {"resource": res, "frac": max(v["valu_busy"], v["l1_lookups_per_clk"]),
+                          "valu_issue": v["valu_busy"], "l1_tag_lookups_per_clk_cu": v["l1_lookups_per_clk"]}
+                if v.get("binding_note"):
+                    per[k]["note"] = v["binding_note"]
+            if per:
+                w = {k: prof[k]["avg_ms"] * prof[k]["launches"] for k in per if k in prof}
+                tot = sum(w.values()) or 1.0
+                top = max(per, key=lambda k: w.get(k, 0.0))
+                binding = {"resource": per[top]["resource"],
+                           "frac": sum(per[k]["frac"] * w.get(k, 0.0) for k in per) / tot,
+                           "kernels": per, "source": "profiles/pmc_issue.json (%s)" % iss.get("source")}
+    except (OSError, ValueError, KeyError):
         pass
     # FP64 utilisation: PMC lane FLOPs per launch over the same live launch time
     flops = {k: load_pmc("pmc_fp64", case_name, k, "lane_flops_per_launch") for k in prof}
@@ -365,6 +395,7 @@ def main():
                      "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
                      "avg_launch_ms": units[dom]["ms"],
                      "step_frac": B_ALG_STEP * value / world / (HBM_PEAK_GBPS * 1e9),
+                     "binding": binding,
                      "stages": {u: {"ms": round(v["ms"], 5),
                                     "frac": v["bytes"] / (v["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS}
                                 for u, v in units.items()}},

@@ -43,9 +43,11 @@ struct MphDist {
     // transport: RCCL communicator, or a host callback (tests / hosts without RCCL)
     bool rccl = false;
     bool graphs = false;          // steps replayed from captured graphs (RCCL transport)
-    // pass B of the inner particles overlaps the pass-A halo (MPH_SLAB_OVERLAP=0: halo, then one
-    // pass B over all particles)
-    bool overlap = !(std::getenv("MPH_SLAB_OVERLAP") && std::string(std::getenv("MPH_SLAB_OVERLAP")) == "0");
+    // MPH_SLAB_OVERLAP=1: pass B of the inner particles overlaps the pass-A halo (and the early send
+    // below); default off -- halo, then one pass B over all particles.  One rank at a time at D16M / 8
+    // the split pass B and the early classify cost 0.13 ms per step more than they can hide
+    // (profiles/r04/serial_d16m_8_overlap*.json)
+    bool overlap = std::getenv("MPH_SLAB_OVERLAP") && std::string(std::getenv("MPH_SLAB_OVERLAP")) == "1";
     // early send: within a batch of steps, the redistribution messages of the next step leave
     // while the interior pass B of this one runs (no elastic particles; MPH_SLAB_EARLY=0: off)
     bool early = !(std::getenv("MPH_SLAB_EARLY") && std::string(std::getenv("MPH_SLAB_EARLY")) == "0");
@@ -103,6 +105,7 @@ struct MphCtx {
     double *vir = nullptr, *vpres = nullptr;   // VirialStress [cap][9] / VirialPressure (A order), lazy
     int *nbr = nullptr, *ncount = nullptr;
     int* list_hdr = nullptr;     // per-wave headers of the compact 16-bit lists (kLhdr ints each)
+    int2* win_hdr = nullptr;     // MPH_PA_STAGED builds: per-wave column windows (kWinHdr each)
     double *pres = nullptr, *gx = nullptr, *gy = nullptr, *gz = nullptr, *pa = nullptr;
     double4 *force = nullptr, *acc = nullptr, *fpart = nullptr, *rec = nullptr;
     double *dens_a = nullptr, *vstrain = nullptr, *divp = nullptr;

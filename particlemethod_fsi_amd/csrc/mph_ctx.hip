@@ -53,6 +53,8 @@ int ctx_state_status(MphCtx* c, const DevState& hs)
     if (hs.overflow & 1)
         return ctx_fail(c, MPH_ERR_NEIGHBOR_OVERFLOW, "a particle has more than 512 neighbours");
     if (hs.overflow & 2) return ctx_fail(c, MPH_ERR_CAPACITY, "a particle moved past a neighbouring slab");
+    if (hs.overflow & 32)   // MPH_DIAG_PA builds only
+        return ctx_fail(c, MPH_ERR_HIP, "diagnostic: staged pass A left list entries over (MPH_DIAG_PA)");
     if (hs.overflow & 8)   // MPH_DIAG_BOUNDS builds only
         return ctx_fail(c, MPH_ERR_HIP, "diagnostic: a search window out of range (MPH_DIAG_BOUNDS)");
     return MPH_OK;
@@ -71,7 +73,7 @@ void ctx_fill_launch(MphCtx* c)
     // returned through A.id), so k_rank_scatter skips that scatter; slab mode uses dst_of.
     L.A = c->A; L.B = c->B; L.rank_of = nullptr; L.dst_of = nullptr;
     L.key = c->key; L.slot = c->slot; L.tmp = c->tmp; L.cnt = c->cnt; L.start = c->start; L.bsum = c->bsum;
-    L.nbr = c->nbr; L.ncount = c->ncount;
+    L.nbr = c->nbr; L.ncount = c->ncount; L.whdr = c->win_hdr;
     // compact 16-bit lists of interior wavefronts (MPH_LIST16=1), or 32-bit ELL rows everywhere
     // (MPH_LIST16=0); unset: kListCompact
     const char* l16 = std::getenv("MPH_LIST16");
@@ -425,6 +427,9 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     if (hipMemset(c->ncount, 0, sizeof(int) * cap) != hipSuccess) return MPH_ERR_HIP;
 #endif
     CK(dalloc(c, &c->list_hdr, ntile * kLhdr));
+#if defined(MPH_PA_STAGED) && MPH_PA_STAGED
+    CK(dalloc(c, &c->win_hdr, (ntile + 4) * kWinHdr));
+#endif
     CK(dalloc(c, &c->pres, cap)); CK(dalloc(c, &c->gx, cap)); CK(dalloc(c, &c->gy, cap)); CK(dalloc(c, &c->gz, cap));
     CK(dalloc(c, &c->pa, cap)); CK(dalloc(c, &c->force, cap)); CK(dalloc(c, &c->acc, cap));
     CK(dalloc(c, &c->fpart, cap)); CK(dalloc(c, &c->rec, cap));

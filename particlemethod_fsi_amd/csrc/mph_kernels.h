@@ -96,6 +96,7 @@ struct Launch {
     int *nbr = nullptr, *ncount = nullptr;
     int* lhdr = nullptr;          // per-wave headers of the compact 16-bit lists (kLhdr each)
     int* wface = nullptr;         // slab mode: face-wavefront flags written by pass B (early send)
+    int2* whdr = nullptr;         // MPH_PA_STAGED builds: per-wave column windows (kWinHdr each)
     VSrc vsrc;                    // slab mode: where the sort finds the kept entries of its input
     // fewest particles for the work-balanced XCD map of the passes (k_xcd_split each step);
     // MPH_XCD_BAL_MIN overrides it at creation (tests force the map on small cases)

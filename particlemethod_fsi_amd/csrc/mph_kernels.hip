@@ -79,6 +79,19 @@
 #define MPH_LDS_CAP 176
 #endif
 
+#ifndef MPH_PA_STAGED
+// pass A reads each stencil column's window of 48-byte records from LDS, staged once per wave
+// (the search writes the windows per wave: kWinHdr), instead of per-lane gathers through L1
+// (measured, opt-in)
+#define MPH_PA_STAGED 0
+#endif
+#ifndef MPH_DIAG_PA
+#define MPH_DIAG_PA 0   // diagnostic builds: the staged pass A checks it used every entry (DevState.overflow 32)
+#endif
+#ifndef MPH_PA_CAP
+#define MPH_PA_CAP 160   // records staged per column window (7.5 KB per wave; 4 waves per SIMD)
+#endif
+
 namespace mph {
 
 // Buffer descriptor of a device array (gfx9 raw-buffer format word, 4 GiB of records): loads through
@@ -367,7 +380,7 @@ __device__ __forceinline__ int list_block(const DevState* st, int n)
 }
 
 // The search's contribution to the work histogram: its wave's longest list (all lanes converged;
-// one atomic per wave, spread over the 512 runs).
+// one atomic per wave, spread over the 4096 runs).
 __device__ __forceinline__ void add_wave_work(DevState* st, int cnt, int i, int n)
 {
     if (!MPH_XCD_BAL || !st) return;
@@ -380,6 +393,10 @@ __device__ __forceinline__ void add_wave_work(DevState* st, int cnt, int i, int 
 }
 
 __device__ __forceinline__ int nbr_entry(int j, int type) { return j | (type << kTypeShift); }
+
+// MPH_PA_STAGED: a wave's column windows {mn, mx} for pass A (kWinCols of them) and its format flag
+// (entry kWinCols: 1 = written by the staged search), kWinHdr int2 per wave (Launch.whdr)
+constexpr int kWinCols = kGroups * kGroups;   // 3-D stencil columns (2-D uses the first kGroups)
 
 // Velocity of sorted particle i for the list passes: from its 48-byte gather record {x, y, z, vx,
 // vy, vz} (k_rank_scatter then skips the SoA velocity stores), or the SoA arrays.
@@ -1204,7 +1221,7 @@ template <int DIM, int PERM, bool C16, int SB = MPH_SB, int CAP = MPH_LDS_CAP>
 __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa& A, const int* start,
                                                    int i, bool act, double xi, double yi, double zi,
                                                    int cx, int cy, int cz, int* out, double* sx,
-                                                   int* lh, unsigned short* o16, DevState* dst)
+                                                   int* lh, unsigned short* o16, DevState* dst, int2* whdr)
 {
     constexpr int SD = stage_d(CAP, SB);
     double* sy = sx + SD;
@@ -1341,6 +1358,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
         // normally has the lowest jb and the last the highest je -- read those two lanes, and take
         // the DPP reductions only when a lane says otherwise (wave-uniform check)
         const unsigned long long am = __ballot(any);
+        if (MPH_PA_STAGED && whdr && !am && lane == 0) whdr[col] = make_int2(0, 0);
         if (!am) {   // wave-uniform: no lane has candidates in this column
             // wait here for column col + 1's start[] loads, so that every path into the next column
             // has them landed and its first use needs no wait (which would also wait for this
@@ -1359,6 +1377,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             __builtin_amdgcn_s_waitcnt(0x0F70);
             return;
         }
+        if (MPH_PA_STAGED && whdr && lane == 0) whdr[col] = make_int2(mn, mx);   // pass A's column windows
         const int span = mx - mn;
         if (MPH_DIAG_SEARCH & 2) {   // never true: empty lists
             __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -1535,13 +1554,17 @@ __device__ __forceinline__ void slab_wave_flag(const DevParams& P, const Soa& A,
 
 template <int DIM, int PERM, bool C16, int REDO>
 __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, const int* start, int* nbr,
-                                               int* ncount, int* lhdr, DevState* st, double* stage, int i)
+                                               int* ncount, int* lhdr, DevState* st, double* stage, int i,
+                                               int2* whdr_all = nullptr)
 {
     const int n = dev_n(P);
     const bool live = i < n;
     const int ii = live ? i : n - 1;
     // list format of the wave: the 32-bit ELL row unless the interior search below goes compact
     const int tile = __builtin_amdgcn_readfirstlane(i >> 6);
+    // a wave past the last particle (the launch has whole blocks of 4 waves): nothing to do, and its
+    // tile lies past the list and header arrays (sized for the particles' tiles)
+    if (tile * kTile >= n) return 0;
     int* lh = C16 && !REDO ? lhdr + (size_t)tile * kLhdr : nullptr;   // REDO: a marked wave, now into ELL rows
     if (C16 && (threadIdx.x & 63) == 0) lhdr[(size_t)tile * kLhdr + kHdrFlag] = 0;
     if (wave_all_ghosts(P, A, live, ii)) {
@@ -1557,15 +1580,18 @@ __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, 
     const int cy = cell_axis(yi, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
     const int cz = DIM == 3 ? cell_axis(zi, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
     int* out = nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
+    // MPH_PA_STAGED: the wave's column windows for pass A, flag kWinCols: 1 = written
+    int2* whdr = MPH_PA_STAGED && !C16 && !REDO && whdr_all ? whdr_all + (size_t)tile * kWinHdr : nullptr;
+    if (whdr && (threadIdx.x & 63) == 0) whdr[kWinCols] = make_int2(fast ? 1 : 0, 0);
     if (MPH_SEARCH_LDS && fast) {
         if (C16 && !REDO) {
             cnt = scan_candidates_lds<DIM, PERM, true>(P, A, start, i, own, xi, yi, zi, cx, cy, cz, out, stage, lh,
                                                        reinterpret_cast<unsigned short*>(
-                                                           nbr + (size_t)tile * (kTile * kMaxNeighbor)), st);
+                                                           nbr + (size_t)tile * (kTile * kMaxNeighbor)), st, nullptr);
             if ((threadIdx.x & 63) == 0 && lh[kHdrFlag] == 2) atomicAdd(&st->list_redo, 1);
         } else {
             cnt = scan_candidates_lds<DIM, PERM, false>(P, A, start, i, own, xi, yi, zi, cx, cy, cz, out, stage,
-                                                        nullptr, nullptr, st);
+                                                        nullptr, nullptr, st, whdr);
         }
         if (live) ncount[i] = cnt;
     } else {
@@ -1590,7 +1616,7 @@ __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, 
 template <int DIM, int PERM, bool C16>
 __global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_WPE))) void k_neighbors(
     DevParams P, Soa A, const int* __restrict__ start, int* __restrict__ nbr, int* __restrict__ ncount,
-    int* __restrict__ lhdr, DevState* __restrict__ st, int* __restrict__ wface, int bal)
+    int* __restrict__ lhdr, DevState* __restrict__ st, int* __restrict__ wface, int bal, int2* __restrict__ whdr)
 {
     const int n = dev_n(P);
     if ((int)blockIdx.x >= list_blocks(n)) return;
@@ -1598,7 +1624,8 @@ __global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_W
     __shared__ __attribute__((aligned(16))) double stage[kWB][stage_words(MPH_LDS_CAP, MPH_SB)];
     const int i = xcd_block(blockIdx.x, list_blocks(n)) * blockDim.x + threadIdx.x;
     slab_wave_flag(P, A, i, n, wface);
-    const int cnt = neighbors_body<DIM, PERM, C16, 0>(P, A, start, nbr, ncount, lhdr, st, stage[threadIdx.x >> 6], i);
+    const int cnt = neighbors_body<DIM, PERM, C16, 0>(P, A, start, nbr, ncount, lhdr, st,
+                                                      stage[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], i, whdr);
     if (bal) add_wave_work(st, cnt, i, n);
 }
 
@@ -1727,6 +1754,74 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
     }
 }
 
+// Pass A of an interior wave from LDS-staged column windows (MPH_PA_STAGED): the search recorded the
+// wave's window [mn, mx) of every stencil column (whdr); per column the wave stages the window's
+// 48-byte records {x, y, z, vx, vy, vz} with coalesced buffer loads into LDS (16 bytes per lane,
+// 1 KB per instruction: ~8 L1 lines instead of ~24 per 16-byte gather of the list loop), then every
+// lane takes its next list entries below the window's end mx (a lane's entries ascend through the
+// columns) and reads the records of those inside [mn, mx) from LDS.  An entry below mn -- a later
+// column of a lane that had no candidates in this one, when the wave spans two cell rows -- is read
+// from global memory.  Same entries in the same order, same pass_a_term: every sum is bit-identical
+// to pass_a_loop.  Windows wider than CAP read their records from global memory.  Every lane of the
+// wave takes part (act: it has a particle).
+template <int DIM, bool EQR, int CAP = MPH_PA_CAP>
+__device__ __forceinline__ void pass_a_staged(const DevParams& P, const double* s_ratio, const double* s_mu,
+                                              const Soa& A, const NbrList& NL, const int2* whdr, int cnt, int ti,
+                                              bool solid, double xi, double yi, double zi, double vxi, double vyi,
+                                              double vzi, PassA& o, double2* stage, const DevState* st = nullptr)
+{
+    constexpr int NCOL = DIM == 3 ? kGroups * kGroups : kGroups;
+    const int lane = threadIdx.x & 63;
+    const __amdgpu_buffer_rsrc_t rp = arr_rsrc(A.p6);
+    const unsigned lane16 = (unsigned)lane * 16u;
+    int k = 0;
+    int j0 = INT_MAX, t0 = 0, j1 = INT_MAX, t1 = 0;   // the lane's next two entries
+    if (0 < cnt) nbr_at<false>(NL, 0, j0, t0);
+    if (1 < cnt) nbr_at<false>(NL, 1, j1, t1);
+    for (int col = 0; col < NCOL; ++col) {
+        const int2 w = whdr[col];   // wave-uniform
+        if (w.y <= w.x) continue;
+        const int mn = w.x, mx = w.y;
+        const bool staged = mx - mn <= CAP;
+        if (staged) {
+            // the window's bytes [48 mn, 48 mx) in 16-byte pieces, 64 per instruction
+            const int pieces = 3 * (mx - mn);
+            const unsigned so = (unsigned)mn * 48u;
+            for (int p = 0; p * 64 < pieces; ++p)   // wave-uniform
+                if (lane < pieces - p * 64)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rp, lds_ptr(stage + p * 64), 16, lane16, so + p * 1024u, 0, 0);
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+            __builtin_amdgcn_wave_barrier();
+        }
+        for (;;) {
+            const bool a = j0 < mx;   // (j0 = INT_MAX past the lane's last entry)
+            if (!__ballot(a)) break;
+            if (a) {
+                double2 r0, r1, r2;
+                if (staged && j0 >= mn) {
+                    const double2* q = stage + 3 * (j0 - mn);
+                    r0 = q[0]; r1 = q[1]; r2 = q[2];
+                } else {
+                    const double2* q = A.p6 + 3 * (size_t)j0;
+                    r0 = q[0]; r1 = q[1]; r2 = q[2];
+                }
+                const double q0 = image_exact<true>(r0.x - xi, P.dw[0], P.hw[0], P.w075[0]);
+                const double q1 = image_exact<true>(r0.y - yi, P.dw[1], P.hw[1], P.w075[1]);
+                const double q2 = image_exact<true>(r1.x - zi, P.dw[2], P.hw[2], P.w075[2]);
+                pass_a_term<true, EQR>(P, s_ratio, s_mu, ti, t0, solid, q0, q1, q2, r2_exact(q0, q1, q2),
+                                       r1.y - vxi, r2.x - vyi, r2.y - vzi, o);
+                ++k;
+                j0 = j1;
+                t0 = t1;
+                j1 = INT_MAX;
+                if (k + 1 < cnt) nbr_at<false>(NL, k + 1, j1, t1);
+            }
+        }
+        if (staged) __builtin_amdgcn_wave_barrier();   // every lane done reading before the next staging
+    }
+    if (MPH_DIAG_PA && k != cnt && st) atomicOr(&const_cast<DevState*>(st)->overflow, 32);   // entries left over
+}
+
 #ifndef MPH_PA_WPE
 #define MPH_PA_WPE 4   // pass A at <= 128 VGPRs: 4 waves per SIMD
 #endif
@@ -1740,7 +1835,7 @@ __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, cons
                                                 const int* __restrict__ nbr,
                                                 const int* __restrict__ ncount,
                                                 const int* __restrict__ lhdr, PassAOut pout,
-                                                const DevState* __restrict__ st)
+                                                const DevState* __restrict__ st, const int2* __restrict__ whdr)
 {
     const int n = dev_n(P);
     const int lb = list_block(st, n);
@@ -1769,6 +1864,24 @@ __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, cons
     const bool own = live && !ghost;
     // the search's rule (its list order and the fast minimum image go together)
     const bool fast = wave_search_interior(P, st, own, xi, yi, zi);
+    if (MPH_PA_STAGED && whdr && fast && pass_a_equal_radii(P)) {
+        const int2* h = whdr + (size_t)__builtin_amdgcn_readfirstlane(i >> 6) * kWinHdr;
+        if (h[kWinCols].x == 1) {   // wave-uniform: the staged search wrote this wave's windows
+            __shared__ __attribute__((aligned(16))) double2 pstage[kWB][3 * MPH_PA_CAP];
+            double vxi = 0.0, vyi = 0.0, vzi = 0.0;
+            if (own) own_velocity(A, i, vxi, vyi, vzi);
+            const int ti = A.type[ii];
+            const bool solid = dev_is_struct(ti);
+            const int cnt = own ? (ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor) : 0;
+            __shared__ int s_gb2[kWB][8];
+            const NbrList NL = nbr_list(nbr, nullptr, i, s_gb2[threadIdx.x >> 6]);
+            PassA o;
+            pass_a_staged<DIM, true>(P, s_ratio, s_mu, A, NL, h, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o,
+                                     pstage[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], st);
+            if (own) pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
+            return;
+        }
+    }
     if (!own) return;
     double vxi, vyi, vzi;
     own_velocity(A, i, vxi, vyi, vzi);
@@ -3019,14 +3132,17 @@ void launch_neighbors(const Launch& L)
     // the second launch (REDO) only when compact lists are on; its waves exit at once unless the
     // first marked them
     const int bal = MPH_XCD_BAL && P.n >= L.xcd_bal_min;
+    const int nb_grid = blocks(P.n, MPH_LB);
 #define MPH_NEIGHBORS(D, PERM)                                                                               \
     do {                                                                                                     \
         if (L.lhdr)                                                                                          \
-            MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM, true>), dim3(blocks(P.n, MPH_LB)),        \
-                       dim3(MPH_LB), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.lhdr, L.st, L.wface, bal); \
+            MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM, true>), dim3(nb_grid),                     \
+                       dim3(MPH_LB), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.lhdr, L.st, L.wface, bal, \
+                       L.whdr);                                                                              \
         else                                                                                                 \
-            MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM, false>), dim3(blocks(P.n, MPH_LB)),       \
-                       dim3(MPH_LB), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.lhdr, L.st, L.wface, bal); \
+            MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM, false>), dim3(nb_grid),                    \
+                       dim3(MPH_LB), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.lhdr, L.st, L.wface, bal, \
+                       L.whdr);                                                                              \
         if (bal)                                                                                             \
             MPH_LAUNCH("xcd_split", L.stream, k_xcd_split, dim3(1), dim3(kXcdSplitThreads), 0, L.stream, L.st); \
         if (L.lhdr)                                                                                          \
@@ -3055,10 +3171,10 @@ void launch_pass_a(const Launch& L)
     const PassAOut po = pass_a_out(L);
     if (P.dim == 3)
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<3>, dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, L.lhdr, po, L.st);
+                   L.A, L.nbr, L.ncount, L.lhdr, po, L.st, MPH_PA_STAGED && !L.lhdr ? L.whdr : nullptr);
     else
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<2>, dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, L.lhdr, po, L.st);
+                   L.A, L.nbr, L.ncount, L.lhdr, po, L.st, MPH_PA_STAGED && !L.lhdr ? L.whdr : nullptr);
 }
 
 // calculateNeighbor + the pass-A sums (the search, the XCD split of the passes, pass A)

@@ -50,6 +50,8 @@ constexpr int kHdrFlag = 7;
 #endif
 constexpr bool kListCompact = MPH_LIST_COMPACT;
 constexpr int kLhdr = 8 + 2 * 64;
+// per-wave column windows of the staged pass A (MPH_PA_STAGED, mph_kernels.hip): int2 entries
+constexpr int kWinHdr = (2 * 3 + 1) * (2 * 3 + 1) + 1;
 static_assert(kGroups <= kHdrFlag, "group bases overlap the format flag");
 
 inline bool is_fluid(int t) { return t >= 0 && t < 2; }   // main.cpp:69-70

@@ -153,7 +153,11 @@ def load_library() -> ctypes.CDLL:
         "mph_phase_timing": (ip, [vp, ip]),
         "mph_phase_times": (ip, [vp, vp]),
     }
+    # entry points an older library may lack (A/B runs against earlier builds)
+    optional = {"mph_phase_timing", "mph_phase_times"}
     for name, (res, args) in sig.items():
+        if name in optional and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args

@@ -6,6 +6,9 @@ single-context run, which the smaller parity tests pin to the oracle:
 
 1. one context (~37 GB of HBM): a rerun is bitwise identical, Time advances by exactly Dt per step,
    no neighbour overflow and NeighborCount within the lattice bound (<= 80 at rc = 2.6 dx);
+   NeighborCount after creation and after steps 1, 10, 29 and 52 equals the CPU oracle's bit for bit
+   (sha256 of the whole array, tests/golden/d16m_ncount.json from tools/make_d16m_ncount.py: the
+   oracle fits this container's host memory with 128-entry list rows);
 2. the 8-way z-slab decomposition that the driver's 8-GPU job runs (8 ranks sharing the one test
    GPU, host-staged transport) against the single context after 3 steps: ownership is a partition
    of all particles, NeighborCount exact, positions 1e-12 m, velocities 1e-9 m/s, PressureP
@@ -44,6 +47,31 @@ def _single(nsteps):
         out["time"] = s.time
         out["mean_max"] = s.neighbor_stats()
     return cfg, n, out
+
+
+def _ncount_stats(nc):
+    import hashlib
+    nc = np.ascontiguousarray(nc, np.int32)
+    return {"sum": int(nc.astype(np.int64).sum()), "min": int(nc.min()), "max": int(nc.max()),
+            "sha256": hashlib.sha256(nc.tobytes()).hexdigest()}
+
+
+def test_d16m_neighbor_count_matches_oracle_fixture():
+    import json
+    import os
+    fix = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "d16m_ncount.json")))
+    cfg, parts = cases.get("d16m").build()
+    assert parts.n == fix["particles"]
+    with MphSolver(cfg, parts) as s:
+        del parts
+        assert _ncount_stats(s.get("NeighborCount")) == fix["init"]
+        done = 0
+        for k in (1, 10, 29, 52):
+            if "step%d" % k not in fix:
+                break
+            s.step(k - done)
+            done = k
+            assert _ncount_stats(s.get("NeighborCount")) == fix["step%d" % k], k
 
 
 def test_d16m_single_context_rerun_time_and_counts():

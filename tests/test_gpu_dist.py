@@ -156,11 +156,13 @@ def test_rccl_exchange_selftest():
 
 @pytest.mark.parametrize("case,world", [("channel3d", 3), ("channel2d", 4), ("bar2d", 3), ("gate2d_sub", 2)])
 def test_slab_early_send_bitwise(tmp_path, case, world, monkeypatch):
-    """The early send of the redistribution messages (MPH_SLAB_EARLY, default on: inside a batch,
+    """The early send of the redistribution messages (MPH_SLAB_EARLY, default on with the overlap: inside a batch,
     the next step's messages leave from pass B's face wavefronts while the interior ones run;
     with elastic particles, after the substeps) sends exactly the bytes the late pack would, so
-    every field is bit-identical to MPH_SLAB_EARLY=0 -- over batches of 1, 4 and 15 steps."""
+    every field is bit-identical to MPH_SLAB_EARLY=0 -- over batches of 1, 4 and 15 steps.  The early
+    send rides on the split pass B, so the overlap is switched on (MPH_SLAB_OVERLAP=1, default off)."""
     fields = STRUCT_FIELDS if case.startswith(("bar", "gate")) else FIELDS
+    monkeypatch.setenv("MPH_SLAB_OVERLAP", "1")
     out = {}
     for mode in ("1", "0"):
         monkeypatch.setenv("MPH_SLAB_EARLY", mode)

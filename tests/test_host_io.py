@@ -325,3 +325,23 @@ def test_boid_parser_refuses_what_the_generator_would_drop(bad, msg):
     head = "ParticleDistance 0.001\nLowerDomain 0 0 0\nUpperDomain 1 1 1\n"
     with pytest.raises(mphio.BoidError, match=msg):
         mphio.parse_boid(head + bad)
+
+
+def test_search_uncounted_loads_land_before_use(tmp_path):
+    """The search issues its start[] loads in inline asm, which hipcc does not count
+    (mph_kernels.hip start_load2): on every control-flow path from such a load to the next
+    s_waitcnt vmcnt(0) no instruction may read, copy or overwrite its destination register
+    (tools/asm_load_audit.py over the gfx950 assembly of every k_neighbors instantiation)."""
+    import shutil
+    import subprocess
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    csrc = os.path.join(ROOT, "particlemethod_fsi_amd", "csrc")
+    asm = str(tmp_path / "kernels.s")
+    subprocess.run([hipcc, "-O3", "-std=c++17", "-I" + os.path.join(ROOT, "include"), "--offload-arch=gfx950",
+                    "-munsafe-fp-atomics", "--cuda-device-only", "-S", os.path.join(csrc, "mph_kernels.hip"),
+                    "-o", asm], check=True, capture_output=True, timeout=600)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "asm_load_audit.py"), asm, "k_neighbors"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "clean" in r.stdout, r.stdout[-2000:]

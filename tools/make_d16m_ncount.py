@@ -1,13 +1,14 @@
 #!/usr/bin/env python3
 """Fixture for tests/test_gpu_d16m.py: the CPU oracle's NeighborCount of BASELINE configs[4]
-(D16M, 16,205,500 particles) after creation and after the first step -- sum, extremes and the
-sha256 of the int32 array in original particle order -- so that the GPU test checks the whole
-array bit for bit without the oracle on the GPU box.
+(D16M, 16,205,500 particles) after creation and after steps 1, 10, 29 and 52 (the bench's
+horizon) -- sum, extremes and the sha256 of the int32 array in original particle order -- so that
+the GPU test checks the whole array bit for bit without the oracle on the GPU box.
 
 The oracle (oracle/mph_oracle.c, bit-identical to the reference on every golden case) runs here
 with 128-entry list rows (oracle/Makefile `oracle128`: the case's lists hold at most 80
 neighbours, overflow is still detected) so its lists take 8 GB instead of 33 GB of host memory.
-Writes tests/golden/d16m_ncount.json.  Run: python tools/make_d16m_ncount.py (≈ 2 min, 8 cores).
+Writes tests/golden/d16m_ncount.json.  Run: python tools/make_d16m_ncount.py (≈ 1 min per step on
+8 cores; the file is rewritten after every checkpoint).
 """
 import hashlib
 import json
@@ -45,11 +46,14 @@ def main():
     out = {"case": "d16m", "particles": n, "source": "oracle/mph_oracle.c (MPH_ORACLE_MAXN=128), "
            "tools/make_d16m_ncount.py", "init": stats(o.get("NeighborCount"))}
     print("init", out["init"], "%.1f s" % (time.time() - t0), flush=True)
-    o.step(1)
-    out["step1"] = stats(o.get("NeighborCount"))
-    print("step1", out["step1"], "%.1f s" % (time.time() - t0), flush=True)
-    with open(os.path.join(ROOT, "tests", "golden", "d16m_ncount.json"), "w") as fh:
-        json.dump(out, fh, indent=1)
+    done = 0
+    for k in (1, 10, 29, 52):
+        o.step(k - done)
+        done = k
+        out["step%d" % k] = stats(o.get("NeighborCount"))
+        print("step%d" % k, out["step%d" % k], "%.1f s" % (time.time() - t0), flush=True)
+        with open(os.path.join(ROOT, "tests", "golden", "d16m_ncount.json"), "w") as fh:
+            json.dump(out, fh, indent=1)
 
 
 if __name__ == "__main__":
