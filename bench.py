@@ -245,18 +245,26 @@ def main():
     value = n_total * args.steps / elapsed   # every particle of the whole job, once per step
 
     # the drop-in binding's own call pattern: one mph_step(ctx, 1) per
-    # time-loop iteration (1-step graph, every output-only field stored, one readback of the step's
-    # error flags per call) over the same number of steps
+    # time-loop iteration over the same number of steps, with step batching on as INTEGRATION.md
+    # recommends (mph_set_step_batching: the steps run 8 per graph, flushed by the synchronize that
+    # closes the timed region), and without it ("sync": a 1-step graph that stores every
+    # output-only field and one readback of the error flags per call)
     step1 = None
     if world == 1:
-        barrier()
-        t1 = time.perf_counter()
-        for _ in range(args.steps):
-            solver.step(1)
-        barrier()
-        e1 = time.perf_counter() - t1
-        step1 = {"value": n_total * args.steps / e1, "ms_per_step": e1 * 1e3 / args.steps,
-                 "gap": 1.0 - (n_total * args.steps / e1) / value}
+        def per_call(batched):
+            solver.step_batching(batched)
+            barrier()
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                solver.step(1)
+            barrier()
+            e1 = time.perf_counter() - t1
+            solver.step_batching(False)
+            return n_total * args.steps / e1, e1 * 1e3 / args.steps
+        v_sync, ms_sync = per_call(False)
+        v_b, ms_b = per_call(True)
+        step1 = {"value": v_b, "ms_per_step": ms_b, "gap": 1.0 - v_b / value, "batching": True,
+                 "sync": {"value": v_sync, "ms_per_step": ms_sync, "gap": 1.0 - v_sync / value}}
 
     mean_nb, max_nb = solver.neighbor_stats()
     prof = solver.profile(args.profile_steps)

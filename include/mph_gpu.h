@@ -222,7 +222,20 @@ int mph_create(MphCtx** ctx, const MphConfig* cfg, int n, const int* property,
  * replayed batch, so after a successful mph_step they hold that step's values; after an error
  * they are undefined (the state itself -- Position, Velocity -- is the failing step's).        */
 int mph_step(MphCtx* ctx, int nsteps);
-/* Wait for all work the context enqueued (slab mode: both of its streams). */
+/* Step batching for the drop-in loop that calls mph_step(ctx, 1) once per iteration
+ * (INTEGRATION.md section 2); single contexts only (slab mode: MPH_ERR_ARG for on != 0).
+ * With it on, mph_step only counts the steps and launches them 8 at a time from the 8-step
+ * graph, with the output-only stores on each batch's last step -- the cost of one
+ * mph_step(ctx, 8) instead of eight synchronised single steps.  Time (mph_time) advances per call.
+ * Steps still pending run, and the error flags of everything launched are read, at the next
+ * flush point: mph_synchronize, mph_get, mph_set, every writer, mph_compute_virial,
+ * mph_neighbor_stats, mph_profile_steps, mph_phase_timing, turning batching off, mph_destroy; so
+ * every field read after a step is that step's, bit for bit as without batching.  A launched
+ * batch's error is also reported by a later mph_step once its flags have landed (no wait).
+ * Errors therefore surface up to two batches late, or at the next flush point.  Off by default. */
+int mph_set_step_batching(MphCtx* ctx, int on);
+/* Wait for all work the context enqueued (slab mode: both of its streams); with step batching,
+ * launches the pending steps first and returns their status. */
 int mph_synchronize(MphCtx* ctx);
 /* Copy a field to host, AoS, original particle order.                                      */
 int mph_get(MphCtx* ctx, int field, void* host_out);

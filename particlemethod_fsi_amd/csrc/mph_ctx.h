@@ -82,6 +82,14 @@ struct MphCtx {
     bool stepped = false;
     hipStream_t stream = nullptr;
     hipGraphExec_t graph1 = nullptr, graph8 = nullptr;
+    // step batching (mph_set_step_batching): single mph_step calls accumulate into 8-step graphs;
+    // `pending` steps are accepted but not launched yet, `unchecked`: batches launched whose error
+    // flags have not been read; the flags of the last launched batch land in hs_pin (pinned)
+    bool batch_steps = false;
+    int pending = 0;
+    bool unchecked = false;
+    void* hs_pin = nullptr;
+    hipEvent_t ev_status = nullptr;
     // phase timing (mph_phase_timing): steps launched directly (no graph) with events at every
     // step's phase boundaries -- before the sort, after the search, after the elastic substeps --
     // three per step of a batch of up to 8 (ev8), and around the virial (ev_vir)

@@ -659,6 +659,67 @@ int mph_create(MphCtx** out, const MphConfig* cfg, int n, const int* property, c
     return ctx_create(out, cfg, n, property, pos, pos0, vel, device, nullptr);
 }
 
+// Step batching: launch the steps accepted but not launched (single-step graphs, each storing the
+// output-only fields, so the last one leaves them current) and read the error flags of everything
+// launched.  Every entry point that reads or changes the state, or waits for it, calls this first.
+static int ctx_flush(MphCtx* c)
+{
+    if (!c->pending && !c->unchecked) return MPH_OK;
+    HIP_OK(c, hipSetDevice(c->device));
+    if (c->pending && !c->graph1) CK(capture(c, 1, &c->graph1));
+    for (; c->pending > 0; --c->pending) HIP_OK(c, hipGraphLaunch(c->graph1, c->stream));
+    c->unchecked = false;
+    DevState hs;
+    HIP_OK(c, hipMemcpyAsync(&hs, c->dst, kStateHead, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    return ctx_state_status(c, hs);
+}
+
+// mph_step with batching on: the steps are counted and launched 8 at a time from the 8-step graph
+// (output-only fields stored on each batch's last step, as a multi-step mph_step does); the error
+// flags of the last launched batch are copied back behind it and read without waiting once they
+// have landed, so an error surfaces at most a batch or two late, and at the latest at the next
+// flush point (mph_synchronize, mph_get, the writers, ...).
+static int step_batched(MphCtx* c, int nsteps)
+{
+    for (int k = 0; k < nsteps; ++k) c->time += c->cfg.dt;
+    c->stepped = true;
+    c->pending += nsteps;
+    bool launched = false;
+    if (c->pending >= 8 && !c->graph8) CK(capture(c, 8, &c->graph8));
+    while (c->pending >= 8) {
+        HIP_OK(c, hipGraphLaunch(c->graph8, c->stream));
+        c->pending -= 8;
+        launched = true;
+    }
+    if (launched) {
+        HIP_OK(c, hipMemcpyAsync(c->hs_pin, c->dst, kStateHead, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(c, hipEventRecord(c->ev_status, c->stream));
+        c->unchecked = true;
+    }
+    if (c->unchecked && hipEventQuery(c->ev_status) == hipSuccess) {
+        DevState hs;
+        std::memcpy(&hs, c->hs_pin, kStateHead);
+        CK(ctx_state_status(c, hs));
+    }
+    return MPH_OK;
+}
+
+int mph_set_step_batching(MphCtx* c, int on)
+{
+    if (!c) return MPH_ERR_ARG;
+    if (c->dist) return on ? fail(c, MPH_ERR_ARG, "step batching is not available in slab mode") : MPH_OK;
+    HIP_OK(c, hipSetDevice(c->device));
+    if (!on) {
+        c->batch_steps = false;
+        return ctx_flush(c);
+    }
+    if (!c->hs_pin) HIP_OK(c, hipHostMalloc(&c->hs_pin, kStateHead, hipHostMallocDefault));
+    if (!c->ev_status) HIP_OK(c, hipEventCreateWithFlags(&c->ev_status, hipEventDisableTiming));
+    c->batch_steps = true;
+    return MPH_OK;
+}
+
 int mph_step(MphCtx* c, int nsteps)
 {
     if (!c || nsteps < 0) return MPH_ERR_ARG;
@@ -668,6 +729,8 @@ int mph_step(MphCtx* c, int nsteps)
         for (int k = 0; k < nsteps; ++k) c->time += c->cfg.dt;
         return MPH_OK;
     }
+    if (c->batch_steps && !c->phase_timing) return step_batched(c, nsteps);
+    CK(ctx_flush(c));
     int left = nsteps;
     if (c->phase_timing) {
         // the graphs' batches (8 steps, then single steps; the output-only stores on each batch's
@@ -698,6 +761,7 @@ int mph_step(MphCtx* c, int nsteps)
 int mph_synchronize(MphCtx* c)
 {
     if (!c) return MPH_ERR_ARG;
+    CK(ctx_flush(c));
     HIP_OK(c, hipStreamSynchronize(c->stream));
     // slab mode: the second stream too (halo, face pass B, early send, elastic ghost exchanges)
     if (c->dist && c->dist->stream2) HIP_OK(c, hipStreamSynchronize(c->dist->stream2));
@@ -718,6 +782,7 @@ int mph_get_scalars(const MphCtx* c, double* out)
 int mph_get(MphCtx* c, int field, void* out)
 {
     if (!c || !out) return MPH_ERR_ARG;
+    CK(ctx_flush(c));
     HIP_OK(c, hipSetDevice(c->device));
     double* o = (double*)out;
     int* oi = (int*)out;
@@ -806,6 +871,7 @@ int mph_get(MphCtx* c, int field, void* out)
 int mph_compute_virial(MphCtx* c)
 {
     if (!c) return MPH_ERR_ARG;
+    CK(ctx_flush(c));
     HIP_OK(c, hipSetDevice(c->device));
     if (!c->vir) {
         // slab mode: the array capacity (c->P.n), the held count changes every step
@@ -831,6 +897,7 @@ int mph_compute_virial(MphCtx* c)
 int mph_set(MphCtx* c, int field, const void* in)
 {
     if (!c || !in) return MPH_ERR_ARG;
+    CK(ctx_flush(c));
     if (field != MPH_FIELD_POSITION && field != MPH_FIELD_VELOCITY)
         return fail(c, MPH_ERR_ARG, "mph_set supports Position and Velocity");
     HIP_OK(c, hipSetDevice(c->device));
@@ -852,6 +919,7 @@ int mph_set(MphCtx* c, int field, const void* in)
 int mph_set_initial_velocity_profile(MphCtx* c)
 {
     if (!c) return MPH_ERR_ARG;
+    CK(ctx_flush(c));
     HIP_OK(c, hipSetDevice(c->device));
     const size_t n = (size_t)c->n_glob;
     // slab mode: mph_get fills the owned entries and mph_set writes only those back
@@ -955,6 +1023,7 @@ int mph_write_vtk_async(MphCtx* c, const char* path)
 int mph_phase_timing(MphCtx* c, int on)
 {
     if (!c) return MPH_ERR_ARG;
+    CK(ctx_flush(c));
     if (c->dist) return on ? fail(c, MPH_ERR_ARG, "phase timing is not available in slab mode") : MPH_OK;
     HIP_OK(c, hipSetDevice(c->device));
     const bool want = on != 0;
@@ -980,6 +1049,7 @@ int mph_phase_times(const MphCtx* c, double* out3)
 int mph_profile_steps(MphCtx* c, int nsteps, double* avg_ms, int* launches, char* names32)
 {
     if (!c || nsteps <= 0 || !avg_ms || !launches || !names32) return MPH_ERR_ARG;
+    CK(ctx_flush(c));
     HIP_OK(c, hipSetDevice(c->device));
     EventProfiler prof;
     if (c->dist) {
@@ -1043,6 +1113,7 @@ int mph_profile_steps(MphCtx* c, int nsteps, double* avg_ms, int* launches, char
 int mph_neighbor_stats(MphCtx* c, double* mean, int* mx)
 {
     if (!c || !mean || !mx) return MPH_ERR_ARG;
+    CK(ctx_flush(c));
     HIP_OK(c, hipSetDevice(c->device));
     // NeighborCount of the particles held here (slab mode: owned + ghosts), reduced on the host
     std::vector<int> h(c->n);
@@ -1058,6 +1129,7 @@ int mph_neighbor_stats(MphCtx* c, double* mean, int* mx)
 int mph_list_formats(MphCtx* c, int* out2)
 {
     if (!c || !out2) return MPH_ERR_ARG;
+    CK(ctx_flush(c));
     HIP_OK(c, hipSetDevice(c->device));
     const int nt = (c->n + kTile - 1) / kTile;
     int compact = 0;
@@ -1097,6 +1169,9 @@ void mph_destroy(MphCtx* c)
     if (!c) return;
     if (c->out_thread.joinable()) c->out_thread.join();
     (void)hipSetDevice(c->device);
+    (void)ctx_flush(c);   // steps accepted under batching still run (their errors are dropped)
+    if (c->hs_pin) (void)hipHostFree(c->hs_pin);
+    if (c->ev_status) (void)hipEventDestroy(c->ev_status);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->graph1) (void)hipGraphExecDestroy(c->graph1);
     if (c->graph8) (void)hipGraphExecDestroy(c->graph8);

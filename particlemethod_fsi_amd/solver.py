@@ -57,6 +57,7 @@ EXPORTED_SYMBOLS = [
     "mph_write_vtu_arrays", "mph_write_vtu", "mph_velocity_profile_arrays",
     "mph_set_initial_velocity_profile", "mph_dist_info", "mph_create_slab", "mph_slab_window",
     "mph_list_formats", "mph_abi_version", "mph_phase_timing", "mph_phase_times",
+    "mph_set_step_batching",
 ]
 
 ABI_VERSION = 3   # MPH_ABI_VERSION of include/mph_gpu.h that these bindings follow
@@ -152,9 +153,10 @@ def load_library() -> ctypes.CDLL:
         "mph_slab_window": (ip, [cfgp, ip, ip, ip, vp, vp]),
         "mph_phase_timing": (ip, [vp, ip]),
         "mph_phase_times": (ip, [vp, vp]),
+        "mph_set_step_batching": (ip, [vp, ip]),
     }
     # entry points an older library may lack (A/B runs against earlier builds)
-    optional = {"mph_phase_timing", "mph_phase_times"}
+    optional = {"mph_phase_timing", "mph_phase_times", "mph_set_step_batching"}
     for name, (res, args) in sig.items():
         if name in optional and not hasattr(L, name):
             continue
@@ -420,6 +422,11 @@ class MphSolver:
             nm = raw[32 * i:32 * (i + 1)].split(b"\0", 1)[0].decode()
             out[nm] = {"avg_ms": float(avg[i]), "launches": int(cnt[i])}
         return out
+
+    def step_batching(self, on: bool = True):
+        """mph_set_step_batching: step(1) per time-loop iteration costs what step(8) does; pending
+        steps run (and their errors surface) at the next synchronize/get/write."""
+        _check(self._L.mph_set_step_batching(self._h, 1 if on else 0), self._h)
 
     def phase_timing(self, on: bool = True):
         """Record HIP events at every step's phase boundaries inside the step graphs (the

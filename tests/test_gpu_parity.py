@@ -186,6 +186,52 @@ def test_gpu_graph_chunking_equivalence(case):
             assert np.array_equal(a.get(f), b.get(f), equal_nan=True), (case, f)
 
 
+@pytest.mark.parametrize("case", ["box3d", "box3d_st", "gate2d", "bar2d"])
+def test_gpu_step_batching_equivalence(case):
+    """mph_set_step_batching: 21 x mph_step(1) (two 8-step graphs launched by the calls, 5 steps
+    pending) then mph_get == mph_step(21), bitwise, for every field and the virial; Time advances
+    per call; after a flush the context steps on unbatched (the drop-in loop of INTEGRATION.md)."""
+    cfg, parts = cases.get(case).build()
+    with MphSolver(cfg, parts) as a, MphSolver(cfg, parts) as b:
+        a.step(21)
+        b.step_batching(True)
+        for k in range(21):
+            b.step(1)
+        assert a.time == b.time
+        for f in CHUNK_FIELDS:   # the first get launches the 5 pending steps
+            assert np.array_equal(a.get(f), b.get(f), equal_nan=True), (case, f)
+        a.compute_virial()
+        b.compute_virial()
+        for f in ["VirialStressAtParticle", "VirialPressureAtParticle"]:
+            assert np.array_equal(a.get(f), b.get(f), equal_nan=True), (case, f)
+        a.step(3)
+        for _ in range(3):
+            b.step(1)
+        b.step_batching(False)   # flushes
+        b.step(2)
+        a.step(2)
+        for f in ["Position", "Velocity", "Force", "PressureP"]:
+            assert np.array_equal(a.get(f), b.get(f), equal_nan=True), (case, f)
+
+
+def test_gpu_step_batching_reports_errors():
+    """With step batching a diverged state is still MPH_ERR_NONFINITE: from a later mph_step once
+    the launched batch's flags have landed, or at the latest from mph_synchronize."""
+    from particlemethod_fsi_amd.solver import MphError
+    cfg, parts = cases.get("dam2d").build()
+    with MphSolver(cfg, parts) as s:
+        s.step(2)
+        pos = s.get("Position")
+        pos[100, 0] = np.nan
+        s.set("Position", pos)
+        s.step_batching(True)
+        with pytest.raises(MphError) as e:
+            for _ in range(24):
+                s.step(1)
+            s.synchronize()
+        assert e.value.code == -9
+
+
 def test_gpu_nonfinite_state_is_an_error_not_a_fault():
     """A diverged state (NaN position) is reported as MPH_ERR_NONFINITE by the next step; every
     index the kernels derive from it stays in range (no device fault)."""

@@ -6,7 +6,7 @@ text file): per kernel and launch
                      1024 SIMDs x the launch's quad-cycles (GRBM_GUI_ACTIVE summed over 8 XCDs)
   l1_lookups_per_clk L1 (TCP) tag lookups per clock per CU (one per clock is the ceiling)
   valu_per_wave, vmem_per_wave, tcp_per_vmem, lds_conflict_frac (bank-conflict cycles over the
-                     launch's cycles per CU)
+                     launch's cycles per CU), ta_busy (texture-address unit busy fraction)
 
 usage: python tools/pmc_issue.py gpurun_out/pmc_base.txt case > profiles/pmc_issue.json
 """
@@ -46,6 +46,9 @@ def main():
             "vmem_per_wave": round(c.get("SQ_INSTS_VMEM_RD", 0) / w, 1),
             "tcp_per_vmem": round(c.get("TCP_TOTAL_CACHE_ACCESSES_sum", 0) / max(c.get("SQ_INSTS_VMEM_RD", 0), 1), 2),
             "lds_conflict_frac": round(c.get("SQ_LDS_BANK_CONFLICT", 0) / (NCU * cyc), 4),
+            # texture-address unit: TA_BUSY_avr (busy cycles averaged over the TA instances) over
+            # the launch's cycles
+            "ta_busy": round(c.get("TA_BUSY_avr", 0) / cyc, 4),
             "cycles_per_xcd": round(cyc),
         }
     json.dump(res, sys.stdout, indent=1)

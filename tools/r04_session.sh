@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${OUT:-r04s}
 mkdir -p $OUT
 if [ "${K-}" != none ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread ${K:+-k "$K"} \
+  timeout -k 10 ${PYT_TIMEOUT:-900} python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread ${K:+-k "$K"} \
       > $OUT/pytest_gpu.log 2>&1
   rc=$?
   echo "pytest rc=$rc" >> $OUT/pytest_gpu.log
