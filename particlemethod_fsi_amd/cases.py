@@ -314,6 +314,13 @@ _reg(Case("seam3d", 3, "dam", 0.001, (0.0, 0.0, 0.0), (0.03, 0.04, 0.02), [
     Cuboid(1, (0.0, 0.0, 0.0), (0.03, 0.006, 0.02), 0.001, (0.0, -_U, 0.0)),
     Cuboid(1, (0.0, 0.034, 0.0), (0.03, 0.04, 0.02), 0.001, (_U, 0.0, 0.0)),
 ], note="fluid across the periodic y face, empty band between (grid origin / face rule)"))
+# a box of water on a floor 11 m along a 12 m periodic z axis: ~9,200 GPU cells along the search's
+# contiguous axis, the water at cell ~8,460, past the 8,192 where an absolute FP32 cell coordinate
+# would lose the 1e-3-cell margin of the search's column ranges
+_reg(Case("longz3d", 3, "dam", 0.001, (-0.01, -0.01, 0.0), (0.04, 0.04, 12.0), [
+    Cuboid(4, (0.0, 0.0, 11.0), (0.03, 0.003, 11.03), 0.001),
+    Cuboid(1, (0.003, 0.003, 11.003), (0.027, 0.02, 11.027), 0.001),
+], note="water on a floor far along a long contiguous cell axis"))
 _reg(Case("channel3d_st", 3, "dam", 0.001, CASES["channel3d"].lower, CASES["channel3d"].upper,
           CASES["channel3d"].cuboids, data_changes=_ST, note="channel3d with surface tension"))
 

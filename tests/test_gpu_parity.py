@@ -81,7 +81,7 @@ def test_gpu_matches_reference_golden(case):
 @pytest.mark.parametrize("case,nsteps", [("dam2d", 20), ("gate3d", 12), ("gate3d_sub", 20),
                                           ("box3d_st", 20), ("rolling2d", 20), ("rolling3d", 20),
                                           ("turek2d", 20), ("movwall3d", 10), ("hydro2d", 20),
-                                          ("channel3d", 10), ("seam3d", 10)])
+                                          ("channel3d", 10), ("seam3d", 10), ("longz3d", 10)])
 def test_gpu_matches_oracle_every_step(case, nsteps):
     """Step-by-step against the oracle: all fields, including the ones the golden files do not
     store at every step (Force, DensityA, GravityCenter, VolStrainP, ...).  gate3d (ElasticDt =
