@@ -114,6 +114,7 @@ struct MphCtx {
     int *nbr = nullptr, *ncount = nullptr;
     int* list_hdr = nullptr;     // per-wave headers of the compact 16-bit lists (kLhdr ints each)
     int2* win_hdr = nullptr;     // MPH_PA_STAGED builds: per-wave column windows (kWinHdr each)
+    unsigned long long* wave_log = nullptr;   // MPH_DIAG_XCD >= 2 builds: the search's per-wave log
     double *pres = nullptr, *gx = nullptr, *gy = nullptr, *gz = nullptr, *pa = nullptr;
     double4 *force = nullptr, *acc = nullptr, *fpart = nullptr, *rec = nullptr;
     double *dens_a = nullptr, *vstrain = nullptr, *divp = nullptr;

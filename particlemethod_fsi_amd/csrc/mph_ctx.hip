@@ -1172,6 +1172,27 @@ __attribute__((visibility("default"))) int mph_diag_xcd(MphCtx* c, unsigned long
     }
     return MPH_OK;
 }
+
+// Diagnostic builds (MPH_DIAG_XCD >= 2): the search's per-wave log {start, end, XCC_ID} of its last
+// launch (wall_clock64 ticks), up to max_waves records into out; returns the record count.
+__attribute__((visibility("default"))) int mph_diag_waves(MphCtx* c, unsigned long long* out, int max_waves)
+{
+    if (!c || !out) return MPH_ERR_ARG;
+    HIP_OK(c, hipSetDevice(c->device));
+    const int nw = ((c->n + 255) / 256) * 4;   // the search grid at MPH_LB = 256
+    if (!c->wave_log) {   // first call: allocate and hand the log to the kernels
+        CK(dalloc(c, &c->wave_log, 3 * (size_t)nw));
+        HIP_OK(c, hipMemset(c->wave_log, 0, sizeof(unsigned long long) * 3 * (size_t)nw));
+        char* dev = reinterpret_cast<char*>(c->dst);
+        HIP_OK(c, hipMemcpy(dev + offsetof(DevState, wave_log), &c->wave_log, sizeof(void*), hipMemcpyHostToDevice));
+        HIP_OK(c, hipMemcpy(dev + offsetof(DevState, wave_log_n), &nw, sizeof(int), hipMemcpyHostToDevice));
+        return 0;
+    }
+    HIP_OK(c, hipDeviceSynchronize());
+    const int k = std::min(nw, max_waves);
+    HIP_OK(c, hipMemcpy(out, c->wave_log, sizeof(unsigned long long) * 3 * (size_t)k, hipMemcpyDeviceToHost));
+    return k;
+}
 #endif
 
 void mph_destroy(MphCtx* c)

@@ -300,8 +300,11 @@ __device__ __forceinline__ int xcd_block(int b, int nb)
 struct XcdProbe {
     unsigned long long* d;
     unsigned long long t0;
+    unsigned long long* log;
+    int log_n;
     __device__ XcdProbe(const DevState* st, int k)
-        : d(st ? &const_cast<DevState*>(st)->xcd_diag[k][0][0] : nullptr), t0(wall_clock64()) {}
+        : d(st ? &const_cast<DevState*>(st)->xcd_diag[k][0][0] : nullptr), t0(wall_clock64()),
+          log(st && k == 0 ? st->wave_log : nullptr), log_n(st ? st->wave_log_n : 0) {}
     __device__ ~XcdProbe()
     {
         if (d && __lane_id() == 0) {
@@ -311,6 +314,14 @@ struct XcdProbe {
             atomicMax(d + 8 + x, t1);
             atomicAdd(d + 16 + x, t1 - t0);
             atomicAdd(d + 24 + x, 1ull);
+            if (MPH_DIAG_XCD >= 2 && log) {   // the search's waves, one record each
+                const int slot = (int)blockIdx.x * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
+                if (slot < log_n) {
+                    log[3 * (size_t)slot] = t0;
+                    log[3 * (size_t)slot + 1] = t1;
+                    log[3 * (size_t)slot + 2] = (unsigned long long)x;
+                }
+            }
         }
     }
 };

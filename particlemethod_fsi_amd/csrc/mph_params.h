@@ -183,6 +183,10 @@ struct DevState {
     // diagnostic build only (tools/xcd_diag.py): per list kernel (search, pass A, pass B) and XCD,
     // the first wave's start, the last wave's end (wall_clock64), the summed wave time, the waves
     unsigned long long xcd_diag[3][4][8];
+    // per-wave log of the search (MPH_DIAG_XCD >= 2): {start, end, XCC_ID} per wave slot of the launch
+    unsigned long long* wave_log;
+    int wave_log_n;
+    int wave_log_pad;
 #endif
 };
 // the part of DevState the host reads back after steps (the error bits and the step scalars)
