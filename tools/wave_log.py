@@ -32,7 +32,7 @@ def main():
         fn = s._L.mph_diag_waves
         fn.restype = ctypes.c_int
         fn.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-        nmax = ((parts.n + 255) // 256) * 4
+        nmax = (((parts.n + 255) // 256) * 5 // 4 + 16) * 4
         buf = (ctypes.c_ulonglong * (3 * nmax))()
         fn(s._h, buf, nmax)          # allocates the log
         s.step(args.warmup)
@@ -40,11 +40,13 @@ def main():
         k = fn(s._h, buf, nmax)
     a = np.frombuffer(buf, dtype=np.uint64, count=3 * k).reshape(k, 3).astype(np.int64)
     a = a[a[:, 1] > 0]
+    idle = int(((a[:, 1] - a[:, 0]) * TICK_US < 2.0).sum())   # waves of a slack grid that found no tile
+    a = a[(a[:, 1] - a[:, 0]) * TICK_US >= 2.0]
     t0, t1, x = a[:, 0], a[:, 1], a[:, 2]
     base = t0.min()
     dur = (t1 - t0) * TICK_US
     span = (t1.max() - base) * TICK_US
-    out = {"case": args.case, "waves": int(len(a)), "span_us": round(span, 2),
+    out = {"case": args.case, "waves": int(len(a)), "idle_waves": idle, "span_us": round(span, 2),
            "wave_us": {p: round(float(np.percentile(dur, q)), 2) for p, q in
                        (("p10", 10), ("p50", 50), ("p90", 90), ("p99", 99), ("max", 100))},
            "wave_us_mean": round(float(dur.mean()), 2)}
@@ -68,6 +70,11 @@ def main():
                        "last_start_us": round(float(s0[m].max()), 2),
                        "mean_wave_us": round(float(dur[m].mean()), 2)}
     out["per_xcd"] = per
+    # the hardware's block -> XCD assignment: per logical XCD j = block & 7, the XCC_IDs its waves ran on
+    slots = np.nonzero((np.frombuffer(buf, dtype=np.uint64, count=3 * k).reshape(k, 3)[:, 1] > 0))[0]
+    raw = np.frombuffer(buf, dtype=np.uint64, count=3 * k).reshape(k, 3)[slots]
+    logical = (slots // 4) % 8
+    out["logical_to_xcc"] = {int(j): sorted({int(v) for v in raw[logical == j, 2]}) for j in range(8)}
     # the slowest waves: their slot (block * 4 + wave) and duration
     order = np.argsort(-dur)[:20]
     out["slowest"] = [[int(i), round(float(dur[i]), 2), round(float(s0[i]), 2)] for i in order]
