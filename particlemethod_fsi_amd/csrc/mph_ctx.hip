@@ -426,6 +426,8 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         CK(dalloc(c, &s->type, m)); CK(dalloc(c, &s->id, m));
     }
     CK(dalloc(c, &c->A.p6, 3 * (size_t)cap));
+    // the search's FP32 candidate records (MPH_SEARCH_F32 builds read them; kPad past the last)
+    CK(dalloc(c, &c->A.f4, (size_t)cap + kPad));
     CK(dalloc(c, &c->rank_of, cap));
     CK(dalloc(c, &c->key, cap)); CK(dalloc(c, &c->slot, cap)); CK(dalloc(c, &c->tmp, cap));
     CK(dalloc(c, &c->cnt, c->P.ncell)); CK(dalloc(c, &c->start, (size_t)c->P.ncell + 1));

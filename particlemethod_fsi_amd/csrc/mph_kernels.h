@@ -60,6 +60,9 @@ struct Soa {
     // (profiles/r01: TA ~64 % busy in pass A); the type of j travels in the list entry instead
     // (kTypeShift), so a neighbour costs 48 gathered bytes instead of 64.
     double2* p6 = nullptr;
+    // MPH_SEARCH_F32 builds: {x, y, z} - domain centre in FP32 and the type's bits, 16 bytes, the
+    // search's staged candidate records (sorted set A only)
+    float4* f4 = nullptr;
 };
 
 // Slab mode: the kept part [0, *n) of the redistributed set C is not copied -- entry v lives in

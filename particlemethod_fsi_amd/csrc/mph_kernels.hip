@@ -85,6 +85,14 @@
 // (measured, opt-in)
 #define MPH_PA_STAGED 0
 #endif
+#ifndef MPH_SEARCH_F32
+// the search stages 16-byte FP32 candidate records {x, y, z, type} (Soa.f4, written by
+// k_rank_scatter) instead of 28 bytes of FP64 x, y, z and type, and decides in FP32 outside a band
+// around the cutoff wide enough for the records' rounding (DevParams.rc2f_lo/hi, set_uniforms);
+// inside it the FP64 test on the global positions decides, so the lists are identical (D1M search
+// -7.5 %, profiles/r04/search_f32/)
+#define MPH_SEARCH_F32 1
+#endif
 #ifndef MPH_DIAG_PA
 #define MPH_DIAG_PA 0   // diagnostic builds: the staged pass A checks it used every entry (DevState.overflow 32)
 #endif
@@ -902,6 +910,9 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
         q[1] = make_double2(B.z[b], B.vx[b]);
         q[2] = make_double2(B.vy[b], B.vz[b]);
     }
+    if (MPH_SEARCH_F32 && A.f4)
+        A.f4[dst] = make_float4((float)(B.x[b] - P.cref[0]), (float)(B.y[b] - P.cref[1]),
+                                (float)(B.z[b] - P.cref[2]), __int_as_float(B.type[b]));
     if (dst_of) dst_of[p] = dst;   // slab mode: ids are global (ghosts negative)
     else if (rank_of) rank_of[id] = dst;
 }
@@ -1395,7 +1406,51 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             soff += span == 0x7fffffff ? 256 : 0;
             return;
         }
-        if (span <= CAP) {
+        if (MPH_SEARCH_F32 && !C16 && span <= CAP) {
+            // FP32 records: candidate j at record j - mn, 64 records (1 KB) per instruction
+            float4* s4 = reinterpret_cast<float4*>(sx);
+            for (int p = 0; p * 64 < span; ++p)   // wave-uniform
+                if (p * 64 + lane < span) __builtin_amdgcn_global_load_lds(A.f4 + mn + p * 64 + lane, s4 + p * 64, 16, 0, 0);
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the records (and column col + 1's start[]) landed
+            __builtin_amdgcn_wave_barrier();
+            const float xf = (float)(xi - P.cref[0]), yf = (float)(yi - P.cref[1]), zf = (float)(zi - P.cref[2]);
+            const float lof = P.rc2f_lo, hif = P.rc2f_hi;
+            auto test32 = [&](auto self_tag) {
+                constexpr bool SELF = decltype(self_tag)::value;
+                for (int j0 = jb; j0 < je; j0 += SB) {
+                    float4 r[SB];
+#pragma unroll
+                    for (int u = 0; u < SB; ++u) r[u] = s4[j0 - mn + u];
+#pragma unroll
+                    for (int u = 0; u < SB; ++u) {
+                        const int j = j0 + u;
+                        const float dx = r[u].x - xf, dy = r[u].y - yf, dz = r[u].z - zf;
+                        const float r2f = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
+                        bool live = true;
+                        if (u > 0) live = j < je;
+                        if (SELF) live = live && j != i;
+                        bool a = live && r2f <= lof;
+                        const bool band = live && !a && r2f <= hif;
+                        if (__ballot(band)) {   // rare: the FP64 test on the global positions
+                            if (band) {
+                                const double ddx = A.x[j] - xi, ddy = A.y[j] - yi, ddz = A.z[j] - zi;
+                                const double r2a = fma(ddx, ddx, fma(ddy, ddy, ddz * ddz));
+                                const bool in = r2a <= lo2;
+                                a = in;
+                                if ((r2a <= hi2) != in) a = accept_band(P, ddx, ddy, ddz);
+                            }
+                        }
+                        if (a) {
+                            __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, __float_as_int(r[u].w)), tile_rsrc, soff, 0, 0);
+                            soff += 256;
+                        }
+                    }
+                }
+            };
+            if (col == kSelfCol) test32(std::true_type{});
+            else test32(std::false_type{});
+            __builtin_amdgcn_wave_barrier();   // every lane done reading before the next staging
+        } else if (span <= CAP) {
             // the window from a 16-byte-aligned start: candidate j sits at j - mn + da in x, y, z
             // and at j - mn + ta in the types; pieces of 128 doubles / 256 ints per instruction,
             // lanes past the window masked (the arrays hold kPad elements beyond any window)

@@ -1,6 +1,7 @@
 // mph_params.h -- plain-old-data structures shared by the host layer (mph_host.cpp) and the
 // HIP kernels (mph_kernels.hip).  No HIP types here, so the host files build with g++/hipcc alike.
 #pragma once
+#include <cmath>
 
 #include <cstddef>
 #include <cstdint>
@@ -139,6 +140,8 @@ struct DevParams {
     double rc2_trim;         // rc2 (1 + 4e-6): the column-trimming bound
     double cwid[3];          // 1 / ginv: GPU cell widths
     double rg_r2g;           // rg / r2g (GravityCenter, DiffuseInterface)
+    double cref[3];          // MPH_SEARCH_F32: the domain centre the FP32 records are taken from
+    float rc2f_lo, rc2f_hi;  // MPH_SEARCH_F32: below lo the FP32 r^2 accepts, above hi it rejects
 };
 
 // Derived uniforms of DevParams (same expressions the kernels used, so the same bits).
@@ -149,6 +152,18 @@ inline void set_uniforms(DevParams& P)
     P.rc2_trim = P.rc2 * (1.0 + 4e-6);
     for (int d = 0; d < 3; ++d) P.cwid[d] = 1.0 / P.ginv[d];
     P.rg_r2g = P.rg / P.r2g;
+    // FP32 records (MPH_SEARCH_F32): coordinates within half a domain width of the centre, each
+    // rounded once (<= 2^-24 x that); a difference is off by <= 2^-23 hw, r^2 near the cutoff by
+    // <= 2 sqrt(3) 2^-23 hw / rc relative plus the FP32 sum's few ulp: the band is twice that
+    double hwm = 0.0;
+    for (int d = 0; d < 3; ++d) {
+        P.cref[d] = P.dmin[d] + P.hw[d];
+        hwm = P.hw[d] > hwm ? P.hw[d] : hwm;
+    }
+    const double rc = std::sqrt(P.rc2);
+    const double delta = 2.0 * (2.0 * 1.7320508 * hwm * 1.1920929e-7 / rc) + 4.0e-6;
+    P.rc2f_lo = (float)(P.rc2 * (1.0 - delta));
+    P.rc2f_hi = (float)(P.rc2 * (1.0 + delta));
 }
 
 // work histogram of the XCD map: waves in 4096 equal runs (D16M: ~60 waves per run, so the
