@@ -1428,12 +1428,21 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                         const float r2f = fmaf(dx, dx, fmaf(dy, dy, dz * dz));
                         bool live = true;
                         if (u > 0) live = j < je;
-                        if (SELF) live = live && j != i;
-                        bool a = live && r2f <= lof;
-                        const bool band = live && !a && r2f <= hif;
-                        if (__ballot(band)) {   // rare: the FP64 test on the global positions
-                            if (band) {
-                                const double ddx = A.x[j] - xi, ddy = A.y[j] - yi, ddz = A.z[j] - zi;
+                        if (SELF) live = live & (j != i);
+                        // two compares; the band as wave masks (SALU), its lane bit read only inside
+                        // the rare branch
+                        const bool le_lo = r2f <= lof, le_hi = r2f <= hif;
+                        bool a = live & le_lo;
+                        const unsigned long long mband = __builtin_amdgcn_ballot_w64(le_hi) &
+                                                         ~__builtin_amdgcn_ballot_w64(le_lo) &
+                                                         __builtin_amdgcn_ballot_w64(live);
+                        if (mband) {   // rare (wave-uniform): the FP64 test on the global positions
+                            if (le_hi & !le_lo & live) {
+                                // the index hidden from the loop's induction analysis, so the addresses
+                                // are formed here and not carried through the loop
+                                int jj = j;
+                                asm volatile("" : "+v"(jj));
+                                const double ddx = A.x[jj] - xi, ddy = A.y[jj] - yi, ddz = A.z[jj] - zi;
                                 const double r2a = fma(ddx, ddx, fma(ddy, ddy, ddz * ddz));
                                 const bool in = r2a <= lo2;
                                 a = in;
