@@ -78,6 +78,9 @@
 // waves (8 per SIMD) fit the 160 KB of LDS; wider windows take the global-gather loop
 #define MPH_LDS_CAP 176
 #endif
+#ifndef MPH_CAP32
+#define MPH_CAP32 1   // FP32-record windows up to the staging area's 16-byte capacity (313 at 176)
+#endif
 
 #ifndef MPH_PA_STAGED
 // pass A reads each stencil column's window of 48-byte records from LDS, staged once per wave
@@ -1246,6 +1249,8 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                                                    int* lh, unsigned short* o16, DevState* dst, int2* whdr)
 {
     constexpr int SD = stage_d(CAP, SB);
+    // FP32 records fill the whole FP64 staging area: 16 bytes each, SB past the window's end
+    constexpr int kCap32 = MPH_CAP32 ? stage_words(CAP, SB) / 2 - SB - 1 : CAP;
     double* sy = sx + SD;
     double* sz = sx + 2 * SD;
     int* st = reinterpret_cast<int*>(sx + 3 * SD);
@@ -1406,7 +1411,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             soff += span == 0x7fffffff ? 256 : 0;
             return;
         }
-        if (MPH_SEARCH_F32 && !C16 && span <= CAP) {
+        if (MPH_SEARCH_F32 && !C16 && span <= kCap32) {
             // FP32 records: candidate j at record j - mn, 64 records (1 KB) per instruction
             float4* s4 = reinterpret_cast<float4*>(sx);
             for (int p = 0; p * 64 < span; ++p)   // wave-uniform
