@@ -78,6 +78,9 @@
 // waves (8 per SIMD) fit the 160 KB of LDS; wider windows take the global-gather loop
 #define MPH_LDS_CAP 176
 #endif
+#ifndef MPH_SPLIT32
+#define MPH_SPLIT32 1   // a wave across two cell rows stages its two runs of FP32 records (scan_candidates_lds)
+#endif
 #ifndef MPH_CAP32
 #define MPH_CAP32 1   // FP32-record windows up to the staging area's 16-byte capacity (313 at 176)
 #endif
@@ -1411,11 +1414,45 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             soff += span == 0x7fffffff ? 256 : 0;
             return;
         }
-        if (MPH_SEARCH_F32 && !C16 && span <= kCap32) {
-            // FP32 records: candidate j at record j - mn, 64 records (1 KB) per instruction
+        // A window wider than the staging area is mostly a wave across two cell rows: its lanes' ranges
+        // form two runs far apart.  Split the lanes at the widest gap (a lane whose range starts past
+        // every earlier lane's end) and stage each run's window, one after the other, when both fit.
+        int lbase = mn, n1 = span, m2 = 0, n2 = 0;   // lane's record index j - lbase; the two windows
+        bool two = false;
+        if (MPH_SEARCH_F32 && MPH_SPLIT32 != 0 && !C16 && span > (MPH_SPLIT32 > 1 ? MPH_SPLIT32 : kCap32)) {   // wave-uniform, rare
+            int pm = any ? je : -1;   // running max of the ends over the lanes below and at this one
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int v = __shfl_up(pm, o, 64);
+                if (lane >= o) pm = max(pm, v);
+            }
+            int ex = __shfl_up(pm, 1, 64);
+            if (lane == 0) ex = -1;
+            const int gap = any && ex >= 0 ? jb - ex : -1;
+            const int gmax = wave_max(gap);
+            if (gmax > 0) {
+                const int sl = __ffsll((long long)__ballot(gap == gmax)) - 1;
+                const bool hi_run = lane >= sl;
+                const int m1 = wave_min(any && !hi_run ? jb : 0x7fffffff);
+                const int x1 = __builtin_amdgcn_readlane(ex, sl);   // the low run's end
+                m2 = wave_min(any && hi_run ? jb : 0x7fffffff);
+                n1 = x1 - m1;
+                n2 = mx - m2;
+                if (n1 + n2 <= kCap32) {
+                    two = true;
+                    lbase = hi_run ? m2 - n1 : m1;
+                    mn = m1;
+                }
+            }
+        }
+        if (MPH_SEARCH_F32 && !C16 && (span <= kCap32 || two)) {
+            // FP32 records: candidate j at record j - lbase, 64 records (1 KB) per instruction
             float4* s4 = reinterpret_cast<float4*>(sx);
-            for (int p = 0; p * 64 < span; ++p)   // wave-uniform
-                if (p * 64 + lane < span) __builtin_amdgcn_global_load_lds(A.f4 + mn + p * 64 + lane, s4 + p * 64, 16, 0, 0);
+            for (int p = 0; p * 64 < n1; ++p)   // wave-uniform
+                if (p * 64 + lane < n1) __builtin_amdgcn_global_load_lds(A.f4 + mn + p * 64 + lane, s4 + p * 64, 16, 0, 0);
+            for (int p = 0; p * 64 < n2; ++p)   // the second run (two), after the first
+                if (p * 64 + lane < n2)
+                    __builtin_amdgcn_global_load_lds(A.f4 + m2 + p * 64 + lane, s4 + n1 + p * 64, 16, 0, 0);
             __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the records (and column col + 1's start[]) landed
             __builtin_amdgcn_wave_barrier();
             const float xf = (float)(xi - P.cref[0]), yf = (float)(yi - P.cref[1]), zf = (float)(zi - P.cref[2]);
@@ -1425,7 +1462,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                 for (int j0 = jb; j0 < je; j0 += SB) {
                     float4 r[SB];
 #pragma unroll
-                    for (int u = 0; u < SB; ++u) r[u] = s4[j0 - mn + u];
+                    for (int u = 0; u < SB; ++u) r[u] = s4[j0 - lbase + u];
 #pragma unroll
                     for (int u = 0; u < SB; ++u) {
                         const int j = j0 + u;
