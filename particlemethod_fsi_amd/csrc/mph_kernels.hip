@@ -78,6 +78,9 @@
 // waves (8 per SIMD) fit the 160 KB of LDS; wider windows take the global-gather loop
 #define MPH_LDS_CAP 176
 #endif
+#ifndef MPH_COLR_LEAN
+#define MPH_COLR_LEAN 1   // scan_candidates_lds: the column ranges in fewer operations (same bounds)
+#endif
 #ifndef MPH_SPLIT32
 #define MPH_SPLIT32 1   // a wave across two cell rows stages its two runs of FP32 records (scan_candidates_lds)
 #endif
@@ -1287,21 +1290,45 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     // (ua ginv - c lies in [0, 1) for an interior lane), so the margin holds on any grid size.
     // The gap along the slowest axis changes once per group of columns (visited in order).
     constexpr float kDn = 1.0f - 1.0f / (1 << 20), kUp = 1.0f + 1.0f / (1 << 19);
+#if MPH_COLR_LEAN
+    // The lean form (same bounds, fewer operations per column): an inactive lane gets a negative
+    // cutoff (no column opens); the gap margin mu is folded into the subtracted offsets; the range
+    // ends carry a bias of kBias cells, so truncation is floor (the ends lie within a few cells of
+    // the own cell) and the bias comes off in the row base.  Each added rounding is below 1e-5 cells
+    // or 2^-24 of a cell width, far inside the margins.
+    constexpr float kBias = 32.0f;
+    const float rcm2f = act ? (float)P.rc2_trim * kUp : -1.0f;
+#else
     const float rcm2f = (float)P.rc2_trim * kUp;
+#endif
     float gx2f = 0.0f;
     const int c0l = cc[X::A0], c1l = DIM == 3 ? cc[X::A1] : 0;
     const float cw0f = (float)cw0, cw1f = (float)cw1;
     const float f0 = (float)(uu[X::A0] - c0l * cw0), f1 = DIM == 3 ? (float)(uu[X::A1] - c1l * cw1) : 0.0f;
-    const float g0p = f0, g0m = cw0f - f0, g1p = f1, g1m = cw1f - f1;   // subtracted for d > 0 / d < 0
     const float mu0 = cw0f * (1.0f / (1 << 20)), mu1 = cw1f * (1.0f / (1 << 20));
+#if MPH_COLR_LEAN
+    const float g0p = f0 + mu0, g0m = (cw0f - f0) + mu0, g1p = f1 + mu1, g1m = (cw1f - f1) + mu1;
+#else
+    const float g0p = f0, g0m = cw0f - f0, g1p = f1, g1m = cw1f - f1;   // subtracted for d > 0 / d < 0
+#endif
     const float ginvaf = (float)ginva;
     const float caf = (float)(ua * ginva - (double)cca);   // offset inside the own cell, cells
+#if MPH_COLR_LEAN
+    const float cal = (caf - 1e-3f) + kBias, cah = (caf + 1e-3f) + kBias;
+    const float rgf = kUp * ginvaf;
+    const int rowbase = (DIM == 3 ? (c0l * P.gc[X::A1] + c1l) * P.gc[X::A2] : c0l * P.gc[1]) + cca - (int)kBias;
+#else
     const int rowbase = (DIM == 3 ? (c0l * P.gc[X::A1] + c1l) * P.gc[X::A2] : c0l * P.gc[1]) + cca;
+#endif
     const int sa = P.sa;
     const __amdgpu_buffer_rsrc_t srs = arr_rsrc(start);
     auto gap32 = [](int d, float cwf, float gp, float gm, float mu) {
         if (d == 0) return 0.0f;
+#if MPH_COLR_LEAN
+        const float v = (float)(d > 0 ? d : -d) * cwf - (d > 0 ? gp : gm);
+#else
         const float v = (float)(d > 0 ? d : -d) * cwf - (d > 0 ? gp : gm) - mu;
+#endif
         return v > 0.0f ? v : 0.0f;
     };
     auto col_range = [&](int col, int& jb, int& je) {
@@ -1322,10 +1349,17 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             d2f = gx * gx * kDn;
             cofs = dxc * P.gc[1];
         }
+#if MPH_COLR_LEAN
+        const bool ok = d2f <= rcm2f;
+        const float rc = __builtin_amdgcn_sqrtf(fmaxf(rcm2f - d2f, 0.0f)) * rgf;   // half range, cells
+        const int lo = max((int)(cal - rc), (int)kBias - sa);
+        const int hi = min((int)(cah + rc), (int)kBias + sa);
+#else
         const bool ok = act && d2f <= rcm2f;
         const float rc = __builtin_amdgcn_sqrtf(fmaxf(rcm2f - d2f, 0.0f)) * kUp * ginvaf;   // half range, cells
         const int lo = max((int)floorf(caf - rc - 1e-3f), -sa);
         const int hi = min((int)floorf(caf + rc + 1e-3f), sa);
+#endif
         const int b = rowbase + cofs;
         // a lane without candidates reads start[0] twice (empty range)
         start_load2(srs, ok ? (unsigned)(b + lo) * 4u : 0u, ok ? (unsigned)(b + hi + 1) * 4u : 0u, jb, je);
