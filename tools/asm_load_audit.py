@@ -94,6 +94,9 @@ def audit(name, lines):
                     other = ops[2] if ops[1] == 'exec' else ops[1]
                     kv = dict(known).get(other)
                     vcc = 'nz' if kv == '-1' else ('z' if kv == '0' else None)
+                elif op == 's_andn2_b64' and dst == 'vcc' and len(ops) == 3 and ops[1] == 'exec':
+                    kv = dict(known).get(ops[2])   # vcc = exec & ~pair
+                    vcc = 'z' if kv == '-1' else ('nz' if kv == '0' else None)
                 elif dst == 'vcc' or (op.startswith('v_cmp') and 'vcc' in t.split()[1:2][0] if len(t.split()) > 1 else False):
                     vcc = None
                 if op == 's_branch':
