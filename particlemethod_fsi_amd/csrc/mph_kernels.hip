@@ -78,6 +78,9 @@
 // waves (8 per SIMD) fit the 160 KB of LDS; wider windows take the global-gather loop
 #define MPH_LDS_CAP 176
 #endif
+#ifndef MPH_BAND_MASK
+#define MPH_BAND_MASK 1   // scan_candidates_lds: the FP32 band's lanes selected by its wave mask
+#endif
 #ifndef MPH_COLR_LEAN
 #define MPH_COLR_LEAN 1   // scan_candidates_lds: the column ranges in fewer operations (same bounds)
 #endif
@@ -1513,7 +1516,8 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                                                          ~__builtin_amdgcn_ballot_w64(le_lo) &
                                                          __builtin_amdgcn_ballot_w64(live);
                         if (mband) {   // rare (wave-uniform): the FP64 test on the global positions
-                            if (le_hi & !le_lo & live) {
+                            // the band lanes straight from the mask (no per-lane compare)
+                            if (MPH_BAND_MASK ? __builtin_amdgcn_inverse_ballot_w64(mband) : (le_hi & !le_lo & live)) {
                                 // the index hidden from the loop's induction analysis, so the addresses
                                 // are formed here and not carried through the loop
                                 int jj = j;
