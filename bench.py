@@ -347,8 +347,10 @@ def main():
                 # fewer VALU per wave did not shorten it), else the larger of the two rates
                 res = v.get("binding") or ("valu_issue" if v["valu_busy"] >= v["l1_lookups_per_clk"]
                                            else "l1_tag_lookups")
-                per[k] = {"resource": res, "frac": max(v["valu_busy"], v["l1_lookups_per_clk"]),
-                          "valu_issue": v["valu_busy"], "l1_tag_lookups_per_clk_cu": v["l1_lookups_per_clk"]}
+                ta = v.get("ta_busy", 0.0)   # texture-address unit busy fraction
+                per[k] = {"resource": res, "frac": max(v["valu_busy"], v["l1_lookups_per_clk"], ta),
+                          "valu_issue": v["valu_busy"], "l1_tag_lookups_per_clk_cu": v["l1_lookups_per_clk"],
+                          "ta_busy": ta}
                 if v.get("binding_note"):
                     per[k]["note"] = v["binding_note"]
             if per:
