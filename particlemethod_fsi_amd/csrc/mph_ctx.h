@@ -82,6 +82,7 @@ struct MphCtx {
     bool stepped = false;
     hipStream_t stream = nullptr;
     hipGraphExec_t graph1 = nullptr, graph8 = nullptr;
+    hipGraphExec_t graph1t = nullptr;   // one step without the output-only stores (single context)
     // step batching (mph_set_step_batching): single mph_step calls accumulate into 8-step graphs;
     // `pending` steps are accepted but not launched yet, `unchecked`: batches launched whose error
     // flags have not been read; the flags of the last launched batch land in hs_pin (pinned)

@@ -138,11 +138,13 @@ void enqueue_step(const Launch& L, bool last, hipEvent_t* ev = nullptr)
     if (ev) (void)hipEventRecord(ev[2], L.stream);
 }
 
-int capture(MphCtx* c, int steps, hipGraphExec_t* out)
+// store_last = false: no step of the graph stores the output-only fields (graph1t, the steps of a
+// remainder before its last one)
+int capture(MphCtx* c, int steps, hipGraphExec_t* out, bool store_last = true)
 {
     hipGraph_t g = nullptr;
     HIP_OK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    for (int k = 0; k < steps; ++k) enqueue_step(c->L, k == steps - 1);
+    for (int k = 0; k < steps; ++k) enqueue_step(c->L, store_last && k == steps - 1);
     HIP_OK(c, hipStreamEndCapture(c->stream, &g));
     HIP_OK(c, hipGraphInstantiate(out, g, nullptr, nullptr, 0));
     HIP_OK(c, hipGraphDestroy(g));
@@ -150,13 +152,22 @@ int capture(MphCtx* c, int steps, hipGraphExec_t* out)
     return MPH_OK;
 }
 
-// Both step graphs, captured at the first mph_step whatever its count: a caller that warms up with
+// The step graphs, captured at the first mph_step whatever its count: a caller that warms up with
 // fewer than 8 steps (the driver's bench: 5) would otherwise capture and upload the 8-step graph
 // inside its first long run.
 static int capture_graphs(MphCtx* c)
 {
     if (!c->graph1) CK(capture(c, 1, &c->graph1));
+    if (!c->graph1t) CK(capture(c, 1, &c->graph1t, false));
     if (!c->graph8) CK(capture(c, 8, &c->graph8));
+    return MPH_OK;
+}
+
+// `left` (< 8) single steps: the output-only stores on the last one only, as in an 8-step batch
+static int launch_singles(MphCtx* c, int left)
+{
+    for (; left > 1; --left) HIP_OK(c, hipGraphLaunch(c->graph1t, c->stream));
+    if (left == 1) HIP_OK(c, hipGraphLaunch(c->graph1, c->stream));
     return MPH_OK;
 }
 
@@ -680,7 +691,8 @@ static int ctx_flush(MphCtx* c)
     if (!c->pending && !c->unchecked) return MPH_OK;
     HIP_OK(c, hipSetDevice(c->device));
     if (c->pending) CK(capture_graphs(c));
-    for (; c->pending > 0; --c->pending) HIP_OK(c, hipGraphLaunch(c->graph1, c->stream));
+    if (c->pending) CK(launch_singles(c, c->pending));
+    c->pending = 0;
     c->unchecked = false;
     DevState hs;
     HIP_OK(c, hipMemcpyAsync(&hs, c->dst, kStateHead, hipMemcpyDeviceToHost, c->stream));
@@ -759,7 +771,7 @@ int mph_step(MphCtx* c, int nsteps)
     } else {
         CK(capture_graphs(c));
         while (left >= 8) { HIP_OK(c, hipGraphLaunch(c->graph8, c->stream)); left -= 8; }
-        while (left > 0) { HIP_OK(c, hipGraphLaunch(c->graph1, c->stream)); left -= 1; }
+        CK(launch_singles(c, left));
     }
     for (int k = 0; k < nsteps; ++k) c->time += c->cfg.dt;
     c->stepped = true;
@@ -1207,6 +1219,7 @@ void mph_destroy(MphCtx* c)
     if (c->ev_status) (void)hipEventDestroy(c->ev_status);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->graph1) (void)hipGraphExecDestroy(c->graph1);
+    if (c->graph1t) (void)hipGraphExecDestroy(c->graph1t);
     if (c->graph8) (void)hipGraphExecDestroy(c->graph8);
     for (auto* v : {&c->ev8, &c->ev_vir})
         for (hipEvent_t e : *v) (void)hipEventDestroy(e);

@@ -186,6 +186,23 @@ def test_gpu_graph_chunking_equivalence(case):
             assert np.array_equal(a.get(f), b.get(f), equal_nan=True), (case, f)
 
 
+@pytest.mark.parametrize("case", ["box3d_st", "gate2d"])
+def test_gpu_remainder_steps_equivalence(case):
+    """mph_step(13) (one 8-step graph, then 4 single steps without the output-only stores and one
+    with them) == 13 x mph_step(1), bitwise, for every field mph_get returns and the virial."""
+    cfg, parts = cases.get(case).build()
+    with MphSolver(cfg, parts) as a, MphSolver(cfg, parts) as b:
+        a.step(13)
+        for _ in range(13):
+            b.step(1)
+        for f in CHUNK_FIELDS:
+            assert np.array_equal(a.get(f), b.get(f), equal_nan=True), (case, f)
+        a.compute_virial()
+        b.compute_virial()
+        for f in ["VirialStressAtParticle", "VirialPressureAtParticle"]:
+            assert np.array_equal(a.get(f), b.get(f), equal_nan=True), (case, f)
+
+
 @pytest.mark.parametrize("case", ["box3d", "box3d_st", "gate2d", "bar2d"])
 def test_gpu_step_batching_equivalence(case):
     """mph_set_step_batching: 21 x mph_step(1) (two 8-step graphs launched by the calls, 5 steps
