@@ -808,7 +808,7 @@ __global__ __launch_bounds__(1024) void k_scan_top(int* __restrict__ bsum, int n
 // top: bsum holds the raw block totals and every block sums its predecessors' itself (no
 // k_scan_top launch; used while the block count is small, kScanFusedTop)
 #ifndef MPH_SCAN_FUSED_TOP
-#define MPH_SCAN_FUSED_TOP 4096
+#define MPH_SCAN_FUSED_TOP 8192   // (the D16M / 8 slab ranks: no k_scan_top launch)
 #endif
 constexpr int kScanFusedTop = MPH_SCAN_FUSED_TOP;
 __global__ __launch_bounds__(kScanThreads) void k_scan_down(int* __restrict__ cnt, int ncell,
