@@ -382,6 +382,15 @@ int mph_dist_info(const MphCtx* ctx, int* out8);
  * ELL rows).  The compact format is opt-in at the default stencil (MPH_LIST16=1 at creation,
  * equal radii only; MPH_LIST16=0 forces ELL rows everywhere).                                 */
 int mph_list_formats(MphCtx* ctx, int* out2);
+/* The neighbour lists of calculateNeighbor themselves (main.cpp:1764-1772: Neighbor[i][k] = j for
+ * k < 512), for verification: the sets of the `count` particles [first, first + count) (original
+ * order) from the last search, each row as ascending original indices (the reference's rows are in
+ * its cell-scan order; the sets are what both define).  counts[count] receives each particle's
+ * NeighborCount; ids the rows back to back (row k starts at the sum of min(counts, 512) before
+ * it), ids_cap its capacity in ints.  Returns the number of ids written, or a negative MphStatus
+ * (MPH_ERR_ARG when ids_cap is too small).  Single contexts with 32-bit ELL rows only
+ * (MPH_ERR_UNSUPPORTED in slab mode or while a wave holds a compact 16-bit list).              */
+int mph_neighbor_rows(MphCtx* ctx, int first, int count, int* counts, int* ids, long long ids_cap);
 /* Particles currently owned by this rank (after the last migration); their original indices.  */
 int mph_owned_count(const MphCtx* ctx);
 int mph_owned_ids(MphCtx* ctx, int* out_ids);

@@ -62,6 +62,9 @@ class Case:
     # reference functions run once after the initialisation sums, e.g. the commented
     # setInitialVelocityProfile() call of main.cpp:571
     init_calls: tuple = ()
+    # off-lattice parity cases: every coordinate moved by a deterministic offset in
+    # [-jitter, jitter) x spacing (mphio.jitter); 0 = the generator's lattice
+    jitter: float = 0.0
 
     @property
     def ref_variant(self) -> str:
@@ -80,12 +83,18 @@ class Case:
     def build(self):
         """-> (MphConfig, Particles), exactly what the reference reads from data + grid files."""
         cfg, _ = self._config()
-        return cfg, mphio.generate(self.cuboids)
+        return cfg, self._particles()
+
+    def _particles(self):
+        p = mphio.generate(self.cuboids)
+        return mphio.jitter(p, self.spacing, self.jitter, self.dim) if self.jitter else p
 
     def build_window(self, axis: int, lo: float, hi: float):
         """-> (MphConfig, Particles, ids, n_glob): only the particles whose coordinate along `axis`
         lies in the periodic window [lo, hi) (a slab rank's share, mph_slab_window), generated
         without the rest of the problem; ids are their indices in build()'s order."""
+        if self.jitter:
+            raise ValueError("slab-local generation of a jittered case")
         cfg, _ = self._config()
         W = cfg.domain_max[axis] - cfg.domain_min[axis]
         parts, ids, n_glob = mphio.generate_window(self.cuboids, axis, lo, hi, cfg.domain_min[axis], W)
@@ -103,8 +112,7 @@ class Case:
         return cfg, None
 
     def grid_text(self) -> str:
-        return mphio.format_grid(mphio.generate(self.cuboids), self.spacing, self.lower, self.upper,
-                                 self.time0)
+        return mphio.format_grid(self._particles(), self.spacing, self.lower, self.upper, self.time0)
 
 
 def _apply_data(cfg, values):
@@ -290,6 +298,17 @@ _reg(Case("gate2d_sub", 2, "dam", 0.001, CASES["gate2d"].lower, CASES["gate2d"].
           CASES["gate2d"].cuboids, data_changes={"ElasticDt": [2e-5]}, note="gate2d, 5 substeps"))
 _reg(Case("gate3d_sub", 3, "dam", 0.001, CASES["gate3d"].lower, CASES["gate3d"].upper,
           CASES["gate3d"].cuboids, data_changes={"ElasticDt": [2.5e-5]}, note="gate3d, 4 substeps"))
+
+
+# Off-lattice 3-D cases: every particle of box3d / the sub-stepped gate moved by up to
+# +-0.3 dx per axis, so neighbour distances are no longer whole multiples of dx and pairs lie
+# anywhere around the cutoff -- the regime of a developed flow, for the search's FP32 band and the
+# sums' tolerances.
+_reg(Case("box3d_jit", 3, "dam", 0.001, CASES["box3d"].lower, CASES["box3d"].upper, CASES["box3d"].cuboids,
+          jitter=0.3, note="box3d with +-0.3 dx deterministic offsets"))
+_reg(Case("gate3d_jit", 3, "dam", 0.001, CASES["gate3d"].lower, CASES["gate3d"].upper, CASES["gate3d"].cuboids,
+          data_changes={"ElasticDt": [2.5e-5]}, jitter=0.3,
+          note="gate3d_sub with +-0.3 dx deterministic offsets"))
 
 
 # Slab-decomposition (multi-GPU) parity cases: a fluid layer over a floor, periodic along the

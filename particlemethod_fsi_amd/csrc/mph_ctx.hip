@@ -1167,6 +1167,65 @@ int mph_list_formats(MphCtx* c, int* out2)
     return MPH_OK;
 }
 
+int mph_neighbor_rows(MphCtx* c, int first, int count, int* counts, int* ids, long long ids_cap)
+{
+    if (!c || first < 0 || count < 0 || !counts || (!ids && ids_cap > 0)) return MPH_ERR_ARG;
+    CK(ctx_flush(c));
+    if (c->dist) return fail(c, MPH_ERR_UNSUPPORTED, "mph_neighbor_rows: single contexts only");
+    if ((long long)first + count > c->n) return fail(c, MPH_ERR_ARG, "mph_neighbor_rows: range past the particle count");
+    if (!count) return 0;
+    HIP_OK(c, hipSetDevice(c->device));
+    const int n = c->n, nt = (n + kTile - 1) / kTile;
+    if (c->L.lhdr) {   // the compact 16-bit rows are not decoded here
+        std::vector<int> h((size_t)nt * kLhdr);
+        HIP_OK(c, hipMemcpy(h.data(), c->list_hdr, sizeof(int) * h.size(), hipMemcpyDeviceToHost));
+        for (int t = 0; t < nt; ++t)
+            if (h[(size_t)t * kLhdr + kHdrFlag] == 1)
+                return fail(c, MPH_ERR_UNSUPPORTED, "mph_neighbor_rows: compact lists in use (MPH_LIST16)");
+    }
+    // the last search's rows are in its sorted order A: A.id maps a row (and an entry) back to the
+    // original index, ncount holds NeighborCount in the same order
+    std::vector<int> id(n), nc(n);
+    HIP_OK(c, hipMemcpy(id.data(), c->A.id, sizeof(int) * n, hipMemcpyDeviceToHost));
+    HIP_OK(c, hipMemcpy(nc.data(), c->ncount, sizeof(int) * n, hipMemcpyDeviceToHost));
+    std::vector<int> row_of(count, -1);
+    for (int s = 0; s < n; ++s)
+        if (id[s] >= first && id[s] < first + count) row_of[id[s] - first] = s;
+    long long total = 0;
+    for (int k = 0; k < count; ++k) {
+        if (row_of[k] < 0) return fail(c, MPH_ERR_HIP, "mph_neighbor_rows: particle missing from the sorted set");
+        counts[k] = nc[row_of[k]];
+        total += std::min(counts[k], kMaxNeighbor);
+    }
+    if (total > ids_cap) return fail(c, MPH_ERR_ARG, "mph_neighbor_rows: ids_cap too small (" + std::to_string(total) + " needed)");
+    // every ELL tile holding a requested row, down to the longest row of its lanes (entry k of lane l
+    // at [k][l], 64 ints per entry: one contiguous copy per tile)
+    std::map<int, std::vector<int>> tiles;
+    for (int k = 0; k < count; ++k) {
+        const int t = row_of[k] >> 6;
+        if (tiles.count(t)) continue;
+        int m = 0;
+        for (int s = t * kTile; s < std::min(n, (t + 1) * kTile); ++s) m = std::max(m, std::min(nc[s], kMaxNeighbor));
+        std::vector<int>& buf = tiles[t];
+        buf.resize((size_t)m * kTile);
+        if (m) HIP_OK(c, hipMemcpy(buf.data(), c->nbr + (size_t)t * kTile * kMaxNeighbor, sizeof(int) * buf.size(),
+                                   hipMemcpyDeviceToHost));
+    }
+    long long w = 0;
+    for (int k = 0; k < count; ++k) {
+        const int s = row_of[k], m = std::min(counts[k], kMaxNeighbor);
+        const std::vector<int>& buf = tiles[s >> 6];
+        for (int e = 0; e < m; ++e) {
+            const int j = buf[(size_t)e * kTile + (s & 63)] & kIndexMask;
+            if (j >= n) return fail(c, MPH_ERR_HIP, "mph_neighbor_rows: list entry past the particle count");
+            ids[w + e] = id[j];
+        }
+        std::sort(ids + w, ids + w + m);
+        w += m;
+    }
+    return (int)std::min<long long>(w, 0x7fffffff);
+}
+
 #if MPH_DIAG_XCD
 // Diagnostic builds only (not in include/mph_gpu.h): copies DevState.xcd_diag (3 x 4 x 8 words,
 // see XcdProbe in mph_kernels.hip) to out after draining the device; reset != 0 then restarts it.

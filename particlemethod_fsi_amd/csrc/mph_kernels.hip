@@ -1065,9 +1065,11 @@ __device__ __forceinline__ void pass_a_finish(const DevParams& P, const DevTable
 // ---------------------------------------------------------------------- neighbour search ----
 
 // calculateNeighbor (main.cpp:1743-1810).  The reference scans (2*3+1)^d cells of width dx; here
-// cells are >= rc/2 wide, so a +-2 stencil covers the acceptance sphere: 25 columns (3-D) or 5
-// (2-D) along which the cells of the last axis are contiguous in memory.  Acceptance is the
-// reference's own test  q0^2+q1^2+q2^2 <= (MaxRadius+MARGIN)^2  with the Mod-based minimum image.
+// cells are >= rc/kReach (rc/3) wide across the two column axes and >= rc/kContigReach (rc/2)
+// along the contiguous one, so a +-kReach stencil covers the acceptance sphere: (2 kReach + 1)^2
+// = 49 columns (3-D) or 7 (2-D), each one contiguous index range of +-kContigReach cells of the
+// last axis.  Acceptance is the reference's own test  q0^2+q1^2+q2^2 <= (MaxRadius+MARGIN)^2
+// with the Mod-based minimum image.
 // Offset of x from the grid origin, wrapped once into [0, w) (as cell_axis).
 __device__ __forceinline__ double grid_offset(double x, double org, double w)
 {

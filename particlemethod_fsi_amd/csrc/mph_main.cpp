@@ -74,14 +74,15 @@ static void kill_children()
 
 static void on_sigchld(int)
 {
+    // only the registered ranks are reaped: any other child (a library's helper process) keeps its
+    // exit status for its owner and cannot end the run
     const int saved = errno;
-    for (;;) {
+    for (int k = 0; k < g_nchildren; ++k) {
+        if (g_child_done[k] != 0 || g_child_pid[k] <= 0) continue;
         int st = 0;
-        const pid_t pid = waitpid(-1, &st, WNOHANG);
-        if (pid <= 0) break;
+        if (waitpid(g_child_pid[k], &st, WNOHANG) != g_child_pid[k]) continue;
         const bool ok = WIFEXITED(st) && WEXITSTATUS(st) == 0;
-        for (int k = 0; k < g_nchildren; ++k)
-            if (g_child_pid[k] == pid) g_child_done[k] = ok ? 1 : 2;
+        g_child_done[k] = ok ? 1 : 2;
         if (!ok) {
             static const char msg[] = "error: a slab rank failed; stopping the other ranks\n";
             (void)!write(2, msg, sizeof(msg) - 1);
@@ -336,9 +337,11 @@ int main(int argc, char** argv)
         time_t t = time(nullptr);
         logf("start main roop at %s\n", ctime(&t));
     }
-    // the reference's timing buckets (main.cpp:695-700) from HIP events in the step graphs
-    // (single GPU; MPH_PHASE_TIMING=0 turns them off)
-    const bool phases = nslabs == 1 && !(std::getenv("MPH_PHASE_TIMING") && std::atoi(std::getenv("MPH_PHASE_TIMING")) == 0);
+    // the reference's timing buckets (main.cpp:695-700) from HIP events, opt-in (single GPU,
+    // MPH_PHASE_TIMING=1): with them on, mph_step launches every step's kernels directly instead of
+    // replaying the captured graphs (HIP cannot time events inside a graph) and waits for the
+    // events after every batch of up to 8 steps
+    const bool phases = nslabs == 1 && std::getenv("MPH_PHASE_TIMING") && std::atoi(std::getenv("MPH_PHASE_TIMING")) == 1;
     if (phases) {
         rc = mph_phase_timing(ctx, 1);
         if (rc) die(ctx, rc, "mph_phase_timing");

@@ -325,6 +325,29 @@ def generate(cuboids: list[Cuboid]) -> Particles:
                      velocity=np.ascontiguousarray(np.concatenate(vel)) if vel else np.zeros((0, 3)))
 
 
+def jitter(p: Particles, spacing: float, amp: float, dim: int, seed: int = 0) -> Particles:
+    """Off-lattice variant of a generated set (parity cases only; the reference generator has no
+    such option): every coordinate of the active axes moves by a deterministic offset in
+    [-amp, amp) x spacing -- a splitmix64 hash of (seed, particle, axis), no RNG state -- and is
+    rounded through the same %e text as the generator's, so the reference reads the exact values.
+    Position and InitialPosition stay equal (the grid file carries x twice, generator.cpp:853)."""
+    n = p.n
+    m = np.uint64(0xFFFFFFFFFFFFFFFF)
+    k = (np.arange(n, dtype=np.uint64)[:, None] * np.uint64(3) + np.arange(3, dtype=np.uint64)[None, :]
+         + np.uint64(seed) * np.uint64(0x9E3779B97F4A7C15)) & m
+    with np.errstate(over="ignore"):
+        z = (k + np.uint64(0x9E3779B97F4A7C15)) & m
+        z = ((z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & m
+        z = ((z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & m
+        z = z ^ (z >> np.uint64(31))
+    u = (z >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0) * 2.0 - 1.0   # [-1, 1)
+    if dim == 2:
+        u[:, 2] = 0.0
+    x = np.vectorize(_e, otypes=[np.float64])(p.position + amp * spacing * u)
+    return Particles(property=p.property.copy(), position=np.ascontiguousarray(x),
+                     initial_position=x.copy(), velocity=p.velocity.copy())
+
+
 def generate_window(cuboids: list[Cuboid], axis: int, lo: float, hi: float, dmin: float, width: float):
     """The particles of ``generate(cuboids)`` whose coordinate along ``axis`` lies in the periodic
     window [lo, hi) of a domain starting at ``dmin`` with ``width``, without building the others

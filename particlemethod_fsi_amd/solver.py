@@ -57,7 +57,7 @@ EXPORTED_SYMBOLS = [
     "mph_write_vtu_arrays", "mph_write_vtu", "mph_velocity_profile_arrays",
     "mph_set_initial_velocity_profile", "mph_dist_info", "mph_create_slab", "mph_slab_window",
     "mph_list_formats", "mph_abi_version", "mph_phase_timing", "mph_phase_times",
-    "mph_set_step_batching",
+    "mph_set_step_batching", "mph_neighbor_rows",
 ]
 
 ABI_VERSION = 3   # MPH_ABI_VERSION of include/mph_gpu.h that these bindings follow
@@ -154,9 +154,10 @@ def load_library() -> ctypes.CDLL:
         "mph_phase_timing": (ip, [vp, ip]),
         "mph_phase_times": (ip, [vp, vp]),
         "mph_set_step_batching": (ip, [vp, ip]),
+        "mph_neighbor_rows": (ip, [vp, ip, ip, vp, vp, ctypes.c_longlong]),
     }
     # entry points an older library may lack (A/B runs against earlier builds)
-    optional = {"mph_phase_timing", "mph_phase_times", "mph_set_step_batching"}
+    optional = {"mph_phase_timing", "mph_phase_times", "mph_set_step_batching", "mph_neighbor_rows"}
     for name, (res, args) in sig.items():
         if name in optional and not hasattr(L, name):
             continue
@@ -429,8 +430,10 @@ class MphSolver:
         _check(self._L.mph_set_step_batching(self._h, 1 if on else 0), self._h)
 
     def phase_timing(self, on: bool = True):
-        """Record HIP events at every step's phase boundaries inside the step graphs (the
-        reference's clock() buckets, main.cpp:695-700); read the sums with phase_times()."""
+        """Time the reference's clock() buckets (main.cpp:695-700) with HIP events at every step's
+        phase boundaries; read the sums with phase_times().  While on, mph_step launches the steps'
+        kernels directly instead of replaying the captured graphs (HIP cannot time events inside a
+        graph) and waits for the events after every batch of up to 8 steps, so it is slower."""
         _check(self._L.mph_phase_timing(self._h, 1 if on else 0), self._h)
 
     def phase_times(self) -> dict:
@@ -452,6 +455,26 @@ class MphSolver:
         a = np.zeros(2, np.int32)
         _check(self._L.mph_list_formats(self._h, a.ctypes.data), self._h)
         return int(a[0]), int(a[1])
+
+    def neighbor_rows(self, first: int = 0, count: int | None = None):
+        """(counts, offsets, ids): the neighbour sets of the particles [first, first + count) from
+        the last search (mph_neighbor_rows; calculateNeighbor's Neighbor[i][k], main.cpp:1764-1772),
+        each row as ascending original indices, row k = ids[offsets[k]:offsets[k + 1]]."""
+        if count is None:
+            count = self.n - first
+        counts = np.zeros(count, np.int32)
+        cap = max(1, count * 128)
+        while True:
+            ids = np.zeros(cap, np.int32)
+            r = self._L.mph_neighbor_rows(self._h, int(first), int(count), counts.ctypes.data, ids.ctypes.data, cap)
+            need = int(np.minimum(counts, 512).sum()) if r == -1 else 0
+            if r == -1 and need > cap:
+                cap = need
+                continue
+            _check(r, self._h)
+            break
+        offsets = np.concatenate([[0], np.cumsum(np.minimum(counts, 512))]).astype(np.int64)
+        return counts, offsets, ids[:r].copy()
 
     def dist_info(self) -> dict:
         """Slab-mode facts (mph_dist_info): slab ranks, RCCL communicator size (0: host-staged),

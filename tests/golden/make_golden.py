@@ -58,6 +58,9 @@ PLAN = {  # case -> steps (cumulative) to snapshot; the first is the full-field 
     "gate2d_rolling1": [1, 10, 100],
     "hydro2d": [1, 10, 100],
     "bar2d_ivp": [1, 10, 100],
+    # off-lattice (cases.py jitter): the 3-D search and sums away from lattice distances
+    "box3d_jit": [1, 10, 100],
+    "gate3d_jit": [1, 10, 100],
 }
 
 
@@ -109,7 +112,7 @@ def run_case(name: str):
             # only the two virial arrays, so the run continues unchanged
             ref.call("calculateVirialStressAtParticle")
             snap("s%d" % s, ["VirialStressAtParticle", "VirialPressureAtParticle"], True)
-        if k == 0 and name == "dam2d":
+        if k == 0 and name in ("dam2d", "box3d_jit"):
             rows = [np.sort(ref.neighbors(i)) for i in range(ref.n)]
             out["s%d/nbr_offsets" % s] = np.cumsum([0] + [len(r) for r in rows]).astype(np.int32)
             out["s%d/nbr_ids" % s] = np.concatenate(rows).astype(np.int32)

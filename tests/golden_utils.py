@@ -10,7 +10,7 @@ import numpy as np
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CASES = ["dam2d", "gate2d", "bar2d", "box3d", "gate3d", "dam2d_st", "box3d_st", "gate2d_sub",
          "gate3d_sub", "rolling2d", "rolling3d", "movwall2d", "movwall3d", "turek2d", "gate2d_rolling1",
-         "hydro2d", "bar2d_ivp"]
+         "hydro2d", "bar2d_ivp", "box3d_jit", "gate3d_jit"]
 
 
 class Golden:

@@ -124,16 +124,39 @@ def test_gpu_matches_oracle_every_step(case, nsteps):
                     assert float(np.max(np.abs(a - b))) <= t, (k, f)
 
 
-def test_gpu_neighbor_sets_exact_dam():
-    """NeighborCount is exact by construction; check the acceptance itself on the golden lists:
-    every reference neighbour is within the cutoff the GPU uses and counts agree per particle."""
-    g = Golden("dam2d")
-    cfg, parts = cases.get("dam2d").build()
+@pytest.mark.parametrize("case", ["dam2d", "box3d_jit"])
+def test_gpu_neighbor_sets_match_reference_golden(case):
+    """The neighbour SETS themselves (mph_neighbor_rows), not only their sizes: after one step every
+    particle's row equals the reference's Neighbor[i][0..count) (main.cpp:1764-1772, sorted; the
+    golden rows of make_golden.py) -- on the lattice (dam2d) and off it (box3d_jit)."""
+    g = Golden(case)
+    cfg, parts = cases.get(case).build()
     with MphSolver(cfg, parts) as s:
         s.step(1)
-        nc = s.get("NeighborCount")
-        off = g.get(1, "nbr_offsets")
-        assert np.array_equal(nc, np.diff(off))
+        counts, offsets, ids = s.neighbor_rows()
+        assert np.array_equal(counts, np.diff(g.get(1, "nbr_offsets")))
+        assert np.array_equal(offsets, g.get(1, "nbr_offsets"))
+        assert np.array_equal(ids, g.get(1, "nbr_ids"))
+        # a sub-range returns the same rows
+        c2, o2, i2 = s.neighbor_rows(1000, 500)
+        assert np.array_equal(i2, ids[offsets[1000]:offsets[1500]])
+
+
+@pytest.mark.parametrize("case,nsteps", [("box3d", 10), ("gate3d_jit", 10), ("seam3d", 10)])
+def test_gpu_neighbor_sets_match_oracle(case, nsteps):
+    """Neighbour sets after several steps against the oracle's lists (bit-identical to the
+    reference's): every row, as sets of original indices."""
+    from oracle_bindings import OracleSolver
+    cfg, parts = cases.get(case).build()
+    o = OracleSolver(cfg, parts)
+    o.init()
+    o.step(nsteps)
+    with MphSolver(cfg, parts) as s:
+        s.step(nsteps)
+        counts, offsets, ids = s.neighbor_rows()
+        assert np.array_equal(counts, o.get("NeighborCount"))
+        for i in range(parts.n):
+            assert np.array_equal(ids[offsets[i]:offsets[i + 1]], np.sort(o.neighbors(i))), (case, i)
 
 
 def test_gpu_deterministic_rerun():

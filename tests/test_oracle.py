@@ -60,9 +60,12 @@ def test_oracle_matches_reference_golden(case):
         pass  # neighbour lists are compared in test_oracle_neighbor_lists
 
 
-def test_oracle_neighbor_lists_dam():
-    g = Golden("dam2d")
-    cfg, parts = cases.get("dam2d").build()
+@pytest.mark.parametrize("case", ["dam2d", "box3d_jit"])
+def test_oracle_neighbor_lists(case):
+    """The oracle's neighbour sets after one step equal the reference's (sorted rows of
+    Neighbor[i][k], main.cpp:1764-1772) -- on the lattice (dam2d) and off it (box3d_jit)."""
+    g = Golden(case)
+    cfg, parts = cases.get(case).build()
     o = OracleSolver(cfg, parts)
     o.init()
     o.step(1)
@@ -103,7 +106,7 @@ print("OK")
 """
 
 
-@pytest.mark.parametrize("case", ["gate2d", "gate3d", "turek2d", "hydro2d", "movwall3d"])
+@pytest.mark.parametrize("case", ["gate2d", "gate3d", "turek2d", "hydro2d", "movwall3d", "gate3d_jit"])
 def test_oracle_per_kernel_against_live_reference(case):
     c = cases.get(case)
     if not ref_available(c.dim, c.ref_variant):
