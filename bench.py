@@ -189,6 +189,9 @@ def main():
     # this many steps in all (D1M: t = 0.25 s of the reference's 1 s dam run, main.cpp:581 with
     # results/Dam/dam.data EndTime 1.0) and times --steps more there; 0 skips it
     ap.add_argument("--developed-steps", type=int, default=None)
+    # start from a saved state instead of the generator's lattice (a binary grid of
+    # tools/dev_state.py: Time, x, x0, v -- the reference's .prof restart); profiles of the developed flow
+    ap.add_argument("--state", default=None)
     args = ap.parse_args()
 
     rank, world, local = dist_env()
@@ -224,6 +227,15 @@ def main():
         n_local = len(solver.owned_ids())
     else:
         cfg, parts = case.build()
+        if args.state:
+            from particlemethod_fsi_amd.solver import read_case_files
+            d = tempfile.mkdtemp(prefix="mphstate_")
+            with open(os.path.join(d, "c.data"), "w") as fh:
+                fh.write(cases.data_text(case.data()))
+            scfg, sparts = read_case_files(os.path.join(d, "c.data"), args.state, case.dim, case.module)
+            assert sparts.n == parts.n and (sparts.property == parts.property).all(), "state of another case"
+            cfg.time = scfg.time
+            parts = sparts
         n_total = parts.n
         solver = MphSolver(cfg, parts, device=device)
         n_local = n_total
@@ -376,7 +388,8 @@ def main():
     # developed flow -- the dam collapsed for t = 0.25 s, particles off the lattice, neighbour sets
     # changed -- is timed on the same context after running on untimed.
     developed = None
-    dev_total = args.developed_steps if args.developed_steps is not None else (2500 if case_name == "d1m" else 0)
+    dev_total = args.developed_steps if args.developed_steps is not None else (
+        2500 if case_name == "d1m" and not args.state else 0)
     done = args.warmup + 3 * args.steps + args.profile_steps if world == 1 else 0
     if world == 1 and dev_total > done + args.warmup:
         solver.step(dev_total - done)
