@@ -53,6 +53,8 @@ int ctx_state_status(MphCtx* c, const DevState& hs)
     if (hs.overflow & 1)
         return ctx_fail(c, MPH_ERR_NEIGHBOR_OVERFLOW, "a particle has more than 512 neighbours");
     if (hs.overflow & 2) return ctx_fail(c, MPH_ERR_CAPACITY, "a particle moved past a neighbouring slab");
+    if (hs.overflow & 64)   // k_place: a cell start + slot past the particle count (never a fault)
+        return ctx_fail(c, MPH_ERR_HIP, "cell sort: histogram inconsistent with the keys (placement out of range)");
     if (hs.overflow & 32)   // MPH_DIAG_PA builds only
         return ctx_fail(c, MPH_ERR_HIP, "diagnostic: staged pass A left list entries over (MPH_DIAG_PA)");
     if (hs.overflow & 8)   // MPH_DIAG_BOUNDS builds only
@@ -442,7 +444,10 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     CK(dalloc(c, &c->rank_of, cap));
     CK(dalloc(c, &c->key, cap)); CK(dalloc(c, &c->slot, cap)); CK(dalloc(c, &c->tmp, cap));
     CK(dalloc(c, &c->cnt, c->P.ncell)); CK(dalloc(c, &c->start, (size_t)c->P.ncell + 1));
-    CK(dalloc(c, &c->bsum, (size_t)c->P.ncell / 4096 + 2));
+    // the cell scan's block totals: two parity buffers filled by k_prep (MPH_PREP_BSUM) and a
+    // scratch third for the other scans (structure init, MPH_PREP_BSUM=0); all zero at the start
+    const size_t bs = (size_t)c->P.ncell / 4096 + 2;
+    CK(dalloc(c, &c->bsum, 3 * bs));
     CK(dalloc(c, &c->nbr, ntile * kTile * kMaxNeighbor)); CK(dalloc(c, &c->ncount, cap));
 #if (defined(MPH_DIAG_NOSTORE) && MPH_DIAG_NOSTORE) || (defined(MPH_DIAG_SEARCH) && (MPH_DIAG_SEARCH & 4))
     // diagnostic builds: the search stores no list (or skips the waves near a periodic face, whose
@@ -459,6 +464,7 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     CK(dalloc(c, &c->fpart, cap)); CK(dalloc(c, &c->rec, cap));
     CK(dalloc(c, &c->dens_a, cap)); CK(dalloc(c, &c->vstrain, cap)); CK(dalloc(c, &c->divp, cap));
     HIP_OK(c, hipMemsetAsync(c->cnt, 0, sizeof(int) * c->P.ncell, c->stream));
+    HIP_OK(c, hipMemsetAsync(c->bsum, 0, sizeof(int) * 3 * bs, c->stream));
     HIP_OK(c, hipMemsetAsync(c->force, 0, sizeof(double4) * std::max(cap, 1), c->stream));
     HIP_OK(c, hipMemsetAsync(c->acc, 0, sizeof(double4) * std::max(cap, 1), c->stream));
     HIP_OK(c, hipMemcpyAsync(c->dT, &c->T, sizeof(DevTables), hipMemcpyHostToDevice, c->stream));

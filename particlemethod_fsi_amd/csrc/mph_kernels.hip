@@ -654,9 +654,28 @@ __device__ __forceinline__ int vsrc_entry(const VSrc& vs, const Soa& C, int p, S
     return p;
 }
 
+constexpr int kScanThreads = 256;
+#ifndef MPH_SCAN_ITEMS
+#define MPH_SCAN_ITEMS 16
+#endif
+constexpr int kScanItems = MPH_SCAN_ITEMS;   // cells per thread (a multiple of 4)
+constexpr int kScanBlock = kScanThreads * kScanItems;   // 4096 cells per block (bsum arrays: ncell / 4096 + 2)
+// Block totals of the cell histogram from k_prep (MPH_PREP_BSUM, default): one atomic per run of equal
+// 4096-cell blocks among a wavefront's lanes adds the run's particles to the step's totals, so the
+// scan needs no k_scan_reduce pass over the whole histogram.  The totals live in two buffers of
+// bsum_stride(ncell) ints selected by the step's parity (DevState.seam_step, advanced by k_place):
+// k_prep adds into this step's buffer, k_scan_down reads it and clears the other one (all of its
+// blocks, so every entry a later k_prep can reach is zero), and mph_create zeroes both.
+#ifndef MPH_PREP_BSUM
+#define MPH_PREP_BSUM 1
+#endif
+__host__ __device__ inline int bsum_stride(int ncell) { return ncell / kScanBlock + 2; }
+static_assert(kScanBlock == 4096, "mph_ctx.hip sizes the bsum buffers for 4096-cell blocks");
+
 __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __restrict__ st, Soa C,
                                               int* __restrict__ key, int* __restrict__ slot,
-                                              int* __restrict__ cnt, int mode, VSrc vs)
+                                              int* __restrict__ cnt, int mode, VSrc vs,
+                                              int* __restrict__ bsum2)
 {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     const int n = dev_n(P);
@@ -690,6 +709,17 @@ __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __res
         if (live && head) base = atomicAdd(&cnt[k], next - lane);
         base = __shfl(base, hl, 64);
         if (live) slot[p] = base + (lane - hl);
+        if (bsum2) {
+            // this step's block totals: one atomic per run of equal 4096-cell blocks (dead lanes
+            // past n carry distinct negative blocks, so they never join a live run nor add)
+            int* bsum = bsum2 + (st->seam_step & 1) * bsum_stride(P.ncell);
+            const int blk = live ? k / kScanBlock : k;
+            const int bprev = __shfl_up(blk, 1, 64);
+            const bool bhead = lane == 0 || bprev != blk;
+            const unsigned long long babove = __ballot(bhead) & ~upto;
+            const int bnext = babove ? __ffsll((long long)babove) - 1 : 64;
+            if (live && bhead) atomicAdd(&bsum[blk], bnext - lane);
+        }
         // the block's face bits: OR-ed in LDS, then one device atomic per block, only for bits the
         // step's word does not hold yet (few blocks: the particles near a periodic face)
         __shared__ int s_occ;
@@ -715,6 +745,7 @@ __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __res
     const int k = cell_id(P, x, y, z);
     key[p] = k;
     slot[p] = atomicAdd(&cnt[k], 1);
+    if (bsum2) atomicAdd(&bsum2[(st->seam_step & 1) * bsum_stride(P.ncell) + k / kScanBlock], 1);
     const int occ = seam_bits(P, x, y, z);
     if (occ) {
         int* w = const_cast<int*>(&st->seam_occ[st->seam_step & 1]);
@@ -722,13 +753,9 @@ __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __res
     }
 }
 
-// Exclusive scan of the cell histogram: 3 launches (block reduce, top-level scan, down-sweep).
-constexpr int kScanThreads = 256;
-#ifndef MPH_SCAN_ITEMS
-#define MPH_SCAN_ITEMS 16
-#endif
-constexpr int kScanItems = MPH_SCAN_ITEMS;   // cells per thread (a multiple of 4)
-constexpr int kScanBlock = kScanThreads * kScanItems;   // 4096 cells per block (bsum arrays: ncell / 4096 + 2)
+// Exclusive scan of the cell histogram (constants above k_prep): block totals (k_prep's atomics, or
+// a k_scan_reduce launch), the top-level scan (inside k_scan_down up to kScanFusedTop blocks, else a
+// k_scan_top launch) and the down-sweep.
 
 __device__ __forceinline__ int block_exclusive_scan(int v, int* lds, int& total)
 {
@@ -786,8 +813,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const int* __restr
     if (threadIdx.x == 0) bsum[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(1024) void k_scan_top(int* __restrict__ bsum, int nb)
+// st non-null: bsum is the pair of parity buffers of MPH_PREP_BSUM (this step's is scanned)
+__global__ __launch_bounds__(1024) void k_scan_top(int* __restrict__ bsum, int nb, const DevState* __restrict__ st,
+                                                   int stride)
 {
+    if (st) bsum += (st->seam_step & 1) * stride;
     __shared__ int lds[16];
     __shared__ int carry;
     if (threadIdx.x == 0) carry = 0;
@@ -814,9 +844,17 @@ constexpr int kScanFusedTop = MPH_SCAN_FUSED_TOP;
 __global__ __launch_bounds__(kScanThreads) void k_scan_down(int* __restrict__ cnt, int ncell,
                                                             const int* __restrict__ bsum,
                                                             int* __restrict__ start, int n,
-                                                            const int* __restrict__ n_dev, int top)
+                                                            const int* __restrict__ n_dev, int top,
+                                                            const DevState* __restrict__ st, int stride)
 {
     __shared__ int lds[kScanThreads / 64];
+    if (st) {
+        // MPH_PREP_BSUM: this step's totals (from k_prep's atomics); the other parity's entry of this
+        // block is cleared for the next step's k_prep (nothing reads it during this step)
+        const int par = st->seam_step & 1;
+        if (threadIdx.x == 0) const_cast<int*>(bsum)[(par ^ 1) * stride + blockIdx.x] = 0;
+        bsum += par * stride;
+    }
     const int base = blockIdx.x * kScanBlock + threadIdx.x * kScanItems;
     int v[kScanItems];
     load16(cnt, base, ncell, v);
@@ -880,8 +918,16 @@ __global__ __launch_bounds__(256) void k_place(DevParams P, DevState* __restrict
             st->time += P.dt;
         }
     }
-    if (p >= dev_n(P)) return;
-    tmp[start[key[p]] + slot[p]] = p;
+    const int n = dev_n(P);
+    if (p >= n) return;
+    // a histogram inconsistent with the keys (it cannot happen while the block totals and the
+    // counts agree) becomes an error flag, never a store out of range
+    const int d = start[key[p]] + slot[p];
+    if ((unsigned)d >= (unsigned)n) {
+        atomicOr(&st->overflow, 64);
+        return;
+    }
+    tmp[d] = p;
 }
 
 // Deterministic stable order inside a cell: rank = number of cell-mates with a smaller previous
@@ -3261,15 +3307,30 @@ void launch_sort(const Launch& L, int mode)
     const DevParams& P = *L.P;
     const int n = P.n;
     if (n == 0) return;
-    MPH_LAUNCH("prep", L.stream, k_prep, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.B,
-               L.key, L.slot, L.cnt, mode, L.vsrc);
     const int nb = blocks(P.ncell, kScanBlock);
     const int top = nb <= kScanFusedTop;
-    MPH_LAUNCH("scan_reduce", L.stream, k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt,
-               P.ncell, L.bsum);
-    if (!top) MPH_LAUNCH("scan_top", L.stream, k_scan_top, dim3(1), dim3(1024), 0, L.stream, L.bsum, nb);
-    MPH_LAUNCH("scan_down", L.stream, k_scan_down, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt,
-               P.ncell, L.bsum, L.start, n, P.n_dev, top);
+    const int bs = bsum_stride(P.ncell);
+    if (MPH_PREP_BSUM) {
+        // block totals from k_prep into this step's parity buffer of L.bsum (no k_scan_reduce)
+        MPH_LAUNCH("prep", L.stream, k_prep, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.B,
+                   L.key, L.slot, L.cnt, mode, L.vsrc, L.bsum);
+        if (!top)
+            MPH_LAUNCH("scan_top", L.stream, k_scan_top, dim3(1), dim3(1024), 0, L.stream, L.bsum, nb,
+                       (const DevState*)L.st, bs);
+        MPH_LAUNCH("scan_down", L.stream, k_scan_down, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt,
+                   P.ncell, L.bsum, L.start, n, P.n_dev, top, (const DevState*)L.st, bs);
+    } else {
+        int* bsum = L.bsum + 2 * bs;   // the scratch third of L.bsum
+        MPH_LAUNCH("prep", L.stream, k_prep, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.B,
+                   L.key, L.slot, L.cnt, mode, L.vsrc, (int*)nullptr);
+        MPH_LAUNCH("scan_reduce", L.stream, k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt,
+                   P.ncell, bsum);
+        if (!top)
+            MPH_LAUNCH("scan_top", L.stream, k_scan_top, dim3(1), dim3(1024), 0, L.stream, bsum, nb,
+                       (const DevState*)nullptr, 0);
+        MPH_LAUNCH("scan_down", L.stream, k_scan_down, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt,
+                   P.ncell, bsum, L.start, n, P.n_dev, top, (const DevState*)nullptr, 0);
+    }
     MPH_LAUNCH("place", L.stream, k_place, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.key,
                L.slot, L.start, L.tmp, mode);
     MPH_LAUNCH("rank_scatter", L.stream, k_rank_scatter, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P,
@@ -3480,7 +3541,7 @@ int launch_struct_init(const Launch& L, int ns, const double4* x0, int* key, int
     const dim3 g(blocks(ns, 256)), b(256);
     // bin the slots on the grid (L.cnt is zero between steps and the scan re-zeroes it)
     MPH_LAUNCH("sinit_bin", L.stream, k_sinit_bin, g, b, 0, L.stream, P, ns, x0, key, L.cnt, slot);
-    launch_scan(L.cnt, P.ncell, L.bsum, L.start, ns, L.stream, prof);
+    launch_scan(L.cnt, P.ncell, L.bsum + 2 * bsum_stride(P.ncell), L.start, ns, L.stream, prof);   // scratch third
     MPH_LAUNCH("sinit_place", L.stream, k_sinit_place, g, b, 0, L.stream, ns, key, slot, L.start, tmp, sorted, 0);
     MPH_LAUNCH("sinit_place", L.stream, k_sinit_place, g, b, 0, L.stream, ns, key, slot, L.start, tmp, sorted, 1);
     if (P.dim == 3)
@@ -3556,9 +3617,10 @@ void launch_scan(int* cnt, int ncell, int* bsum, int* start, int total, hipStrea
     const int nb = blocks(ncell, kScanBlock);
     const int top = nb <= kScanFusedTop;
     MPH_LAUNCH("scan_reduce", stream, k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, stream, cnt, ncell, bsum);
-    if (!top) MPH_LAUNCH("scan_top", stream, k_scan_top, dim3(1), dim3(1024), 0, stream, bsum, nb);
+    if (!top)
+        MPH_LAUNCH("scan_top", stream, k_scan_top, dim3(1), dim3(1024), 0, stream, bsum, nb, (const DevState*)nullptr, 0);
     MPH_LAUNCH("scan_down", stream, k_scan_down, dim3(nb), dim3(kScanThreads), 0, stream, cnt, ncell, bsum,
-               start, total, (const int*)nullptr, top);
+               start, total, (const int*)nullptr, top, (const DevState*)nullptr, 0);
 }
 
 int dist_blocks(int n) { return blocks(n > 0 ? n : 1, 256); }
