@@ -169,6 +169,7 @@ def slab_checks(solver, dist, n_total, case_name, steps_done):
     except (OSError, ValueError, KeyError):
         pass
     return {"slab_ranks": info["nranks"], "rccl_nranks": info["rccl_ranks"],
+            "pass_b_mode": solver.dist_overlap(),
             "transport": "rccl" if info["rccl_ranks"] else "host-staged",
             "graphs": bool(info["graphs"]), "partition_ok": bool(partition), "owned_total": int(tot[0]),
             "steps_done": steps_done, "neighbor_count_sum": int(tot[2]),

@@ -377,6 +377,12 @@ int mph_dist_selftest(int device);
  * local array capacity, largest send / receive message capacity (particles), particles held
  * (owned + ghosts)}.                                                                          */
 int mph_dist_info(const MphCtx* ctx, int* out8);
+/* Pass-B mode of a slab context (out5; all -1 without slabs): {overlap on (1) / off (0), how it
+ * was set: 1 / 0 forced by MPH_SLAB_OVERLAP, -1 chosen at creation by the ranks together, then
+ * the creation probe's maxima over ranks in ms -- halo exchange, redistribution exchange (both at
+ * their message capacities), the cost of pass B split into interior and face launches over one
+ * launch (-1: not probed)}.  Overlap is chosen when the two exchanges take longer than the split. */
+int mph_dist_overlap(const MphCtx* ctx, double* out5);
 /* Neighbour-list formats of the last search: out2 = {wavefronts with the compact 16-bit list,
  * wavefronts in all} (the others, near a periodic face or with long group ranges, keep 32-bit
  * ELL rows).  The compact format is opt-in at the default stencil (MPH_LIST16=1 at creation,

@@ -43,11 +43,18 @@ struct MphDist {
     // transport: RCCL communicator, or a host callback (tests / hosts without RCCL)
     bool rccl = false;
     bool graphs = false;          // steps replayed from captured graphs (RCCL transport)
-    // MPH_SLAB_OVERLAP=1: pass B of the inner particles overlaps the pass-A halo (and the early send
-    // below); default off -- halo, then one pass B over all particles.  One rank at a time at D16M / 8
-    // the split pass B and the early classify cost 0.13 ms per step more than they can hide
-    // (profiles/r04/serial_d16m_8_overlap*.json)
-    bool overlap = std::getenv("MPH_SLAB_OVERLAP") && std::string(std::getenv("MPH_SLAB_OVERLAP")) == "1";
+    // overlap: pass B of the inner particles overlaps the pass-A halo (and the early send below);
+    // off: halo, then one pass B over all particles.  MPH_SLAB_OVERLAP=1 / =0 forces the mode;
+    // unset (or "auto") the ranks choose it together at creation (overlap_probe, mph_dist.hip): on
+    // when the measured exchanges take longer than the split pass B costs over the single one
+    bool overlap = false;
+    int overlap_mode = [] {
+        const char* e = std::getenv("MPH_SLAB_OVERLAP");
+        return (e && std::string(e) == "1") ? 1 : ((e && std::string(e) == "0") ? 0 : -1);
+    }();
+    // the probe's measurements, max over ranks (ms): halo exchange, redistribution exchange (both at
+    // their message capacities), pass B split in two launches minus pass B in one; -1: not probed
+    double probe_ms[3] = {-1.0, -1.0, -1.0};
     // early send: within a batch of steps, the redistribution messages of the next step leave
     // while the interior pass B of this one runs (no elastic particles; MPH_SLAB_EARLY=0: off)
     bool early = !(std::getenv("MPH_SLAB_EARLY") && std::string(std::getenv("MPH_SLAB_EARLY")) == "0");

@@ -474,6 +474,84 @@ int struct_substeps(MphCtx* c, Profiler* prof)
     return MPH_OK;
 }
 
+// Element-wise max of v[0..n) over all ranks (every rank ends with the same values): RCCL
+// all-reduce, or n-1 rounds along the ring of the host transport (each passes its running max left).
+int collective_max(MphCtx* c, double* v, int n)
+{
+    MphDist& D = *c->dist;
+    if (D.rccl) {
+        double* d = nullptr;
+        MPH_HIP_OK(c, hipMalloc((void**)&d, sizeof(double) * n));
+        std::unique_ptr<double, void (*)(double*)> guard(d, [](double* q) { (void)hipFree(q); });
+        MPH_HIP_OK(c, hipMemcpyAsync(d, v, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+        RCCL_OK(c, ncclAllReduce(d, d, n, ncclDouble, ncclMax, (ncclComm_t)D.comm, c->stream));
+        MPH_HIP_OK(c, hipMemcpyAsync(v, d, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+        MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
+        return MPH_OK;
+    }
+    std::vector<double> in((size_t)n);
+    for (int round = 1; round < D.nranks; ++round) {
+        if (D.host_fn(D.host_user, v, sizeof(double) * n, nullptr, 0, nullptr, 0, in.data(), sizeof(double) * n) != 0)
+            return ctx_fail(c, MPH_ERR_TRANSPORT, "host exchange callback failed (collective max)");
+        for (int k = 0; k < n; ++k) v[k] = std::max(v[k], in[k]);
+    }
+    return MPH_OK;
+}
+
+// MPH_SLAB_OVERLAP unset ("auto"): the ranks choose the pass-B mode together at creation, from
+// what this machine and transport do.  On the initial state (after the init sums) every rank times,
+// with events on its stream, best of three after a warm-up:
+//   th  the halo exchange of the pass-A values (the step's own, at its message capacities),
+//   tr  an exchange of the redistribution messages at their capacities (dry: nothing is unpacked),
+//   ts  pass B as the overlap splits it (interior, then face waves) minus pass B in one launch;
+// the maxima over ranks decide: overlap when th + tr > ts, i.e. when the exchanges it can hide
+// behind the interior pass B (and, with the early send, behind the next partition) cost more than
+// splitting pass B does.  The probe's pass B writes B, which is then restored from A (the state
+// dist_init left).  Contexts with elastic particles keep the overlap off (their substeps write
+// the slot arrays from pass B).
+int overlap_probe(MphCtx* c)
+{
+    MphDist& D = *c->dist;
+    D.overlap = D.overlap_mode == 1;
+    if (D.overlap_mode >= 0 || c->P.n_struct > 0) return MPH_OK;
+    Launch L = c->L;
+    L.wface = D.wface;
+    hipEvent_t e[5] = {};
+    struct Ev {
+        hipEvent_t* e;
+        ~Ev() { for (int k = 0; k < 5; ++k) if (e[k]) (void)hipEventDestroy(e[k]); }
+    } guard{e};
+    for (auto& x : e) MPH_HIP_OK(c, hipEventCreate(&x));
+    double best[3] = {1e30, 1e30, 1e30};
+    for (int rep = 0; rep < 4; ++rep) {
+        MPH_HIP_OK(c, hipEventRecord(e[0], c->stream));
+        MPH_CK(halo_exchange(c, nullptr, c->stream));
+        MPH_HIP_OK(c, hipEventRecord(e[1], c->stream));
+        MPH_CK(exchange(c, c->stream, D.send_l, kMsgHead + kMsgBytes * D.cap_sl, D.send_r,
+                        kMsgHead + kMsgBytes * D.cap_sr, D.recv_l, kMsgHead + kMsgBytes * D.cap_rl, D.recv_r,
+                        kMsgHead + kMsgBytes * D.cap_rr));
+        MPH_HIP_OK(c, hipEventRecord(e[2], c->stream));
+        launch_pass_b(L, 0);
+        MPH_HIP_OK(c, hipEventRecord(e[3], c->stream));
+        launch_pass_b(L, 1);
+        launch_pass_b(L, 2);
+        MPH_HIP_OK(c, hipEventRecord(e[4], c->stream));
+        MPH_HIP_OK(c, hipGetLastError());
+        MPH_HIP_OK(c, hipEventSynchronize(e[4]));
+        float ms[4];
+        for (int k = 0; k < 4; ++k) MPH_HIP_OK(c, hipEventElapsedTime(&ms[k], e[k], e[k + 1]));
+        if (rep == 0) continue;   // warm-up: the first exchanges set up the transport
+        best[0] = std::min(best[0], (double)ms[0]);
+        best[1] = std::min(best[1], (double)ms[1]);
+        best[2] = std::min(best[2], (double)ms[3] - (double)ms[2]);
+    }
+    MPH_CK(copy_soa(c, c->B, c->A, c->n));
+    MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
+    MPH_CK(collective_max(c, best, 3));
+    for (int k = 0; k < 3; ++k) D.probe_ms[k] = best[k];
+    D.overlap = best[0] + best[1] > best[2];
+    return MPH_OK;
+}
 
 }  // namespace
 
@@ -725,6 +803,8 @@ int dist_init(MphCtx* c)
     // the integrated-state set B starts as the sorted local set (owned + ghosts, ids signed)
     MPH_CK(copy_soa(c, c->B, c->A, c->n));
     MPH_HIP_OK(c, hipGetLastError());
+    MPH_CK(dist_sync(c, false));
+    MPH_CK(overlap_probe(c));   // MPH_SLAB_OVERLAP auto: the pass-B mode, the same on every rank
     return dist_sync(c, false);
 }
 
@@ -1306,6 +1386,18 @@ int mph_dist_selftest(int device)
     for (void* p : c.allocs) (void)hipFree(p);
     if (c.stream) (void)hipStreamDestroy(c.stream);
     return status;
+}
+
+int mph_dist_overlap(const MphCtx* c, double* out5)
+{
+    if (!c || !out5) return MPH_ERR_ARG;
+    for (int k = 0; k < 5; ++k) out5[k] = -1.0;
+    if (!c->dist) return MPH_OK;
+    const MphDist& D = *c->dist;
+    out5[0] = D.overlap ? 1.0 : 0.0;
+    out5[1] = D.overlap_mode;
+    for (int k = 0; k < 3; ++k) out5[2 + k] = D.probe_ms[k];
+    return MPH_OK;
 }
 
 int mph_dist_info(const MphCtx* c, int* out8)

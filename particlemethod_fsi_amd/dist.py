@@ -22,14 +22,23 @@ class GlooExchange:
     TAG_LEFTWARD = 17
     TAG_RIGHTWARD = 23
 
-    def __init__(self, rank: int, nranks: int, group=None):
+    def __init__(self, rank: int, nranks: int, group=None, delay_ms: float | None = None):
         self.rank, self.nranks, self.group = rank, nranks, group
         self.left = (rank - 1) % nranks
         self.right = (rank + 1) % nranks
+        # diagnostics / tests of the overlap probe: every exchange takes this much longer
+        # (MPH_HOST_EXCHANGE_DELAY_MS), as over a slow link
+        if delay_ms is None:
+            import os
+            delay_ms = float(os.environ.get("MPH_HOST_EXCHANGE_DELAY_MS", "0"))
+        self.delay_s = delay_ms * 1e-3
 
     def __call__(self, send_l, send_r, recv_l, recv_r):
         import torch
         import torch.distributed as dist
+        if self.delay_s > 0:
+            import time
+            time.sleep(self.delay_s)
 
         def t(mv):
             return torch.from_numpy(np.frombuffer(mv, dtype=np.uint8))

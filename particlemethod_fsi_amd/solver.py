@@ -57,7 +57,7 @@ EXPORTED_SYMBOLS = [
     "mph_write_vtu_arrays", "mph_write_vtu", "mph_velocity_profile_arrays",
     "mph_set_initial_velocity_profile", "mph_dist_info", "mph_create_slab", "mph_slab_window",
     "mph_list_formats", "mph_abi_version", "mph_phase_timing", "mph_phase_times",
-    "mph_set_step_batching", "mph_neighbor_rows",
+    "mph_set_step_batching", "mph_neighbor_rows", "mph_dist_overlap",
 ]
 
 ABI_VERSION = 3   # MPH_ABI_VERSION of include/mph_gpu.h that these bindings follow
@@ -155,9 +155,11 @@ def load_library() -> ctypes.CDLL:
         "mph_phase_times": (ip, [vp, vp]),
         "mph_set_step_batching": (ip, [vp, ip]),
         "mph_neighbor_rows": (ip, [vp, ip, ip, vp, vp, ctypes.c_longlong]),
+        "mph_dist_overlap": (ip, [vp, vp]),
     }
     # entry points an older library may lack (A/B runs against earlier builds)
-    optional = {"mph_phase_timing", "mph_phase_times", "mph_set_step_batching", "mph_neighbor_rows"}
+    optional = {"mph_phase_timing", "mph_phase_times", "mph_set_step_batching", "mph_neighbor_rows",
+                "mph_dist_overlap"}
     for name, (res, args) in sig.items():
         if name in optional and not hasattr(L, name):
             continue
@@ -483,6 +485,15 @@ class MphSolver:
         _check(self._L.mph_dist_info(self._h, a.ctypes.data), self._h)
         keys = ["nranks", "rank", "rccl_ranks", "graphs", "cap", "cap_send", "cap_recv", "held"]
         return {k: int(v) for k, v in zip(keys, a)}
+
+    def dist_overlap(self) -> dict:
+        """Pass-B mode of a slab context (mph_dist_overlap): overlap on/off, whether MPH_SLAB_OVERLAP
+        forced it or the creation probe chose it, and the probe's maxima over ranks (ms)."""
+        a = np.zeros(5)
+        _check(self._L.mph_dist_overlap(self._h, a.ctypes.data), self._h)
+        return {"overlap": bool(a[0] == 1.0), "chosen_by": {-1: "probe", 0: "forced", 1: "forced"}.get(int(a[1]), "none"),
+                "halo_exchange_ms": float(a[2]), "redistribution_exchange_ms": float(a[3]),
+                "split_pass_b_cost_ms": float(a[4])}
 
     def compute_virial(self):
         """calculateVirialStressAtParticle (main.cpp:3077-3318) on the current state; read the result

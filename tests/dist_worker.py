@@ -58,6 +58,10 @@ def gpu_worker(rank, world, port, case, checkpoints, fields, out_path, local=Fal
         slab = gloo_slab(rank, world, axis, cuts=cuts)
     res = {}
     with MphSolver(cfg, parts, device=0, slab=slab) as s:
+        ov = s.dist_overlap()
+        res["overlap"] = np.array([float(ov["overlap"]), ov["halo_exchange_ms"], ov["redistribution_exchange_ms"],
+                                   ov["split_pass_b_cost_ms"]])
+
         def owner_map():
             parts_ = [None] * world
             dist.all_gather_object(parts_, s.owned_ids())

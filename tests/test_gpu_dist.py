@@ -185,6 +185,31 @@ def test_slab_structure_overlap_bitwise(tmp_path, case, world, monkeypatch):
         assert np.array_equal(out["1"][k], out["0"][k]), k
 
 
+def test_slab_overlap_probe(tmp_path, monkeypatch):
+    """MPH_SLAB_OVERLAP unset: the ranks choose the pass-B mode together at creation from their
+    measured halo / redistribution exchange times against the cost of splitting pass B (max over
+    ranks, mph_dist_overlap).  With 25 ms injected into every host exchange (a slow link) the
+    exchanges dominate and the overlap is chosen; the rule holds in every run; and the chosen mode
+    gives the bits of either forced mode (the probe's trial pass B is undone)."""
+    monkeypatch.delenv("MPH_SLAB_OVERLAP", raising=False)
+    monkeypatch.setenv("MPH_HOST_EXCHANGE_DELAY_MS", "25")
+    slow = run_slab("channel3d", 2, [1, 9], str(tmp_path / "slow.npz"))
+    on, th, tr, ts = slow["overlap"]
+    assert th >= 25.0 and tr >= 25.0, (th, tr, ts)
+    assert on == 1.0, slow["overlap"]
+    monkeypatch.delenv("MPH_HOST_EXCHANGE_DELAY_MS")
+    fast = run_slab("channel3d", 2, [1, 9], str(tmp_path / "fast.npz"))
+    on, th, tr, ts = fast["overlap"]
+    assert th >= 0.0 and tr >= 0.0 and on == float(th + tr > ts), fast["overlap"]
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MPH_SLAB_OVERLAP", mode)
+        forced = run_slab("channel3d", 2, [1, 9], str(tmp_path / ("forced%s.npz" % mode)))
+        assert forced["overlap"][0] == float(mode) and forced["overlap"][1] == -1.0   # not probed
+        for k in forced.files:
+            if k != "overlap":
+                assert np.array_equal(forced[k], slow[k]) and np.array_equal(forced[k], fast[k]), (mode, k)
+
+
 def _run_capacity(tmp_path, tag, case, world, batches):
     ctx = mp.get_context("spawn")
     port = _free_port()
