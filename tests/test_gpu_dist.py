@@ -169,7 +169,8 @@ def test_slab_early_send_bitwise(tmp_path, case, world, monkeypatch):
         out[mode] = run_slab(case, world, [1, 5, 20], str(tmp_path / ("slab%s.npz" % mode)), fields,
                              local=True)
     for k in out["1"].files:
-        assert np.array_equal(out["1"][k], out["0"][k]), k
+        if k != "overlap":   # (the pass-B mode report differs by construction)
+            assert np.array_equal(out["1"][k], out["0"][k]), k
 
 
 @pytest.mark.parametrize("case,world", [("bar2d", 3), ("bar3d", 2)])
@@ -182,7 +183,8 @@ def test_slab_structure_overlap_bitwise(tmp_path, case, world, monkeypatch):
         monkeypatch.setenv("MPH_SLAB_OVERLAP", mode)
         out[mode] = run_slab(case, world, [1, 7], str(tmp_path / ("slab%s.npz" % mode)), STRUCT_FIELDS)
     for k in out["1"].files:
-        assert np.array_equal(out["1"][k], out["0"][k]), k
+        if k != "overlap":   # (the pass-B mode report differs by construction)
+            assert np.array_equal(out["1"][k], out["0"][k]), k
 
 
 def test_slab_overlap_probe(tmp_path, monkeypatch):
