@@ -444,9 +444,8 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     CK(dalloc(c, &c->rank_of, cap));
     CK(dalloc(c, &c->key, cap)); CK(dalloc(c, &c->slot, cap)); CK(dalloc(c, &c->tmp, cap));
     CK(dalloc(c, &c->cnt, c->P.ncell)); CK(dalloc(c, &c->start, (size_t)c->P.ncell + 1));
-    // the cell scan's block totals filled by k_prep (MPH_PREP_BSUM; zero at the start, zeroed again by
-    // the scan), the block prefixes of the scan_top path, and scratch for the other scans (structure
-    // init, MPH_PREP_BSUM=0)
+    // the cell scan's block totals: two parity buffers filled by k_prep (MPH_PREP_BSUM builds), and a
+    // scratch third for the other scans (k_scan_reduce, structure init); all zero at the start
     const size_t bs = (size_t)c->P.ncell / 4096 + 2;
     CK(dalloc(c, &c->bsum, 3 * bs));
     CK(dalloc(c, &c->nbr, ntile * kTile * kMaxNeighbor)); CK(dalloc(c, &c->ncount, cap));

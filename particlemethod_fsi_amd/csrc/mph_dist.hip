@@ -545,7 +545,10 @@ int overlap_probe(MphCtx* c)
         best[1] = std::min(best[1], (double)ms[1]);
         best[2] = std::min(best[2], (double)ms[3] - (double)ms[2]);
     }
+    // undo the trial pass B: B as dist_init left it, Force / Acceleration zero as after creation
     MPH_CK(copy_soa(c, c->B, c->A, c->n));
+    MPH_HIP_OK(c, hipMemsetAsync(c->force, 0, sizeof(double4) * std::max(c->P.n, 1), c->stream));
+    MPH_HIP_OK(c, hipMemsetAsync(c->acc, 0, sizeof(double4) * std::max(c->P.n, 1), c->stream));
     MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
     MPH_CK(collective_max(c, best, 3));
     for (int k = 0; k < 3; ++k) D.probe_ms[k] = best[k];

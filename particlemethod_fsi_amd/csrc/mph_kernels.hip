@@ -661,15 +661,13 @@ constexpr int kScanThreads = 256;
 constexpr int kScanItems = MPH_SCAN_ITEMS;   // cells per thread (a multiple of 4)
 constexpr int kScanBlock = kScanThreads * kScanItems;   // 4096 cells per block (bsum arrays: ncell / 4096 + 2)
 // Block totals of the cell histogram from k_prep (MPH_PREP_BSUM, default): one atomic per run of equal
-// 4096-cell blocks among a wavefront's lanes adds the run's particles to the totals, so the scan
-// needs no k_scan_reduce pass over the whole histogram.  L.bsum holds bsum_stride(ncell) ints of
-// totals (zeroed by mph_create), then the scratch of the other scans.  Once consumed the totals are
-// zeroed for the next step: by k_scan_top (many blocks: it writes the block prefixes into the scratch
-// part and clears the totals it read) or by the last k_scan_down block to finish (fused top: every
-// block sums its predecessors' totals itself, so they stay until all blocks have read them; the
-// counter sits in the totals' spare last entry).
+// 4096-cell blocks among a wavefront's lanes adds the run's particles to the step's totals, so the
+// scan needs no k_scan_reduce pass over the whole histogram.  The totals live in two buffers of
+// bsum_stride(ncell) ints selected by the step's parity (DevState.seam_step, advanced by k_place):
+// k_prep adds into this step's buffer, k_scan_down reads it and clears the other one (all of its
+// blocks, so every entry a later k_prep can reach is zero), and mph_create zeroes both.
 #ifndef MPH_PREP_BSUM
-#define MPH_PREP_BSUM 1
+#define MPH_PREP_BSUM 0   // opt-in: same-box A/B D16M -0.3 %, D1M +0.3 % (profiles/r05/prep_bsum/)
 #endif
 __host__ __device__ inline int bsum_stride(int ncell) { return ncell / kScanBlock + 2; }
 static_assert(kScanBlock == 4096, "mph_ctx.hip sizes the bsum buffers for 4096-cell blocks");
@@ -712,9 +710,9 @@ __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __res
         base = __shfl(base, hl, 64);
         if (live) slot[p] = base + (lane - hl);
         if (bsum2) {
-            // the block totals: one atomic per run of equal 4096-cell blocks (dead lanes past n
-            // carry distinct negative blocks, so they never join a live run nor add)
-            int* bsum = bsum2;
+            // this step's block totals: one atomic per run of equal 4096-cell blocks (dead lanes
+            // past n carry distinct negative blocks, so they never join a live run nor add)
+            int* bsum = bsum2 + (st->seam_step & 1) * bsum_stride(P.ncell);
             const int blk = live ? k / kScanBlock : k;
             const int bprev = __shfl_up(blk, 1, 64);
             const bool bhead = lane == 0 || bprev != blk;
@@ -747,7 +745,7 @@ __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __res
     const int k = cell_id(P, x, y, z);
     key[p] = k;
     slot[p] = atomicAdd(&cnt[k], 1);
-    if (bsum2) atomicAdd(&bsum2[k / kScanBlock], 1);
+    if (bsum2) atomicAdd(&bsum2[(st->seam_step & 1) * bsum_stride(P.ncell) + k / kScanBlock], 1);
     const int occ = seam_bits(P, x, y, z);
     if (occ) {
         int* w = const_cast<int*>(&st->seam_occ[st->seam_step & 1]);
@@ -815,10 +813,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const int* __restr
     if (threadIdx.x == 0) bsum[blockIdx.x] = total;
 }
 
-// The block prefixes of totals `bsum` into `out` (in place when out == bsum); clear: zero the totals
-// read (MPH_PREP_BSUM: k_prep's totals, ready for the next step)
-__global__ __launch_bounds__(1024) void k_scan_top(int* __restrict__ bsum, int nb, int* __restrict__ out, int clear)
+// st non-null: bsum is the pair of parity buffers of MPH_PREP_BSUM (this step's is scanned)
+__global__ __launch_bounds__(1024) void k_scan_top(int* __restrict__ bsum, int nb, const DevState* __restrict__ st,
+                                                   int stride)
 {
+    if (st) bsum += (st->seam_step & 1) * stride;
     __shared__ int lds[16];
     __shared__ int carry;
     if (threadIdx.x == 0) carry = 0;
@@ -829,10 +828,7 @@ __global__ __launch_bounds__(1024) void k_scan_top(int* __restrict__ bsum, int n
         int total;
         const int ex = block_exclusive_scan(v, lds, total);
         const int c = carry;
-        if (i < nb) {
-            if (clear) bsum[i] = 0;
-            out[i] = ex + c;
-        }
+        if (i < nb) bsum[i] = ex + c;
         __syncthreads();
         if (threadIdx.x == 0) carry = c + total;
         __syncthreads();
@@ -849,9 +845,16 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_down(int* __restrict__ cn
                                                             const int* __restrict__ bsum,
                                                             int* __restrict__ start, int n,
                                                             const int* __restrict__ n_dev, int top,
-                                                            int* __restrict__ clear_ctr)
+                                                            const DevState* __restrict__ st, int stride)
 {
     __shared__ int lds[kScanThreads / 64];
+    if (st) {
+        // MPH_PREP_BSUM: this step's totals (from k_prep's atomics); the other parity's entry of this
+        // block is cleared for the next step's k_prep (nothing reads it during this step)
+        const int par = st->seam_step & 1;
+        if (threadIdx.x == 0) const_cast<int*>(bsum)[(par ^ 1) * stride + blockIdx.x] = 0;
+        bsum += par * stride;
+    }
     const int base = blockIdx.x * kScanBlock + threadIdx.x * kScanItems;
     int v[kScanItems];
     load16(cnt, base, ncell, v);
@@ -893,22 +896,6 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_down(int* __restrict__ cn
             }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) start[ncell] = n_dev ? *n_dev : n;
-    if (clear_ctr) {
-        // fused top over k_prep's totals (MPH_PREP_BSUM): the last block to finish -- every block
-        // read its predecessors' totals before counting itself in -- zeroes them for the next step
-        __shared__ int s_last;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __threadfence();
-            s_last = atomicAdd(clear_ctr, 1) == (int)gridDim.x - 1;
-        }
-        __syncthreads();
-        if (s_last) {
-            int* b = const_cast<int*>(bsum);
-            for (int k = threadIdx.x; k < (int)gridDim.x; k += kScanThreads) b[k] = 0;
-            if (threadIdx.x == 0) *clear_ctr = 0;
-        }
-    }
 }
 
 // Unordered placement; block 0 also advances Time and WallCenter (main.cpp:685, 3066-3070)
@@ -3324,22 +3311,25 @@ void launch_sort(const Launch& L, int mode)
     const int top = nb <= kScanFusedTop;
     const int bs = bsum_stride(P.ncell);
     if (MPH_PREP_BSUM) {
-        // block totals from k_prep (no k_scan_reduce), zeroed again by the scan (see bsum_stride)
+        // block totals from k_prep into this step's parity buffer of L.bsum (no k_scan_reduce)
         MPH_LAUNCH("prep", L.stream, k_prep, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.B,
                    L.key, L.slot, L.cnt, mode, L.vsrc, L.bsum);
         if (!top)
-            MPH_LAUNCH("scan_top", L.stream, k_scan_top, dim3(1), dim3(1024), 0, L.stream, L.bsum, nb, L.bsum + bs, 1);
+            MPH_LAUNCH("scan_top", L.stream, k_scan_top, dim3(1), dim3(1024), 0, L.stream, L.bsum, nb,
+                       (const DevState*)L.st, bs);
         MPH_LAUNCH("scan_down", L.stream, k_scan_down, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt,
-                   P.ncell, top ? L.bsum : L.bsum + bs, L.start, n, P.n_dev, top, top ? L.bsum + bs - 1 : (int*)nullptr);
+                   P.ncell, L.bsum, L.start, n, P.n_dev, top, (const DevState*)L.st, bs);
     } else {
         int* bsum = L.bsum + 2 * bs;   // the scratch third of L.bsum
         MPH_LAUNCH("prep", L.stream, k_prep, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.B,
                    L.key, L.slot, L.cnt, mode, L.vsrc, (int*)nullptr);
         MPH_LAUNCH("scan_reduce", L.stream, k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt,
                    P.ncell, bsum);
-        if (!top) MPH_LAUNCH("scan_top", L.stream, k_scan_top, dim3(1), dim3(1024), 0, L.stream, bsum, nb, bsum, 0);
+        if (!top)
+            MPH_LAUNCH("scan_top", L.stream, k_scan_top, dim3(1), dim3(1024), 0, L.stream, bsum, nb,
+                       (const DevState*)nullptr, 0);
         MPH_LAUNCH("scan_down", L.stream, k_scan_down, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt,
-                   P.ncell, bsum, L.start, n, P.n_dev, top, (int*)nullptr);
+                   P.ncell, bsum, L.start, n, P.n_dev, top, (const DevState*)nullptr, 0);
     }
     MPH_LAUNCH("place", L.stream, k_place, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.key,
                L.slot, L.start, L.tmp, mode);
@@ -3628,9 +3618,9 @@ void launch_scan(int* cnt, int ncell, int* bsum, int* start, int total, hipStrea
     const int top = nb <= kScanFusedTop;
     MPH_LAUNCH("scan_reduce", stream, k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, stream, cnt, ncell, bsum);
     if (!top)
-        MPH_LAUNCH("scan_top", stream, k_scan_top, dim3(1), dim3(1024), 0, stream, bsum, nb, bsum, 0);
+        MPH_LAUNCH("scan_top", stream, k_scan_top, dim3(1), dim3(1024), 0, stream, bsum, nb, (const DevState*)nullptr, 0);
     MPH_LAUNCH("scan_down", stream, k_scan_down, dim3(nb), dim3(kScanThreads), 0, stream, cnt, ncell, bsum,
-               start, total, (const int*)nullptr, top, (int*)nullptr);
+               start, total, (const int*)nullptr, top, (const DevState*)nullptr, 0);
 }
 
 int dist_blocks(int n) { return blocks(n > 0 ? n : 1, 256); }
