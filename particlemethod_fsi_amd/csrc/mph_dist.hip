@@ -388,6 +388,7 @@ HaloFields halo_fields(MphCtx* c)
     F.f[0] = c->pres;
     F.nf = 1;
     F.rec = c->rec;
+    F.rec_stride = c->P.n;   // the plane stride of the pass-B records (capacity)
     if (c->P.surface) {
         F.f[1] = c->gx; F.f[2] = c->gy; F.f[3] = c->gz; F.f[4] = c->pa;
         F.nf = 5;

@@ -141,7 +141,8 @@ void launch_virial(const Launch& L, const Soa& X, double* vir, double* vpres);  
 struct HaloFields {
     double* f[5];
     int nf;
-    double4* rec;   // f[0] (PressureP) is also the .w of the pass-B record
+    double4* rec;   // f[0] (PressureP) is also the P of the pass-B record (its plane stride rec_stride)
+    int rec_stride;
 };
 void launch_scan(int* cnt, int ncell, int* bsum, int* start, int total, hipStream_t stream, Profiler* prof);
 int dist_blocks(int n);

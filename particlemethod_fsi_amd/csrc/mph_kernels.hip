@@ -429,13 +429,28 @@ __device__ __forceinline__ int nbr_entry(int j, int type) { return j | (type << 
 // (entry kWinCols: 1 = written by the staged search), kWinHdr int2 per wave (Launch.whdr)
 constexpr int kWinCols = kGroups * kGroups;   // 3-D stencil columns (2-D uses the first kGroups)
 
-// Velocity of sorted particle i for the list passes: from its 48-byte gather record {x, y, z, vx,
-// vy, vz} (k_rank_scatter then skips the SoA velocity stores), or the SoA arrays.
-__device__ __forceinline__ void own_velocity(const Soa& A, int i, double& vx, double& vy, double& vz)
+// The gather records of the list passes -- pass A's {x, y, z, vx, vy, vz} (Soa.p6) and pass B's
+// {x, y, z, PressureP} (Launch.rec) -- are split into 16-byte planes (MPH_PLANES, default): piece k
+// of particle j sits at [k * ps + j], ps = the array capacity (DevParams.n).  Each 16-byte gather
+// instruction of a wavefront then reads one plane: 64 lanes whose neighbours are consecutive
+// particles touch 1 KB (8 cache lines of 128 B) instead of the 3 KB (24 lines) of 48-byte records,
+// and the list passes are bound by the L1 tag-lookup rate (one per clock per CU).
+// The instructions per neighbour stay three (pass A) and two (pass B).  MPH_PLANES=0: interleaved
+// records, piece k of j at [3 j + k] (pass A) / one double4 (pass B).
+#ifndef MPH_PLANES
+#define MPH_PLANES 1
+#endif
+__device__ __forceinline__ size_t p6_at(int ps, int j, int k)
+{
+    return MPH_PLANES ? (size_t)k * ps + j : 3 * (size_t)j + k;
+}
+
+// Velocity of sorted particle i for the list passes: from its gather record {x, y, z, vx, vy, vz}
+// (k_rank_scatter then skips the SoA velocity stores), or the SoA arrays.  ps: DevParams.n.
+__device__ __forceinline__ void own_velocity(const Soa& A, int i, double& vx, double& vy, double& vz, int ps)
 {
     if (MPH_AOS_GATHER && A.p6) {
-        const double2* q = A.p6 + 3 * (size_t)i;
-        const double2 b = q[1], c = q[2];
+        const double2 b = A.p6[p6_at(ps, i, 1)], c = A.p6[p6_at(ps, i, 2)];
         vx = b.y; vy = c.x; vz = c.y;
     } else {
         vx = A.vx[i]; vy = A.vy[i]; vz = A.vz[i];
@@ -963,10 +978,9 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
     const int id = mig ? -1 - B.id[b] : B.id[b];
     A.id[dst] = id;
     if (A.p6) {
-        double2* q = A.p6 + 3 * (size_t)dst;
-        q[0] = make_double2(B.x[b], B.y[b]);
-        q[1] = make_double2(B.z[b], B.vx[b]);
-        q[2] = make_double2(B.vy[b], B.vz[b]);
+        A.p6[p6_at(P.n, dst, 0)] = make_double2(B.x[b], B.y[b]);
+        A.p6[p6_at(P.n, dst, 1)] = make_double2(B.z[b], B.vx[b]);
+        A.p6[p6_at(P.n, dst, 2)] = make_double2(B.vy[b], B.vz[b]);
     }
     if (MPH_SEARCH_F32 && A.f4)
         A.f4[dst] = make_float4((float)(B.x[b] - P.cref[0]), (float)(B.y[b] - P.cref[1]),
@@ -1078,6 +1092,35 @@ struct PassAOut {
     double4 *fpart, *rec;
 };
 
+// pass B's gather record {x, y, z, PressureP} of sorted particle i (planes {x, y} and {z, P}, see
+// p6_at; ps = DevParams.n), and its PressureP alone (the halo)
+__device__ __forceinline__ void rec_store(double4* rec, int ps, int i, double x, double y, double z, double p)
+{
+    if (MPH_PLANES) {
+        double2* r = reinterpret_cast<double2*>(rec);
+        r[i] = make_double2(x, y);
+        r[(size_t)ps + i] = make_double2(z, p);
+    } else {
+        rec[i] = make_double4(x, y, z, p);
+    }
+}
+__device__ __forceinline__ void rec_store_p(double4* rec, int ps, int i, double p)
+{
+    if (MPH_PLANES) reinterpret_cast<double2*>(rec)[(size_t)ps + i].y = p;
+    else rec[i].w = p;
+}
+__device__ __forceinline__ void rec_load(const double4* rec, int ps, int j, double& x, double& y, double& z, double& p)
+{
+    if (MPH_PLANES) {
+        const double2* r = reinterpret_cast<const double2*>(rec);
+        const double2 a = r[j], b = r[(size_t)ps + j];
+        x = a.x; y = a.y; z = b.x; p = b.y;
+    } else {
+        const double4 r4 = rec[j];
+        x = r4.x; y = r4.y; z = r4.z; p = r4.w;
+    }
+}
+
 __device__ __forceinline__ void pass_a_finish(const DevParams& P, const DevTables* T, int ti, int i,
                                               const PassA& o, const PassAOut& out, double xi = 0.0,
                                               double yi = 0.0, double zi = 0.0)
@@ -1104,7 +1147,7 @@ __device__ __forceinline__ void pass_a_finish(const DevParams& P, const DevTable
     }
     if (out.fpart) {
         out.fpart[i] = make_double4(p * o.s0 + o.v0, p * o.s1 + o.v1, p * o.s2 + o.v2, 0.0);
-        out.rec[i] = make_double4(xi, yi, zi, p);
+        rec_store(out.rec, P.n, i, xi, yi, zi, p);
     }
 }
 
@@ -1935,8 +1978,8 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (MPH_AOS_GATHER) {
-                const double2* q = A.p6 + 3 * (size_t)jj[u];
-                const double2 a = q[0], b = q[1], c = q[2];
+                const double2 a = A.p6[p6_at(P.n, jj[u], 0)], b = A.p6[p6_at(P.n, jj[u], 1)],
+                              c = A.p6[p6_at(P.n, jj[u], 2)];
                 X[u] = a.x; Y[u] = a.y; Z[u] = b.x;
                 VX[u] = b.y; VY[u] = c.x; VZ[u] = c.y;
             } else {
@@ -1986,7 +2029,16 @@ __device__ __forceinline__ void pass_a_staged(const DevParams& P, const double* 
         if (w.y <= w.x) continue;
         const int mn = w.x, mx = w.y;
         const bool staged = mx - mn <= CAP;
-        if (staged) {
+        if (staged && MPH_PLANES) {
+            // the window [mn, mx) of each 16-byte plane, 64 pieces per instruction; plane k at stage + k CAP
+            for (int k = 0; k < 3; ++k)
+                for (int p = 0; p * 64 < mx - mn; ++p)   // wave-uniform
+                    if (lane < mx - mn - p * 64)
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(rp, lds_ptr(stage + k * CAP + p * 64), 16, lane16,
+                                                                 (unsigned)(p6_at(P.n, mn, k) * 16 + p * 1024), 0, 0);
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+            __builtin_amdgcn_wave_barrier();
+        } else if (staged) {
             // the window's bytes [48 mn, 48 mx) in 16-byte pieces, 64 per instruction
             const int pieces = 3 * (mx - mn);
             const unsigned so = (unsigned)mn * 48u;
@@ -2002,11 +2054,14 @@ __device__ __forceinline__ void pass_a_staged(const DevParams& P, const double* 
             if (a) {
                 double2 r0, r1, r2;
                 if (staged && j0 >= mn) {
-                    const double2* q = stage + 3 * (j0 - mn);
-                    r0 = q[0]; r1 = q[1]; r2 = q[2];
+                    if (MPH_PLANES) {
+                        r0 = stage[j0 - mn]; r1 = stage[CAP + j0 - mn]; r2 = stage[2 * CAP + j0 - mn];
+                    } else {
+                        const double2* q = stage + 3 * (j0 - mn);
+                        r0 = q[0]; r1 = q[1]; r2 = q[2];
+                    }
                 } else {
-                    const double2* q = A.p6 + 3 * (size_t)j0;
-                    r0 = q[0]; r1 = q[1]; r2 = q[2];
+                    r0 = A.p6[p6_at(P.n, j0, 0)]; r1 = A.p6[p6_at(P.n, j0, 1)]; r2 = A.p6[p6_at(P.n, j0, 2)];
                 }
                 const double q0 = image_exact<true>(r0.x - xi, P.dw[0], P.hw[0], P.w075[0]);
                 const double q1 = image_exact<true>(r0.y - yi, P.dw[1], P.hw[1], P.w075[1]);
@@ -2058,12 +2113,12 @@ __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, cons
     if (wave_all_ghosts(P, A, live, ii)) {
         // ghosts: PressureP (+ GravityCenter, PressureA) arrive in the halo, which also fills the
         // .w of the pass-B record; its position part is written here
-        if (live && pout.rec) pout.rec[i] = make_double4(xi, yi, zi, 0.0);
+        if (live && pout.rec) rec_store(pout.rec, P.n, i, xi, yi, zi, 0.0);
         return;
     }
     // likewise the ghost lanes of a mixed wave
     const bool ghost = live && P.slab_axis >= 0 && A.id[ii] < 0;
-    if (ghost && pout.rec) pout.rec[i] = make_double4(xi, yi, zi, 0.0);
+    if (ghost && pout.rec) rec_store(pout.rec, P.n, i, xi, yi, zi, 0.0);
     const bool own = live && !ghost;
     // the search's rule (its list order and the fast minimum image go together)
     const bool fast = wave_search_interior(P, st, own, xi, yi, zi);
@@ -2072,7 +2127,7 @@ __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, cons
         if (h[kWinCols].x == 1) {   // wave-uniform: the staged search wrote this wave's windows
             __shared__ __attribute__((aligned(16))) double2 pstage[kWB][3 * MPH_PA_CAP];
             double vxi = 0.0, vyi = 0.0, vzi = 0.0;
-            if (own) own_velocity(A, i, vxi, vyi, vzi);
+            if (own) own_velocity(A, i, vxi, vyi, vzi, P.n);
             const int ti = A.type[ii];
             const bool solid = dev_is_struct(ti);
             const int cnt = own ? (ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor) : 0;
@@ -2087,7 +2142,7 @@ __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, cons
     }
     if (!own) return;
     double vxi, vyi, vzi;
-    own_velocity(A, i, vxi, vyi, vzi);
+    own_velocity(A, i, vxi, vyi, vzi, P.n);
     const int ti = A.type[i];
     const bool solid = dev_is_struct(ti);
     const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
@@ -2209,8 +2264,7 @@ __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (MPH_PB_REC) {
-                const double4 r4 = rec[jj[u]];
-                X[u] = r4.x; Y[u] = r4.y; Z[u] = r4.z; PJ[u] = r4.w;
+                rec_load(rec, P.n, jj[u], X[u], Y[u], Z[u], PJ[u]);
             } else {
                 X[u] = A.x[jj[u]]; Y[u] = A.y[jj[u]]; Z[u] = A.z[jj[u]];
                 PJ[u] = pres[jj[u]];
@@ -2307,7 +2361,7 @@ __global__ __launch_bounds__(MPH_LB) MPH_PB_ATTR void k_pass_b(DevParams P, cons
         pass_b_loop<false, false, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, NL, cnt, ti, solid, xi, yi,
                                              zi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
     double vxi, vyi, vzi;
-    own_velocity(A, i, vxi, vyi, vzi);
+    own_velocity(A, i, vxi, vyi, vzi, P.n);
     double vo0 = vxi, vo1 = vyi, vo2 = vzi;
     double xo0 = xi, xo1 = yi, xo2 = zi;
     double4 ao = make_double4(0.0, 0.0, 0.0, 0.0);
@@ -3264,7 +3318,7 @@ __global__ __launch_bounds__(256) void k_halo_unpack(const double* __restrict__ 
     if (k >= m) return;
     const int a = dst_of[k < n1 ? o1 + k : o2 + (k - n1)];
     for (int f = 0; f < F.nf; ++f) F.f[f][a] = buf[(size_t)f * m + k];
-    if (F.rec) F.rec[a].w = buf[k];
+    if (F.rec) rec_store_p(F.rec, F.rec_stride, a, buf[k]);
 }
 
 // ---------------------------------------------------------------------------- launchers -----
