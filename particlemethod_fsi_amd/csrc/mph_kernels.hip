@@ -430,19 +430,23 @@ __device__ __forceinline__ int nbr_entry(int j, int type) { return j | (type << 
 constexpr int kWinCols = kGroups * kGroups;   // 3-D stencil columns (2-D uses the first kGroups)
 
 // The gather records of the list passes -- pass A's {x, y, z, vx, vy, vz} (Soa.p6) and pass B's
-// {x, y, z, PressureP} (Launch.rec) -- are split into 16-byte planes (MPH_PLANES, default): piece k
-// of particle j sits at [k * ps + j], ps = the array capacity (DevParams.n).  Each 16-byte gather
-// instruction of a wavefront then reads one plane: 64 lanes whose neighbours are consecutive
-// particles touch 1 KB (8 cache lines of 128 B) instead of the 3 KB (24 lines) of 48-byte records,
-// and the list passes are bound by the L1 tag-lookup rate (one per clock per CU).
-// The instructions per neighbour stay three (pass A) and two (pass B).  MPH_PLANES=0: interleaved
-// records, piece k of j at [3 j + k] (pass A) / one double4 (pass B).
+// {x, y, z, PressureP} (Launch.rec) -- can be split into 16-byte planes: piece k of particle j at
+// [k * ps + j], ps = the array capacity (DevParams.n).  A 16-byte gather instruction of a wavefront
+// then reads one plane: 64 lanes whose neighbours are consecutive particles touch 1 KB (8 lines of
+// 128 B) instead of 2-3 KB of whole records, the same instruction count, but a record's pieces now
+// come from 2-3 lines instead of 1-2.  Measured same box (profiles/r05/planes/): pass B's 32-byte
+// records gain (D1M 0.271 -> 0.251 ms, D16M 2.89 -> 2.66 ms: MPH_PLANES, default on), pass A's
+// 48-byte ones lose (0.376 -> 0.446 ms at rest, 0.510 -> 0.543 developed, D16M 3.81 -> 4.37 ms:
+// MPH_P6_PLANES, default off).
 #ifndef MPH_PLANES
 #define MPH_PLANES 1
 #endif
+#ifndef MPH_P6_PLANES
+#define MPH_P6_PLANES 0
+#endif
 __device__ __forceinline__ size_t p6_at(int ps, int j, int k)
 {
-    return MPH_PLANES ? (size_t)k * ps + j : 3 * (size_t)j + k;
+    return MPH_P6_PLANES ? (size_t)k * ps + j : 3 * (size_t)j + k;
 }
 
 // Velocity of sorted particle i for the list passes: from its gather record {x, y, z, vx, vy, vz}
@@ -2029,7 +2033,7 @@ __device__ __forceinline__ void pass_a_staged(const DevParams& P, const double* 
         if (w.y <= w.x) continue;
         const int mn = w.x, mx = w.y;
         const bool staged = mx - mn <= CAP;
-        if (staged && MPH_PLANES) {
+        if (staged && MPH_P6_PLANES) {
             // the window [mn, mx) of each 16-byte plane, 64 pieces per instruction; plane k at stage + k CAP
             for (int k = 0; k < 3; ++k)
                 for (int p = 0; p * 64 < mx - mn; ++p)   // wave-uniform
@@ -2054,7 +2058,7 @@ __device__ __forceinline__ void pass_a_staged(const DevParams& P, const double* 
             if (a) {
                 double2 r0, r1, r2;
                 if (staged && j0 >= mn) {
-                    if (MPH_PLANES) {
+                    if (MPH_P6_PLANES) {
                         r0 = stage[j0 - mn]; r1 = stage[CAP + j0 - mn]; r2 = stage[2 * CAP + j0 - mn];
                     } else {
                         const double2* q = stage + 3 * (j0 - mn);
