@@ -444,10 +444,13 @@ constexpr int kWinCols = kGroups * kGroups;   // 3-D stencil columns (2-D uses t
 #ifndef MPH_P6_PLANES
 #define MPH_P6_PLANES 0
 #endif
+// MPH_P6_PLANES=2: {x, y, z, vx} as 32-byte records, {vy, vz} in a 16-byte plane behind them
 __device__ __forceinline__ size_t p6_at(int ps, int j, int k)
 {
+    if (MPH_P6_PLANES == 2) return k < 2 ? 2 * (size_t)j + k : 2 * (size_t)ps + j;
     return MPH_P6_PLANES ? (size_t)k * ps + j : 3 * (size_t)j + k;
 }
+static_assert(!(MPH_PA_STAGED && MPH_P6_PLANES == 2), "the staged pass A stages whole records or three planes");
 
 // Velocity of sorted particle i for the list passes: from its gather record {x, y, z, vx, vy, vz}
 // (k_rank_scatter then skips the SoA velocity stores), or the SoA arrays.  ps: DevParams.n.

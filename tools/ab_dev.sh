@@ -1,0 +1,21 @@
+#!/bin/bash
+# Same-box A/B of library builds (particlemethod_fsi_amd/lib_<name>; "base" = lib/) at rest (D1M),
+# in the developed flow (D1M from t = 0.25 s, tools/dev_state.py) and, with D16M=1, on D16M;
+# ROUNDS alternating rounds.  Output: $OUT/{rest,dev,d16m}_<name>_<round>.json (tools/ab_dev_summary.py)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=${OUT:-gpurun_out/abdev}
+mkdir -p $OUT
+timeout -k 10 120 python3 tools/dev_state.py d1m 2500 $OUT/d1m_dev.gridb > $OUT/dev_state.log 2>&1 || exit 21
+for r in $(seq 1 ${ROUNDS:-2}); do
+  for v in base ${VARIANTS}; do
+    lib=$PWD/particlemethod_fsi_amd/lib/libmph_gpu.so
+    [ $v != base ] && lib=$PWD/particlemethod_fsi_amd/lib_$v/libmph_gpu.so
+    MPH_GPU_LIB=$lib timeout -k 10 300 python3 bench.py --developed-steps 0 --steps 20 --warmup 4 --no-cpu-baseline > $OUT/rest_${v}_$r.json 2> $OUT/rest_$v.err || exit 22
+    MPH_GPU_LIB=$lib timeout -k 10 300 python3 bench.py --state $OUT/d1m_dev.gridb --steps 20 --warmup 4 --no-cpu-baseline > $OUT/dev_${v}_$r.json 2> $OUT/dev_$v.err || exit 23
+    if [ "${D16M:-0}" = 1 ]; then
+      MPH_GPU_LIB=$lib timeout -k 10 300 python3 bench.py --case d16m --steps 12 --warmup 4 --no-cpu-baseline > $OUT/d16m_${v}_$r.json 2> $OUT/d16m_$v.err || exit 24
+    fi
+  done
+done
+rm -f $OUT/d1m_dev.gridb
