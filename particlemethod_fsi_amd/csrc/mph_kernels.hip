@@ -92,9 +92,10 @@
 #endif
 
 #ifndef MPH_PA_STAGED
-// pass A reads each stencil column's window of 48-byte records from LDS, staged once per wave
-// (the search writes the windows per wave: kWinHdr), instead of per-lane gathers through L1
-// (measured, opt-in)
+// pass A of the interior waves in a kernel of its own (k_pass_a_st) that reads each stencil column's
+// window of 48-byte records from LDS, staged once per wave (the search writes the windows per wave:
+// kWinHdr), instead of per-lane gathers through L1; its lean register budget buys the occupancy that
+// hides the staging round trips (measured, opt-in)
 #define MPH_PA_STAGED 0
 #endif
 #ifndef MPH_SEARCH_F32
@@ -109,7 +110,7 @@
 #define MPH_DIAG_PA 0   // diagnostic builds: the staged pass A checks it used every entry (DevState.overflow 32)
 #endif
 #ifndef MPH_PA_CAP
-#define MPH_PA_CAP 160   // records staged per column window (7.5 KB per wave; 4 waves per SIMD)
+#define MPH_PA_CAP 128   // records staged per column window (6 KB per wave; MPH_PAS_WPE waves per SIMD)
 #endif
 
 namespace mph {
@@ -2007,84 +2008,119 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
     }
 }
 
+// The waves k_pass_a_st takes (MPH_PA_STAGED): interior waves of a single context whose search wrote
+// their column windows, at equal radii.  k_pass_a evaluates the same predicate and leaves them.
+__device__ __forceinline__ bool pa_staged_wave(const DevParams& P, const int2* whdr, int i, bool fast)
+{
+    if (!MPH_PA_STAGED || !whdr || !fast || P.slab_axis >= 0 || !pass_a_equal_radii(P)) return false;
+    return whdr[(size_t)__builtin_amdgcn_readfirstlane(i >> 6) * kWinHdr + kWinCols].x == 1;
+}
+
 // Pass A of an interior wave from LDS-staged column windows (MPH_PA_STAGED): the search recorded the
 // wave's window [mn, mx) of every stencil column (whdr); per column the wave stages the window's
-// 48-byte records {x, y, z, vx, vy, vz} with coalesced buffer loads into LDS (16 bytes per lane,
-// 1 KB per instruction: ~8 L1 lines instead of ~24 per 16-byte gather of the list loop), then every
-// lane takes its next list entries below the window's end mx (a lane's entries ascend through the
-// columns) and reads the records of those inside [mn, mx) from LDS.  An entry below mn -- a later
-// column of a lane that had no candidates in this one, when the wave spans two cell rows -- is read
-// from global memory.  Same entries in the same order, same pass_a_term: every sum is bit-identical
-// to pass_a_loop.  Windows wider than CAP read their records from global memory.  Every lane of the
-// wave takes part (act: it has a particle).
-template <int DIM, bool EQR, int CAP = MPH_PA_CAP>
+// 48-byte records {x, y, z, vx, vy, vz} with coalesced buffer loads into LDS (1 KB per instruction,
+// 8 L1 lines, instead of per-lane 16-byte gathers touching ~24-35 lines each), then every lane takes
+// its next list entries below the window's end mx (a lane's entries ascend through the columns)
+// and reads their records from LDS -- an entry below mn (a later column of a lane with no candidates
+// in this one, when the wave spans two cell rows) or in a window wider than CAP from global memory.
+// Same entries in the same order, same pass_a_term: every sum is bit-identical to pass_a_loop.  The
+// lane's entries come four at a time, the next four loaded while the current ones are used.
+template <int DIM, int CAP = MPH_PA_CAP>
 __device__ __forceinline__ void pass_a_staged(const DevParams& P, const double* s_ratio, const double* s_mu,
-                                              const Soa& A, const NbrList& NL, const int2* whdr, int cnt, int ti,
+                                              const Soa& A, const int* row, const int2* whdr, int cnt, int ti,
                                               bool solid, double xi, double yi, double zi, double vxi, double vyi,
-                                              double vzi, PassA& o, double2* stage, const DevState* st = nullptr)
+                                              double vzi, PassA& o, double2* stage, const DevState* st)
 {
     constexpr int NCOL = DIM == 3 ? kGroups * kGroups : kGroups;
     const int lane = threadIdx.x & 63;
     const __amdgpu_buffer_rsrc_t rp = arr_rsrc(A.p6);
     const unsigned lane16 = (unsigned)lane * 16u;
-    int k = 0;
-    int j0 = INT_MAX, t0 = 0, j1 = INT_MAX, t1 = 0;   // the lane's next two entries
-    if (0 < cnt) nbr_at<false>(NL, 0, j0, t0);
-    if (1 < cnt) nbr_at<false>(NL, 1, j1, t1);
+    // entry k of the lane's ELL row, or a sentinel past every window (index 2^28 - 1)
+    auto ld = [&](int k) { return k < cnt ? row[(size_t)k * kTile] : 0x7fffffff; };
+    int c0 = ld(0), c1 = ld(1), c2 = ld(2), c3 = ld(3);
+    int x0 = ld(4), x1 = ld(5), x2 = ld(6), x3 = ld(7);
+    int p = 0, kn = 8, used = 0;
     for (int col = 0; col < NCOL; ++col) {
         const int2 w = whdr[col];   // wave-uniform
         if (w.y <= w.x) continue;
         const int mn = w.x, mx = w.y;
         const bool staged = mx - mn <= CAP;
-        if (staged && MPH_P6_PLANES) {
-            // the window [mn, mx) of each 16-byte plane, 64 pieces per instruction; plane k at stage + k CAP
-            for (int k = 0; k < 3; ++k)
-                for (int p = 0; p * 64 < mx - mn; ++p)   // wave-uniform
-                    if (lane < mx - mn - p * 64)
-                        __builtin_amdgcn_raw_ptr_buffer_load_lds(rp, lds_ptr(stage + k * CAP + p * 64), 16, lane16,
-                                                                 (unsigned)(p6_at(P.n, mn, k) * 16 + p * 1024), 0, 0);
-            __builtin_amdgcn_s_waitcnt(0x0F70);
-            __builtin_amdgcn_wave_barrier();
-        } else if (staged) {
+        if (staged) {
             // the window's bytes [48 mn, 48 mx) in 16-byte pieces, 64 per instruction
             const int pieces = 3 * (mx - mn);
             const unsigned so = (unsigned)mn * 48u;
-            for (int p = 0; p * 64 < pieces; ++p)   // wave-uniform
-                if (lane < pieces - p * 64)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rp, lds_ptr(stage + p * 64), 16, lane16, so + p * 1024u, 0, 0);
+            for (int q = 0; q * 64 < pieces; ++q)   // wave-uniform
+                if (lane < pieces - q * 64)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rp, lds_ptr(stage + q * 64), 16, lane16, so + q * 1024u, 0, 0);
             __builtin_amdgcn_s_waitcnt(0x0F70);
             __builtin_amdgcn_wave_barrier();
         }
         for (;;) {
-            const bool a = j0 < mx;   // (j0 = INT_MAX past the lane's last entry)
+            const int e = p == 0 ? c0 : (p == 1 ? c1 : (p == 2 ? c2 : c3));
+            const int j = e & kIndexMask;
+            const bool a = j < mx;
             if (!__ballot(a)) break;
             if (a) {
                 double2 r0, r1, r2;
-                if (staged && j0 >= mn) {
-                    if (MPH_P6_PLANES) {
-                        r0 = stage[j0 - mn]; r1 = stage[CAP + j0 - mn]; r2 = stage[2 * CAP + j0 - mn];
-                    } else {
-                        const double2* q = stage + 3 * (j0 - mn);
-                        r0 = q[0]; r1 = q[1]; r2 = q[2];
-                    }
+                if (staged && j >= mn) {
+                    const double2* q = stage + 3 * (j - mn);
+                    r0 = q[0]; r1 = q[1]; r2 = q[2];
                 } else {
-                    r0 = A.p6[p6_at(P.n, j0, 0)]; r1 = A.p6[p6_at(P.n, j0, 1)]; r2 = A.p6[p6_at(P.n, j0, 2)];
+                    r0 = A.p6[p6_at(P.n, j, 0)]; r1 = A.p6[p6_at(P.n, j, 1)]; r2 = A.p6[p6_at(P.n, j, 2)];
                 }
                 const double q0 = image_exact<true>(r0.x - xi, P.dw[0], P.hw[0], P.w075[0]);
                 const double q1 = image_exact<true>(r0.y - yi, P.dw[1], P.hw[1], P.w075[1]);
                 const double q2 = image_exact<true>(r1.x - zi, P.dw[2], P.hw[2], P.w075[2]);
-                pass_a_term<true, EQR>(P, s_ratio, s_mu, ti, t0, solid, q0, q1, q2, r2_exact(q0, q1, q2),
-                                       r1.y - vxi, r2.x - vyi, r2.y - vzi, o);
-                ++k;
-                j0 = j1;
-                t0 = t1;
-                j1 = INT_MAX;
-                if (k + 1 < cnt) nbr_at<false>(NL, k + 1, j1, t1);
+                pass_a_term<true, true>(P, s_ratio, s_mu, ti, e >> kTypeShift, solid, q0, q1, q2,
+                                        r2_exact(q0, q1, q2), r1.y - vxi, r2.x - vyi, r2.y - vzi, o);
+                ++used;
+                if (++p == 4) {   // the next four entries (loaded four entries ago), and four more
+                    c0 = x0; c1 = x1; c2 = x2; c3 = x3;
+                    x0 = ld(kn); x1 = ld(kn + 1); x2 = ld(kn + 2); x3 = ld(kn + 3);
+                    kn += 4;
+                    p = 0;
+                }
             }
         }
         if (staged) __builtin_amdgcn_wave_barrier();   // every lane done reading before the next staging
     }
-    if (MPH_DIAG_PA && k != cnt && st) atomicOr(&const_cast<DevState*>(st)->overflow, 32);   // entries left over
+    if (MPH_DIAG_PA && used != cnt) atomicOr(&const_cast<DevState*>(st)->overflow, 32);   // entries left over
+}
+
+#ifndef MPH_PAS_WPE
+#define MPH_PAS_WPE 6   // k_pass_a_st: <= 84 VGPRs, 24 waves per CU with 6 KB of LDS each
+#endif
+template <int DIM>
+__global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_PAS_WPE))) void k_pass_a_st(
+    DevParams P, const DevTables* __restrict__ T, Soa A, const int* __restrict__ nbr, const int* __restrict__ ncount,
+    PassAOut pout, const DevState* __restrict__ st, const int2* __restrict__ whdr)
+{
+    const int n = dev_n(P);
+    const int lb = list_block(st, n);
+    if (lb < 0) return;
+    __shared__ double s_ratio[kTypes * kTypes];
+    __shared__ double s_mu[kTypes * kTypes];
+    __shared__ __attribute__((aligned(16))) double2 pstage[kWB][3 * MPH_PA_CAP];
+    if (threadIdx.x < kTypes * kTypes) {
+        s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
+        s_mu[threadIdx.x] = T->mu_ij[threadIdx.x] * (-P.cvis * P.cdv * P.vol);   // pass_a_term's viscous factor
+    }
+    __syncthreads();
+    const int i = lb * blockDim.x + threadIdx.x;
+    const bool live = i < n;
+    const int ii = live ? i : n - 1;
+    const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
+    const bool fast = wave_search_interior(P, st, live, xi, yi, zi);
+    if (!pa_staged_wave(P, whdr, i, fast)) return;
+    double vxi = 0.0, vyi = 0.0, vzi = 0.0;
+    own_velocity(A, ii, vxi, vyi, vzi, P.n);
+    const int ti = A.type[ii];
+    const int cnt = live ? min(ncount[i], kMaxNeighbor) : 0;
+    PassA o;
+    pass_a_staged<DIM>(P, s_ratio, s_mu, A, nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63),
+                       whdr + (size_t)__builtin_amdgcn_readfirstlane(i >> 6) * kWinHdr, cnt, ti, dev_is_struct(ti),
+                       xi, yi, zi, vxi, vyi, vzi, o, pstage[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], st);
+    if (live) pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
 }
 
 #ifndef MPH_PA_WPE
@@ -2129,24 +2165,7 @@ __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, cons
     const bool own = live && !ghost;
     // the search's rule (its list order and the fast minimum image go together)
     const bool fast = wave_search_interior(P, st, own, xi, yi, zi);
-    if (MPH_PA_STAGED && whdr && fast && pass_a_equal_radii(P)) {
-        const int2* h = whdr + (size_t)__builtin_amdgcn_readfirstlane(i >> 6) * kWinHdr;
-        if (h[kWinCols].x == 1) {   // wave-uniform: the staged search wrote this wave's windows
-            __shared__ __attribute__((aligned(16))) double2 pstage[kWB][3 * MPH_PA_CAP];
-            double vxi = 0.0, vyi = 0.0, vzi = 0.0;
-            if (own) own_velocity(A, i, vxi, vyi, vzi, P.n);
-            const int ti = A.type[ii];
-            const bool solid = dev_is_struct(ti);
-            const int cnt = own ? (ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor) : 0;
-            __shared__ int s_gb2[kWB][8];
-            const NbrList NL = nbr_list(nbr, nullptr, i, s_gb2[threadIdx.x >> 6]);
-            PassA o;
-            pass_a_staged<DIM, true>(P, s_ratio, s_mu, A, NL, h, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o,
-                                     pstage[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], st);
-            if (own) pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
-            return;
-        }
-    }
+    if (pa_staged_wave(P, whdr, i, fast)) return;   // k_pass_a_st's wave
     if (!own) return;
     double vxi, vyi, vzi;
     own_velocity(A, i, vxi, vyi, vzi, P.n);
@@ -3448,12 +3467,21 @@ void launch_pass_a(const Launch& L)
     const DevParams& P = *L.P;
     if (P.n == 0) return;
     const PassAOut po = pass_a_out(L);
+    const int2* wh = MPH_PA_STAGED && !L.lhdr ? L.whdr : nullptr;
+    if (wh && P.slab_axis < 0) {   // the interior waves first (k_pass_a leaves them)
+        if (P.dim == 3)
+            MPH_LAUNCH("pass_a_st", L.stream, k_pass_a_st<3>, dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P,
+                       L.T, L.A, L.nbr, L.ncount, po, L.st, wh);
+        else
+            MPH_LAUNCH("pass_a_st", L.stream, k_pass_a_st<2>, dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P,
+                       L.T, L.A, L.nbr, L.ncount, po, L.st, wh);
+    }
     if (P.dim == 3)
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<3>, dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, L.lhdr, po, L.st, MPH_PA_STAGED && !L.lhdr ? L.whdr : nullptr);
+                   L.A, L.nbr, L.ncount, L.lhdr, po, L.st, wh);
     else
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<2>, dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, L.lhdr, po, L.st, MPH_PA_STAGED && !L.lhdr ? L.whdr : nullptr);
+                   L.A, L.nbr, L.ncount, L.lhdr, po, L.st, wh);
 }
 
 // calculateNeighbor + the pass-A sums (the search, the XCD split of the passes, pass A)
