@@ -394,8 +394,11 @@ int mph_list_formats(MphCtx* ctx, int* out2);
  * its cell-scan order; the sets are what both define).  counts[count] receives each particle's
  * NeighborCount; ids the rows back to back (row k starts at the sum of min(counts, 512) before
  * it), ids_cap its capacity in ints.  Returns the number of ids written, or a negative MphStatus
- * (MPH_ERR_ARG when ids_cap is too small).  Single contexts with 32-bit ELL rows only
- * (MPH_ERR_UNSUPPORTED in slab mode or while a wave holds a compact 16-bit list).              */
+ * (MPH_ERR_ARG when ids_cap is too small).  Single contexts with the reference's whole lists only
+ * (created with MPH_LIST_FULL=1 in the environment: by default the lists keep only the pairs
+ * within the largest radius of the passes' sums, NeighborCount still counts every neighbour) and
+ * 32-bit ELL rows (MPH_ERR_UNSUPPORTED in slab mode, without MPH_LIST_FULL=1, or while a wave
+ * holds a compact 16-bit list).                                                                */
 int mph_neighbor_rows(MphCtx* ctx, int first, int count, int* counts, int* ids, long long ids_cap);
 /* Particles currently owned by this rank (after the last migration); their original indices.  */
 int mph_owned_count(const MphCtx* ctx);

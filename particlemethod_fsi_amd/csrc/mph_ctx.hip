@@ -66,6 +66,9 @@ void ctx_fill_launch(MphCtx* c)
 {
     Launch& L = c->L;
     set_uniforms(c->P);
+    // MPH_LIST_FULL=1: the lists keep every neighbour within the search radius, like the reference's
+    // Neighbor[] (mph_neighbor_rows needs them); else only those the passes' sums can take
+    if (std::getenv("MPH_LIST_FULL") && std::atoi(std::getenv("MPH_LIST_FULL")) == 1) c->P.rlf = 3.0e38f;
     L.P = &c->P;
     L.T = c->dT;
     L.st = c->dst;
@@ -75,7 +78,7 @@ void ctx_fill_launch(MphCtx* c)
     // returned through A.id), so k_rank_scatter skips that scatter; slab mode uses dst_of.
     L.A = c->A; L.B = c->B; L.rank_of = nullptr; L.dst_of = nullptr;
     L.key = c->key; L.slot = c->slot; L.tmp = c->tmp; L.cnt = c->cnt; L.start = c->start; L.bsum = c->bsum;
-    L.nbr = c->nbr; L.ncount = c->ncount; L.whdr = c->win_hdr;
+    L.nbr = c->nbr; L.ncount = c->ncount; L.nbcount = c->nbcount; L.whdr = c->win_hdr;
     // compact 16-bit lists of interior wavefronts (MPH_LIST16=1), or 32-bit ELL rows everywhere
     // (MPH_LIST16=0); unset: kListCompact
     const char* l16 = std::getenv("MPH_LIST16");
@@ -449,11 +452,13 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     const size_t bs = (size_t)c->P.ncell / 4096 + 2;
     CK(dalloc(c, &c->bsum, 3 * bs));
     CK(dalloc(c, &c->nbr, ntile * kTile * kMaxNeighbor)); CK(dalloc(c, &c->ncount, cap));
+    CK(dalloc(c, &c->nbcount, cap));
 #if (defined(MPH_DIAG_NOSTORE) && MPH_DIAG_NOSTORE) || (defined(MPH_DIAG_SEARCH) && (MPH_DIAG_SEARCH & 4))
     // diagnostic builds: the search stores no list (or skips the waves near a periodic face, whose
     // counts then stay 0), so the passes read index 0 (never garbage)
     if (hipMemset(c->nbr, 0, sizeof(int) * ntile * kTile * kMaxNeighbor) != hipSuccess) return MPH_ERR_HIP;
     if (hipMemset(c->ncount, 0, sizeof(int) * cap) != hipSuccess) return MPH_ERR_HIP;
+    if (hipMemset(c->nbcount, 0, sizeof(int) * cap) != hipSuccess) return MPH_ERR_HIP;
 #endif
     CK(dalloc(c, &c->list_hdr, ntile * kLhdr));
 #if defined(MPH_PA_STAGED) && MPH_PA_STAGED
@@ -836,7 +841,7 @@ int mph_get(MphCtx* c, int field, void* out)
     case MPH_FIELD_DENSITY_A: return download_scalar(c, c->dens_a, c->A.id, o);
     case MPH_FIELD_VOL_STRAIN_P: return download_scalar(c, c->vstrain, c->A.id, o);
     case MPH_FIELD_DIVERGENCE_P: return download_scalar(c, c->divp, c->A.id, o);
-    case MPH_FIELD_NEIGHBOR_COUNT: return download_scalar(c, c->ncount, c->A.id, oi);
+    case MPH_FIELD_NEIGHBOR_COUNT: return download_scalar(c, c->nbcount, c->A.id, oi);
     case MPH_FIELD_MASS:
         for (int k = 0; k < nin; ++k) o[glob_id(c, k)] = c->cfg.density[c->prop[k]] * c->h.vol;
         return MPH_OK;
@@ -1147,7 +1152,7 @@ int mph_neighbor_stats(MphCtx* c, double* mean, int* mx)
     HIP_OK(c, hipSetDevice(c->device));
     // NeighborCount of the particles held here (slab mode: owned + ghosts), reduced on the host
     std::vector<int> h(c->n);
-    if (c->n) HIP_OK(c, hipMemcpy(h.data(), c->ncount, sizeof(int) * c->n, hipMemcpyDeviceToHost));
+    if (c->n) HIP_OK(c, hipMemcpy(h.data(), c->nbcount, sizeof(int) * c->n, hipMemcpyDeviceToHost));
     long long sum = 0;
     int m = 0;
     for (int v : h) { sum += v; m = v > m ? v : m; }
@@ -1182,6 +1187,9 @@ int mph_neighbor_rows(MphCtx* c, int first, int count, int* counts, int* ids, lo
     if (!count) return 0;
     HIP_OK(c, hipSetDevice(c->device));
     const int n = c->n, nt = (n + kTile - 1) / kTile;
+    if (c->P.rlf < 3.0e38f)
+        return fail(c, MPH_ERR_UNSUPPORTED, "mph_neighbor_rows: the lists keep only the pairs within the passes' "
+                                            "radius (create the context with MPH_LIST_FULL=1 for the reference's lists)");
     if (c->L.lhdr) {   // the compact 16-bit rows are not decoded here
         std::vector<int> h((size_t)nt * kLhdr);
         HIP_OK(c, hipMemcpy(h.data(), c->list_hdr, sizeof(int) * h.size(), hipMemcpyDeviceToHost));

@@ -1037,7 +1037,7 @@ int pack_owned(MphCtx* c, std::vector<char>& buf)
     std::vector<double> x, y, z, vx, vy, vz;
     std::vector<double4> f, a;
     MPH_CK(fetch(c, (const int*)c->A.id, id, n));
-    MPH_CK(fetch(c, (const int*)c->ncount, nc, n));
+    MPH_CK(fetch(c, (const int*)c->nbcount, nc, n));
     MPH_CK(fetch(c, (const double*)c->B.x, x, n));
     MPH_CK(fetch(c, (const double*)c->B.y, y, n));
     MPH_CK(fetch(c, (const double*)c->B.z, z, n));

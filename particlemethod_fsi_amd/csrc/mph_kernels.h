@@ -96,7 +96,9 @@ struct Launch {
     int* rank_of = nullptr;
     int* dst_of = nullptr;        // slab mode: pre-sort index -> sorted index (else rank_of[id])
     int *key = nullptr, *slot = nullptr, *tmp = nullptr, *cnt = nullptr, *start = nullptr, *bsum = nullptr;
-    int *nbr = nullptr, *ncount = nullptr;
+    // ncount: each list's length (what the passes walk); nbcount: NeighborCount (every neighbour within
+    // the search radius; the lists keep only r^2 <= DevParams.rlf)
+    int *nbr = nullptr, *ncount = nullptr, *nbcount = nullptr;
     int* lhdr = nullptr;          // per-wave headers of the compact 16-bit lists (kLhdr each)
     int* wface = nullptr;         // slab mode: face-wavefront flags written by pass B (early send)
     int2* whdr = nullptr;         // MPH_PA_STAGED builds: per-wave column windows (kWinHdr each)

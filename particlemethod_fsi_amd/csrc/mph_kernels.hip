@@ -425,6 +425,9 @@ __device__ __forceinline__ void add_wave_work(DevState* st, int cnt, int i, int 
 }
 
 __device__ __forceinline__ int nbr_entry(int j, int type) { return j | (type << kTypeShift); }
+// The search's per-lane counter (scan_candidates_lds): the byte offset of the next list slot in the
+// wave's ELL tile (stored entries x 256 + lane x 4, bits 0-16) and every accepted neighbour x 2^17
+constexpr int kListKeep = 256 + (1 << 17), kListTotal = 1 << 17, kSoffMask = 0x1FFFF;
 
 // MPH_PA_STAGED: a wave's column windows {mn, mx} for pass A (kWinCols of them) and its format flag
 // (entry kWinCols: 1 = written by the staged search), kWinHdr int2 per wave (Launch.whdr)
@@ -1354,7 +1357,8 @@ template <int DIM, int PERM, bool C16, int SB = MPH_SB, int CAP = MPH_LDS_CAP>
 __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa& A, const int* start,
                                                    int i, bool act, double xi, double yi, double zi,
                                                    int cx, int cy, int cz, int* out, double* sx,
-                                                   int* lh, unsigned short* o16, DevState* dst, int2* whdr)
+                                                   int* lh, unsigned short* o16, DevState* dst, int2* whdr,
+                                                   int* stored)
 {
     constexpr int SD = stage_d(CAP, SB);
     // FP32 records fill the whole FP64 staging area: 16 bytes each, SB past the window's end
@@ -1499,7 +1503,9 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
         if (kGroups > 5) lh[8 + 64 + lane] = 0x7F7F7F7F;
     }
     // the lane's next list slot: C16 counts entries (cnt); the ELL rows keep the slot's byte offset
-    // in the wave's tile, soff = cnt * 256 + lane * 4 (one add per entry, no address arithmetic)
+    // in the wave's tile, soff = stored * 256 + lane * 4 (one add per entry, no address arithmetic);
+    // bits 17 and up count every accepted neighbour (NeighborCount), bits 8-16 the stored ones (the
+    // FP32 path keeps only r^2 <= P.rlf: kListTotal, kListKeep), so the store offset is soff & kSoffMask
     int soff = lane << 2;
     constexpr int kSelfCol = DIM == 3 ? kReach * kGroups + kReach : kReach;   // the lane's own column
     // one stencil column: its range [jb, je) was loaded one column ahead; (nb_jb, nb_je) receive
@@ -1547,7 +1553,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
         const int span = mx - mn;
         if (MPH_DIAG_SEARCH & 2) {   // never true: empty lists
             __builtin_amdgcn_s_waitcnt(0x0F70);
-            soff += span == 0x7fffffff ? 256 : 0;
+            soff += span == 0x7fffffff ? kListKeep : 0;
             return;
         }
         // A window wider than the staging area is mostly a wave across two cell rows: its lanes' ranges
@@ -1629,8 +1635,13 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                             }
                         }
                         if (a) {
-                            __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, __float_as_int(r[u].w)), tile_rsrc, soff, 0, 0);
-                            soff += 256;
+                            // stored when within the passes' largest radius (FP32, an upper bound:
+                            // the passes' own exact tests decide); counted always
+                            const bool keep = r2f <= P.rlf;
+                            if (keep)
+                                __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, __float_as_int(r[u].w)), tile_rsrc,
+                                                                      soff & kSoffMask, 0, 0);
+                            soff += keep ? kListKeep : kListTotal;
                         }
                     }
                 }
@@ -1657,7 +1668,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the pieces (and column col + 1's start[]) landed
             const int kofs = da, tofs = ta - da;
             __builtin_amdgcn_wave_barrier();
-            if (MPH_DIAG_SEARCH & 1) { soff += sx[lane] == -1.25e300 ? 256 : 0; return; }   // (never true)
+            if (MPH_DIAG_SEARCH & 1) { soff += sx[lane] == -1.25e300 ? kListKeep : 0; return; }   // (never true)
             // this lane's candidates [jb, je) sit at staged position k = j - jd (types at k + tofs);
             // the staging arrays are padded by SB entries, so a batch may read past je (masked).
             // Per candidate: the FP64 distance (6), two compares -- the decision r2 <= rc2 (1 -
@@ -1697,15 +1708,15 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                                 ++cnt;
                             } else if (MPH_DIAG_NOSTORE == 2) {   // diagnostic: same stores, one row
                                 list_store(out, nbr_entry(j, ts[u]));
-                                soff += 256;
+                                soff += kListKeep;
                             } else if (MPH_DIAG_NOSTORE) {
-                                soff += 256;
+                                soff += kListKeep;
                             } else if (!C16) {
-                                // byte offset into the wave's tile (SGPR descriptor); past kMaxNeighbor
-                                // entries the store falls outside the descriptor's range and is
-                                // dropped, and the overflow flag ends the run (MPH_ERR_NEIGHBOR_OVERFLOW)
-                                __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, ts[u]), tile_rsrc, soff, 0, 0);
-                                soff += 256;
+                                // byte offset into the wave's tile (SGPR descriptor); an overflowing
+                                // lane (>= 512 neighbours) ends the run (MPH_ERR_NEIGHBOR_OVERFLOW)
+                                __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, ts[u]), tile_rsrc, soff & kSoffMask,
+                                                                      0, 0);
+                                soff += kListKeep;
                             } else {
                                 __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, ts[u]), tile_rsrc,
                                                                       (min(cnt, kMaxNeighbor - 1) << 8) + (lane << 2),
@@ -1743,9 +1754,9 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                             }
                             ++cnt;
                         } else {
-                            if (!MPH_DIAG_NOSTORE && soff < kMaxNeighbor * 256)
-                                list_store(out + (soff >> 8) * kTile, nbr_entry(j, A.type[j]));
-                            soff += 256;
+                            if (!MPH_DIAG_NOSTORE && (soff >> 17) < kMaxNeighbor)
+                                list_store(out + ((soff & kSoffMask) >> 8) * kTile, nbr_entry(j, A.type[j]));
+                            soff += kListKeep;
                         }
                     }
                 }
@@ -1760,7 +1771,12 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
         column(col, ra_b, ra_e, rb_b, rb_e);
         if (col + 1 < NCOL) column(col + 1, rb_b, rb_e, ra_b, ra_e);
     }
-    if (!C16) cnt = soff >> 8;
+    if (!C16) {
+        cnt = soff >> 17;                 // every neighbour (NeighborCount)
+        *stored = (soff >> 8) & 0x1FF;    // the list's length (r^2 <= P.rlf)
+    } else {
+        *stored = cnt;
+    }
     if (C16 && c16) {
         // the group ends are bytes below 128 (nbr_at): a wave with a lane past 127 neighbours (the
         // reference allows 511) is marked for the ELL search of launch_neighbors' second launch
@@ -1806,10 +1822,12 @@ __device__ __forceinline__ void slab_wave_flag(const DevParams& P, const Soa& A,
     if ((threadIdx.x & 63) == 0) wface[i >> 6] = face ? 1 : 0;
 }
 
+// ncount: the length of each particle's stored list (what the passes walk); nbcount: NeighborCount,
+// every neighbour within the search radius (the two differ where the lists keep only r^2 <= P.rlf)
 template <int DIM, int PERM, bool C16, int REDO>
 __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, const int* start, int* nbr,
-                                               int* ncount, int* lhdr, DevState* st, double* stage, int i,
-                                               int2* whdr_all = nullptr)
+                                               int* ncount, int* nbcount, int* lhdr, DevState* st, double* stage,
+                                               int i, int2* whdr_all = nullptr)
 {
     const int n = dev_n(P);
     const bool live = i < n;
@@ -1823,13 +1841,14 @@ __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, 
     if (C16 && (threadIdx.x & 63) == 0) lhdr[(size_t)tile * kLhdr + kHdrFlag] = 0;
     if (wave_all_ghosts(P, A, live, ii)) {
         if (live) ncount[i] = 0;
+        if (live) nbcount[i] = 0;
         return 0;
     }
     // the ghost lanes of a mixed wave take no part either (empty list)
     const bool own = live && !(P.slab_axis >= 0 && A.id[ii] < 0);
     const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
     const bool fast = wave_search_interior(P, st, own, xi, yi, zi);
-    int cnt = 0;
+    int cnt = 0, stored = 0;
     const int cx = cell_axis(xi, P.corg[0], P.dw[0], P.ginv[0], P.gc[0]);
     const int cy = cell_axis(yi, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
     const int cz = DIM == 3 ? cell_axis(zi, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
@@ -1841,24 +1860,28 @@ __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, 
         if (C16 && !REDO) {
             cnt = scan_candidates_lds<DIM, PERM, true>(P, A, start, i, own, xi, yi, zi, cx, cy, cz, out, stage, lh,
                                                        reinterpret_cast<unsigned short*>(
-                                                           nbr + (size_t)tile * (kTile * kMaxNeighbor)), st, nullptr);
+                                                           nbr + (size_t)tile * (kTile * kMaxNeighbor)), st, nullptr,
+                                                       &stored);
             if ((threadIdx.x & 63) == 0 && lh[kHdrFlag] == 2) atomicAdd(&st->list_redo, 1);
         } else {
             cnt = scan_candidates_lds<DIM, PERM, false>(P, A, start, i, own, xi, yi, zi, cx, cy, cz, out, stage,
-                                                        nullptr, nullptr, st, whdr);
+                                                        nullptr, nullptr, st, whdr, &stored);
         }
-        if (live) ncount[i] = cnt;
+        if (live) ncount[i] = stored;
+        if (live) nbcount[i] = cnt;
     } else {
         if (own && !(MPH_DIAG_SEARCH & 4))
             cnt = fast ? scan_candidates<DIM, true, PERM>(P, A, start, i, xi, yi, zi, cx, cy, cz, out)
                        : scan_candidates<DIM, false, PERM>(P, A, start, i, xi, yi, zi, cx, cy, cz, out);
+        stored = cnt;
         if (live && !(MPH_DIAG_SEARCH & 4)) ncount[i] = cnt;
+        if (live && !(MPH_DIAG_SEARCH & 4)) nbcount[i] = cnt;
     }
     // overflow flag (main.cpp:1766-1768 is the reference's limit).  No per-step statistics here:
     // one same-address device atomic per wave serialises at ~11 ns each (21.8k waves at D1M took
     // 0.5 ms); mph_neighbor_stats reduces ncount on demand.
     if (cnt > kMaxNeighbor) atomicOr(&st->overflow, 1);
-    return cnt;
+    return stored;
 }
 
 // one kernel per cell order (DevParams.perm) and list format, so each keeps its own register
@@ -1870,7 +1893,8 @@ __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, 
 template <int DIM, int PERM, bool C16>
 __global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_WPE))) void k_neighbors(
     DevParams P, Soa A, const int* __restrict__ start, int* __restrict__ nbr, int* __restrict__ ncount,
-    int* __restrict__ lhdr, DevState* __restrict__ st, int* __restrict__ wface, int bal, int2* __restrict__ whdr)
+    int* __restrict__ nbcount, int* __restrict__ lhdr, DevState* __restrict__ st, int* __restrict__ wface, int bal,
+    int2* __restrict__ whdr)
 {
     const int n = dev_n(P);
     if ((int)blockIdx.x >= list_blocks(n)) return;
@@ -1878,7 +1902,7 @@ __global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_W
     __shared__ __attribute__((aligned(16))) double stage[kWB][stage_words(MPH_LDS_CAP, MPH_SB)];
     const int i = xcd_block(blockIdx.x, list_blocks(n)) * blockDim.x + threadIdx.x;
     slab_wave_flag(P, A, i, n, wface);
-    const int cnt = neighbors_body<DIM, PERM, C16, 0>(P, A, start, nbr, ncount, lhdr, st,
+    const int cnt = neighbors_body<DIM, PERM, C16, 0>(P, A, start, nbr, ncount, nbcount, lhdr, st,
                                                       stage[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], i, whdr);
     if (bal) add_wave_work(st, cnt, i, n);
 }
@@ -1937,7 +1961,8 @@ __global__ __launch_bounds__(kXcdSplitThreads) void k_xcd_split(DevState* __rest
 template <int DIM, int PERM>
 __global__ __launch_bounds__(256) void k_neighbors_redo(DevParams P, Soa A, const int* __restrict__ start,
                                                         int* __restrict__ nbr, int* __restrict__ ncount,
-                                                        int* __restrict__ lhdr, DevState* __restrict__ st)
+                                                        int* __restrict__ nbcount, int* __restrict__ lhdr,
+                                                        DevState* __restrict__ st)
 {
     if (st->list_redo == 0) return;
     const int n = dev_n(P);
@@ -1950,7 +1975,8 @@ __global__ __launch_bounds__(256) void k_neighbors_redo(DevParams P, Soa A, cons
         while (m) {
             const int b = __ffsll((long long)m) - 1;
             m &= m - 1;
-            neighbors_body<DIM, PERM, true, 1>(P, A, start, nbr, ncount, lhdr, st, stage[wave], (t0 + b) * kTile + lane);
+            neighbors_body<DIM, PERM, true, 1>(P, A, start, nbr, ncount, nbcount, lhdr, st, stage[wave],
+                                               (t0 + b) * kTile + lane);
         }
     }
     __syncthreads();
@@ -3435,17 +3461,17 @@ void launch_neighbors(const Launch& L)
     do {                                                                                                     \
         if (L.lhdr)                                                                                          \
             MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM, true>), dim3(nb_grid),                     \
-                       dim3(MPH_LB), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.lhdr, L.st, L.wface, bal, \
+                       dim3(MPH_LB), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.nbcount, L.lhdr, L.st, L.wface, bal, \
                        L.whdr);                                                                              \
         else                                                                                                 \
             MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM, false>), dim3(nb_grid),                    \
-                       dim3(MPH_LB), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.lhdr, L.st, L.wface, bal, \
+                       dim3(MPH_LB), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.nbcount, L.lhdr, L.st, L.wface, bal, \
                        L.whdr);                                                                              \
         if (bal)                                                                                             \
             MPH_LAUNCH("xcd_split", L.stream, k_xcd_split, dim3(1), dim3(kXcdSplitThreads), 0, L.stream, L.st); \
         if (L.lhdr)                                                                                          \
             MPH_LAUNCH("neighbors_redo", L.stream, (k_neighbors_redo<D, PERM>), dim3(1),                     \
-                       dim3(256), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.lhdr, L.st);               \
+                       dim3(256), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.nbcount, L.lhdr, L.st);    \
     } while (0)
     if (P.dim == 3) {
         switch (P.perm) {

@@ -142,6 +142,12 @@ struct DevParams {
     double rg_r2g;           // rg / r2g (GravityCenter, DiffuseInterface)
     double cref[3];          // MPH_SEARCH_F32: the domain centre the FP32 records are taken from
     float rc2f_lo, rc2f_hi;  // MPH_SEARCH_F32: below lo the FP32 r^2 accepts, above hi it rejects
+    // The search stores a neighbour in the list only if its FP32 r^2 <= rlf: the largest radius of
+    // the passes' sums (MaxRadius, main.cpp:1199) squared, widened by the FP32 records' error band,
+    // so the list holds every pair any sum can take (the passes' exact tests decide) and not the
+    // shell MaxRadius < r <= MaxRadius + MARGIN that the reference's list carries and NeighborCount
+    // counts.  FLT_MAX (MPH_LIST_FULL=1): the reference's whole list.
+    float rlf;
 };
 
 // Derived uniforms of DevParams (same expressions the kernels used, so the same bits).
@@ -164,6 +170,8 @@ inline void set_uniforms(DevParams& P)
     const double delta = 2.0 * (2.0 * 1.7320508 * hwm * 1.1920929e-7 / rc) + 4.0e-6;
     P.rc2f_lo = (float)(P.rc2 * (1.0 - delta));
     P.rc2f_hi = (float)(P.rc2 * (1.0 + delta));
+    const double rmax = std::fmax(std::fmax(P.ra, P.rg), std::fmax(P.rp, P.rv));
+    P.rlf = (float)(rmax * rmax * (1.0 + delta));
 }
 
 // work histogram of the XCD map: waves in 4096 equal runs (D16M: ~60 waves per run, so the

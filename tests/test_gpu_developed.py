@@ -9,8 +9,8 @@ state (Position, Velocity, Time -- everything the step carries; walls are static
 handed to the CPU oracle, bit-identical to the reference, as the reference's own restart from a
 .prof file would read it (main.cpp:788-955), and both advance 1 and 10 more steps:
 
-  * NeighborCount exact, and the neighbour SETS of sample ranges (mph_neighbor_rows) equal to the
-    oracle's lists (main.cpp:1764-1772);
+  * NeighborCount exact; the neighbour SETS of sample ranges (mph_neighbor_rows of a context built
+    from the state with the reference's whole lists) equal to the oracle's lists (main.cpp:1764-1772);
   * Position 1e-12 m, Velocity 1e-9 m/s, PressureP / VolStrainP / DivergenceP / Force within 1e-8 of
     their largest magnitude plus the roundoff floors of test_gpu_parity.py;
   * the state did leave the lattice: NeighborCount differs from the creation's for >= 1 % of the
@@ -50,8 +50,20 @@ def test_d1m_developed_matches_oracle():
         # restart of the reference from that state (a .prof holds Time, x, x0, v)
         rcfg = cfg.copy()
         rcfg.time = s.time
-        o = OracleSolver(rcfg, mphio.Particles(parts.property, pos, parts.initial_position, vel))
+        state = mphio.Particles(parts.property, pos, parts.initial_position, vel)
+        o = OracleSolver(rcfg, state)
         o.init()
+        # the neighbour SETS of sample ranges at the restart (main.cpp:1764-1772): a context built
+        # from that state with the reference's whole lists (MPH_LIST_FULL=1) against the oracle's
+        os.environ["MPH_LIST_FULL"] = "1"
+        try:
+            with MphSolver(rcfg, state) as full:
+                for first, count in SAMPLE_ROWS:
+                    counts, offsets, ids = full.neighbor_rows(first, count)
+                    for i in range(count):
+                        assert np.array_equal(ids[offsets[i]:offsets[i + 1]], np.sort(o.neighbors(first + i))), first + i
+        finally:
+            del os.environ["MPH_LIST_FULL"]
         done = 0
         for k in (1, 10):
             s.step(k - done)
@@ -64,10 +76,4 @@ def test_d1m_developed_matches_oracle():
                 t = {"Position": 1e-12, "Velocity": 1e-9}.get(f, 1e-8 * scale + FLOOR.get(f, 1e-12))
                 err = float(np.max(np.abs(a - b)))
                 assert err <= t, (k, f, err, t)
-            if k == 1:
-                for first, count in SAMPLE_ROWS:
-                    counts, offsets, ids = s.neighbor_rows(first, count)
-                    for i in range(count):
-                        ref = np.sort(o.neighbors(first + i))
-                        assert np.array_equal(ids[offsets[i]:offsets[i + 1]], ref), (first + i)
         assert s.time == o.time

@@ -125,10 +125,12 @@ def test_gpu_matches_oracle_every_step(case, nsteps):
 
 
 @pytest.mark.parametrize("case", ["dam2d", "box3d_jit"])
-def test_gpu_neighbor_sets_match_reference_golden(case):
+def test_gpu_neighbor_sets_match_reference_golden(case, monkeypatch):
     """The neighbour SETS themselves (mph_neighbor_rows), not only their sizes: after one step every
     particle's row equals the reference's Neighbor[i][0..count) (main.cpp:1764-1772, sorted; the
-    golden rows of make_golden.py) -- on the lattice (dam2d) and off it (box3d_jit)."""
+    golden rows of make_golden.py) -- on the lattice (dam2d) and off it (box3d_jit).  MPH_LIST_FULL=1:
+    the lists keep the reference's whole set (by default only the pairs within the passes' radius)."""
+    monkeypatch.setenv("MPH_LIST_FULL", "1")
     g = Golden(case)
     cfg, parts = cases.get(case).build()
     with MphSolver(cfg, parts) as s:
@@ -143,10 +145,11 @@ def test_gpu_neighbor_sets_match_reference_golden(case):
 
 
 @pytest.mark.parametrize("case,nsteps", [("box3d", 10), ("gate3d_jit", 10), ("seam3d", 10)])
-def test_gpu_neighbor_sets_match_oracle(case, nsteps):
+def test_gpu_neighbor_sets_match_oracle(case, nsteps, monkeypatch):
     """Neighbour sets after several steps against the oracle's lists (bit-identical to the
-    reference's): every row, as sets of original indices."""
+    reference's): every row, as sets of original indices (MPH_LIST_FULL=1: the whole lists)."""
     from oracle_bindings import OracleSolver
+    monkeypatch.setenv("MPH_LIST_FULL", "1")
     cfg, parts = cases.get(case).build()
     o = OracleSolver(cfg, parts)
     o.init()
@@ -157,6 +160,26 @@ def test_gpu_neighbor_sets_match_oracle(case, nsteps):
         assert np.array_equal(counts, o.get("NeighborCount"))
         for i in range(parts.n):
             assert np.array_equal(ids[offsets[i]:offsets[i + 1]], np.sort(o.neighbors(i))), (case, i)
+
+
+@pytest.mark.parametrize("case", ["box3d_jit", "gate3d_jit", "dam2d"])
+def test_gpu_trimmed_lists_equal_full_lists(case, monkeypatch):
+    """The default lists keep only the pairs within the largest radius of the passes' sums
+    (DevParams.rlf); NeighborCount still counts every neighbour within MaxRadius + MARGIN.  Against
+    the reference's whole lists (MPH_LIST_FULL=1): NeighborCount bit-identical, every field within
+    the sums' roundoff (the shell's pairs add exact zeros in the full lists: a term outside its
+    radius is never taken), and the trimmed lists are shorter off the lattice."""
+    cfg, parts = cases.get(case).build()
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MPH_LIST_FULL", mode)
+        with MphSolver(cfg, parts) as s:
+            s.step(7)
+            out[mode] = {f: s.get(f) for f in ["NeighborCount", "Position", "Velocity", "PressureP", "Force",
+                                               "DensityA", "VolStrainP", "DivergenceP"]}
+    assert np.array_equal(out["0"]["NeighborCount"], out["1"]["NeighborCount"])
+    for f in out["0"]:
+        assert np.array_equal(out["0"][f], out["1"][f], equal_nan=True), f
 
 
 def test_gpu_deterministic_rerun():
