@@ -178,6 +178,7 @@ int dist_sync(MphCtx* c, bool grow_ok = true);
 constexpr int kOutProf = 0, kOutVtk = 1, kOutVtu = 2, kOutVtkAsync = 3;
 int dist_write_output(MphCtx* c, const char* path, int kind);
 int dist_virial(MphCtx* c);
+int virial_full_lists(MphCtx* c);   // the step's lists again with every neighbour (mph_ctx.hip)
 void dist_free(MphCtx* c);
 
 }  // namespace mph

@@ -903,6 +903,27 @@ int mph_get(MphCtx* c, int field, void* out)
     }
 }
 
+namespace mph {
+// calculateVirialStressAtParticle evaluates the step's lists at the positions after the step
+// (main.cpp:672-673, 3077-3318): a pair of the shell MaxRadius < r <= MaxRadius + MARGIN at the search
+// may have moved inside a radius by then, so the virial needs the reference's whole lists.  With
+// the lists kept to the passes' radius (DevParams.rlf) the step's search is repeated over the same
+// sorted set A and cell table (unchanged since the step's sort) storing every neighbour -- the
+// lists the step would have built with MPH_LIST_FULL=1; the XCD work histogram is left alone.
+int virial_full_lists(MphCtx* c)
+{
+    if (c->P.rlf >= 3.0e38f) return MPH_OK;
+    DevParams Pf = c->P;
+    Pf.rlf = 3.0e38f;
+    Launch L = c->L;
+    L.P = &Pf;
+    L.xcd_bal_min = 0x7fffffff;
+    launch_neighbors(L);
+    HIP_OK(c, hipGetLastError());
+    return MPH_OK;
+}
+}  // namespace mph
+
 int mph_compute_virial(MphCtx* c)
 {
     if (!c) return MPH_ERR_ARG;
@@ -917,6 +938,7 @@ int mph_compute_virial(MphCtx* c)
     if (c->dist) return dist_virial(c);
     // after a step the integrated state B is in A (list) order; before the first step A is current
     if (c->phase_timing) HIP_OK(c, hipEventRecord(c->ev_vir[0], c->stream));
+    CK(virial_full_lists(c));
     launch_virial(c->L, c->stepped ? c->B : c->A, c->vir, c->vpres);
     HIP_OK(c, hipGetLastError());
     if (c->phase_timing) HIP_OK(c, hipEventRecord(c->ev_vir[1], c->stream));

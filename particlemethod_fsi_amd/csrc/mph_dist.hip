@@ -1194,6 +1194,7 @@ int dist_virial(MphCtx* c)
     MPH_CK(halo_exchange(c, nullptr, c->stream, &F));
     F.f[0] = c->B.vx; F.f[1] = c->B.vy; F.f[2] = c->B.vz;
     MPH_CK(halo_exchange(c, nullptr, c->stream, &F));
+    MPH_CK(virial_full_lists(c));
     launch_virial(c->L, c->B, c->vir, c->vpres);
     MPH_HIP_OK(c, hipGetLastError());
     MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
