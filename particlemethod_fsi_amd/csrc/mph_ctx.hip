@@ -94,6 +94,24 @@ void ctx_fill_launch(MphCtx* c)
     L.S = &c->Sd;
 }
 
+// calculateVirialStressAtParticle evaluates the step's lists at the positions after the step
+// (main.cpp:672-673, 3077-3318): a pair of the shell MaxRadius < r <= MaxRadius + MARGIN at the search
+// may have moved inside a radius by then, so the virial needs the reference's whole lists.  With
+// the lists kept to the passes' radius (DevParams.rlf) the step's search is repeated over the same
+// sorted set A and cell table (unchanged since the step's sort) storing every neighbour -- the
+// lists the step would have built with MPH_LIST_FULL=1; the XCD work histogram is left alone.
+int virial_full_lists(MphCtx* c)
+{
+    if (c->P.rlf >= 3.0e38f) return MPH_OK;
+    DevParams Pf = c->P;
+    Pf.rlf = 3.0e38f;
+    Launch L = c->L;
+    L.P = &Pf;
+    L.xcd_bal_min = 0x7fffffff;
+    launch_neighbors(L);
+    MPH_HIP_OK(c, hipGetLastError());
+    return MPH_OK;
+}
 }  // namespace mph
 
 namespace {
@@ -902,27 +920,6 @@ int mph_get(MphCtx* c, int field, void* out)
     default: return fail(c, MPH_ERR_ARG, "unknown field " + std::to_string(field));
     }
 }
-
-namespace mph {
-// calculateVirialStressAtParticle evaluates the step's lists at the positions after the step
-// (main.cpp:672-673, 3077-3318): a pair of the shell MaxRadius < r <= MaxRadius + MARGIN at the search
-// may have moved inside a radius by then, so the virial needs the reference's whole lists.  With
-// the lists kept to the passes' radius (DevParams.rlf) the step's search is repeated over the same
-// sorted set A and cell table (unchanged since the step's sort) storing every neighbour -- the
-// lists the step would have built with MPH_LIST_FULL=1; the XCD work histogram is left alone.
-int virial_full_lists(MphCtx* c)
-{
-    if (c->P.rlf >= 3.0e38f) return MPH_OK;
-    DevParams Pf = c->P;
-    Pf.rlf = 3.0e38f;
-    Launch L = c->L;
-    L.P = &Pf;
-    L.xcd_bal_min = 0x7fffffff;
-    launch_neighbors(L);
-    HIP_OK(c, hipGetLastError());
-    return MPH_OK;
-}
-}  // namespace mph
 
 int mph_compute_virial(MphCtx* c)
 {
