@@ -293,7 +293,7 @@ struct EventProfiler final : Profiler {
     std::vector<Rec> recs;
     std::vector<hipEvent_t> floors;
     std::map<hipStream_t, int> pending;
-    int begin(const char* name, hipStream_t s) override
+    void events(const char* name, hipStream_t s, hipEvent_t* start, hipEvent_t* stop) override
     {
         Rec r{name, nullptr, nullptr, -1};
         const auto it = pending.find(s);
@@ -303,11 +303,10 @@ struct EventProfiler final : Profiler {
         }
         (void)hipEventCreate(&r.a);
         (void)hipEventCreate(&r.b);
-        (void)hipEventRecord(r.a, s);
         recs.push_back(r);
-        return (int)recs.size() - 1;
+        *start = r.a;
+        *stop = r.b;
     }
-    void end(int slot, hipStream_t s) override { (void)hipEventRecord(recs[slot].b, s); }
     void join(hipStream_t waiting, hipStream_t from) override
     {
         hipEvent_t e = nullptr;

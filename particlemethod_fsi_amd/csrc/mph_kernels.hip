@@ -30,6 +30,7 @@
 // neighbour loops are bound by the per-CU texture-address path (profiles/r01: TA ~75% busy with
 // 32-byte records); SoA makes consecutive lanes gather consecutive doubles.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <climits>
 #include <cstddef>
@@ -3387,24 +3388,19 @@ static inline int list_grid(int n)
     return MPH_XCD_BAL ? (nb + nb / 4 + 15) / 8 * 8 : nb;
 }
 
-struct ProfScope {
-    Profiler* p;
-    int slot;
-    hipStream_t s;
-    ProfScope(Profiler* prof, const char* name, hipStream_t st) : p(prof), slot(-1), s(st)
-    {
-        if (p) slot = p->begin(name, st);
-    }
-    ~ProfScope()
-    {
-        if (p) p->end(slot, s);
-    }
-};
-
-#define MPH_LAUNCH(name, stream, ...)                                               \
-    do {                                                                            \
-        ProfScope _ps(prof, name, stream);                                          \
-        hipLaunchKernelGGL(__VA_ARGS__);                                            \
+// A profiled launch (mph_profile_steps) takes its start/stop times from the kernel's dispatch
+// packet (hipExtLaunchKernelGGL): events recorded around a launch add a barrier packet with an L2
+// write-back between consecutive kernels, which cost ~10 us gaps and made the list kernels ~10 %
+// slower than in the graphs the timed steps replay (profiles/r05/final/prof: rocprofv3 trace).
+#define MPH_LAUNCH(name, stream, kernel, grid, block, shm, strm, ...)                          \
+    do {                                                                                       \
+        if (prof) {                                                                            \
+            hipEvent_t _a, _b;                                                                 \
+            prof->events(name, stream, &_a, &_b);                                              \
+            hipExtLaunchKernelGGL(kernel, grid, block, shm, strm, _a, _b, 0u, __VA_ARGS__);    \
+        } else {                                                                               \
+            hipLaunchKernelGGL(kernel, grid, block, shm, strm, __VA_ARGS__);                   \
+        }                                                                                      \
     } while (0)
 
 void launch_sort(const Launch& L, int mode)
