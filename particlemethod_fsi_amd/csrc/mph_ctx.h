@@ -103,6 +103,9 @@ struct MphCtx {
     // three per step of a batch of up to 8 (ev8), and around the virial (ev_vir)
     bool phase_timing = false;
     std::vector<hipEvent_t> ev8, ev_vir;
+    // chunked search + pass A (Launch.chunks): the second stream and its events
+    hipStream_t stream2 = nullptr;
+    std::vector<hipEvent_t> ev_chunk;
     double phase_ms[3] = {0.0, 0.0, 0.0};   // neighbour search, explicit calculation, virial
     // host copies of the static inputs: original order, or -- slab-local creation -- the
     // particles this rank was created with, whose original indices are gid (ascending)

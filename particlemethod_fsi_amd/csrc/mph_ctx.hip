@@ -92,6 +92,24 @@ void ctx_fill_launch(MphCtx* c)
     L.force = c->force; L.acc = c->acc; L.fpart = c->fpart; L.rec = c->rec;
     L.dens_a = c->dens_a; L.vstrain = c->vstrain; L.divp = c->divp;
     L.S = &c->Sd;
+    // MPH_CHUNKS=C (2..16): the search and pass A in C pieces on two streams (launch_search_pass_a);
+    // a single context only (slab ranks overlap their own way)
+    const char* ch = std::getenv("MPH_CHUNKS");
+    const int chunks = ch && *ch ? std::atoi(ch) : kSearchChunks;
+    L.chunks = 1;
+    if (!c->dist && chunks > 1 && chunks <= 16) {
+        bool ok = c->stream2 || hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) == hipSuccess;
+        while (ok && (int)c->ev_chunk.size() < chunks + 1) {
+            hipEvent_t e = nullptr;
+            ok = hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+            if (ok) c->ev_chunk.push_back(e);
+        }
+        if (ok) {
+            L.chunks = chunks;
+            L.stream2 = c->stream2;
+            L.ev_chunk = c->ev_chunk.data();
+        }
+    }
 }
 
 // calculateVirialStressAtParticle evaluates the step's lists at the positions after the step
@@ -146,9 +164,13 @@ void enqueue_step(const Launch& L, bool last, hipEvent_t* ev = nullptr)
         La.dens_a = La.vstrain = La.divp = nullptr;
         if (!L.P->surface) La.gx = La.gy = La.gz = La.pa = nullptr;
     }
-    launch_neighbors(La);
-    if (ev) (void)hipEventRecord(ev[1], L.stream);
-    launch_pass_a(La);
+    if (ev) {   // phase timing: the boundary between the search and pass A
+        launch_neighbors(La);
+        (void)hipEventRecord(ev[1], L.stream);
+        launch_pass_a(La);
+    } else {
+        launch_search_pass_a(La);
+    }
     if (last) {
         launch_pass_b(L);
     } else {
@@ -1312,8 +1334,9 @@ void mph_destroy(MphCtx* c)
     if (c->graph1) (void)hipGraphExecDestroy(c->graph1);
     if (c->graph1t) (void)hipGraphExecDestroy(c->graph1t);
     if (c->graph8) (void)hipGraphExecDestroy(c->graph8);
-    for (auto* v : {&c->ev8, &c->ev_vir})
+    for (auto* v : {&c->ev8, &c->ev_vir, &c->ev_chunk})
         for (hipEvent_t e : *v) (void)hipEventDestroy(e);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->dist) dist_free(c);
     for (void* p : c->allocs) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);

@@ -92,6 +92,10 @@ struct Launch {
     DevState* st = nullptr;
     hipStream_t stream = nullptr;
     Profiler* prof = nullptr;
+    // chunked search + pass A (launch_search_pass_a): pieces, the second stream, chunks + 1 events
+    int chunks = 1;
+    hipStream_t stream2 = nullptr;
+    hipEvent_t* ev_chunk = nullptr;
     // B set: integrated state in the previous order; A set: cell-sorted current order
     Soa A, B;
     int* rank_of = nullptr;
@@ -117,8 +121,8 @@ struct Launch {
 };
 
 void launch_sort(const Launch& L, int mode);   // mode 0 init, 1 step, 2 step (motion done)
-void launch_neighbors(const Launch& L);
-void launch_pass_a(const Launch& L);
+void launch_neighbors(const Launch& L, int ck = 0);
+void launch_pass_a(const Launch& L, int ck = 0);
 // launch_neighbors + launch_pass_a
 void launch_search_pass_a(const Launch& L);
 void launch_pass_b(const Launch& L, int phase = 0);   // phase: 0 all, 1/2 slab inner/near-face

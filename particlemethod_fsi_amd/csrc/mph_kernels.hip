@@ -412,6 +412,22 @@ __device__ __forceinline__ int list_block(const DevState* st, int n)
     return b < nb ? xcd_block(b, nb) : -1;
 }
 
+// Chunked search + pass A (Launch.chunks > 1, launch_search_pass_a): launch c of C takes piece c
+// of every XCD's contiguous range of the equal map (xcd_block), so pass A of piece c, on a second
+// stream, runs beside the search of piece c + 1 and the XCDs keep their own ranges.
+// ck = c << 8 | C; returns the block's tile of MPH_LB particles or -1.
+__device__ __forceinline__ int chunk_block(int b, int nb, int ck)
+{
+    const int C = ck & 0xff, c = ck >> 8;
+    const int xcd = b & 7;
+    const int q = nb >> 3, r = nb & 7;
+    const int len = xcd < r ? q + 1 : q;
+    const int lo = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    const int p0 = (int)(((long long)len * c) / C), p1 = (int)(((long long)len * (c + 1)) / C);
+    const int k = b >> 3;
+    return k < p1 - p0 ? lo + p0 + k : -1;
+}
+
 // The search's contribution to the work histogram: its wave's longest list (all lanes converged;
 // one atomic per wave, spread over the 4096 runs).
 __device__ __forceinline__ void add_wave_work(DevState* st, int cnt, int i, int n)
@@ -1895,13 +1911,15 @@ template <int DIM, int PERM, bool C16>
 __global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_WPE))) void k_neighbors(
     DevParams P, Soa A, const int* __restrict__ start, int* __restrict__ nbr, int* __restrict__ ncount,
     int* __restrict__ nbcount, int* __restrict__ lhdr, DevState* __restrict__ st, int* __restrict__ wface, int bal,
-    int2* __restrict__ whdr)
+    int2* __restrict__ whdr, int ck)
 {
     const int n = dev_n(P);
-    if ((int)blockIdx.x >= list_blocks(n)) return;
+    const int tb = ck ? chunk_block(blockIdx.x, list_blocks(n), ck)
+                      : ((int)blockIdx.x < list_blocks(n) ? xcd_block(blockIdx.x, list_blocks(n)) : -1);
+    if (tb < 0) return;
     XCD_PROBE(st, 0);
     __shared__ __attribute__((aligned(16))) double stage[kWB][stage_words(MPH_LDS_CAP, MPH_SB)];
-    const int i = xcd_block(blockIdx.x, list_blocks(n)) * blockDim.x + threadIdx.x;
+    const int i = tb * blockDim.x + threadIdx.x;
     slab_wave_flag(P, A, i, n, wface);
     const int cnt = neighbors_body<DIM, PERM, C16, 0>(P, A, start, nbr, ncount, nbcount, lhdr, st,
                                                       stage[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], i, whdr);
@@ -2163,10 +2181,11 @@ __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, cons
                                                 const int* __restrict__ nbr,
                                                 const int* __restrict__ ncount,
                                                 const int* __restrict__ lhdr, PassAOut pout,
-                                                const DevState* __restrict__ st, const int2* __restrict__ whdr)
+                                                const DevState* __restrict__ st, const int2* __restrict__ whdr,
+                                                int ck)
 {
     const int n = dev_n(P);
-    const int lb = list_block(st, n);
+    const int lb = ck ? chunk_block(blockIdx.x, list_blocks(n), ck) : list_block(st, n);
     if (lb < 0) return;
     XCD_PROBE(st, 1);
     __shared__ double s_ratio[kTypes * kTypes];
@@ -3444,7 +3463,15 @@ static PassAOut pass_a_out(const Launch& L)
     return PassAOut{L.pres, L.gx, L.gy, L.gz, L.pa, L.dens_a, L.vstrain, L.divp, L.fpart, L.rec};
 }
 
-void launch_neighbors(const Launch& L)
+static inline int chunk_grid(int n, int C)
+{
+    const int q = (blocks(n, MPH_LB) + 7) / 8;
+    return 8 * ((q + C - 1) / C + 1);
+}
+
+// ck: 0 the whole search (then the XCD split and the compact lists' REDO launch), else one piece
+// of a chunked search (launch_search_pass_a launches the split after the last piece)
+void launch_neighbors(const Launch& L, int ck)
 {
     Profiler* prof = L.prof;
     const DevParams& P = *L.P;
@@ -3452,18 +3479,18 @@ void launch_neighbors(const Launch& L)
     // the second launch (REDO) only when compact lists are on; its waves exit at once unless the
     // first marked them
     const int bal = MPH_XCD_BAL && P.n >= L.xcd_bal_min;
-    const int nb_grid = blocks(P.n, MPH_LB);
+    const int nb_grid = ck ? chunk_grid(P.n, ck & 0xff) : blocks(P.n, MPH_LB);
 #define MPH_NEIGHBORS(D, PERM)                                                                               \
     do {                                                                                                     \
         if (L.lhdr)                                                                                          \
             MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM, true>), dim3(nb_grid),                     \
                        dim3(MPH_LB), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.nbcount, L.lhdr, L.st, L.wface, bal, \
-                       L.whdr);                                                                              \
+                       L.whdr, ck);                                                                          \
         else                                                                                                 \
             MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM, false>), dim3(nb_grid),                    \
                        dim3(MPH_LB), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.nbcount, L.lhdr, L.st, L.wface, bal, \
-                       L.whdr);                                                                              \
-        if (bal)                                                                                             \
+                       L.whdr, ck);                                                                          \
+        if (bal && !ck)                                                                                      \
             MPH_LAUNCH("xcd_split", L.stream, k_xcd_split, dim3(1), dim3(kXcdSplitThreads), 0, L.stream, L.st); \
         if (L.lhdr)                                                                                          \
             MPH_LAUNCH("neighbors_redo", L.stream, (k_neighbors_redo<D, PERM>), dim3(1),                     \
@@ -3483,7 +3510,7 @@ void launch_neighbors(const Launch& L)
 #undef MPH_NEIGHBORS
 }
 
-void launch_pass_a(const Launch& L)
+void launch_pass_a(const Launch& L, int ck)
 {
     Profiler* prof = L.prof;
     const DevParams& P = *L.P;
@@ -3498,19 +3525,42 @@ void launch_pass_a(const Launch& L)
             MPH_LAUNCH("pass_a_st", L.stream, k_pass_a_st<2>, dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P,
                        L.T, L.A, L.nbr, L.ncount, po, L.st, wh);
     }
+    const int grid = ck ? chunk_grid(P.n, ck & 0xff) : list_grid(P.n);
     if (P.dim == 3)
-        MPH_LAUNCH("pass_a", L.stream, k_pass_a<3>, dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, L.lhdr, po, L.st, wh);
+        MPH_LAUNCH("pass_a", L.stream, k_pass_a<3>, dim3(grid), dim3(MPH_LB), 0, L.stream, P, L.T,
+                   L.A, L.nbr, L.ncount, L.lhdr, po, L.st, wh, ck);
     else
-        MPH_LAUNCH("pass_a", L.stream, k_pass_a<2>, dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, L.lhdr, po, L.st, wh);
+        MPH_LAUNCH("pass_a", L.stream, k_pass_a<2>, dim3(grid), dim3(MPH_LB), 0, L.stream, P, L.T,
+                   L.A, L.nbr, L.ncount, L.lhdr, po, L.st, wh, ck);
 }
 
-// calculateNeighbor + the pass-A sums (the search, the XCD split of the passes, pass A)
+// calculateNeighbor + the pass-A sums (the search, the XCD split of the passes, pass A).  With
+// Launch.chunks = C > 1 (single context, full lists in ELL, no staged pass A) the search runs in C
+// pieces on L.stream and pass A of each piece on L.stream2 as soon as its piece is listed: pass A
+// (bound by L1 tag lookups) then shares the CUs with the next piece's search (bound by VALU issue
+// and address processing).  Pass A of a piece reads the lists of its own particles only.
 void launch_search_pass_a(const Launch& L)
 {
-    launch_neighbors(L);
-    launch_pass_a(L);
+    const int C = L.chunks;
+    if (C <= 1 || !L.stream2 || !L.ev_chunk || L.lhdr || MPH_PA_STAGED || L.P->slab_axis >= 0 || L.P->n == 0) {
+        launch_neighbors(L);
+        launch_pass_a(L);
+        return;
+    }
+    Profiler* prof = L.prof;
+    Launch La = L;
+    La.stream = L.stream2;
+    for (int c = 0; c < C; ++c) {
+        const int ck = c << 8 | C;
+        launch_neighbors(L, ck);
+        (void)hipEventRecord(L.ev_chunk[c], L.stream);
+        (void)hipStreamWaitEvent(L.stream2, L.ev_chunk[c], 0);
+        launch_pass_a(La, ck);
+    }
+    if (MPH_XCD_BAL && L.P->n >= L.xcd_bal_min)
+        MPH_LAUNCH("xcd_split", L.stream, k_xcd_split, dim3(1), dim3(kXcdSplitThreads), 0, L.stream, L.st);
+    (void)hipEventRecord(L.ev_chunk[C], L.stream2);
+    (void)hipStreamWaitEvent(L.stream, L.ev_chunk[C], 0);
 }
 
 static StructHook struct_hook(const Launch& L)

@@ -51,6 +51,12 @@ constexpr int kHdrFlag = 7;
 #endif
 constexpr bool kListCompact = MPH_LIST_COMPACT;
 constexpr int kLhdr = 8 + 2 * 64;
+// pieces of the chunked search + pass A (launch_search_pass_a; MPH_CHUNKS overrides at creation);
+// 1 = one search launch, then one pass-A launch
+#ifndef MPH_SEARCH_CHUNKS
+#define MPH_SEARCH_CHUNKS 1
+#endif
+constexpr int kSearchChunks = MPH_SEARCH_CHUNKS;
 // per-wave column windows of the staged pass A (MPH_PA_STAGED, mph_kernels.hip): int2 entries
 constexpr int kWinHdr = (2 * 3 + 1) * (2 * 3 + 1) + 1;
 static_assert(kGroups <= kHdrFlag, "group bases overlap the format flag");
