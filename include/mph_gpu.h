@@ -286,6 +286,13 @@ int mph_compute_virial(MphCtx* ctx);
  * their sum where kernels of two streams overlap (slab mode).                                  */
 #define MPH_PROFILE_MAX 24
 int mph_profile_steps(MphCtx* ctx, int nsteps, double* avg_ms, int* launches, char* names32);
+/* The list kernels as the timed steps run them (direct launches of mph_profile_steps take 3-8 %
+ * longer): the search (with the XCD split), pass A and pass B, each captured `reps` (1..64) times
+ * into a graph of its own and replayed between two HIP events on the context's stream; avg_ms3 =
+ * milliseconds per launch (-1: not measured -- pass B with elastic slots).  Each replay recomputes
+ * the last step's results bit for bit, so the state is unchanged.  Single contexts after at
+ * least one step (else MPH_ERR_UNSUPPORTED / MPH_ERR_ARG).                                      */
+int mph_profile_graphs(MphCtx* ctx, int reps, double* avg_ms3);
 /* Phase timing: the reference's clock() buckets of its step loop (main.cpp:695-700) from HIP
  * events.  With on != 0 mph_step launches the kernels of its step batches directly instead of
  * replaying the captured graphs (HIP does not time events recorded inside a graph), with three

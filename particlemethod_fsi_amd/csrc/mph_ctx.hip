@@ -315,7 +315,7 @@ struct EventProfiler final : Profiler {
     std::vector<Rec> recs;
     std::vector<hipEvent_t> floors;
     std::map<hipStream_t, int> pending;
-    void events(const char* name, hipStream_t s, hipEvent_t* start, hipEvent_t* stop) override
+    bool events(const char* name, hipStream_t s, hipEvent_t* start, hipEvent_t* stop) override
     {
         Rec r{name, nullptr, nullptr, -1};
         const auto it = pending.find(s);
@@ -328,6 +328,7 @@ struct EventProfiler final : Profiler {
         recs.push_back(r);
         *start = r.a;
         *stop = r.b;
+        return true;
     }
     void join(hipStream_t waiting, hipStream_t from) override
     {
@@ -1183,6 +1184,63 @@ int mph_profile_steps(MphCtx* c, int nsteps, double* avg_ms, int* launches, char
     HIP_OK(c, hipMemcpy(&hs, c->dst, kStateHead, hipMemcpyDeviceToHost));
     CK(ctx_state_status(c, hs));
     return k;
+}
+
+// The list kernels as the timed steps run them: each one captured `reps` times into a graph of
+// its own (the output-only stores on every 8th, as in the 8-step graph), replayed once to warm,
+// then once between two HIP events.  Each replay recomputes what the last step left (the lists,
+// pass A's products, B from A), bit for bit, so the state does not change; pass B is skipped with
+// elastic slots (the substeps after it have moved them in B).  Needs one step done.
+int mph_profile_graphs(MphCtx* c, int reps, double* avg_ms3)
+{
+    if (!c || reps <= 0 || reps > 64 || !avg_ms3) return MPH_ERR_ARG;
+    if (c->dist) return ctx_fail(c, MPH_ERR_UNSUPPORTED, "mph_profile_graphs: single contexts only");
+    CK(ctx_flush(c));
+    if (!c->stepped) return ctx_fail(c, MPH_ERR_ARG, "mph_profile_graphs: run a step first");
+    HIP_OK(c, hipSetDevice(c->device));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIP_OK(c, hipEventCreate(&e0));
+    HIP_OK(c, hipEventCreate(&e1));
+    int rc = MPH_OK;
+    for (int k = 0; k < 3 && rc == MPH_OK; ++k) {
+        avg_ms3[k] = -1.0;
+        if (k == 2 && c->P.n_struct > 0) continue;
+        hipGraph_t g = nullptr;
+        hipGraphExec_t ge = nullptr;
+        bool ok = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
+        if (ok) {
+            for (int r = 0; r < reps; ++r) {
+                const bool last = r % 8 == 7 || r == reps - 1;
+                Launch La = c->L;
+                if (!last) {
+                    La.dens_a = La.vstrain = La.divp = nullptr;
+                    if (!c->P.surface) La.gx = La.gy = La.gz = La.pa = nullptr;
+                    La.force = La.acc = nullptr;
+                }
+                if (k == 0) launch_neighbors(La);
+                else if (k == 1) launch_pass_a(La);
+                else launch_pass_b(La);
+            }
+            ok = hipStreamEndCapture(c->stream, &g) == hipSuccess && g;
+        }
+        ok = ok && hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) == hipSuccess;
+        if (g) (void)hipGraphDestroy(g);
+        float ms = 0.0f;
+        ok = ok && hipGraphUpload(ge, c->stream) == hipSuccess && hipGraphLaunch(ge, c->stream) == hipSuccess &&
+             hipEventRecord(e0, c->stream) == hipSuccess && hipGraphLaunch(ge, c->stream) == hipSuccess &&
+             hipEventRecord(e1, c->stream) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
+             hipEventElapsedTime(&ms, e0, e1) == hipSuccess;
+        if (ge) (void)hipGraphExecDestroy(ge);
+        if (ok) avg_ms3[k] = ms / reps;
+        else rc = ctx_fail(c, MPH_ERR_HIP, "mph_profile_graphs: graph capture or replay failed");
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    CK(rc);
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    DevState hs;
+    HIP_OK(c, hipMemcpy(&hs, c->dst, kStateHead, hipMemcpyDeviceToHost));
+    return ctx_state_status(c, hs);
 }
 
 int mph_neighbor_stats(MphCtx* c, double* mean, int* mx)

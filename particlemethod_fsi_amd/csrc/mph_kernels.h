@@ -39,10 +39,10 @@ struct StructDev {
 };
 
 // Per-kernel HIP event timing (mph_profile_steps); nullptr in normal runs.  `events` hands out a
-// start/stop pair for one launch, which hipExtLaunchKernelGGL sets from the dispatch packet's own
-// timestamps (no event packets between the kernels, so no cache write-back between them either).
+// start/stop pair for one launch and says how to set them: true, from the dispatch packet's own
+// timestamps (hipExtLaunchKernelGGL); false, recorded on the stream around the launch.
 struct Profiler {
-    virtual void events(const char* name, hipStream_t s, hipEvent_t* start, hipEvent_t* stop) = 0;
+    virtual bool events(const char* name, hipStream_t s, hipEvent_t* start, hipEvent_t* stop) = 0;
     // `waiting` is about to wait for an event `from` has just recorded: the next launch on
     // `waiting` starts no earlier than `from` reaches this point (mph_profile_steps)
     virtual void join(hipStream_t waiting, hipStream_t from) { (void)waiting; (void)from; }

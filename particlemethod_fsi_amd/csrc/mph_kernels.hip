@@ -1655,9 +1655,12 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                             // stored when within the passes' largest radius (FP32, an upper bound:
                             // the passes' own exact tests decide); counted always
                             const bool keep = r2f <= P.rlf;
-                            if (keep)
+                            // diagnostic builds: MPH_DIAG_NOSTORE 1 no store, 2 the same stores to
+                            // the lane's row 0 (the instructions without the list traffic)
+                            if (keep && MPH_DIAG_NOSTORE != 1)
                                 __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, __float_as_int(r[u].w)), tile_rsrc,
-                                                                      soff & kSoffMask, 0, 0);
+                                                                      MPH_DIAG_NOSTORE == 2 ? (soff & 0xFF) : (soff & kSoffMask),
+                                                                      0, 0);
                             soff += keep ? kListKeep : kListTotal;
                         }
                     }
@@ -3407,16 +3410,22 @@ static inline int list_grid(int n)
     return MPH_XCD_BAL ? (nb + nb / 4 + 15) / 8 * 8 : nb;
 }
 
-// A profiled launch (mph_profile_steps) takes its start/stop times from the kernel's dispatch
-// packet (hipExtLaunchKernelGGL): events recorded around a launch add a barrier packet with an L2
-// write-back between consecutive kernels, which cost ~10 us gaps and made the list kernels ~10 %
-// slower than in the graphs the timed steps replay (profiles/r05/final/prof: rocprofv3 trace).
+// A profiled launch (mph_profile_steps): its start/stop events come from the kernel's dispatch
+// packet (hipExtLaunchKernelGGL), or are recorded around it (Profiler::events).  Direct launches
+// run ~9 us apart and start with a written-back L2, so they take 3-8 % longer than the same
+// kernels replayed from a graph (profiles/r05/final/prof: rocprofv3 trace); mph_profile_graphs
+// times the list kernels as graph replays.
 #define MPH_LAUNCH(name, stream, kernel, grid, block, shm, strm, ...)                          \
     do {                                                                                       \
         if (prof) {                                                                            \
             hipEvent_t _a, _b;                                                                 \
-            prof->events(name, stream, &_a, &_b);                                              \
-            hipExtLaunchKernelGGL(kernel, grid, block, shm, strm, _a, _b, 0u, __VA_ARGS__);    \
+            if (prof->events(name, stream, &_a, &_b)) {                                        \
+                hipExtLaunchKernelGGL(kernel, grid, block, shm, strm, _a, _b, 0u, __VA_ARGS__); \
+            } else {                                                                           \
+                (void)hipEventRecord(_a, strm);                                                \
+                hipLaunchKernelGGL(kernel, grid, block, shm, strm, __VA_ARGS__);               \
+                (void)hipEventRecord(_b, strm);                                                \
+            }                                                                                  \
         } else {                                                                               \
             hipLaunchKernelGGL(kernel, grid, block, shm, strm, __VA_ARGS__);                   \
         }                                                                                      \

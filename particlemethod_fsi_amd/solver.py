@@ -49,7 +49,7 @@ EXPORTED_SYMBOLS = [
     "mph_config_default", "mph_read_data_file", "mph_read_grid_header", "mph_read_grid_particles",
     "mph_write_prof_arrays", "mph_write_vtk_arrays", "mph_create", "mph_step", "mph_synchronize",
     "mph_get", "mph_set", "mph_particle_count", "mph_time", "mph_get_scalars", "mph_write_prof",
-    "mph_write_vtk", "mph_last_error", "mph_destroy", "mph_profile_steps", "mph_neighbor_stats",
+    "mph_write_vtk", "mph_last_error", "mph_destroy", "mph_profile_steps", "mph_profile_graphs", "mph_neighbor_stats",
     "mph_dist_unique_id", "mph_create_dist", "mph_owned_count", "mph_derive_scalars",
     "mph_structure_init", "mph_create_dist_host", "mph_owned_ids", "mph_slab_bounds",
     "mph_slab_owner", "mph_dist_selftest", "mph_compute_virial",
@@ -125,6 +125,7 @@ def load_library() -> ctypes.CDLL:
         "mph_last_error": (ctypes.c_char_p, [vp]),
         "mph_destroy": (None, [vp]),
         "mph_profile_steps": (ip, [vp, ip, vp, vp, vp]),
+        "mph_profile_graphs": (ip, [vp, ip, vp]),
         "mph_neighbor_stats": (ip, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
         "mph_dist_unique_id": (ip, [vp]),
         "mph_create_dist": (ip, [ctypes.POINTER(vp), cfgp, ip, vp, vp, vp, vp, ip, ip, ip, vp, ip]),
@@ -425,6 +426,13 @@ class MphSolver:
             nm = raw[32 * i:32 * (i + 1)].split(b"\0", 1)[0].decode()
             out[nm] = {"avg_ms": float(avg[i]), "launches": int(cnt[i])}
         return out
+
+    def profile_graphs(self, reps: int = 16) -> dict:
+        """The list kernels timed as graph replays (mph_profile_graphs): ms per launch of the search
+        (with the XCD split), pass A and pass B; None where not measured."""
+        out = np.zeros(3)
+        _check(self._L.mph_profile_graphs(self._h, int(reps), out.ctypes.data), self._h)
+        return {k: (float(v) if v >= 0 else None) for k, v in zip(("neighbors", "pass_a", "pass_b"), out)}
 
     def step_batching(self, on: bool = True):
         """mph_set_step_batching: step(1) per time-loop iteration costs what step(8) does; pending

@@ -201,6 +201,25 @@ def test_gpu_chunked_search_equals_single(case, chunks, monkeypatch):
         assert np.array_equal(out["1"][f], out[chunks][f], equal_nan=True), f
 
 
+@pytest.mark.parametrize("case", ["box3d_jit", "gate3d_jit"])
+def test_gpu_profile_graphs_leave_state_unchanged(case):
+    """mph_profile_graphs replays the search, pass A and pass B over the last step's state: positive
+    times (pass B not measured with elastic slots), and the run continues bit for bit as without."""
+    cfg, parts = cases.get(case).build()
+    out = []
+    for profiled in (False, True):
+        with MphSolver(cfg, parts) as s:
+            s.step(3)
+            if profiled:
+                t = s.profile_graphs(4)
+                assert t["neighbors"] > 0 and t["pass_a"] > 0
+                assert (t["pass_b"] is None) == (case == "gate3d_jit")
+            s.step(5)
+            out.append({f: s.get(f) for f in ["NeighborCount", "Position", "Velocity", "PressureP", "Force"]})
+    for f in out[0]:
+        assert np.array_equal(out[0][f], out[1][f], equal_nan=True), f
+
+
 def test_gpu_deterministic_rerun():
     cfg, parts = cases.get("gate2d").build()
     outs = []
