@@ -1319,7 +1319,7 @@ int mph_neighbor_rows(MphCtx* c, int first, int count, int* counts, int* ids, lo
         int m = 0;
         for (int s = t * kTile; s < std::min(n, (t + 1) * kTile); ++s) m = std::max(m, std::min(nc[s], kMaxNeighbor));
         std::vector<int>& buf = tiles[t];
-        buf.resize((size_t)m * kTile);
+        buf.resize((size_t)((m + 1) & ~1) * kTile);   // whole pairs (ell_slot)
         if (m) HIP_OK(c, hipMemcpy(buf.data(), c->nbr + (size_t)t * kTile * kMaxNeighbor, sizeof(int) * buf.size(),
                                    hipMemcpyDeviceToHost));
     }
@@ -1328,7 +1328,7 @@ int mph_neighbor_rows(MphCtx* c, int first, int count, int* counts, int* ids, lo
         const int s = row_of[k], m = std::min(counts[k], kMaxNeighbor);
         const std::vector<int>& buf = tiles[s >> 6];
         for (int e = 0; e < m; ++e) {
-            const int j = buf[(size_t)e * kTile + (s & 63)] & kIndexMask;
+            const int j = buf[(size_t)ell_slot(e, s & 63)] & kIndexMask;
             if (j >= n) return fail(c, MPH_ERR_HIP, "mph_neighbor_rows: list entry past the particle count");
             ids[w + e] = id[j];
         }

@@ -510,6 +510,19 @@ __device__ __forceinline__ const int* ell_row(const int* nbr, int i)
     return nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
 }
 
+// entry k of a lane from the lane's ell_row pointer (ell_slot: rows or pairs)
+template <typename T>
+__device__ __forceinline__ T* ell_at(T* row, int lane, int k)
+{
+    return row - lane + ell_slot(k, lane);
+}
+
+// the byte offset of a store slot in the wave's tile from the search's soff = k << 8 | lane << 2
+__device__ __forceinline__ unsigned ell_byte(unsigned soff)
+{
+    return kListPairs ? ((soff & 0x1FE00u) | ((soff & 0xFCu) << 1) | ((soff & 0x100u) >> 6)) : soff;
+}
+
 // Compact neighbour list (MPH_LIST16, the default for interior waves).  The stencil's columns
 // fall into kGroups groups (3-D: the 2 kReach + 1 columns of one slowest-axis offset, which are
 // consecutive in cell order; 2-D: each column), so every neighbour of a group lies in a short
@@ -600,7 +613,7 @@ __device__ __forceinline__ void nbr_at(const NbrList& L, int k, int& j, int& t)
         // entry instead of 64-bit address arithmetic
         using gcchar = const __attribute__((address_space(1))) char;
         using gcint = const __attribute__((address_space(1))) int;
-        gcint* p = (gcint*)((gcchar*)L.tile + (((unsigned)k << 8) | ((unsigned)L.lane << 2)));
+        gcint* p = (gcint*)((gcchar*)L.tile + ((unsigned)ell_slot(k, L.lane) << 2));
         const int e = MPH_LIST_NT ? __builtin_nontemporal_load(p) : *p;
         j = e & kIndexMask;
         t = e >> kTypeShift;
@@ -1305,7 +1318,8 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
                         a = r2_exact(q0, q1, q2) <= P.rc2;
                     }
                     if (a && j < je && j != i) {
-                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor) list_store(out + cnt * kTile, nbr_entry(j, A.type[j]));
+                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor)
+                            list_store(ell_at(out, (int)(threadIdx.x & 63), cnt), nbr_entry(j, A.type[j]));
                         ++cnt;
                     }
                 }
@@ -1659,7 +1673,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                             // the lane's row 0 (the instructions without the list traffic)
                             if (keep && MPH_DIAG_NOSTORE != 1)
                                 __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, __float_as_int(r[u].w)), tile_rsrc,
-                                                                      MPH_DIAG_NOSTORE == 2 ? (soff & 0xFF) : (soff & kSoffMask),
+                                                                      MPH_DIAG_NOSTORE == 2 ? (soff & 0xFF) : ell_byte(soff & kSoffMask),
                                                                       0, 0);
                             soff += keep ? kListKeep : kListTotal;
                         }
@@ -1734,12 +1748,12 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                             } else if (!C16) {
                                 // byte offset into the wave's tile (SGPR descriptor); an overflowing
                                 // lane (>= 512 neighbours) ends the run (MPH_ERR_NEIGHBOR_OVERFLOW)
-                                __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, ts[u]), tile_rsrc, soff & kSoffMask,
-                                                                      0, 0);
+                                __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, ts[u]), tile_rsrc,
+                                                                      ell_byte(soff & kSoffMask), 0, 0);
                                 soff += kListKeep;
                             } else {
                                 __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, ts[u]), tile_rsrc,
-                                                                      (min(cnt, kMaxNeighbor - 1) << 8) + (lane << 2),
+                                                                      ell_slot(min(cnt, kMaxNeighbor - 1), lane) << 2,
                                                                       0, 0);
                                 ++cnt;
                             }
@@ -1770,12 +1784,12 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                                     o16[(((cnt >> 1) * kTile + lane) << 1) + (cnt & 1)] =
                                         (unsigned short)((j - gbase) | (A.type[j] << kOff16));
                                 else
-                                    list_store(out + cnt * kTile, nbr_entry(j, A.type[j]));
+                                    list_store(ell_at(out, lane, cnt), nbr_entry(j, A.type[j]));
                             }
                             ++cnt;
                         } else {
                             if (!MPH_DIAG_NOSTORE && (soff >> 17) < kMaxNeighbor)
-                                list_store(out + ((soff & kSoffMask) >> 8) * kTile, nbr_entry(j, A.type[j]));
+                                list_store(ell_at(out, lane, (soff & kSoffMask) >> 8), nbr_entry(j, A.type[j]));
                             soff += kListKeep;
                         }
                     }
@@ -2084,7 +2098,7 @@ __device__ __forceinline__ void pass_a_staged(const DevParams& P, const double* 
     const __amdgpu_buffer_rsrc_t rp = arr_rsrc(A.p6);
     const unsigned lane16 = (unsigned)lane * 16u;
     // entry k of the lane's ELL row, or a sentinel past every window (index 2^28 - 1)
-    auto ld = [&](int k) { return k < cnt ? row[(size_t)k * kTile] : 0x7fffffff; };
+    auto ld = [&](int k) { return k < cnt ? *ell_at(row, lane, k) : 0x7fffffff; };
     int c0 = ld(0), c1 = ld(1), c2 = ld(2), c3 = ld(3);
     int x0 = ld(4), x1 = ld(5), x2 = ld(6), x3 = ld(7);
     int p = 0, kn = 8, used = 0;
@@ -2520,7 +2534,7 @@ __global__ __launch_bounds__(256) void k_virial(DevParams P, const DevTables* __
         if (NL.c16) {
             nbr_at<true>(NL, k, j, tj);
         } else {
-            const int e = row[k * kTile];
+            const int e = *ell_at(row, (int)(i & 63), k);
             j = e & kIndexMask;
             tj = e >> kTypeShift;
         }

@@ -17,6 +17,20 @@ namespace mph {
 constexpr int kTypes = MPH_TYPE_COUNT;
 constexpr int kMaxNeighbor = MPH_MAX_NEIGHBOR_COUNT;
 constexpr int kTile = 64;  // ELL neighbour-list tile = one wavefront of i-particles
+// Slot of entry k of lane `lane` in its wave's tile (ints).  Rows: entry k of the 64 lanes in one
+// 256-byte row, [k][lane].  MPH_LIST_PAIRS=1: entries 2p, 2p + 1 of a lane side by side,
+// [k / 2][lane][2], so a 128-byte line holds 16 lanes' pairs instead of 32 lanes' single entries.
+#ifndef MPH_LIST_PAIRS
+#define MPH_LIST_PAIRS 0
+#endif
+constexpr bool kListPairs = MPH_LIST_PAIRS;
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+constexpr inline int ell_slot(int k, int lane)
+{
+    return kListPairs ? (((k >> 1) << 7) | (lane << 1) | (k & 1)) : ((k << 6) | lane);
+}
 // Stencil reach along the contiguous axis: cells there are >= rc / kContigReach wide, and a
 // column is the one index range of +-kContigReach cells (thin cells only sharpen the cutoff
 // trimming of each column)
