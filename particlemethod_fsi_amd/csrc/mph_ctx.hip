@@ -1319,7 +1319,8 @@ int mph_neighbor_rows(MphCtx* c, int first, int count, int* counts, int* ids, lo
         int m = 0;
         for (int s = t * kTile; s < std::min(n, (t + 1) * kTile); ++s) m = std::max(m, std::min(nc[s], kMaxNeighbor));
         std::vector<int>& buf = tiles[t];
-        buf.resize((size_t)((m + 1) & ~1) * kTile);   // whole pairs (ell_slot)
+        const int g = 1 << kListLg;   // whole groups of ell_slot (half-wave rows: the whole tile)
+        buf.resize(kListHalf ? (size_t)kTile * kMaxNeighbor : (size_t)((m + g - 1) / g * g) * kTile);
         if (m) HIP_OK(c, hipMemcpy(buf.data(), c->nbr + (size_t)t * kTile * kMaxNeighbor, sizeof(int) * buf.size(),
                                    hipMemcpyDeviceToHost));
     }

@@ -520,7 +520,11 @@ __device__ __forceinline__ T* ell_at(T* row, int lane, int k)
 // the byte offset of a store slot in the wave's tile from the search's soff = k << 8 | lane << 2
 __device__ __forceinline__ unsigned ell_byte(unsigned soff)
 {
-    return kListPairs ? ((soff & 0x1FE00u) | ((soff & 0xFCu) << 1) | ((soff & 0x100u) >> 6)) : soff;
+    constexpr unsigned kLow = (unsigned)((1 << kListLg) - 1);
+    static_assert(kMaxNeighbor == 512, "half-wave rows: the upper half starts at 512 * 128 bytes");
+    if (kListHalf) return ((soff & 0x1FF00u) >> 1) | (soff & 0x7Cu) | ((soff & 0x80u) << 9);
+    return kListPairs ? ((soff & 0x1FF00u & ~(kLow << 8)) | ((soff & 0xFCu) << kListLg) | ((soff >> 6) & (kLow << 2)))
+                      : soff;
 }
 
 // Compact neighbour list (MPH_LIST16, the default for interior waves).  The stencil's columns
@@ -1923,6 +1927,9 @@ __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, 
 // bal: the passes' XCD split runs this step (launch_neighbors), so the waves feed its histogram.
 #ifndef MPH_NB_WPE
 #define MPH_NB_WPE 8
+#endif
+#ifndef MPH_NB_SHM_PAD
+#define MPH_NB_SHM_PAD 0   // diagnostic builds: unused dynamic LDS per block, to cap the search's occupancy
 #endif
 template <int DIM, int PERM, bool C16>
 __global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_WPE))) void k_neighbors(
@@ -3511,7 +3518,7 @@ void launch_neighbors(const Launch& L, int ck)
                        L.whdr, ck);                                                                          \
         else                                                                                                 \
             MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM, false>), dim3(nb_grid),                    \
-                       dim3(MPH_LB), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.nbcount, L.lhdr, L.st, L.wface, bal, \
+                       dim3(MPH_LB), MPH_NB_SHM_PAD, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.nbcount, L.lhdr, L.st, L.wface, bal, \
                        L.whdr, ck);                                                                          \
         if (bal && !ck)                                                                                      \
             MPH_LAUNCH("xcd_split", L.stream, k_xcd_split, dim3(1), dim3(kXcdSplitThreads), 0, L.stream, L.st); \

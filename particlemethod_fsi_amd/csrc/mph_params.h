@@ -18,18 +18,26 @@ constexpr int kTypes = MPH_TYPE_COUNT;
 constexpr int kMaxNeighbor = MPH_MAX_NEIGHBOR_COUNT;
 constexpr int kTile = 64;  // ELL neighbour-list tile = one wavefront of i-particles
 // Slot of entry k of lane `lane` in its wave's tile (ints).  Rows: entry k of the 64 lanes in one
-// 256-byte row, [k][lane].  MPH_LIST_PAIRS=1: entries 2p, 2p + 1 of a lane side by side,
-// [k / 2][lane][2], so a 128-byte line holds 16 lanes' pairs instead of 32 lanes' single entries.
+// 256-byte row, [k][lane].  MPH_LIST_PAIRS=1 / 2: entries of a lane in groups of 2 / 4 side by side,
+// [k / G][lane][G], so a 128-byte line holds the groups of 128 / (4 G) lanes.
 #ifndef MPH_LIST_PAIRS
 #define MPH_LIST_PAIRS 0
 #endif
-constexpr bool kListPairs = MPH_LIST_PAIRS;
+constexpr int kListLg = MPH_LIST_PAIRS;    // log2 of the group
+constexpr bool kListPairs = kListLg > 0;
+// MPH_LIST_HALF=1: each half-wave (32 lanes) has rows of its own, [lane / 32][k][lane % 32], so a
+// row is one 128-byte line written by 32 lanes instead of two lines written by 64
+#ifndef MPH_LIST_HALF
+#define MPH_LIST_HALF 0
+#endif
+constexpr bool kListHalf = MPH_LIST_HALF;
 #if defined(__HIPCC__)
 __host__ __device__
 #endif
 constexpr inline int ell_slot(int k, int lane)
 {
-    return kListPairs ? (((k >> 1) << 7) | (lane << 1) | (k & 1)) : ((k << 6) | lane);
+    return kListHalf ? ((((lane >> 5) * kMaxNeighbor + k) << 5) | (lane & 31))
+                     : (((k >> kListLg) << (6 + kListLg)) | (lane << kListLg) | (k & ((1 << kListLg) - 1)));
 }
 // Stencil reach along the contiguous axis: cells there are >= rc / kContigReach wide, and a
 // column is the one index range of +-kContigReach cells (thin cells only sharpen the cutoff
