@@ -88,6 +88,15 @@
 #ifndef MPH_SPLIT32
 #define MPH_SPLIT32 1   // a wave across two cell rows stages its two runs of FP32 records (scan_candidates_lds)
 #endif
+#ifndef MPH_STAGE_CPOL
+#define MPH_STAGE_CPOL 0   // cache policy of the search's FP32 record staging loads (2: non-temporal)
+#endif
+#ifndef MPH_CHUNK_BUILD
+#define MPH_CHUNK_BUILD 0   // the chunked search + pass A (MPH_CHUNKS, measured and rejected)
+#endif
+#ifndef MPH_LIST_CPOL
+#define MPH_LIST_CPOL 0   // cache policy of the search's list stores (FP32 path)
+#endif
 #ifndef MPH_CAP32
 #define MPH_CAP32 1   // FP32-record windows up to the staging area's 16-byte capacity (313 at 176)
 #endif
@@ -412,7 +421,8 @@ __device__ __forceinline__ int list_block(const DevState* st, int n)
     return b < nb ? xcd_block(b, nb) : -1;
 }
 
-// Chunked search + pass A (Launch.chunks > 1, launch_search_pass_a): launch c of C takes piece c
+// Chunked search + pass A (Launch.chunks > 1, launch_search_pass_a; builds with MPH_CHUNK_BUILD=1
+// only, measured and rejected: profiles/r05/chunks_rejected/): launch c of C takes piece c
 // of every XCD's contiguous range of the equal map (xcd_block), so pass A of piece c, on a second
 // stream, runs beside the search of piece c + 1 and the XCDs keep their own ranges.
 // ck = c << 8 | C; returns the block's tile of MPH_LB particles or -1.
@@ -1626,10 +1636,10 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             // FP32 records: candidate j at record j - lbase, 64 records (1 KB) per instruction
             float4* s4 = reinterpret_cast<float4*>(sx);
             for (int p = 0; p * 64 < n1; ++p)   // wave-uniform
-                if (p * 64 + lane < n1) __builtin_amdgcn_global_load_lds(A.f4 + mn + p * 64 + lane, s4 + p * 64, 16, 0, 0);
+                if (p * 64 + lane < n1) __builtin_amdgcn_global_load_lds(A.f4 + mn + p * 64 + lane, s4 + p * 64, 16, 0, MPH_STAGE_CPOL);
             for (int p = 0; p * 64 < n2; ++p)   // the second run (two), after the first
                 if (p * 64 + lane < n2)
-                    __builtin_amdgcn_global_load_lds(A.f4 + m2 + p * 64 + lane, s4 + n1 + p * 64, 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds(A.f4 + m2 + p * 64 + lane, s4 + n1 + p * 64, 16, 0, MPH_STAGE_CPOL);
             __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the records (and column col + 1's start[]) landed
             __builtin_amdgcn_wave_barrier();
             const float xf = (float)(xi - P.cref[0]), yf = (float)(yi - P.cref[1]), zf = (float)(zi - P.cref[2]);
@@ -1678,7 +1688,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                             if (keep && MPH_DIAG_NOSTORE != 1)
                                 __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, __float_as_int(r[u].w)), tile_rsrc,
                                                                       MPH_DIAG_NOSTORE == 2 ? (soff & 0xFF) : ell_byte(soff & kSoffMask),
-                                                                      0, 0);
+                                                                      0, MPH_LIST_CPOL);
                             soff += keep ? kListKeep : kListTotal;
                         }
                     }
@@ -1938,9 +1948,15 @@ __global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_W
     int2* __restrict__ whdr, int ck)
 {
     const int n = dev_n(P);
+#if MPH_CHUNK_BUILD
     const int tb = ck ? chunk_block(blockIdx.x, list_blocks(n), ck)
                       : ((int)blockIdx.x < list_blocks(n) ? xcd_block(blockIdx.x, list_blocks(n)) : -1);
     if (tb < 0) return;
+#else
+    (void)ck;
+    if ((int)blockIdx.x >= list_blocks(n)) return;
+    const int tb = xcd_block(blockIdx.x, list_blocks(n));
+#endif
     XCD_PROBE(st, 0);
     __shared__ __attribute__((aligned(16))) double stage[kWB][stage_words(MPH_LDS_CAP, MPH_SB)];
     const int i = tb * blockDim.x + threadIdx.x;
@@ -2209,7 +2225,12 @@ __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, cons
                                                 int ck)
 {
     const int n = dev_n(P);
+#if MPH_CHUNK_BUILD
     const int lb = ck ? chunk_block(blockIdx.x, list_blocks(n), ck) : list_block(st, n);
+#else
+    (void)ck;
+    const int lb = list_block(st, n);
+#endif
     if (lb < 0) return;
     XCD_PROBE(st, 1);
     __shared__ double s_ratio[kTypes * kTypes];
@@ -3571,7 +3592,7 @@ void launch_pass_a(const Launch& L, int ck)
 // and address processing).  Pass A of a piece reads the lists of its own particles only.
 void launch_search_pass_a(const Launch& L)
 {
-    const int C = L.chunks;
+    const int C = MPH_CHUNK_BUILD ? L.chunks : 1;
     if (C <= 1 || !L.stream2 || !L.ev_chunk || L.lhdr || MPH_PA_STAGED || L.P->slab_axis >= 0 || L.P->n == 0) {
         launch_neighbors(L);
         launch_pass_a(L);

@@ -160,7 +160,7 @@ def load_library() -> ctypes.CDLL:
     }
     # entry points an older library may lack (A/B runs against earlier builds)
     optional = {"mph_phase_timing", "mph_phase_times", "mph_set_step_batching", "mph_neighbor_rows",
-                "mph_dist_overlap"}
+                "mph_dist_overlap", "mph_profile_graphs"}
     for name, (res, args) in sig.items():
         if name in optional and not hasattr(L, name):
             continue

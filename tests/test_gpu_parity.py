@@ -182,25 +182,6 @@ def test_gpu_trimmed_lists_equal_full_lists(case, monkeypatch):
         assert np.array_equal(out["0"][f], out["1"][f], equal_nan=True), f
 
 
-@pytest.mark.parametrize("case,chunks", [("box3d_jit", "3"), ("gate3d_jit", "4"), ("dam2d", "16")])
-def test_gpu_chunked_search_equals_single(case, chunks, monkeypatch):
-    """MPH_CHUNKS: the search and pass A in pieces on two streams (pass A of a piece beside the
-    next piece's search) give the same bits as one search launch and one pass-A launch, through the
-    8-step graph, a single step and the XCD-balanced map of pass B (forced on with MPH_XCD_BAL_MIN=0;
-    16 pieces on dam2d leave some pieces empty)."""
-    cfg, parts = cases.get(case).build()
-    monkeypatch.setenv("MPH_XCD_BAL_MIN", "0")
-    out = {}
-    for mode in ("1", chunks):
-        monkeypatch.setenv("MPH_CHUNKS", mode)
-        with MphSolver(cfg, parts) as s:
-            s.step(9)
-            out[mode] = {f: s.get(f) for f in ["NeighborCount", "Position", "Velocity", "PressureP", "Force",
-                                               "DensityA", "VolStrainP", "DivergenceP"]}
-    for f in out["1"]:
-        assert np.array_equal(out["1"][f], out[chunks][f], equal_nan=True), f
-
-
 @pytest.mark.parametrize("case", ["box3d_jit", "gate3d_jit"])
 def test_gpu_profile_graphs_leave_state_unchanged(case):
     """mph_profile_graphs replays the search, pass A and pass B over the last step's state: positive

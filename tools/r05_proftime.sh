@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/r05proftime
 mkdir -p $OUT
-timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "profile_graphs or chunked" > $OUT/pytest.log 2>&1 || exit 10
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "profile_graphs" > $OUT/pytest.log 2>&1 || exit 10
 timeout -k 10 300 python3 bench.py --steps 24 --warmup 8 --no-cpu-baseline --developed-steps 0 > $OUT/bench.json 2> $OUT/bench.err || exit 11
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- \
     python3 bench.py --steps 24 --warmup 8 --no-cpu-baseline --developed-steps 0 > $OUT/bench_under_kt.log 2>&1 || exit 12
