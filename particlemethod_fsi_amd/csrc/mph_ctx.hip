@@ -1190,11 +1190,11 @@ int mph_profile_steps(MphCtx* c, int nsteps, double* avg_ms, int* launches, char
 // its own (the output-only stores on every 8th, as in the 8-step graph), replayed once to warm,
 // then once between two HIP events.  Each replay recomputes what the last step left (the lists,
 // pass A's products, B from A), bit for bit, so the state does not change; pass B is skipped with
-// elastic slots (the substeps after it have moved them in B).  Needs one step done.
+// elastic slots (the substeps after it have moved them in B).  Slab contexts: the same on the
+// rank's local set, pass B as its single launch.  Needs one step done.
 int mph_profile_graphs(MphCtx* c, int reps, double* avg_ms3)
 {
     if (!c || reps <= 0 || reps > 64 || !avg_ms3) return MPH_ERR_ARG;
-    if (c->dist) return ctx_fail(c, MPH_ERR_UNSUPPORTED, "mph_profile_graphs: single contexts only");
     CK(ctx_flush(c));
     if (!c->stepped) return ctx_fail(c, MPH_ERR_ARG, "mph_profile_graphs: run a step first");
     HIP_OK(c, hipSetDevice(c->device));
@@ -1212,6 +1212,7 @@ int mph_profile_graphs(MphCtx* c, int reps, double* avg_ms3)
             for (int r = 0; r < reps; ++r) {
                 const bool last = r % 8 == 7 || r == reps - 1;
                 Launch La = c->L;
+                if (c->dist) La.wface = c->dist->wface;   // slab mode: pass B in one launch (phase 0)
                 if (!last) {
                     La.dens_a = La.vstrain = La.divp = nullptr;
                     if (!c->P.surface) La.gx = La.gy = La.gz = La.pa = nullptr;

@@ -135,6 +135,7 @@ def main():
 
 def summary(out):
     return {"max_rank_gpu_ms_per_step": max(o["gpu_ms_per_step"] for o in out),
+            "max_rank_gpu_ms_per_step_graph": max((o.get("gpu_ms_per_step_graph") or 0.0) for o in out) or None,
             "max_rank_gpu_busy_ms_per_step": max(o["gpu_busy_ms_per_step"] or 0.0 for o in out)}
 
 
@@ -171,6 +172,14 @@ def run_ranks(args, R, axis, cuts, locals_, records=None, replay=None):
                 s.synchronize()
                 wall = time.perf_counter() - t0
             ex.record = ex.replay = None
+            # the list kernels as graph replays (mph_profile_graphs; no exchange), as the RCCL
+            # steps replay them: pass B only when it runs as one launch (overlap off)
+            graph = None
+            with token.lock:
+                try:
+                    graph = s.profile_graphs(8)
+                except Exception:  # noqa: BLE001 -- older library
+                    graph = None
             xcd = None
             if os.environ.get("MPH_XCD_DIAG") == "1":   # diagnostic build: tools/xcd_diag.py
                 from xcd_diag import xcd_read
@@ -190,6 +199,14 @@ def run_ranks(args, R, axis, cuts, locals_, records=None, replay=None):
                                       for k, v in prof.items()},
                       "gpu_ms_per_step": sum(v["avg_ms"] * v["launches"] for v in prof.values()) / args.steps,
                       "wall_s": wall}
+            if graph is not None:
+                gk = dict(out[r]["kernels_ms"])
+                for k, v in graph.items():
+                    if v is None or k not in gk or (k == "pass_b" and "pass_b_face" in gk):
+                        continue
+                    gk[k] = round(max(0.0, v - gk.get("xcd_split", 0.0)) if k == "neighbors" else v, 5)
+                out[r]["kernels_ms_graph"] = gk
+                out[r]["gpu_ms_per_step_graph"] = sum(gk[k] * prof[k]["launches"] for k in gk) / args.steps
             if xcd is not None:
                 out[r]["xcd"] = xcd
             with token.lock:
