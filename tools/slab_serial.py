@@ -190,9 +190,11 @@ def run_ranks(args, R, axis, cuts, locals_, records=None, replay=None):
                     s.step(1)
                     s.synchronize()
                     xcd = xcd_read(s, reset=True)
-            info = s.dist_info()
+            with token.lock:   # device copies: not beside another rank's timed work
+                info = s.dist_info()
+                owned = len(s.owned_ids())
             busy = prof.pop("gpu_busy", {}).get("avg_ms")   # union of the kernel intervals per step
-            out[r] = {"rank": r, "owned": len(s.owned_ids()), "held": info["held"],
+            out[r] = {"rank": r, "owned": owned, "held": info["held"],
                       "gpu_busy_ms_per_step": busy,
                       "kernels_ms": {k: round(v["avg_ms"], 5) for k, v in prof.items()},
                       "ms_per_step": {k: round(v["avg_ms"] * v["launches"] / args.steps, 5)
