@@ -123,6 +123,7 @@ struct MphCtx {
     int *key = nullptr, *slot = nullptr, *tmp = nullptr, *cnt = nullptr, *start = nullptr, *bsum = nullptr;
     double *vir = nullptr, *vpres = nullptr;   // VirialStress [cap][9] / VirialPressure (A order), lazy
     int *nbr = nullptr, *ncount = nullptr, *nbcount = nullptr;   // list lengths / NeighborCount
+    int* pred = nullptr;   // MPH_LIST_SPREAD: the last step's NeighborCount in this step's order
     int* list_hdr = nullptr;     // per-wave headers of the compact 16-bit lists (kLhdr ints each)
     int2* win_hdr = nullptr;     // MPH_PA_STAGED builds: per-wave column windows (kWinHdr each)
     unsigned long long* wave_log = nullptr;   // MPH_DIAG_XCD >= 2 builds: the search's per-wave log

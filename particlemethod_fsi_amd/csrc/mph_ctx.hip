@@ -79,6 +79,9 @@ void ctx_fill_launch(MphCtx* c)
     L.A = c->A; L.B = c->B; L.rank_of = nullptr; L.dst_of = nullptr;
     L.key = c->key; L.slot = c->slot; L.tmp = c->tmp; L.cnt = c->cnt; L.start = c->start; L.bsum = c->bsum;
     L.nbr = c->nbr; L.ncount = c->ncount; L.nbcount = c->nbcount; L.whdr = c->win_hdr;
+    // MPH_LIST_SPREAD (single contexts): the sort carries the last NeighborCount to the search
+    c->P.pred = kListSpread && !c->dist ? c->pred : nullptr;
+    c->P.pred_src = c->P.pred ? c->nbcount : nullptr;
     // compact 16-bit lists of interior wavefronts (MPH_LIST16=1), or 32-bit ELL rows everywhere
     // (MPH_LIST16=0); unset: kListCompact
     const char* l16 = std::getenv("MPH_LIST16");
@@ -493,12 +496,14 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     CK(dalloc(c, &c->bsum, 3 * bs));
     CK(dalloc(c, &c->nbr, ntile * kTile * kMaxNeighbor)); CK(dalloc(c, &c->ncount, cap));
     CK(dalloc(c, &c->nbcount, cap));
+    if (kListSpread) CK(dalloc(c, &c->pred, cap));
 #if (defined(MPH_DIAG_NOSTORE) && MPH_DIAG_NOSTORE) || (defined(MPH_DIAG_SEARCH) && (MPH_DIAG_SEARCH & 4))
     // diagnostic builds: the search stores no list (or skips the waves near a periodic face, whose
     // counts then stay 0), so the passes read index 0 (never garbage)
     if (hipMemset(c->nbr, 0, sizeof(int) * ntile * kTile * kMaxNeighbor) != hipSuccess) return MPH_ERR_HIP;
     if (hipMemset(c->ncount, 0, sizeof(int) * cap) != hipSuccess) return MPH_ERR_HIP;
     if (hipMemset(c->nbcount, 0, sizeof(int) * cap) != hipSuccess) return MPH_ERR_HIP;
+    if (c->pred && hipMemset(c->pred, 0, sizeof(int) * cap) != hipSuccess) return MPH_ERR_HIP;
 #endif
     CK(dalloc(c, &c->list_hdr, ntile * kLhdr));
 #if defined(MPH_PA_STAGED) && MPH_PA_STAGED
@@ -1298,16 +1303,18 @@ int mph_neighbor_rows(MphCtx* c, int first, int count, int* counts, int* ids, lo
     }
     // the last search's rows are in its sorted order A: A.id maps a row (and an entry) back to the
     // original index, ncount holds NeighborCount in the same order
-    std::vector<int> id(n), nc(n);
+    // (MPH_LIST_SPREAD: ncount holds the rows walked, sentinels included; nbcount the entries)
+    std::vector<int> id(n), nc(n), nv(n);
     HIP_OK(c, hipMemcpy(id.data(), c->A.id, sizeof(int) * n, hipMemcpyDeviceToHost));
     HIP_OK(c, hipMemcpy(nc.data(), c->ncount, sizeof(int) * n, hipMemcpyDeviceToHost));
+    HIP_OK(c, hipMemcpy(nv.data(), c->nbcount, sizeof(int) * n, hipMemcpyDeviceToHost));
     std::vector<int> row_of(count, -1);
     for (int s = 0; s < n; ++s)
         if (id[s] >= first && id[s] < first + count) row_of[id[s] - first] = s;
     long long total = 0;
     for (int k = 0; k < count; ++k) {
         if (row_of[k] < 0) return fail(c, MPH_ERR_HIP, "mph_neighbor_rows: particle missing from the sorted set");
-        counts[k] = nc[row_of[k]];
+        counts[k] = nv[row_of[k]];
         total += std::min(counts[k], kMaxNeighbor);
     }
     if (total > ids_cap) return fail(c, MPH_ERR_ARG, "mph_neighbor_rows: ids_cap too small (" + std::to_string(total) + " needed)");
@@ -1327,13 +1334,17 @@ int mph_neighbor_rows(MphCtx* c, int first, int count, int* counts, int* ids, lo
     }
     long long w = 0;
     for (int k = 0; k < count; ++k) {
-        const int s = row_of[k], m = std::min(counts[k], kMaxNeighbor);
+        const int s = row_of[k], m = std::min(counts[k], kMaxNeighbor), rows = std::min(nc[s], kMaxNeighbor);
         const std::vector<int>& buf = tiles[s >> 6];
-        for (int e = 0; e < m; ++e) {
-            const int j = buf[(size_t)ell_slot(e, s & 63)] & kIndexMask;
-            if (j >= n) return fail(c, MPH_ERR_HIP, "mph_neighbor_rows: list entry past the particle count");
-            ids[w + e] = id[j];
+        int q = 0;
+        for (int e = 0; e < rows; ++e) {
+            const int v = buf[(size_t)ell_slot(e, s & 63)];
+            if (kListSpread && v < 0) continue;   // a row the lane skipped
+            const int j = v & kIndexMask;
+            if (j >= n || q >= m) return fail(c, MPH_ERR_HIP, "mph_neighbor_rows: list entry past the particle count");
+            ids[w + q++] = id[j];
         }
+        if (q != m) return fail(c, MPH_ERR_HIP, "mph_neighbor_rows: list rows disagree with NeighborCount");
         std::sort(ids + w, ids + w + m);
         w += m;
     }

@@ -101,6 +101,9 @@
 #define MPH_CAP32 1   // FP32-record windows up to the staging area's 16-byte capacity (313 at 176)
 #endif
 
+#if defined(MPH_LIST_SPREAD) && MPH_LIST_SPREAD && defined(MPH_PA_STAGED) && MPH_PA_STAGED
+#error "MPH_LIST_SPREAD lists hold sentinels the staged pass A does not skip"
+#endif
 #ifndef MPH_PA_STAGED
 // pass A of the interior waves in a kernel of its own (k_pass_a_st) that reads each stencil column's
 // window of 48-byte records from LDS, staged once per wave (the search writes the windows per wave:
@@ -1040,6 +1043,7 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
     if (MPH_SEARCH_F32 && A.f4)
         A.f4[dst] = make_float4((float)(B.x[b] - P.cref[0]), (float)(B.y[b] - P.cref[1]),
                                 (float)(B.z[b] - P.cref[2]), __int_as_float(B.type[b]));
+    if (kListSpread && P.pred) P.pred[dst] = P.pred_src[p];   // the row spread's prediction
     if (dst_of) dst_of[p] = dst;   // slab mode: ids are global (ghosts negative)
     else if (rank_of) rank_of[id] = dst;
 }
@@ -1552,6 +1556,29 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     // bits 17 and up count every accepted neighbour (NeighborCount), bits 8-16 the stored ones (the
     // FP32 path keeps only r^2 <= P.rlf: kListTotal, kListKeep), so the store offset is soff & kSoffMask
     int soff = lane << 2;
+#if MPH_LIST_SPREAD
+    // proportional rows (kListSpread): stored entry k at row k * M / np below the prediction np,
+    // M + k - np past it; `cur` is the next row the lane has not written (rows skipped get the
+    // sentinel).  Identity (M = np = 0) without a prediction or above kSpreadMax.
+    int np = !C16 && P.pred && act ? min(P.pred[i], kMaxNeighbor - 1) : 0;
+    int Mw = __builtin_amdgcn_readfirstlane(wave_max(np));
+    if (Mw > kSpreadMax) Mw = 0;
+    if (Mw == 0) np = 0;
+    const unsigned rfx = np > 0 ? ((unsigned)Mw << 14) / (unsigned)np : (1u << 14);
+    int cur = 0;
+    const int sentinel = i | (int)0xF0000000;
+    auto put = [&](int e) {
+        const int k = (soff >> 8) & 0x1FF;
+        const int row = k < np ? (int)(((unsigned)k * rfx) >> 14) : Mw + k - np;
+        for (; cur < row && cur < kMaxNeighbor; ++cur)
+            __builtin_amdgcn_raw_buffer_store_b32(sentinel, tile_rsrc, ((unsigned)cur << 8) | (soff & 0xFC), 0, 0);
+        if (row < kMaxNeighbor)
+            __builtin_amdgcn_raw_buffer_store_b32(e, tile_rsrc, ((unsigned)row << 8) | (soff & 0xFC), 0, 0);
+        else
+            atomicOr(&dst->overflow, 1);   // past the tile (MPH_ERR_NEIGHBOR_OVERFLOW)
+        cur = row + 1;
+    };
+#endif
     constexpr int kSelfCol = DIM == 3 ? kReach * kGroups + kReach : kReach;   // the lane's own column
     // one stencil column: its range [jb, je) was loaded one column ahead; (nb_jb, nb_je) receive
     // column col + 1's.  The loop below is unrolled by two with the roles of the two register pairs
@@ -1685,10 +1712,14 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                             const bool keep = r2f <= P.rlf;
                             // diagnostic builds: MPH_DIAG_NOSTORE 1 no store, 2 the same stores to
                             // the lane's row 0 (the instructions without the list traffic)
+#if MPH_LIST_SPREAD
+                            if (keep) put(nbr_entry(j, __float_as_int(r[u].w)));
+#else
                             if (keep && MPH_DIAG_NOSTORE != 1)
                                 __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, __float_as_int(r[u].w)), tile_rsrc,
                                                                       MPH_DIAG_NOSTORE == 2 ? (soff & 0xFF) : ell_byte(soff & kSoffMask),
                                                                       0, MPH_LIST_CPOL);
+#endif
                             soff += keep ? kListKeep : kListTotal;
                         }
                     }
@@ -1762,8 +1793,12 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                             } else if (!C16) {
                                 // byte offset into the wave's tile (SGPR descriptor); an overflowing
                                 // lane (>= 512 neighbours) ends the run (MPH_ERR_NEIGHBOR_OVERFLOW)
+#if MPH_LIST_SPREAD
+                                put(nbr_entry(j, ts[u]));
+#else
                                 __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, ts[u]), tile_rsrc,
                                                                       ell_byte(soff & kSoffMask), 0, 0);
+#endif
                                 soff += kListKeep;
                             } else {
                                 __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, ts[u]), tile_rsrc,
@@ -1802,8 +1837,12 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                             }
                             ++cnt;
                         } else {
+#if MPH_LIST_SPREAD
+                            put(nbr_entry(j, A.type[j]));
+#else
                             if (!MPH_DIAG_NOSTORE && (soff >> 17) < kMaxNeighbor)
                                 list_store(ell_at(out, lane, (soff & kSoffMask) >> 8), nbr_entry(j, A.type[j]));
+#endif
                             soff += kListKeep;
                         }
                     }
@@ -1822,6 +1861,9 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     if (!C16) {
         cnt = soff >> 17;                 // every neighbour (NeighborCount)
         *stored = (soff >> 8) & 0x1FF;    // the list's length (r^2 <= P.rlf)
+#if MPH_LIST_SPREAD
+        *stored = min(cur, kMaxNeighbor);   // rows the passes walk, sentinels included
+#endif
     } else {
         *stored = cnt;
     }
@@ -2083,6 +2125,7 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (k0 + u >= cnt) break;
+            if (kListSpread && TT[u] < 0) continue;   // a row the lane skipped (sentinel)
             if (MPH_DIAG_GATHER == 2) { o.da += X[u] + Y[u] + Z[u] + VX[u] + VY[u] + VZ[u] + TT[u]; continue; }
             const double q0 = image_exact<FAST>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
             const double q1 = image_exact<FAST>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
@@ -2390,6 +2433,7 @@ __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (k0 + u >= cnt) break;
+            if (kListSpread && TT[u] < 0) continue;   // a row the lane skipped (sentinel)
             if (MPH_DIAG_GATHER == 2) { f0 += X[u] + Y[u] + Z[u] + PJ[u] + TT[u]; continue; }
             pass_b_term<FAST, SURF, DIM>(P, s_ratio, gx, gy, gz, pa, jj[u], TT[u], X[u], Y[u], Z[u], PJ[u], ti,
                                          solid, xi, yi, zi, gxi, gyi, gzi, pai, ai, dscale, cpv, f0, f1, f2);
@@ -2563,6 +2607,7 @@ __global__ __launch_bounds__(256) void k_virial(DevParams P, const DevTables* __
             nbr_at<true>(NL, k, j, tj);
         } else {
             const int e = *ell_at(row, (int)(i & 63), k);
+            if (kListSpread && e < 0) continue;   // a row the lane skipped (sentinel)
             j = e & kIndexMask;
             tj = e >> kTypeShift;
         }

@@ -31,6 +31,15 @@ constexpr bool kListPairs = kListLg > 0;
 #define MPH_LIST_HALF 0
 #endif
 constexpr bool kListHalf = MPH_LIST_HALF;
+// MPH_LIST_SPREAD=1: a lane's k-th stored neighbour goes to row k * M / n of its wave's tile (n:
+// the lane's NeighborCount of the last step, M: the wave's largest), the rows it skips hold a
+// sentinel (its own index with the type bits all set, which the list readers skip), so the lanes
+// fill their rows at the same pace and the wave's rows complete together (mph_kernels.hip search)
+#ifndef MPH_LIST_SPREAD
+#define MPH_LIST_SPREAD 0
+#endif
+constexpr bool kListSpread = MPH_LIST_SPREAD;
+constexpr int kSpreadMax = 192;   // waves predicted above this many neighbours keep rows = k
 #if defined(__HIPCC__)
 __host__ __device__
 #endif
@@ -176,6 +185,10 @@ struct DevParams {
     // shell MaxRadius < r <= MaxRadius + MARGIN that the reference's list carries and NeighborCount
     // counts.  FLT_MAX (MPH_LIST_FULL=1): the reference's whole list.
     float rlf;
+    // MPH_LIST_SPREAD, single contexts: pred[i] the sorted particle i's NeighborCount of the last
+    // step, written by k_rank_scatter from pred_src (the last step's NeighborCount, its order)
+    int* pred = nullptr;
+    const int* pred_src = nullptr;
 };
 
 // Derived uniforms of DevParams (same expressions the kernels used, so the same bits).
