@@ -494,13 +494,13 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     // scratch third for the other scans (k_scan_reduce, structure init); all zero at the start
     const size_t bs = (size_t)c->P.ncell / 4096 + 2;
     CK(dalloc(c, &c->bsum, 3 * bs));
-    CK(dalloc(c, &c->nbr, ntile * kTile * kMaxNeighbor)); CK(dalloc(c, &c->ncount, cap));
+    CK(dalloc(c, &c->nbr, ntile * kTileStride)); CK(dalloc(c, &c->ncount, cap));
     CK(dalloc(c, &c->nbcount, cap));
     if (kListSpread) CK(dalloc(c, &c->pred, cap));
 #if (defined(MPH_DIAG_NOSTORE) && MPH_DIAG_NOSTORE) || (defined(MPH_DIAG_SEARCH) && (MPH_DIAG_SEARCH & 4))
     // diagnostic builds: the search stores no list (or skips the waves near a periodic face, whose
     // counts then stay 0), so the passes read index 0 (never garbage)
-    if (hipMemset(c->nbr, 0, sizeof(int) * ntile * kTile * kMaxNeighbor) != hipSuccess) return MPH_ERR_HIP;
+    if (hipMemset(c->nbr, 0, sizeof(int) * ntile * kTileStride) != hipSuccess) return MPH_ERR_HIP;
     if (hipMemset(c->ncount, 0, sizeof(int) * cap) != hipSuccess) return MPH_ERR_HIP;
     if (hipMemset(c->nbcount, 0, sizeof(int) * cap) != hipSuccess) return MPH_ERR_HIP;
     if (c->pred && hipMemset(c->pred, 0, sizeof(int) * cap) != hipSuccess) return MPH_ERR_HIP;
@@ -1329,7 +1329,7 @@ int mph_neighbor_rows(MphCtx* c, int first, int count, int* counts, int* ids, lo
         std::vector<int>& buf = tiles[t];
         const int g = 1 << kListLg;   // whole groups of ell_slot (half-wave rows: the whole tile)
         buf.resize(kListHalf ? (size_t)kTile * kMaxNeighbor : (size_t)((m + g - 1) / g * g) * kTile);
-        if (m) HIP_OK(c, hipMemcpy(buf.data(), c->nbr + (size_t)t * kTile * kMaxNeighbor, sizeof(int) * buf.size(),
+        if (m) HIP_OK(c, hipMemcpy(buf.data(), c->nbr + (size_t)t * kTileStride, sizeof(int) * buf.size(),
                                    hipMemcpyDeviceToHost));
     }
     long long w = 0;

@@ -520,7 +520,7 @@ __device__ __forceinline__ void list_store(int* p, int v)
 
 __device__ __forceinline__ const int* ell_row(const int* nbr, int i)
 {
-    return nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
+    return nbr + (size_t)(i >> 6) * kTileStride + (i & 63);
 }
 
 // entry k of a lane from the lane's ell_row pointer (ell_slot: rows or pairs)
@@ -578,7 +578,7 @@ __device__ __forceinline__ NbrList nbr_list(const int* nbr, const int* lhdr, int
 {
     NbrList L;
     const int tile = __builtin_amdgcn_readfirstlane(i >> 6);
-    L.tile = nbr + (size_t)tile * (kTile * kMaxNeighbor);
+    L.tile = nbr + (size_t)tile * kTileStride;
     L.lane = i & 63;
     L.gb = sb;
     const int* h = lhdr ? lhdr + (size_t)tile * kLhdr : nullptr;
@@ -1942,7 +1942,7 @@ __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, 
     const int cx = cell_axis(xi, P.corg[0], P.dw[0], P.ginv[0], P.gc[0]);
     const int cy = cell_axis(yi, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
     const int cz = DIM == 3 ? cell_axis(zi, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
-    int* out = nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63);
+    int* out = nbr + (size_t)(i >> 6) * kTileStride + (i & 63);
     // MPH_PA_STAGED: the wave's column windows for pass A, flag kWinCols: 1 = written
     int2* whdr = MPH_PA_STAGED && !C16 && !REDO && whdr_all ? whdr_all + (size_t)tile * kWinHdr : nullptr;
     if (whdr && (threadIdx.x & 63) == 0) whdr[kWinCols] = make_int2(fast ? 1 : 0, 0);
@@ -1950,7 +1950,7 @@ __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, 
         if (C16 && !REDO) {
             cnt = scan_candidates_lds<DIM, PERM, true>(P, A, start, i, own, xi, yi, zi, cx, cy, cz, out, stage, lh,
                                                        reinterpret_cast<unsigned short*>(
-                                                           nbr + (size_t)tile * (kTile * kMaxNeighbor)), st, nullptr,
+                                                           nbr + (size_t)tile * kTileStride), st, nullptr,
                                                        &stored);
             if ((threadIdx.x & 63) == 0 && lh[kHdrFlag] == 2) atomicAdd(&st->list_redo, 1);
         } else {
@@ -2245,7 +2245,7 @@ __global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_PAS_
     const int ti = A.type[ii];
     const int cnt = live ? min(ncount[i], kMaxNeighbor) : 0;
     PassA o;
-    pass_a_staged<DIM>(P, s_ratio, s_mu, A, nbr + (size_t)(i >> 6) * (kTile * kMaxNeighbor) + (i & 63),
+    pass_a_staged<DIM>(P, s_ratio, s_mu, A, nbr + (size_t)(i >> 6) * kTileStride + (i & 63),
                        whdr + (size_t)__builtin_amdgcn_readfirstlane(i >> 6) * kWinHdr, cnt, ti, dev_is_struct(ti),
                        xi, yi, zi, vxi, vyi, vzi, o, pstage[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], st);
     if (live) pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);

@@ -17,6 +17,14 @@ namespace mph {
 constexpr int kTypes = MPH_TYPE_COUNT;
 constexpr int kMaxNeighbor = MPH_MAX_NEIGHBOR_COUNT;
 constexpr int kTile = 64;  // ELL neighbour-list tile = one wavefront of i-particles
+// Ints from one wave's list tile to the next: kMaxNeighbor rows of 64, plus MPH_TILE_PAD rows, so
+// that the tiles do not all start on the same power-of-two boundary.  One row: the search 3-4 %
+// faster at rest and in the developed flow (five same-box rounds; 4 and 9 rows no faster; the
+// list's write-backs unchanged), steps within noise (profiles/r05/tile_pad/)
+#ifndef MPH_TILE_PAD
+#define MPH_TILE_PAD 1
+#endif
+constexpr int kTileStride = kTile * (kMaxNeighbor + MPH_TILE_PAD);
 // Slot of entry k of lane `lane` in its wave's tile (ints).  Rows: entry k of the 64 lanes in one
 // 256-byte row, [k][lane].  MPH_LIST_PAIRS=1 / 2: entries of a lane in groups of 2 / 4 side by side,
 // [k / G][lane][G], so a 128-byte line holds the groups of 128 / (4 G) lanes.
