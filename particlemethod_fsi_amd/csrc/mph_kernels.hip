@@ -59,8 +59,9 @@
                              // 2 = every store goes to the lane's row 0 (same instructions, no list traffic)
 #endif
 #ifndef MPH_DIAG_GATHER
-#define MPH_DIAG_GATHER 0   // diagnostic builds only: 1 = list passes gather a coalesced dummy
-                            // neighbour (j = lane id ^ 1) instead of the listed one, 2 = gathers only
+#define MPH_DIAG_GATHER 0   // diagnostic builds only: 1 = list passes gather a dummy neighbour that does
+                            // not depend on the entry (j = lane id ^ 1; hipcc hoists those loads out of
+                            // the loop, so this times the passes without gathers), 2 = gathers only
 #endif
 #ifndef MPH_SB
 // candidates per batch in the search: 2 (64 VGPRs) with the LDS capacity below gives 8 waves per
