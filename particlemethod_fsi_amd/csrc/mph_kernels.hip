@@ -400,7 +400,11 @@ __device__ __forceinline__ int list_blocks(int n) { return (n + MPH_LB - 1) / MP
 #endif
 constexpr int kWaveCost = 16;   // a wave's fixed cost, in list entries, for the work histogram
 
-__device__ __forceinline__ int list_block(const DevState* st, int n)
+#if MPH_CU_AFFINE
+__device__ int cu_affine_tile(DevState* st, int kern, int lo, int len);
+#endif
+// kern (MPH_CU_AFFINE builds): 1 pass A, 2 pass B -- the CU-affine claim inside the XCD range
+__device__ __forceinline__ int list_block(const DevState* st, int n, int kern = -1)
 {
     const int nb = list_blocks(n);
     const int b = blockIdx.x;
@@ -418,6 +422,9 @@ __device__ __forceinline__ int list_block(const DevState* st, int n)
             lo = hi;
         }
         if (ok) {
+#if MPH_CU_AFFINE
+            if (kern >= 0) return cu_affine_tile(const_cast<DevState*>(st), kern, mine_lo, mine_c);
+#endif
             const int q = b >> 3;
             return q < mine_c ? mine_lo + q : -1;
         }
@@ -441,6 +448,48 @@ __device__ __forceinline__ int chunk_block(int b, int nb, int ck)
     const int k = b >> 3;
     return k < p1 - p0 ? lo + p0 + k : -1;
 }
+
+#if MPH_CU_AFFINE
+// CU-affine tile claim (MPH_CU_AFFINE): the logical XCD j = blockIdx & 7 keeps its contiguous range
+// [lo, lo + len) of tiles, split into kCuQueues contiguous queues; a block takes the next tile of
+// the queue of the CU it runs on (hardware HW_ID: CU, SH, SE), else steals from the other queues of
+// its XCD, so the four blocks resident on a CU work on neighbouring tiles (shared L1 lines) instead
+// of tiles 32 blocks apart.  Every block first takes a ticket; a launch's blocks all take one, so
+// ticket / gridDim is the launch's generation, which tags the queue counters (a stale counter is
+// reset by compare-and-swap): no reset pass, and each tile is claimed exactly once.  Returns the
+// block's tile or -1 (block-uniform, through LDS).
+__device__ int cu_affine_tile(DevState* st, int kern, int lo, int len)
+{
+    __shared__ int s_tile;
+    if (threadIdx.x == 0) {
+        const unsigned long long t = atomicAdd(&st->cu_tick[kern], 1ull);
+        const unsigned gen = (unsigned)(t / gridDim.x);
+        const int j = blockIdx.x & 7;
+        const unsigned hw = __builtin_amdgcn_s_getreg((7 << 11) | (8 << 6) | 4);   // HW_ID[15:8]: CU, SH, SE
+        const int q0 = (int)(hw % kCuQueues);
+        int tile = -1;
+        for (int r = 0; r < kCuQueues && tile < 0; ++r) {
+            const int q = (q0 + r) % kCuQueues;
+            const int a = lo + (int)(((long long)len * q) / kCuQueues);
+            const int b = lo + (int)(((long long)len * (q + 1)) / kCuQueues);
+            if (b <= a) continue;
+            unsigned long long* Q = &st->cu_q[kern][j][q];
+            unsigned long long v = __hip_atomic_load(Q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            while ((unsigned)(v >> 32) != gen) {
+                const unsigned long long w = atomicCAS(Q, v, (unsigned long long)gen << 32);
+                v = w == v ? (unsigned long long)gen << 32 : w;
+            }
+            if ((int)(unsigned)v >= b - a) continue;   // exhausted (no increment past it)
+            const unsigned long long old = atomicAdd(Q, 1ull);
+            const int k = (int)(unsigned)old;
+            if ((unsigned)(old >> 32) == gen && k < b - a) tile = a + k;
+        }
+        s_tile = tile;
+    }
+    __syncthreads();
+    return s_tile;
+}
+#endif
 
 // The search's contribution to the work histogram: its wave's longest list (all lanes converged;
 // one atomic per wave, spread over the 4096 runs).
@@ -1997,8 +2046,19 @@ __global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_W
     if (tb < 0) return;
 #else
     (void)ck;
+#if MPH_CU_AFFINE
+    int tb;
+    if (bal && st) {   // the equal XCD ranges of xcd_block, CU-affine inside them
+        const int nb = list_blocks(n), xq = nb >> 3, xr = nb & 7, j = blockIdx.x & 7;
+        tb = cu_affine_tile(st, 0, j < xr ? j * (xq + 1) : xr * (xq + 1) + (j - xr) * xq, j < xr ? xq + 1 : xq);
+    } else {
+        tb = (int)blockIdx.x < list_blocks(n) ? xcd_block(blockIdx.x, list_blocks(n)) : -1;
+    }
+    if (tb < 0) return;
+#else
     if ((int)blockIdx.x >= list_blocks(n)) return;
     const int tb = xcd_block(blockIdx.x, list_blocks(n));
+#endif
 #endif
     XCD_PROBE(st, 0);
     __shared__ __attribute__((aligned(16))) double stage[kWB][stage_words(MPH_LDS_CAP, MPH_SB)];
@@ -2273,7 +2333,7 @@ __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, cons
     const int lb = ck ? chunk_block(blockIdx.x, list_blocks(n), ck) : list_block(st, n);
 #else
     (void)ck;
-    const int lb = list_block(st, n);
+    const int lb = list_block(st, n, 1);
 #endif
     if (lb < 0) return;
     XCD_PROBE(st, 1);
@@ -2471,7 +2531,7 @@ __global__ __launch_bounds__(MPH_LB) MPH_PB_ATTR void k_pass_b(DevParams P, cons
                                                 const DevState* __restrict__ st)
 {
     const int n = dev_n(P);
-    const int lb = list_block(st, n);
+    const int lb = list_block(st, n, 2);
     if (lb < 0) return;
     XCD_PROBE(st, 2);
     __shared__ double s_ratio[kTypes * kTypes];

@@ -226,6 +226,12 @@ inline void set_uniforms(DevParams& P)
 // work histogram of the XCD map: waves in 4096 equal runs (D16M: ~60 waves per run, so the
 // search's per-wave atomics spread over ~100 addresses at a time; 512 runs cost its search 7 %)
 constexpr int kXcdSegs = 4096;
+// MPH_CU_AFFINE=1: each CU takes the list kernels' tiles from a contiguous range of its own, so
+// the blocks resident on a CU are neighbours in the cell order and share L1 lines
+#ifndef MPH_CU_AFFINE
+#define MPH_CU_AFFINE 0
+#endif
+constexpr int kCuQueues = 32;
 constexpr int kXcdSplitThreads = 1024;   // k_xcd_split: 4 runs per thread
 
 // Mutable per-step device scalars (so a captured hipGraph can replay many steps).
@@ -251,6 +257,14 @@ struct DevState {
     int seg_work[kXcdSegs];
     int xcd_frac[9];
     int xcd_pad[3];
+#if MPH_CU_AFFINE
+    // CU-affine tiles of the list kernels (mph_kernels.hip, cu_affine_tile): per kernel a block
+    // ticket counter (its generation: ticket / blocks of the launch) and per logical XCD and queue
+    // the claimed count of the queue's tiles, tagged with the generation in the high 32 bits
+    unsigned long long cu_tick[3];
+    unsigned long long cu_pad;
+    unsigned long long cu_q[3][8][kCuQueues];
+#endif
 #if MPH_DIAG_XCD
     // diagnostic build only (tools/xcd_diag.py): per list kernel (search, pass A, pass B) and XCD,
     // the first wave's start, the last wave's end (wall_clock64), the summed wave time, the waves
