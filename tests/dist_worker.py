@@ -75,6 +75,9 @@ def gpu_worker(rank, world, port, case, checkpoints, fields, out_path, local=Fal
         for k in checkpoints:
             s.step(k - done)
             done = k
+            if os.environ.get("MPH_TEST_PROFILE_GRAPHS") == "1" and k == checkpoints[0]:
+                res["graph_ms"] = np.array([v if v is not None else -1.0
+                                            for v in s.profile_graphs(4).values()])   # no exchange
             for f in fields:
                 res["s%d/%s" % (k, f)] = gather_field(s, f)
             res["s%d/owner" % k] = owner_map()

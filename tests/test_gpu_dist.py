@@ -212,6 +212,20 @@ def test_slab_overlap_probe(tmp_path, monkeypatch):
                 assert np.array_equal(forced[k], slow[k]) and np.array_equal(forced[k], fast[k]), (mode, k)
 
 
+def test_slab_profile_graphs_leave_state_unchanged(tmp_path, monkeypatch):
+    """mph_profile_graphs on slab ranks (tools/slab_serial.py times the list kernels that way):
+    each rank replays its search, pass A and pass B on its own state, no exchange; the run then
+    continues bit for bit as without it (pass B in one launch: MPH_SLAB_OVERLAP=0)."""
+    monkeypatch.setenv("MPH_SLAB_OVERLAP", "0")
+    plain = run_slab("channel3d", 2, [1, 9], str(tmp_path / "plain.npz"))
+    monkeypatch.setenv("MPH_TEST_PROFILE_GRAPHS", "1")
+    prof = run_slab("channel3d", 2, [1, 9], str(tmp_path / "prof.npz"))
+    assert (prof["graph_ms"] > 0).all(), prof["graph_ms"]
+    for k in plain.files:
+        if k != "overlap":
+            assert np.array_equal(plain[k], prof[k]), k
+
+
 def _run_capacity(tmp_path, tag, case, world, batches):
     ctx = mp.get_context("spawn")
     port = _free_port()
