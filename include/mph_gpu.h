@@ -290,8 +290,8 @@ int mph_profile_steps(MphCtx* ctx, int nsteps, double* avg_ms, int* launches, ch
  * longer): the search (with the XCD split), pass A and pass B, each captured `reps` (1..64) times
  * into a graph of its own and replayed between two HIP events on the context's stream; avg_ms3 =
  * milliseconds per launch (-1: not measured -- pass B with elastic slots).  Each replay recomputes
- * the last step's results bit for bit, so the state is unchanged.  Single contexts after at
- * least one step (else MPH_ERR_UNSUPPORTED / MPH_ERR_ARG).                                      */
+ * the last step's results bit for bit, so the state is unchanged (slab contexts: on the rank's
+ * own set, no exchange, pass B as one launch).  After at least one step (else MPH_ERR_ARG).     */
 int mph_profile_graphs(MphCtx* ctx, int reps, double* avg_ms3);
 /* Phase timing: the reference's clock() buckets of its step loop (main.cpp:695-700) from HIP
  * events.  With on != 0 mph_step launches the kernels of its step batches directly instead of
