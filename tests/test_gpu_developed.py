@@ -3,7 +3,8 @@
 The full-size tests of test_gpu_fullsize.py stop at 52 steps, where D1M's fluid has moved ~0.01 dx
 and every neighbour set is still the initial lattice's.  The reference's own Dam run is 10,001
 steps (main.cpp:581; results/Dam/dam.data EndTime 1.0 at Dt 1e-4).  Here the GPU runs D1M
-(BASELINE configs[1], 1,397,200 particles) to t = 0.25 s (2,500 steps): the column has collapsed
+(BASELINE configs[1], 1,397,200 particles) to t = 0.25 s (2,500 steps) and to t = 1.0 s (10,000
+steps, the end of the reference's run): the column has collapsed
 along the floor, particles are off the lattice and the neighbour sets have changed.  That exact
 state (Position, Velocity, Time -- everything the step carries; walls are static in this case) is
 handed to the CPU oracle, bit-identical to the reference, as the reference's own restart from a
@@ -30,14 +31,15 @@ DEVELOPED_STEPS = 2500           # t = 0.25 s at Dt = 1e-4
 SAMPLE_ROWS = [(0, 4000), (485000, 4000), (966000, 4000), (1200000, 4000)]   # fluid (3) and wall
 
 
-def test_d1m_developed_matches_oracle():
+@pytest.mark.parametrize("steps", [DEVELOPED_STEPS, 10000])   # t = 0.25 s, and t = 1.0 s: the reference's whole Dam run
+def test_d1m_developed_matches_oracle(steps):
     from oracle_bindings import OracleSolver
     OracleSolver.set_threads(min(16, os.cpu_count() or 1))
     cfg, parts = cases.get("d1m").build()
     fluid = parts.property < 2
     with MphSolver(cfg, parts) as s:
         nc0 = s.get("NeighborCount")
-        s.step(DEVELOPED_STEPS)
+        s.step(steps)
         pos, vel = s.get("Position"), s.get("Velocity")
         nc_dev = s.get("NeighborCount")
         changed = float((nc_dev != nc0).mean())
