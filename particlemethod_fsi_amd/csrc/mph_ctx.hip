@@ -303,10 +303,14 @@ int download_struct_m33(MphCtx* c, const double* d, double* out)
     const int ns = c->Sd.n_own;   // slots computed here (slab mode: owned)
     std::memset(out, 0, sizeof(double) * 9 * (size_t)c->n_glob);
     if (ns == 0) return MPH_OK;
-    std::vector<double> h((size_t)ns * 9);
-    HIP_OK(c, hipMemcpyAsync(h.data(), d, sizeof(double) * 9 * ns, hipMemcpyDeviceToHost, c->stream));
+    const size_t fes = (size_t)c->Sd.fes;   // nine element planes (StructDev)
+    std::vector<double> h(fes * 9);
+    HIP_OK(c, hipMemcpyAsync(h.data(), d, sizeof(double) * 9 * fes, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipStreamSynchronize(c->stream));
-    for (int s = 0; s < ns; ++s) std::memcpy(out + (size_t)9 * c->sl_orig[s], &h[(size_t)9 * s], sizeof(double) * 9);
+    for (int s = 0; s < ns; ++s) {
+        double* o = out + (size_t)9 * c->sl_orig[s];
+        for (int e = 0; e < 9; ++e) o[e] = h[e * fes + s];
+    }
     return MPH_OK;
 }
 
@@ -573,6 +577,7 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         CK(dalloc(c, &D.clamp, nl)); CK(dalloc(c, &D.x0, nl)); CK(dalloc(c, &D.x, nl)); CK(dalloc(c, &D.v, nl));
         CK(dalloc(c, &D.u, nl)); CK(dalloc(c, &D.P, (size_t)nl * (sd == 2 ? 1 : 3))); CK(dalloc(c, &D.F, (size_t)nl * 9));
         CK(dalloc(c, &D.E, (size_t)nl * 9)); CK(dalloc(c, &D.S, (size_t)nl * 9));
+        D.fes = nl;
         std::vector<double2> lame(nl);
         std::vector<double> irho(nl);
         std::vector<int> clamp(nl);
@@ -831,9 +836,14 @@ int mph_step(MphCtx* c, int nsteps)
     }
     for (int k = 0; k < nsteps; ++k) c->time += c->cfg.dt;
     c->stepped = true;
-    DevState hs;
-    HIP_OK(c, hipMemcpyAsync(&hs, c->dst, kStateHead, hipMemcpyDeviceToHost, c->stream));
+    // the error flags, copied into pinned memory behind the steps (a pageable copy is staged by the
+    // runtime).  Polling the stream instead of the blocking wait measured the same per call
+    // (profiles/r05/sync_path/).
+    if (!c->hs_pin) HIP_OK(c, hipHostMalloc(&c->hs_pin, kStateHead, hipHostMallocDefault));
+    HIP_OK(c, hipMemcpyAsync(c->hs_pin, c->dst, kStateHead, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipStreamSynchronize(c->stream));
+    DevState hs;
+    std::memcpy(&hs, c->hs_pin, kStateHead);
     CK(ctx_state_status(c, hs));
     return MPH_OK;
 }
@@ -1354,6 +1364,21 @@ int mph_neighbor_rows(MphCtx* c, int first, int count, int* counts, int* ids, lo
     }
     return (int)std::min<long long>(w, 0x7fffffff);
 }
+
+#if MPH_DIAG_PATHS
+// Diagnostic builds only (not in include/mph_gpu.h): copies DevState.path_diag (16 words, see
+// scan_candidates_lds) to out after draining the device; reset != 0 then zeroes it.
+__attribute__((visibility("default"))) int mph_diag_paths(MphCtx* c, unsigned long long* out, int reset)
+{
+    if (!c) return MPH_ERR_ARG;
+    HIP_OK(c, hipSetDevice(c->device));
+    HIP_OK(c, hipDeviceSynchronize());
+    char* dev = reinterpret_cast<char*>(c->dst) + offsetof(DevState, path_diag);
+    if (out) HIP_OK(c, hipMemcpy(out, dev, sizeof(DevState::path_diag), hipMemcpyDeviceToHost));
+    if (reset) HIP_OK(c, hipMemset(dev, 0, sizeof(DevState::path_diag)));
+    return MPH_OK;
+}
+#endif
 
 #if MPH_DIAG_XCD
 // Diagnostic builds only (not in include/mph_gpu.h): copies DevState.xcd_diag (3 x 4 x 8 words,

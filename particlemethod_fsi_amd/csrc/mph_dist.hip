@@ -1048,9 +1048,10 @@ int pack_owned(MphCtx* c, std::vector<char>& buf)
     MPH_CK(fetch(c, (const double4*)c->acc, a, n));
     const int ns = c->Sd.n_own;
     std::vector<double> S, E;
+    const size_t fes = (size_t)c->Sd.fes;   // nine element planes (StructDev)
     if (ns) {
-        MPH_CK(fetch(c, (const double*)c->Sd.S, S, 9 * (size_t)ns));
-        MPH_CK(fetch(c, (const double*)c->Sd.E, E, 9 * (size_t)ns));
+        MPH_CK(fetch(c, (const double*)c->Sd.S, S, 9 * fes));
+        MPH_CK(fetch(c, (const double*)c->Sd.E, E, 9 * fes));
     }
     MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
     std::vector<OutRec> rec;
@@ -1080,8 +1081,10 @@ int pack_owned(MphCtx* c, std::vector<char>& buf)
     for (int s = 0; s < ns; ++s) {
         sl[s].id = c->sl_orig[s];
         sl[s].isnc = c->S.count[c->sl_s[s]];
-        std::memcpy(sl[s].S, &S[9 * (size_t)s], sizeof(sl[s].S));
-        std::memcpy(sl[s].E, &E[9 * (size_t)s], sizeof(sl[s].E));
+        for (int e = 0; e < 9; ++e) {
+            sl[s].S[e] = S[e * fes + s];
+            sl[s].E[e] = E[e * fes + s];
+        }
     }
     const long long cnt[2] = {(long long)rec.size(), (long long)sl.size()};
     buf.resize(sizeof(cnt) + sizeof(OutRec) * rec.size() + sizeof(OutSlot) * sl.size());

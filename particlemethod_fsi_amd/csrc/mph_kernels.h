@@ -33,9 +33,11 @@ struct StructDev {
     double4* v = nullptr;
     double4* u = nullptr;         // displacement Mod(x - x0) (main.cpp:2700-2712), per substep
     double4* P = nullptr;         // first Piola-Kirchhoff F S L: 2-D one double4 {P00,P01,P10,P11}, 3-D 3 rows
-    double* F = nullptr;          // DeformGradient [ns][9]
-    double* E = nullptr;          // Strain
-    double* S = nullptr;          // Stress
+    // DeformGradient, Strain, Stress: nine planes each, element 3a + b of slot s at [(3a + b) fes + s]
+    double* F = nullptr;
+    double* E = nullptr;
+    double* S = nullptr;
+    int fes = 0;                  // their plane stride (slots allocated)
 };
 
 // Per-kernel HIP event timing (mph_profile_steps); nullptr in normal runs.  `events` hands out a

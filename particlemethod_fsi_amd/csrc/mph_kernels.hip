@@ -1709,6 +1709,22 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                 }
             }
         }
+#if MPH_DIAG_PATHS
+        {
+            const int path = MPH_SEARCH_F32 && !C16 && (span <= kCap32 || two) ? (two ? 1 : 0) : span <= CAP ? 2 : 3;
+            int cand = any ? je - jb : 0;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) cand += __shfl_xor(cand, o, 64);
+            if (lane == 0) {
+                atomicAdd(&dst->path_diag[path], 1ull);
+                atomicAdd(&dst->path_diag[4 + path], (unsigned long long)cand);
+                atomicAdd(&dst->path_diag[8 + path], (unsigned long long)(two ? n1 + n2 : span));
+                if (span > kCap32) atomicAdd(&dst->path_diag[two ? 14 : (n2 > 0 ? 13 : 12)], 1ull);
+                if (col == 0) atomicAdd(&dst->path_diag[15], 1ull);
+                if (span > 64) atomicAdd(&dst->path_diag[span > 256 ? 39 : span > 192 ? 38 : span > 160 ? 37 : span > 128 ? 36 : span > 96 ? 35 : 34], 1ull);
+            }
+        }
+#endif
         if (MPH_SEARCH_F32 && !C16 && (span <= kCap32 || two)) {
             // FP32 records: candidate j at record j - lbase, 64 records (1 KB) per instruction
             float4* s4 = reinterpret_cast<float4*>(sx);
@@ -1901,13 +1917,58 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             __builtin_amdgcn_s_waitcnt(0x0F70);   // column col + 1's start[] loads (wide windows are rare)
         }
     };
+#if MPH_DIAG_PATHS
+    // diagnostic: the LDS row ring a wave would keep for its list (DevState.path_diag[16..33])
+    int sim_fl[2][4] = {};
+    int sim_prev = 0;
+    auto wsum = [](int v) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        return v;
+    };
+    auto ring_sim = [&]() {
+        const int c = (soff >> 8) & 0x1FF;
+        const int minc = wave_min(act ? c : 0x7fffffff), maxc = wave_max(act ? c : 0);
+        if (minc == 0x7fffffff) return;
+#pragma unroll
+        for (int rule = 0; rule < 2; ++rule)
+#pragma unroll
+            for (int ri = 0; ri < 4; ++ri) {
+                const int R = 4 << ri, fl = sim_fl[rule][ri];
+                const int ahead = wsum(max(0, c - max(sim_prev, fl + R)));
+                const int lag = wsum(max(0, min(c, fl) - sim_prev));
+                if (lane == 0) {
+                    atomicAdd(&dst->path_diag[16 + (rule * 4 + ri) * 2], (unsigned long long)ahead);
+                    atomicAdd(&dst->path_diag[17 + (rule * 4 + ri) * 2], (unsigned long long)lag);
+                }
+                const int nf = max(fl, rule == 0 ? minc : max(minc, maxc - R / 2));
+                if (lane == 0 && rule == 1 && ri == 2) atomicAdd(&dst->path_diag[33], (unsigned long long)(nf - fl));
+                sim_fl[rule][ri] = nf;
+            }
+        sim_prev = c;
+    };
+#endif
     int ra_b, ra_e, rb_b = 0, rb_e = 0;   // the two register pairs of the column ranges
     col_range(0, ra_b, ra_e);
     __builtin_amdgcn_s_waitcnt(0x0F70);
     for (int col = 0; col < NCOL; col += 2) {
         column(col, ra_b, ra_e, rb_b, rb_e);
-        if (col + 1 < NCOL) column(col + 1, rb_b, rb_e, ra_b, ra_e);
+#if MPH_DIAG_PATHS
+        ring_sim();
+#endif
+        if (col + 1 < NCOL) {
+            column(col + 1, rb_b, rb_e, ra_b, ra_e);
+#if MPH_DIAG_PATHS
+            ring_sim();
+#endif
+        }
     }
+#if MPH_DIAG_PATHS
+    if (!C16) {
+        const int tot = wsum(act ? (soff >> 8) & 0x1FF : 0);
+        if (lane == 0) atomicAdd(&dst->path_diag[32], (unsigned long long)tot);
+    }
+#endif
     if (!C16) {
         cnt = soff >> 17;                 // every neighbour (NeighborCount)
         *stored = (soff >> 8) & 0x1FF;    // the list's length (r^2 <= P.rlf)
@@ -2770,7 +2831,7 @@ __global__ __launch_bounds__(256) void k_struct_stress(DevParams P, int s0, int 
                                                        const double2* __restrict__ lame,
                                                        double4* __restrict__ sP, double* __restrict__ sF,
                                                        double* __restrict__ sE, double* __restrict__ sS,
-                                                       int store)
+                                                       int fes, int store)
 {
     const int s = s0 + (int)((blockIdx.x * blockDim.x + threadIdx.x) / G);   // slots [s0, ns)
     const int g = (int)threadIdx.x & (G - 1);
@@ -2865,17 +2926,16 @@ __global__ __launch_bounds__(256) void k_struct_stress(DevParams P, int s0, int 
         for (int a = 0; a < DIM; ++a) sP[(size_t)s * 3 + a] = make_double4(PK[a][0], PK[a][1], PK[a][DIM - 1], 0.0);
     }
     if (!store) return;   // F, E, S are outputs only: the last substep of a batch's last step
-    double* oF = sF + (size_t)s * 9;
-    double* oE = sE + (size_t)s * 9;
-    double* oS = sS + (size_t)s * 9;
+    // element planes (StructDev): consecutive slots of the wave store one run per element; in 2-D
+    // the third row and column stay the zeros set at creation
 #pragma unroll
-    for (int a = 0; a < 3; ++a)
+    for (int a = 0; a < DIM; ++a)
 #pragma unroll
-        for (int b = 0; b < 3; ++b) {
-            const bool in = a < DIM && b < DIM;
-            oF[3 * a + b] = in ? F[a < DIM ? a : 0][b < DIM ? b : 0] : 0.0;
-            oE[3 * a + b] = in ? E[a < DIM ? a : 0][b < DIM ? b : 0] : 0.0;
-            oS[3 * a + b] = in ? S[a < DIM ? a : 0][b < DIM ? b : 0] : 0.0;
+        for (int b = 0; b < DIM; ++b) {
+            const size_t o = (size_t)(3 * a + b) * fes + s;
+            sF[o] = F[a][b];
+            sE[o] = E[a][b];
+            sS[o] = S[a][b];
         }
 }
 
@@ -3823,7 +3883,7 @@ void launch_struct_stress(const Launch& L, bool store, int s0, int s1)
     store = true;   // A/B timing of the output stores
 #endif
     MPH_STRUCT_DISPATCH(k_struct_stress, "struct_stress", P, s0, s1, S.wo, S.ocnt, S.eo_nb, S.x0, S.u, S.L,
-                        S.lame, S.P, S.F, S.E, S.S, store ? 1 : 0);
+                        S.lame, S.P, S.F, S.E, S.S, S.fes, store ? 1 : 0);
 }
 
 void launch_struct_velocity(const Launch& L, bool last, int s0, int s1)

@@ -11,6 +11,9 @@
 #ifndef MPH_DIAG_XCD
 #define MPH_DIAG_XCD 0   // 1: per-XCD wave timing of the list kernels (diagnostic builds only)
 #endif
+#ifndef MPH_DIAG_PATHS
+#define MPH_DIAG_PATHS 0   // 1: the search's column paths counted (diagnostic builds only, mph_diag_paths)
+#endif
 
 namespace mph {
 
@@ -264,6 +267,18 @@ struct DevState {
     unsigned long long cu_tick[3];
     unsigned long long cu_pad;
     unsigned long long cu_q[3][8][kCuQueues];
+#endif
+#if MPH_DIAG_PATHS
+    // diagnostic build only (tools/search_paths.py): per search path of a wave's stencil column
+    // (0 one FP32 window, 1 two FP32 runs, 2 FP64 staged, 3 per-lane global loads) the columns, the
+    // lanes' candidates (sum of je - jb) and the window's records (span, or n1 + n2); [12..15]
+    // the split's outcome when the window was too wide (no gap, runs too wide, ok) and the waves;
+    // [16..31] a simulated LDS row ring of R = 4, 8, 16, 32 rows (flushed at column ends: rule 0
+    // the rows every lane has passed, rule 1 also partial rows to keep R / 2 rows of headroom): the
+    // stored entries it could not take, {ahead of the ring, behind it} per (rule, R); [32] the
+    // stored entries; [33] the rows flushed by rule 1 with R = 16; [34..39] the columns whose window
+    // spans (64, 96], (96, 128], (128, 160], (160, 192], (192, 256], > 256 records
+    unsigned long long path_diag[40];
 #endif
 #if MPH_DIAG_XCD
     // diagnostic build only (tools/xcd_diag.py): per list kernel (search, pass A, pass B) and XCD,
