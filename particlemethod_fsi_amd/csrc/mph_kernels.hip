@@ -1920,7 +1920,8 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
 #if MPH_DIAG_PATHS
     // diagnostic: the LDS row ring a wave would keep for its list (DevState.path_diag[16..33])
     int sim_fl[2][4] = {};
-    int sim_prev = 0;
+    int sim_prev = 0, sim_col = 0, sim_g0 = 0;
+    unsigned long long rows_col = 0, rows_grp = 0;
     auto wsum = [](int v) {
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -1928,8 +1929,14 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     };
     auto ring_sim = [&]() {
         const int c = (soff >> 8) & 0x1FF;
+        rows_col += wave_max(act ? c - sim_prev : 0);
+        if (sim_col % kGroups == kGroups - 1) {
+            rows_grp += wave_max(act ? c - sim_g0 : 0);
+            sim_g0 = c;
+        }
+        ++sim_col;
         const int minc = wave_min(act ? c : 0x7fffffff), maxc = wave_max(act ? c : 0);
-        if (minc == 0x7fffffff) return;
+        if (minc == 0x7fffffff) { sim_prev = c; return; }
 #pragma unroll
         for (int rule = 0; rule < 2; ++rule)
 #pragma unroll
@@ -1966,7 +1973,13 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
 #if MPH_DIAG_PATHS
     if (!C16) {
         const int tot = wsum(act ? (soff >> 8) & 0x1FF : 0);
-        if (lane == 0) atomicAdd(&dst->path_diag[32], (unsigned long long)tot);
+        const int longest = wave_max(act ? (soff >> 8) & 0x1FF : 0);
+        if (lane == 0) {
+            atomicAdd(&dst->path_diag[32], (unsigned long long)tot);
+            atomicAdd(&dst->path_diag[40], rows_col);
+            atomicAdd(&dst->path_diag[41], rows_grp);
+            atomicAdd(&dst->path_diag[42], (unsigned long long)longest);
+        }
     }
 #endif
     if (!C16) {

@@ -277,8 +277,9 @@ struct DevState {
     // the rows every lane has passed, rule 1 also partial rows to keep R / 2 rows of headroom): the
     // stored entries it could not take, {ahead of the ring, behind it} per (rule, R); [32] the
     // stored entries; [33] the rows flushed by rule 1 with R = 16; [34..39] the columns whose window
-    // spans (64, 96], (96, 128], (128, 160], (160, 192], (192, 256], > 256 records
-    unsigned long long path_diag[40];
+    // spans (64, 96], (96, 128], (128, 160], (160, 192], (192, 256], > 256 records; [40..42] the rows
+    // of column-aligned lists (per column, per group of kGroups columns) and of today's (the longest)
+    unsigned long long path_diag[48];
 #endif
 #if MPH_DIAG_XCD
     // diagnostic build only (tools/xcd_diag.py): per list kernel (search, pass A, pass B) and XCD,

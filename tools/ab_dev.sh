@@ -1,12 +1,12 @@
 #!/bin/bash
 # Same-box A/B of library builds (particlemethod_fsi_amd/lib_<name>; "base" = lib/) at rest (D1M),
-# in the developed flow (D1M from t = 0.25 s, tools/dev_state.py) and, with D16M=1, on D16M;
+# in the developed flow (D1M from t = 0.25 s, or DEV_STEPS steps; tools/dev_state.py) and, with D16M=1, on D16M;
 # ROUNDS alternating rounds.  Output: $OUT/{rest,dev,d16m}_<name>_<round>.json (tools/ab_dev_summary.py)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=${OUT:-gpurun_out/abdev}
 mkdir -p $OUT
-timeout -k 10 120 python3 tools/dev_state.py d1m 2500 $OUT/d1m_dev.gridb > $OUT/dev_state.log 2>&1 || exit 21
+timeout -k 10 120 python3 tools/dev_state.py d1m ${DEV_STEPS:-2500} $OUT/d1m_dev.gridb > $OUT/dev_state.log 2>&1 || exit 21
 for r in $(seq 1 ${ROUNDS:-2}); do
   for v in base ${VARIANTS}; do
     lib=$PWD/particlemethod_fsi_amd/lib/libmph_gpu.so

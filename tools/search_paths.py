@@ -26,7 +26,7 @@ def read(s, reset=True):
     fn = s._L.mph_diag_paths
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-    buf = (ctypes.c_ulonglong * 40)()
+    buf = (ctypes.c_ulonglong * 48)()
     rc = fn(s._h, buf, 1 if reset else 0)
     if rc != 0:
         raise RuntimeError("mph_diag_paths: %d" % rc)
@@ -72,6 +72,10 @@ def main():
                                                           "behind": w[17 + (r * 4 + ri) * 2] / tot}
                            for r in range(2) for ri in range(4)}
             out["ring_rows_flushed_r1_R16"] = w[33]
+            out["rows"] = {"aligned_per_column": w[40], "aligned_per_group": w[41], "today": w[42],
+                           "lane_fill_today": w[32] / max(64 * w[42], 1),
+                           "lane_fill_per_column": w[32] / max(64 * w[40], 1),
+                           "lane_fill_per_group": w[32] / max(64 * w[41], 1)}
             out["span_hist"] = dict(zip(("64-96", "96-128", "128-160", "160-192", "192-256", ">256"),
                                         [x / max(cols, 1) for x in w[34:40]]))
             print(json.dumps(out), flush=True)
