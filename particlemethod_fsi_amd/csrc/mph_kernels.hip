@@ -795,11 +795,69 @@ constexpr int kScanBlock = kScanThreads * kScanItems;   // 4096 cells per block 
 __host__ __device__ inline int bsum_stride(int ncell) { return ncell / kScanBlock + 2; }
 static_assert(kScanBlock == 4096, "mph_ctx.hip sizes the bsum buffers for 4096-cell blocks");
 
+// The XCD split of the list passes (see list_block) from the search's work histogram: an inclusive
+// scan of the runs' work (kXcdSegs / blockDim.x consecutive runs per thread), the 7 inner cut
+// points at equal shares of the total (interpolated inside their run), then the histogram cleared.
+// One whole block calls it (k_xcd_split, or block 0 of k_prep with MPH_SPLIT_IN_PREP).
+template <int T>
+__device__ __forceinline__ void xcd_split_block(DevState* st)
+{
+    constexpr int R = kXcdSegs / T;
+    static_assert(kXcdSegs % T == 0, "whole runs per thread");
+    __shared__ long long s[T];
+    const int t = threadIdx.x;
+    long long sum = 0;
+    for (int r = 0; r < R; ++r) sum += max(st->seg_work[t * R + r], 0);
+    s[t] = sum;
+    __syncthreads();
+    for (int o = 1; o < T; o <<= 1) {
+        const long long v = t >= o ? s[t - o] : 0;
+        __syncthreads();
+        s[t] += v;
+        __syncthreads();
+    }
+    const long long tot = s[T - 1];
+    int* fr = st->xcd_frac;
+    if (tot < 8) {
+        if (t < 9) fr[t] = 8192 * t;
+    } else {
+        for (int x = 1; x < 8; ++x) {
+            const long long tgt = tot * x / 8;
+            long long prev = t ? s[t - 1] : 0;
+            if (!(prev < tgt && s[t] >= tgt)) continue;
+            for (int r = 0; r < R; ++r) {
+                const int w = max(st->seg_work[t * R + r], 0);
+                if (w > 0 && prev < tgt && prev + w >= tgt) {
+                    const double f = (t * R + r + (double)(tgt - prev) / (double)w) / kXcdSegs;
+                    fr[x] = min(65536, max(0, (int)(f * 65536.0 + 0.5)));
+                }
+                prev += w;
+            }
+        }
+        if (t == 0) {
+            fr[0] = 0;
+            fr[8] = 65536;
+        }
+    }
+    __syncthreads();   // every thread has read its runs
+    for (int r = 0; r < R; ++r) st->seg_work[t * R + r] = 0;
+}
+
+// MPH_SPLIT_IN_PREP: the split runs in block 0 of one of the next step's sort kernels (1: k_prep,
+// 2: k_rank_scatter, the longest, where it hides best), from the previous step's search (a wave's
+// work changes little from one step to the next, and the map only decides which block handles
+// which wave), so no launch of its own sits between the search and pass A; 0: k_xcd_split after
+// the search
+#ifndef MPH_SPLIT_IN_PREP
+#define MPH_SPLIT_IN_PREP 2
+#endif
+
 __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __restrict__ st, Soa C,
                                               int* __restrict__ key, int* __restrict__ slot,
                                               int* __restrict__ cnt, int mode, VSrc vs,
-                                              int* __restrict__ bsum2)
+                                              int* __restrict__ bsum2, int split)
 {
+    if (MPH_SPLIT_IN_PREP == 1 && split && blockIdx.x == 0) xcd_split_block<256>(const_cast<DevState*>(st));
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     const int n = dev_n(P);
     Soa B = C;
@@ -1059,8 +1117,9 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
                                                       const int* __restrict__ start,
                                                       const int* __restrict__ tmp, Soa C, Soa A,
                                                       int* __restrict__ rank_of, int* __restrict__ dst_of,
-                                                      int mode, VSrc vs)
+                                                      int mode, VSrc vs, DevState* __restrict__ st, int split)
 {
+    if (MPH_SPLIT_IN_PREP == 2 && split && blockIdx.x == 0) xcd_split_block<256>(st);
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= dev_n(P)) return;
     const int k = key[p];
@@ -2148,46 +2207,7 @@ __global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_W
 // equal shares of the total (interpolated inside their run), then the histogram cleared.
 __global__ __launch_bounds__(kXcdSplitThreads) void k_xcd_split(DevState* __restrict__ st)
 {
-    constexpr int R = kXcdSegs / kXcdSplitThreads;
-    __shared__ long long s[kXcdSplitThreads];
-    const int t = threadIdx.x;
-    int w[R];
-    long long sum = 0;
-    for (int r = 0; r < R; ++r) {
-        w[r] = max(st->seg_work[t * R + r], 0);
-        st->seg_work[t * R + r] = 0;
-        sum += w[r];
-    }
-    s[t] = sum;
-    __syncthreads();
-    for (int o = 1; o < kXcdSplitThreads; o <<= 1) {
-        const long long v = t >= o ? s[t - o] : 0;
-        __syncthreads();
-        s[t] += v;
-        __syncthreads();
-    }
-    const long long tot = s[kXcdSplitThreads - 1];
-    int* fr = st->xcd_frac;
-    if (tot < 8) {
-        if (t < 9) fr[t] = 8192 * t;
-        return;
-    }
-    for (int x = 1; x < 8; ++x) {
-        const long long tgt = tot * x / 8;
-        long long prev = t ? s[t - 1] : 0;
-        if (!(prev < tgt && s[t] >= tgt)) continue;
-        for (int r = 0; r < R; ++r) {
-            if (w[r] > 0 && prev < tgt && prev + w[r] >= tgt) {
-                const double f = (t * R + r + (double)(tgt - prev) / (double)w[r]) / kXcdSegs;
-                fr[x] = min(65536, max(0, (int)(f * 65536.0 + 0.5)));
-            }
-            prev += w[r];
-        }
-    }
-    if (t == 0) {
-        fr[0] = 0;
-        fr[8] = 65536;
-    }
+    xcd_split_block<kXcdSplitThreads>(st);
 }
 
 // The second launch, over the waves whose compact list did not fit (scan_candidates_lds marks
@@ -3661,10 +3681,11 @@ void launch_sort(const Launch& L, int mode)
     const int nb = blocks(P.ncell, kScanBlock);
     const int top = nb <= kScanFusedTop;
     const int bs = bsum_stride(P.ncell);
+    const int split = MPH_SPLIT_IN_PREP && MPH_XCD_BAL && n >= L.xcd_bal_min;   // the passes' XCD split (above)
     if (MPH_PREP_BSUM) {
         // block totals from k_prep into this step's parity buffer of L.bsum (no k_scan_reduce)
         MPH_LAUNCH("prep", L.stream, k_prep, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.B,
-                   L.key, L.slot, L.cnt, mode, L.vsrc, L.bsum);
+                   L.key, L.slot, L.cnt, mode, L.vsrc, L.bsum, split);
         if (!top)
             MPH_LAUNCH("scan_top", L.stream, k_scan_top, dim3(1), dim3(1024), 0, L.stream, L.bsum, nb,
                        (const DevState*)L.st, bs);
@@ -3673,7 +3694,7 @@ void launch_sort(const Launch& L, int mode)
     } else {
         int* bsum = L.bsum + 2 * bs;   // the scratch third of L.bsum
         MPH_LAUNCH("prep", L.stream, k_prep, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.B,
-                   L.key, L.slot, L.cnt, mode, L.vsrc, (int*)nullptr);
+                   L.key, L.slot, L.cnt, mode, L.vsrc, (int*)nullptr, split);
         MPH_LAUNCH("scan_reduce", L.stream, k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt,
                    P.ncell, bsum);
         if (!top)
@@ -3685,7 +3706,7 @@ void launch_sort(const Launch& L, int mode)
     MPH_LAUNCH("place", L.stream, k_place, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.key,
                L.slot, L.start, L.tmp, mode);
     MPH_LAUNCH("rank_scatter", L.stream, k_rank_scatter, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P,
-               L.key, L.start, L.tmp, L.B, L.A, L.rank_of, L.dst_of, mode, L.vsrc);
+               L.key, L.start, L.tmp, L.B, L.A, L.rank_of, L.dst_of, mode, L.vsrc, L.st, split);
 }
 
 static PassAOut pass_a_out(const Launch& L)
@@ -3720,7 +3741,7 @@ void launch_neighbors(const Launch& L, int ck)
             MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM, false>), dim3(nb_grid),                    \
                        dim3(MPH_LB), MPH_NB_SHM_PAD, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.nbcount, L.lhdr, L.st, L.wface, bal, \
                        L.whdr, ck);                                                                          \
-        if (bal && !ck)                                                                                      \
+        if (bal && !ck && !MPH_SPLIT_IN_PREP)                                                                \
             MPH_LAUNCH("xcd_split", L.stream, k_xcd_split, dim3(1), dim3(kXcdSplitThreads), 0, L.stream, L.st); \
         if (L.lhdr)                                                                                          \
             MPH_LAUNCH("neighbors_redo", L.stream, (k_neighbors_redo<D, PERM>), dim3(1),                     \
@@ -3787,7 +3808,7 @@ void launch_search_pass_a(const Launch& L)
         (void)hipStreamWaitEvent(L.stream2, L.ev_chunk[c], 0);
         launch_pass_a(La, ck);
     }
-    if (MPH_XCD_BAL && L.P->n >= L.xcd_bal_min)
+    if (MPH_XCD_BAL && L.P->n >= L.xcd_bal_min && !MPH_SPLIT_IN_PREP)
         MPH_LAUNCH("xcd_split", L.stream, k_xcd_split, dim3(1), dim3(kXcdSplitThreads), 0, L.stream, L.st);
     (void)hipEventRecord(L.ev_chunk[C], L.stream2);
     (void)hipStreamWaitEvent(L.stream, L.ev_chunk[C], 0);
