@@ -452,8 +452,9 @@ def test_gpu_compact_lists_bitwise_equal_ell(case, monkeypatch):
 
 @pytest.mark.parametrize("case", ["box3d", "box3d_st", "gate2d", "dam2d", "seam3d", "gate3d_sub"])
 def test_gpu_xcd_balanced_map_bitwise(case, monkeypatch):
-    """The work-balanced XCD block map of passes A and B (k_xcd_split + list_block), which by default
-    runs only from 2^20 particles, forced on small cases (MPH_XCD_BAL_MIN=0; their few blocks also
+    """The work-balanced XCD block map of passes A and B (xcd_split_block in the next step's
+    k_rank_scatter, then list_block), which by default runs only from 2^20 particles, forced on
+    small cases (MPH_XCD_BAL_MIN=0; their few blocks also
     trip the map's fallback to equal ranges when a range exceeds its slack): it only changes which
     block handles which wave, so every field equals the default run bit for bit."""
     cfg, parts = cases.get(case).build()
