@@ -15,7 +15,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 FIELDS = ["Position", "Velocity", "PressureP", "PressureA", "NeighborCount", "Force", "Acceleration",
-          "DensityA", "VolStrainP", "DivergenceP", "GravityCenter"]
+          "DensityA", "VolStrainP", "DivergenceP", "GravityCenter", "DeformGradient", "Strain", "Stress"]
 
 
 def run(out, names):
