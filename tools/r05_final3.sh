@@ -6,7 +6,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/${OUT:-r05final5}
+OUT=gpurun_out/${OUT:-r05final6}
 mkdir -p $OUT
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit 11
 timeout -k 10 400 python bench.py > $OUT/bench_d1m.json 2> $OUT/bench_d1m.err || exit 12
