@@ -1376,6 +1376,9 @@ __attribute__((visibility("default"))) int mph_diag_paths(MphCtx* c, unsigned lo
     char* dev = reinterpret_cast<char*>(c->dst) + offsetof(DevState, path_diag);
     if (out) HIP_OK(c, hipMemcpy(out, dev, sizeof(DevState::path_diag), hipMemcpyDeviceToHost));
     if (reset) HIP_OK(c, hipMemset(dev, 0, sizeof(DevState::path_diag)));
+    const int* prev = c->nbcount;   // the previous step's NeighborCount (sorted order then)
+    HIP_OK(c, hipMemcpy(reinterpret_cast<char*>(c->dst) + offsetof(DevState, diag_prev), &prev, sizeof(prev),
+                        hipMemcpyHostToDevice));
     return MPH_OK;
 }
 #endif

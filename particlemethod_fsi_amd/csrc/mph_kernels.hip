@@ -1665,6 +1665,38 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     // bits 17 and up count every accepted neighbour (NeighborCount), bits 8-16 the stored ones (the
     // FP32 path keeps only r^2 <= P.rlf: kListTotal, kListKeep), so the store offset is soff & kSoffMask
     int soff = lane << 2;
+#if MPH_DIAG_PATHS
+    // diagnostic: this lane's rank in the wave by the previous step's NeighborCount
+    int seg_sorted = 0;
+    {
+        const int pv = act && dst->diag_prev ? dst->diag_prev[i] : 0x7fffffff;
+        int rk = 0;
+        for (int m = 0; m < 64; ++m) {
+            const int o = __builtin_amdgcn_readlane(pv, m);
+            rk += (o < pv || (o == pv && m < lane)) ? 1 : 0;
+        }
+        seg_sorted = rk >> 4;
+    }
+    auto seg_count = [&](bool st_on) {
+        const unsigned long long am = __ballot(st_on);
+        if (!am) return;
+        const int row = (soff >> 8) & 0x1FF;
+        const int kd = row * 4 + (lane >> 4), ks = row * 4 + seg_sorted;
+        bool dd = false, ds = false;
+        for (int m = 0; m < 64; ++m) {
+            if (!((am >> m) & 1ull)) continue;
+            const int od = __builtin_amdgcn_readlane(kd, m), os = __builtin_amdgcn_readlane(ks, m);
+            if (m < lane) { dd = dd || od == kd; ds = ds || os == ks; }
+        }
+        const int nd = __popcll(__ballot(st_on && !dd)), ns = __popcll(__ballot(st_on && !ds));
+        if (lane == 0) {
+            atomicAdd(&dst->path_diag[44], (unsigned long long)nd);
+            atomicAdd(&dst->path_diag[45], (unsigned long long)ns);
+            atomicAdd(&dst->path_diag[46], 1ull);
+            atomicAdd(&dst->path_diag[47], (unsigned long long)__popcll(am));
+        }
+    };
+#endif
 #if MPH_LIST_SPREAD
     // proportional rows (kListSpread): stored entry k at row k * M / np below the prediction np,
     // M + k - np past it; `cur` is the next row the lane has not written (rows skipped get the
@@ -1831,6 +1863,9 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                                 if ((r2a <= hi2) != in) a = accept_band(P, ddx, ddy, ddz);
                             }
                         }
+#if MPH_DIAG_PATHS
+                        seg_count(a && r2f <= P.rlf);
+#endif
                         if (a) {
                             // stored when within the passes' largest radius (FP32, an upper bound:
                             // the passes' own exact tests decide); counted always

@@ -280,6 +280,10 @@ struct DevState {
     // spans (64, 96], (96, 128], (128, 160], (160, 192], (192, 256], > 256 records; [40..42] the rows
     // of column-aligned lists (per column, per group of kGroups columns) and of today's (the longest)
     unsigned long long path_diag[48];
+    // [44..47] of path_diag: the list stores' 64-byte segments per store instruction with the lanes
+    // in order and with the lanes ranked by the previous step's NeighborCount (diag_prev), the
+    // store instructions and their entries
+    const int* diag_prev;
 #endif
 #if MPH_DIAG_XCD
     // diagnostic build only (tools/xcd_diag.py): per list kernel (search, pass A, pass B) and XCD,

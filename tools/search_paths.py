@@ -76,6 +76,10 @@ def main():
                            "lane_fill_today": w[32] / max(64 * w[42], 1),
                            "lane_fill_per_column": w[32] / max(64 * w[40], 1),
                            "lane_fill_per_group": w[32] / max(64 * w[41], 1)}
+            out["store_segments"] = {"instructions": w[46], "entries": w[47],
+                                     "segments_lanes_in_order": w[44], "segments_lanes_by_prev_count": w[45],
+                                     "entries_per_segment_in_order": w[47] / max(w[44], 1),
+                                     "entries_per_segment_sorted": w[47] / max(w[45], 1)}
             out["span_hist"] = dict(zip(("64-96", "96-128", "128-160", "160-192", "192-256", ">256"),
                                         [x / max(cols, 1) for x in w[34:40]]))
             print(json.dumps(out), flush=True)
