@@ -54,6 +54,11 @@
 #define MPH_DIAG_SEARCH 0   // diagnostic builds only: 1 = stage but test nothing, 2 = no staging,
                             // 4 = waves near a periodic face do nothing
 #endif
+#ifndef MPH_DIAG_CHUNK
+#define MPH_DIAG_CHUNK 0   // diagnostic builds only: the search buffers 4 stored entries per lane in LDS
+                           // and writes 16-byte chunks ([k / 4][lane][4] in the tile's unused upper
+                           // half; the passes read stale rows, as with MPH_DIAG_NOSTORE=1: timing only)
+#endif
 #ifndef MPH_DIAG_NOSTORE
 #define MPH_DIAG_NOSTORE 0   // diagnostic builds only: 1 = the search counts but stores no list,
                              // 2 = every store goes to the lane's row 0 (same instructions, no list traffic)
@@ -1520,11 +1525,15 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
 {
     constexpr int SD = stage_d(CAP, SB);
     // FP32 records fill the whole FP64 staging area: 16 bytes each, SB past the window's end
-    constexpr int kCap32 = MPH_CAP32 ? stage_words(CAP, SB) / 2 - SB - 1 : CAP;
+    // MPH_DIAG_CHUNK: the last 1 KB of the wave's staging area holds the lanes' 4-entry chunks
+    constexpr int kChunkWords = MPH_DIAG_CHUNK ? 128 : 0;
+    constexpr int kCap32 = MPH_CAP32 ? (stage_words(CAP, SB) - kChunkWords) / 2 - SB - 1 : CAP;
+
     double* sy = sx + SD;
     double* sz = sx + 2 * SD;
     int* st = reinterpret_cast<int*>(sx + 3 * SD);
     const int lane = threadIdx.x & 63;
+    [[maybe_unused]] int* const cbuf = reinterpret_cast<int*>(sx + stage_words(CAP, SB) - kChunkWords) + 4 * lane;
     // buffer descriptor of the wave's ELL tile (out - lane, wave-uniform): list stores take a 32-bit
     // lane offset instead of a 64-bit address; a store past the tile is dropped by the hardware
     const unsigned long long tb = (unsigned long long)(out - lane);
@@ -1874,6 +1883,19 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                             // the lane's row 0 (the instructions without the list traffic)
 #if MPH_LIST_SPREAD
                             if (keep) put(nbr_entry(j, __float_as_int(r[u].w)));
+#elif MPH_DIAG_CHUNK
+                            if (keep) {
+                                const int k = (soff >> 8) & 3;
+                                cbuf[k] = nbr_entry(j, __float_as_int(r[u].w));
+                                if (k == 3) {
+                                    typedef unsigned u4v __attribute__((ext_vector_type(4)));
+                                    const u4v v = *reinterpret_cast<const u4v*>(cbuf);
+                                    // into the tile's upper half (rows 256 and up, unused), so the
+                                    // passes keep reading the stale rows, as with MPH_DIAG_NOSTORE=1
+                                    __builtin_amdgcn_raw_buffer_store_b128(
+                                        v, tile_rsrc, 65536 + (((soff >> 10) & 0x3F) * 64 + lane) * 16, 0, 0);
+                                }
+                            }
 #else
                             if (keep && MPH_DIAG_NOSTORE != 1)
                                 __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, __float_as_int(r[u].w)), tile_rsrc,

@@ -6,6 +6,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=${OUT:-gpurun_out/abdev}
 mkdir -p $OUT
+trap 'rm -f $OUT/d1m_dev.gridb' EXIT   # the state is ~72 MB: never left for gpurun to copy back
 timeout -k 10 120 python3 tools/dev_state.py d1m ${DEV_STEPS:-2500} $OUT/d1m_dev.gridb > $OUT/dev_state.log 2>&1 || exit 21
 for r in $(seq 1 ${ROUNDS:-2}); do
   for v in base ${VARIANTS}; do
