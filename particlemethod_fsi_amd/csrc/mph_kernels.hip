@@ -1526,14 +1526,15 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     constexpr int SD = stage_d(CAP, SB);
     // FP32 records fill the whole FP64 staging area: 16 bytes each, SB past the window's end
     // MPH_DIAG_CHUNK: the last 1 KB of the wave's staging area holds the lanes' 4-entry chunks
-    constexpr int kChunkWords = MPH_DIAG_CHUNK ? 128 : 0;
+    constexpr int kChunkWords = MPH_DIAG_CHUNK == 2 ? 256 : MPH_DIAG_CHUNK ? 128 : 0;   // 8 / 4 entries per lane
     constexpr int kCap32 = MPH_CAP32 ? (stage_words(CAP, SB) - kChunkWords) / 2 - SB - 1 : CAP;
 
     double* sy = sx + SD;
     double* sz = sx + 2 * SD;
     int* st = reinterpret_cast<int*>(sx + 3 * SD);
     const int lane = threadIdx.x & 63;
-    [[maybe_unused]] int* const cbuf = reinterpret_cast<int*>(sx + stage_words(CAP, SB) - kChunkWords) + 4 * lane;
+    [[maybe_unused]] int* const cbuf = reinterpret_cast<int*>(sx + stage_words(CAP, SB) - kChunkWords) +
+                                       (MPH_DIAG_CHUNK == 2 ? 8 : 4) * lane;
     // buffer descriptor of the wave's ELL tile (out - lane, wave-uniform): list stores take a 32-bit
     // lane offset instead of a 64-bit address; a store past the tile is dropped by the hardware
     const unsigned long long tb = (unsigned long long)(out - lane);
@@ -1884,7 +1885,19 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
 #if MPH_LIST_SPREAD
                             if (keep) put(nbr_entry(j, __float_as_int(r[u].w)));
 #elif MPH_DIAG_CHUNK
-                            if (keep) {
+                            if (keep && MPH_DIAG_CHUNK == 2) {
+                                // 8 entries (one 32-byte sector) per lane and chunk
+                                const int k = (soff >> 8) & 7;
+                                cbuf[k] = nbr_entry(j, __float_as_int(r[u].w));
+                                if (k == 7) {
+                                    typedef unsigned u4v __attribute__((ext_vector_type(4)));
+                                    const u4v v0 = *reinterpret_cast<const u4v*>(cbuf);
+                                    const u4v v1 = *reinterpret_cast<const u4v*>(cbuf + 4);
+                                    const int o = 65536 + (((soff >> 11) & 0x1F) * 64 + lane) * 32;
+                                    __builtin_amdgcn_raw_buffer_store_b128(v0, tile_rsrc, o, 0, 0);
+                                    __builtin_amdgcn_raw_buffer_store_b128(v1, tile_rsrc, o + 16, 0, 0);
+                                }
+                            } else if (keep) {
                                 const int k = (soff >> 8) & 3;
                                 cbuf[k] = nbr_entry(j, __float_as_int(r[u].w));
                                 if (k == 3) {
