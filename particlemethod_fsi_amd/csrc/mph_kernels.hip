@@ -1004,20 +1004,22 @@ __global__ __launch_bounds__(1024) void k_scan_top(int* __restrict__ bsum, int n
                                                    int stride)
 {
     if (st) bsum += (st->seam_step & 1) * stride;
+    // each thread a run of R consecutive totals: its sum, one block scan of the sums, then the
+    // run's exclusive prefixes (one round trip to memory instead of nb / blockDim.x of them)
     __shared__ int lds[16];
-    __shared__ int carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (int base = 0; base < nb; base += blockDim.x) {
-        const int i = base + threadIdx.x;
-        const int v = i < nb ? bsum[i] : 0;
-        int total;
-        const int ex = block_exclusive_scan(v, lds, total);
-        const int c = carry;
-        if (i < nb) bsum[i] = ex + c;
-        __syncthreads();
-        if (threadIdx.x == 0) carry = c + total;
-        __syncthreads();
+    const int t = threadIdx.x;
+    const int R = (nb + (int)blockDim.x - 1) / (int)blockDim.x;
+    const int b0 = min(nb, t * R), b1 = min(nb, b0 + R);
+    int sum = 0;
+#pragma unroll 8
+    for (int b = b0; b < b1; ++b) sum += bsum[b];
+    int total;
+    int run = block_exclusive_scan(sum, lds, total);
+#pragma unroll 8
+    for (int b = b0; b < b1; ++b) {
+        const int v = bsum[b];
+        bsum[b] = run;
+        run += v;
     }
 }
 
