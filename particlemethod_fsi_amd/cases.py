@@ -298,6 +298,13 @@ _reg(Case("gate2d_sub", 2, "dam", 0.001, CASES["gate2d"].lower, CASES["gate2d"].
           CASES["gate2d"].cuboids, data_changes={"ElasticDt": [2e-5]}, note="gate2d, 5 substeps"))
 _reg(Case("gate3d_sub", 3, "dam", 0.001, CASES["gate3d"].lower, CASES["gate3d"].upper,
           CASES["gate3d"].cuboids, data_changes={"ElasticDt": [2.5e-5]}, note="gate3d, 4 substeps"))
+# The FSI workload that runs to completion: configs[3]'s geometry (fsi3d,
+# 2,259,700 particles) with 4 elastic substeps per step, as gate3d_sub.  fsi3d itself keeps the
+# survey's ElasticDt = Dt, at which the reference's own gate is unstable.
+_reg(Case("fsi3d_sub", 3, "dam", 0.001, CASES["fsi3d"].lower, CASES["fsi3d"].upper,
+          CASES["fsi3d"].cuboids, data_changes={"ElasticDt": [2.5e-5]},
+          note="3-D dam break onto an elastic gate, coupled FSI, 4 elastic substeps per step "
+               "(BASELINE configs[3] geometry; the stable FSI workload)"))
 
 
 # Off-lattice 3-D cases: every particle of box3d / the sub-stepped gate moved by up to

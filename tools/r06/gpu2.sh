@@ -1,0 +1,9 @@
+#!/bin/bash
+# round 6: the FSI probe past the impact, then the hand-off test at t = 0.35 s
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+OUT=gpurun_out/r06b
+mkdir -p $OUT
+timeout -k 10 300 python -u tools/fsi_sub_probe.py fsi3d_sub 100 4500 > $OUT/probe_fsi3d_sub.log 2>&1 || exit 11
+timeout -k 10 600 python -u -m pytest -x -v -s --timeout 500 --timeout-method thread \
+    tests/test_gpu_longrun.py -k fsi > $OUT/pytest.log 2>&1 || exit 12
