@@ -510,9 +510,14 @@ __device__ __forceinline__ void add_wave_work(DevState* st, int cnt, int i, int 
 }
 
 __device__ __forceinline__ int nbr_entry(int j, int type) { return j | (type << kTypeShift); }
-// The search's per-lane counter (scan_candidates_lds): the byte offset of the next list slot in the
-// wave's ELL tile (stored entries x 256 + lane x 4, bits 0-16) and every accepted neighbour x 2^17
-constexpr int kListKeep = 256 + (1 << 17), kListTotal = 1 << 17, kSoffMask = 0x1FFFF;
+// The search's per-lane counter (scan_candidates_lds): lane x 4 in bits 0-7, the stored entries in
+// bits 8-17 (up to 1023, so a lane that keeps all 512 entries the reference allows does not carry
+// into the total) and every accepted neighbour from bit 18.  The next list slot's byte offset in the
+// wave's ELL tile is soff & kSoffMask (stored mod 512 rows): only an overflowing lane (> 512, the
+// step's MPH_ERR_NEIGHBOR_OVERFLOW) wraps, and it stays inside its own tile.
+constexpr int kListKeep = 256 + (1 << 18), kListTotal = 1 << 18, kSoffMask = 0x1FFFF;
+__device__ __forceinline__ int soff_total(int soff) { return (int)((unsigned)soff >> 18); }
+__device__ __forceinline__ int soff_stored(int soff) { return (soff >> 8) & 0x3FF; }
 
 // MPH_PA_STAGED: a wave's column windows {mn, mx} for pass A (kWinCols of them) and its format flag
 // (entry kWinCols: 1 = written by the staged search), kWinHdr int2 per wave (Launch.whdr)
@@ -1674,7 +1679,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     }
     // the lane's next list slot: C16 counts entries (cnt); the ELL rows keep the slot's byte offset
     // in the wave's tile, soff = stored * 256 + lane * 4 (one add per entry, no address arithmetic);
-    // bits 17 and up count every accepted neighbour (NeighborCount), bits 8-16 the stored ones (the
+    // bits 18 and up count every accepted neighbour (NeighborCount), bits 8-17 the stored ones (the
     // FP32 path keeps only r^2 <= P.rlf: kListTotal, kListKeep), so the store offset is soff & kSoffMask
     int soff = lane << 2;
 #if MPH_DIAG_PATHS
@@ -2037,7 +2042,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
 #if MPH_LIST_SPREAD
                             put(nbr_entry(j, A.type[j]));
 #else
-                            if (!MPH_DIAG_NOSTORE && (soff >> 17) < kMaxNeighbor)
+                            if (!MPH_DIAG_NOSTORE && soff_total(soff) < kMaxNeighbor)
                                 list_store(ell_at(out, lane, (soff & kSoffMask) >> 8), nbr_entry(j, A.type[j]));
 #endif
                             soff += kListKeep;
@@ -2114,8 +2119,8 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     }
 #endif
     if (!C16) {
-        cnt = soff >> 17;                 // every neighbour (NeighborCount)
-        *stored = (soff >> 8) & 0x1FF;    // the list's length (r^2 <= P.rlf)
+        cnt = soff_total(soff);       // every neighbour (NeighborCount)
+        *stored = soff_stored(soff);  // the list's length (r^2 <= P.rlf)
 #if MPH_LIST_SPREAD
         *stored = min(cur, kMaxNeighbor);   // rows the passes walk, sentinels included
 #endif

@@ -1,8 +1,9 @@
 """GPU: edge cases of the hot path and of the C ABI's error behaviour.
 
 The reference has no tests; these follow its own limits and quirks:
-  * a particle with >= 512 neighbours (MAX_NEIGHBOR_COUNT, main.cpp:100, 1766-1768: the reference
+  * a particle with > 512 neighbours (MAX_NEIGHBOR_COUNT, main.cpp:100, 1766-1768: the reference
     keeps counting and later reads past the row) is MPH_ERR_NEIGHBOR_OVERFLOW here, never a fault;
+    exactly 512 is accepted, as in the reference;
   * empty and single-particle inputs (a lone fluid particle only falls: Kappa is zeroed on tension,
     main.cpp:2113, so P = 0 and the force is m g -- checked bit for bit);
   * a domain narrower than the cell stencil and too many slabs are MPH_ERR_DOMAIN;
@@ -29,6 +30,56 @@ def test_neighbor_overflow_is_an_error_not_a_fault():
     cfg, parts = _case([Cuboid(1, (0.1, 0.1, 0.0), (0.106, 0.106, 0.0002), 0.0002)],
                        (0.0, 0.0, 0.0), (0.2, 0.2, 0.0002))
     assert parts.n == 900
+    with pytest.raises(MphError) as e:
+        MphSolver(cfg, parts)
+    assert e.value.code == -3
+
+
+def _cluster(extra):
+    """3-D fluid: 511 particles of an 8 x 8 x 8 block at 0.18 dx (every pair within 2.2 dx, inside
+    MaxRadius = 2.5 dx, so every neighbour is also a stored list entry) and two hubs 0.75 dx beyond
+    its two x faces, each within 2.2 dx of the whole block but 2.76 dx from the other: every block
+    particle has exactly 512 neighbours, each hub 511.  (The reference counts a particle itself once
+    its count has reached 512, main.cpp:1766-1768; with the hub last in every block particle's scan
+    that never happens here -- the oracle, bit-identical to the reference, counts 512.)  `extra`
+    adds a particle at the block's centre (513 neighbours).  The domain is wide enough that the
+    block's wavefronts take the interior (LDS, FP32) search."""
+    c = cases.Case("cluster", 3, "dam", 0.001, (0.0, 0.0, 0.0), (0.02, 0.02, 0.02), [])
+    cfg, _ = c._config()
+    s, a = 0.00018, 0.00075
+    g = np.arange(8) * s
+    pos = np.stack(np.meshgrid(g, g, g, indexing="ij"), -1).reshape(-1, 3)[:511] + 0.01
+    yc = 0.01 + 3.5 * s
+    hubs = [[0.01 - a, yc, yc], [0.01 + 7 * s + a, yc, yc], [0.01 + 3.5 * s, yc + 1e-6, yc]]
+    pos = np.concatenate([pos, np.array(hubs[:2 + extra])])
+    n = len(pos)
+    return cfg, mphio.Particles(np.ones(n, np.int32), pos.copy(), pos.copy(), np.zeros((n, 3)))
+
+
+def test_exactly_512_neighbors_is_accepted():
+    """MAX_NEIGHBOR_COUNT (main.cpp:100) is a limit the reference accepts: a particle with exactly 512
+    neighbours fills its row (main.cpp:1766-1772) and runs on.  _cluster(0): 511 particles with
+    512 neighbours each, all of them stored list entries (the search's per-lane counter must not
+    carry its 512 stored entries into the total, ADVICE r5).  One step against the oracle;
+    _cluster(1) (513 neighbours) is MPH_ERR_NEIGHBOR_OVERFLOW."""
+    from oracle_bindings import OracleSolver
+    cfg, parts = _cluster(0)
+    assert parts.n == 513
+    o = OracleSolver(cfg, parts)
+    o.init()
+    assert int((o.get("NeighborCount") == 512).sum()) == 511 and int(o.get("NeighborCount").max()) == 512
+    with MphSolver(cfg, parts) as s:
+        assert np.array_equal(s.get("NeighborCount"), o.get("NeighborCount"))
+        assert s.neighbor_stats()[1] == 512
+        s.step(1)
+        o.step(1)
+        assert int((s.get("NeighborCount") == 512).sum()) >= 500
+        assert np.array_equal(s.get("NeighborCount"), o.get("NeighborCount"))
+        for f in ("Position", "Velocity", "PressureP", "Force"):
+            a, b = s.get(f), o.get(f)
+            t = 1e-9 * float(np.max(np.abs(b))) + 1e-15
+            assert float(np.max(np.abs(a - b))) <= t, (f, float(np.max(np.abs(a - b))), t)
+    cfg, parts = _cluster(1)
     with pytest.raises(MphError) as e:
         MphSolver(cfg, parts)
     assert e.value.code == -3
