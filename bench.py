@@ -396,9 +396,10 @@ def main():
     # passes; algorithmic 4 B per entry against the search's measured WRITE_SIZE
     list_info = None
     if world == 1:
-        list_alg = 4.0 * mean_nb * n_local
+        mean_stored = solver.list_stats()[0]   # the stored lists (the passes' radius), not NeighborCount
+        list_alg = 4.0 * mean_stored * n_local
         wr = load_pmc("pmc_traffic", case_name, "neighbors", "write_kib")
-        list_info = {"entries_per_particle": mean_nb, "alg_bytes_written": list_alg,
+        list_info = {"entries_per_particle": mean_stored, "alg_bytes_written": list_alg,
                      "alg_bytes_read_by_passes": 2.0 * list_alg,
                      "search_write_bytes_measured": wr * 1024.0 if wr else None,
                      "write_amplification": (wr * 1024.0 / list_alg) if wr and list_alg else None}

@@ -42,7 +42,7 @@ extern "C" {
 #define MPH_MAX_NEIGHBOR_COUNT 512  /* main.cpp:100 (semantic limit; overflow is an error here) */
 /* Bumped on every incompatible change of a declaration below (3: mph_slab_bounds/_owner/_window
  * take `cuts`; mph_dist_info slot 0/2 meaning); bindings compare mph_abi_version() with it.     */
-#define MPH_ABI_VERSION 3
+#define MPH_ABI_VERSION 4
 
 /* Compile-time case modules of the reference (main.cpp:54-59) as a runtime switch.  The module
  * selects the clamp rule of updateElasticPosition (main.cpp:1918-2044).                        */
@@ -390,11 +390,11 @@ int mph_dist_info(const MphCtx* ctx, int* out8);
  * their message capacities), the cost of pass B split into interior and face launches over one
  * launch (-1: not probed)}.  Overlap is chosen when the two exchanges take longer than the split. */
 int mph_dist_overlap(const MphCtx* ctx, double* out5);
-/* Neighbour-list formats of the last search: out2 = {wavefronts with the compact 16-bit list,
- * wavefronts in all} (the others, near a periodic face or with long group ranges, keep 32-bit
- * ELL rows).  The compact format is opt-in at the default stencil (MPH_LIST16=1 at creation,
- * equal radii only; MPH_LIST16=0 forces ELL rows everywhere).                                 */
-int mph_list_formats(MphCtx* ctx, int* out2);
+/* Mean/max length of the stored neighbour lists of the last search (what the passes walk: the
+ * pairs within the passes' largest radius; with MPH_LIST_FULL=1 at creation every
+ * neighbour, = mph_neighbor_stats).  ABI 4 (round 6): replaces mph_list_formats, which reported
+ * the compact 16-bit list format removed from the product.                                   */
+int mph_list_stats(MphCtx* ctx, double* mean, int* max);
 /* The neighbour lists of calculateNeighbor themselves (main.cpp:1764-1772: Neighbor[i][k] = j for
  * k < 512), for verification: the sets of the `count` particles [first, first + count) (original
  * order) from the last search, each row as ascending original indices (the reference's rows are in

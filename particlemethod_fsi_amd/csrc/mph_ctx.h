@@ -103,9 +103,6 @@ struct MphCtx {
     // three per step of a batch of up to 8 (ev8), and around the virial (ev_vir)
     bool phase_timing = false;
     std::vector<hipEvent_t> ev8, ev_vir;
-    // chunked search + pass A (Launch.chunks): the second stream and its events
-    hipStream_t stream2 = nullptr;
-    std::vector<hipEvent_t> ev_chunk;
     double phase_ms[3] = {0.0, 0.0, 0.0};   // neighbour search, explicit calculation, virial
     // host copies of the static inputs: original order, or -- slab-local creation -- the
     // particles this rank was created with, whose original indices are gid (ascending)
@@ -123,10 +120,6 @@ struct MphCtx {
     int *key = nullptr, *slot = nullptr, *tmp = nullptr, *cnt = nullptr, *start = nullptr, *bsum = nullptr;
     double *vir = nullptr, *vpres = nullptr;   // VirialStress [cap][9] / VirialPressure (A order), lazy
     int *nbr = nullptr, *ncount = nullptr, *nbcount = nullptr;   // list lengths / NeighborCount
-    int* pred = nullptr;   // MPH_LIST_SPREAD: the last step's NeighborCount in this step's order
-    int* list_hdr = nullptr;     // per-wave headers of the compact 16-bit lists (kLhdr ints each)
-    int2* win_hdr = nullptr;     // MPH_PA_STAGED builds: per-wave column windows (kWinHdr each)
-    unsigned long long* wave_log = nullptr;   // MPH_DIAG_XCD >= 2 builds: the search's per-wave log
     double *pres = nullptr, *gx = nullptr, *gy = nullptr, *gz = nullptr, *pa = nullptr;
     double4 *force = nullptr, *acc = nullptr, *fpart = nullptr, *rec = nullptr;
     double *dens_a = nullptr, *vstrain = nullptr, *divp = nullptr;

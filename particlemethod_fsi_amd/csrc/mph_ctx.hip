@@ -55,10 +55,6 @@ int ctx_state_status(MphCtx* c, const DevState& hs)
     if (hs.overflow & 2) return ctx_fail(c, MPH_ERR_CAPACITY, "a particle moved past a neighbouring slab");
     if (hs.overflow & 64)   // k_place: a cell start + slot past the particle count (never a fault)
         return ctx_fail(c, MPH_ERR_HIP, "cell sort: histogram inconsistent with the keys (placement out of range)");
-    if (hs.overflow & 32)   // MPH_DIAG_PA builds only
-        return ctx_fail(c, MPH_ERR_HIP, "diagnostic: staged pass A left list entries over (MPH_DIAG_PA)");
-    if (hs.overflow & 8)   // MPH_DIAG_BOUNDS builds only
-        return ctx_fail(c, MPH_ERR_HIP, "diagnostic: a search window out of range (MPH_DIAG_BOUNDS)");
     return MPH_OK;
 }
 
@@ -78,15 +74,7 @@ void ctx_fill_launch(MphCtx* c)
     // returned through A.id), so k_rank_scatter skips that scatter; slab mode uses dst_of.
     L.A = c->A; L.B = c->B; L.rank_of = nullptr; L.dst_of = nullptr;
     L.key = c->key; L.slot = c->slot; L.tmp = c->tmp; L.cnt = c->cnt; L.start = c->start; L.bsum = c->bsum;
-    L.nbr = c->nbr; L.ncount = c->ncount; L.nbcount = c->nbcount; L.whdr = c->win_hdr;
-    // MPH_LIST_SPREAD (single contexts): the sort carries the last NeighborCount to the search
-    c->P.pred = kListSpread && !c->dist ? c->pred : nullptr;
-    c->P.pred_src = c->P.pred ? c->nbcount : nullptr;
-    // compact 16-bit lists of interior wavefronts (MPH_LIST16=1), or 32-bit ELL rows everywhere
-    // (MPH_LIST16=0); unset: kListCompact
-    const char* l16 = std::getenv("MPH_LIST16");
-    const bool compact = l16 && *l16 ? std::string(l16) != "0" : kListCompact;
-    L.lhdr = compact && pass_a_equal_radii(c->P) ? c->list_hdr : nullptr;
+    L.nbr = c->nbr; L.ncount = c->ncount; L.nbcount = c->nbcount;
     // work-balanced XCD map of the passes from this many particles (MPH_XCD_BAL_MIN: tests force it
     // on small cases, the default keeps it off below 2^20 where the split kernel costs more)
     const char* bm = std::getenv("MPH_XCD_BAL_MIN");
@@ -95,24 +83,6 @@ void ctx_fill_launch(MphCtx* c)
     L.force = c->force; L.acc = c->acc; L.fpart = c->fpart; L.rec = c->rec;
     L.dens_a = c->dens_a; L.vstrain = c->vstrain; L.divp = c->divp;
     L.S = &c->Sd;
-    // MPH_CHUNKS=C (2..16): the search and pass A in C pieces on two streams (launch_search_pass_a);
-    // a single context only (slab ranks overlap their own way)
-    const char* ch = std::getenv("MPH_CHUNKS");
-    const int chunks = ch && *ch ? std::atoi(ch) : kSearchChunks;
-    L.chunks = 1;
-    if (!c->dist && chunks > 1 && chunks <= 16) {
-        bool ok = c->stream2 || hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) == hipSuccess;
-        while (ok && (int)c->ev_chunk.size() < chunks + 1) {
-            hipEvent_t e = nullptr;
-            ok = hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
-            if (ok) c->ev_chunk.push_back(e);
-        }
-        if (ok) {
-            L.chunks = chunks;
-            L.stream2 = c->stream2;
-            L.ev_chunk = c->ev_chunk.data();
-        }
-    }
 }
 
 // calculateVirialStressAtParticle evaluates the step's lists at the positions after the step
@@ -406,8 +376,6 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         // faces are long runs (whole wavefronts) at the ends of every plane (DevParams.perm;
         // MPH_SLAB_PERM=0 keeps (x, y, z); =1..4 force an order on any 3-D context, =force
         // orders a single 3-D context the z-slab way -- A/B timing and the parity tests)
-        const char* lm = std::getenv("MPH_LIST16_MAX");
-        c->P.l16max = lm ? std::max(0, std::min(127, std::atoi(lm))) : 127;
         const char* pe = std::getenv("MPH_SLAB_PERM");
         const std::string pv = pe ? pe : "";
         const bool zslab = cfg->dim == 3 && c->dist && c->dist->g.axis == 2;
@@ -489,36 +457,22 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
         CK(dalloc(c, &s->type, m)); CK(dalloc(c, &s->id, m));
     }
     CK(dalloc(c, &c->A.p6, 3 * (size_t)cap));
-    // the search's FP32 candidate records (MPH_SEARCH_F32 builds read them; kPad past the last)
+    // the search's FP32 candidate records (kPad past the last)
     CK(dalloc(c, &c->A.f4, (size_t)cap + kPad));
     CK(dalloc(c, &c->rank_of, cap));
     CK(dalloc(c, &c->key, cap)); CK(dalloc(c, &c->slot, cap)); CK(dalloc(c, &c->tmp, cap));
     CK(dalloc(c, &c->cnt, c->P.ncell)); CK(dalloc(c, &c->start, (size_t)c->P.ncell + 1));
-    // the cell scan's block totals: two parity buffers filled by k_prep (MPH_PREP_BSUM builds), and a
-    // scratch third for the other scans (k_scan_reduce, structure init); all zero at the start
-    const size_t bs = (size_t)c->P.ncell / 4096 + 2;
-    CK(dalloc(c, &c->bsum, 3 * bs));
+    // the cell scan's block totals (k_scan_reduce; structure init)
+    const size_t bs = (size_t)c->P.ncell / 4096 + 2;   // bsum_stride (mph_kernels.hip)
+    CK(dalloc(c, &c->bsum, bs));
     CK(dalloc(c, &c->nbr, ntile * kTileStride)); CK(dalloc(c, &c->ncount, cap));
     CK(dalloc(c, &c->nbcount, cap));
-    if (kListSpread) CK(dalloc(c, &c->pred, cap));
-#if (defined(MPH_DIAG_NOSTORE) && MPH_DIAG_NOSTORE) || (defined(MPH_DIAG_SEARCH) && (MPH_DIAG_SEARCH & 4))
-    // diagnostic builds: the search stores no list (or skips the waves near a periodic face, whose
-    // counts then stay 0), so the passes read index 0 (never garbage)
-    if (hipMemset(c->nbr, 0, sizeof(int) * ntile * kTileStride) != hipSuccess) return MPH_ERR_HIP;
-    if (hipMemset(c->ncount, 0, sizeof(int) * cap) != hipSuccess) return MPH_ERR_HIP;
-    if (hipMemset(c->nbcount, 0, sizeof(int) * cap) != hipSuccess) return MPH_ERR_HIP;
-    if (c->pred && hipMemset(c->pred, 0, sizeof(int) * cap) != hipSuccess) return MPH_ERR_HIP;
-#endif
-    CK(dalloc(c, &c->list_hdr, ntile * kLhdr));
-#if defined(MPH_PA_STAGED) && MPH_PA_STAGED
-    CK(dalloc(c, &c->win_hdr, (ntile + 4) * kWinHdr));
-#endif
     CK(dalloc(c, &c->pres, cap)); CK(dalloc(c, &c->gx, cap)); CK(dalloc(c, &c->gy, cap)); CK(dalloc(c, &c->gz, cap));
     CK(dalloc(c, &c->pa, cap)); CK(dalloc(c, &c->force, cap)); CK(dalloc(c, &c->acc, cap));
     CK(dalloc(c, &c->fpart, cap)); CK(dalloc(c, &c->rec, cap));
     CK(dalloc(c, &c->dens_a, cap)); CK(dalloc(c, &c->vstrain, cap)); CK(dalloc(c, &c->divp, cap));
     HIP_OK(c, hipMemsetAsync(c->cnt, 0, sizeof(int) * c->P.ncell, c->stream));
-    HIP_OK(c, hipMemsetAsync(c->bsum, 0, sizeof(int) * 3 * bs, c->stream));
+    HIP_OK(c, hipMemsetAsync(c->bsum, 0, sizeof(int) * bs, c->stream));
     HIP_OK(c, hipMemsetAsync(c->force, 0, sizeof(double4) * std::max(cap, 1), c->stream));
     HIP_OK(c, hipMemsetAsync(c->acc, 0, sizeof(double4) * std::max(cap, 1), c->stream));
     HIP_OK(c, hipMemcpyAsync(c->dT, &c->T, sizeof(DevTables), hipMemcpyHostToDevice, c->stream));
@@ -1279,20 +1233,18 @@ int mph_neighbor_stats(MphCtx* c, double* mean, int* mx)
     return MPH_OK;
 }
 
-int mph_list_formats(MphCtx* c, int* out2)
+int mph_list_stats(MphCtx* c, double* mean, int* mx)
 {
-    if (!c || !out2) return MPH_ERR_ARG;
+    if (!c || !mean || !mx) return MPH_ERR_ARG;
     CK(ctx_flush(c));
     HIP_OK(c, hipSetDevice(c->device));
-    const int nt = (c->n + kTile - 1) / kTile;
-    int compact = 0;
-    if (nt && c->L.lhdr) {
-        std::vector<int> h((size_t)nt * kLhdr);
-        HIP_OK(c, hipMemcpy(h.data(), c->list_hdr, sizeof(int) * h.size(), hipMemcpyDeviceToHost));
-        for (int t = 0; t < nt; ++t) compact += h[(size_t)t * kLhdr + kHdrFlag] == 1;
-    }
-    out2[0] = compact;
-    out2[1] = nt;
+    std::vector<int> h(c->n);   // stored list lengths (ncount), reduced on the host
+    if (c->n) HIP_OK(c, hipMemcpy(h.data(), c->ncount, sizeof(int) * c->n, hipMemcpyDeviceToHost));
+    long long sum = 0;
+    int m = 0;
+    for (int v : h) { sum += v; m = v > m ? v : m; }
+    *mean = c->n ? (double)sum / c->n : 0.0;
+    *mx = m;
     return MPH_OK;
 }
 
@@ -1304,20 +1256,12 @@ int mph_neighbor_rows(MphCtx* c, int first, int count, int* counts, int* ids, lo
     if ((long long)first + count > c->n) return fail(c, MPH_ERR_ARG, "mph_neighbor_rows: range past the particle count");
     if (!count) return 0;
     HIP_OK(c, hipSetDevice(c->device));
-    const int n = c->n, nt = (n + kTile - 1) / kTile;
+    const int n = c->n;
     if (c->P.rlf < 3.0e38f)
         return fail(c, MPH_ERR_UNSUPPORTED, "mph_neighbor_rows: the lists keep only the pairs within the passes' "
                                             "radius (create the context with MPH_LIST_FULL=1 for the reference's lists)");
-    if (c->L.lhdr) {   // the compact 16-bit rows are not decoded here
-        std::vector<int> h((size_t)nt * kLhdr);
-        HIP_OK(c, hipMemcpy(h.data(), c->list_hdr, sizeof(int) * h.size(), hipMemcpyDeviceToHost));
-        for (int t = 0; t < nt; ++t)
-            if (h[(size_t)t * kLhdr + kHdrFlag] == 1)
-                return fail(c, MPH_ERR_UNSUPPORTED, "mph_neighbor_rows: compact lists in use (MPH_LIST16)");
-    }
     // the last search's rows are in its sorted order A: A.id maps a row (and an entry) back to the
-    // original index, ncount holds NeighborCount in the same order
-    // (MPH_LIST_SPREAD: ncount holds the rows walked, sentinels included; nbcount the entries)
+    // original index, ncount holds the list's length and nbcount NeighborCount in the same order
     std::vector<int> id(n), nc(n), nv(n);
     HIP_OK(c, hipMemcpy(id.data(), c->A.id, sizeof(int) * n, hipMemcpyDeviceToHost));
     HIP_OK(c, hipMemcpy(nc.data(), c->ncount, sizeof(int) * n, hipMemcpyDeviceToHost));
@@ -1341,8 +1285,7 @@ int mph_neighbor_rows(MphCtx* c, int first, int count, int* counts, int* ids, lo
         int m = 0;
         for (int s = t * kTile; s < std::min(n, (t + 1) * kTile); ++s) m = std::max(m, std::min(nc[s], kMaxNeighbor));
         std::vector<int>& buf = tiles[t];
-        const int g = 1 << kListLg;   // whole groups of ell_slot (half-wave rows: the whole tile)
-        buf.resize(kListHalf ? (size_t)kTile * kMaxNeighbor : (size_t)((m + g - 1) / g * g) * kTile);
+        buf.resize((size_t)m * kTile);
         if (m) HIP_OK(c, hipMemcpy(buf.data(), c->nbr + (size_t)t * kTileStride, sizeof(int) * buf.size(),
                                    hipMemcpyDeviceToHost));
     }
@@ -1353,7 +1296,6 @@ int mph_neighbor_rows(MphCtx* c, int first, int count, int* counts, int* ids, lo
         int q = 0;
         for (int e = 0; e < rows; ++e) {
             const int v = buf[(size_t)ell_slot(e, s & 63)];
-            if (kListSpread && v < 0) continue;   // a row the lane skipped
             const int j = v & kIndexMask;
             if (j >= n || q >= m) return fail(c, MPH_ERR_HIP, "mph_neighbor_rows: list entry past the particle count");
             ids[w + q++] = id[j];
@@ -1364,66 +1306,6 @@ int mph_neighbor_rows(MphCtx* c, int first, int count, int* counts, int* ids, lo
     }
     return (int)std::min<long long>(w, 0x7fffffff);
 }
-
-#if MPH_DIAG_PATHS
-// Diagnostic builds only (not in include/mph_gpu.h): copies DevState.path_diag (16 words, see
-// scan_candidates_lds) to out after draining the device; reset != 0 then zeroes it.
-__attribute__((visibility("default"))) int mph_diag_paths(MphCtx* c, unsigned long long* out, int reset)
-{
-    if (!c) return MPH_ERR_ARG;
-    HIP_OK(c, hipSetDevice(c->device));
-    HIP_OK(c, hipDeviceSynchronize());
-    char* dev = reinterpret_cast<char*>(c->dst) + offsetof(DevState, path_diag);
-    if (out) HIP_OK(c, hipMemcpy(out, dev, sizeof(DevState::path_diag), hipMemcpyDeviceToHost));
-    if (reset) HIP_OK(c, hipMemset(dev, 0, sizeof(DevState::path_diag)));
-    const int* prev = c->nbcount;   // the previous step's NeighborCount (sorted order then)
-    HIP_OK(c, hipMemcpy(reinterpret_cast<char*>(c->dst) + offsetof(DevState, diag_prev), &prev, sizeof(prev),
-                        hipMemcpyHostToDevice));
-    return MPH_OK;
-}
-#endif
-
-#if MPH_DIAG_XCD
-// Diagnostic builds only (not in include/mph_gpu.h): copies DevState.xcd_diag (3 x 4 x 8 words,
-// see XcdProbe in mph_kernels.hip) to out after draining the device; reset != 0 then restarts it.
-__attribute__((visibility("default"))) int mph_diag_xcd(MphCtx* c, unsigned long long* out, int reset)
-{
-    if (!c) return MPH_ERR_ARG;
-    HIP_OK(c, hipSetDevice(c->device));
-    HIP_OK(c, hipDeviceSynchronize());
-    constexpr size_t kBytes = sizeof(DevState::xcd_diag);
-    char* dev = reinterpret_cast<char*>(c->dst) + offsetof(DevState, xcd_diag);
-    if (out) HIP_OK(c, hipMemcpy(out, dev, kBytes, hipMemcpyDeviceToHost));
-    if (reset) {
-        unsigned long long h[3][4][8] = {};
-        for (auto& k : h)
-            for (auto& v : k[0]) v = ~0ull;
-        HIP_OK(c, hipMemcpy(dev, h, kBytes, hipMemcpyHostToDevice));
-    }
-    return MPH_OK;
-}
-
-// Diagnostic builds (MPH_DIAG_XCD >= 2): the search's per-wave log {start, end, XCC_ID} of its last
-// launch (wall_clock64 ticks), up to max_waves records into out; returns the record count.
-__attribute__((visibility("default"))) int mph_diag_waves(MphCtx* c, unsigned long long* out, int max_waves)
-{
-    if (!c || !out) return MPH_ERR_ARG;
-    HIP_OK(c, hipSetDevice(c->device));
-    const int nw = ((c->n + 255) / 256) * 4;   // the search grid at MPH_LB = 256
-    if (!c->wave_log) {   // first call: allocate and hand the log to the kernels
-        CK(dalloc(c, &c->wave_log, 3 * (size_t)nw));
-        HIP_OK(c, hipMemset(c->wave_log, 0, sizeof(unsigned long long) * 3 * (size_t)nw));
-        char* dev = reinterpret_cast<char*>(c->dst);
-        HIP_OK(c, hipMemcpy(dev + offsetof(DevState, wave_log), &c->wave_log, sizeof(void*), hipMemcpyHostToDevice));
-        HIP_OK(c, hipMemcpy(dev + offsetof(DevState, wave_log_n), &nw, sizeof(int), hipMemcpyHostToDevice));
-        return 0;
-    }
-    HIP_OK(c, hipDeviceSynchronize());
-    const int k = std::min(nw, max_waves);
-    HIP_OK(c, hipMemcpy(out, c->wave_log, sizeof(unsigned long long) * 3 * (size_t)k, hipMemcpyDeviceToHost));
-    return k;
-}
-#endif
 
 void mph_destroy(MphCtx* c)
 {
@@ -1437,9 +1319,8 @@ void mph_destroy(MphCtx* c)
     if (c->graph1) (void)hipGraphExecDestroy(c->graph1);
     if (c->graph1t) (void)hipGraphExecDestroy(c->graph1t);
     if (c->graph8) (void)hipGraphExecDestroy(c->graph8);
-    for (auto* v : {&c->ev8, &c->ev_vir, &c->ev_chunk})
+    for (auto* v : {&c->ev8, &c->ev_vir})
         for (hipEvent_t e : *v) (void)hipEventDestroy(e);
-    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->dist) dist_free(c);
     for (void* p : c->allocs) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);

@@ -63,8 +63,8 @@ struct Soa {
     // (profiles/r01: TA ~64 % busy in pass A); the type of j travels in the list entry instead
     // (kTypeShift), so a neighbour costs 48 gathered bytes instead of 64.
     double2* p6 = nullptr;
-    // MPH_SEARCH_F32 builds: {x, y, z} - domain centre in FP32 and the type's bits, 16 bytes, the
-    // search's staged candidate records (sorted set A only)
+    // {x, y, z} - domain centre in FP32 and the type's bits, 16 bytes, the search's staged
+    // candidate records (sorted set A only)
     float4* f4 = nullptr;
 };
 
@@ -94,10 +94,6 @@ struct Launch {
     DevState* st = nullptr;
     hipStream_t stream = nullptr;
     Profiler* prof = nullptr;
-    // chunked search + pass A (launch_search_pass_a): pieces, the second stream, chunks + 1 events
-    int chunks = 1;
-    hipStream_t stream2 = nullptr;
-    hipEvent_t* ev_chunk = nullptr;
     // B set: integrated state in the previous order; A set: cell-sorted current order
     Soa A, B;
     int* rank_of = nullptr;
@@ -106,11 +102,9 @@ struct Launch {
     // ncount: each list's length (what the passes walk); nbcount: NeighborCount (every neighbour within
     // the search radius; the lists keep only r^2 <= DevParams.rlf)
     int *nbr = nullptr, *ncount = nullptr, *nbcount = nullptr;
-    int* lhdr = nullptr;          // per-wave headers of the compact 16-bit lists (kLhdr each)
     int* wface = nullptr;         // slab mode: face-wavefront flags written by pass B (early send)
-    int2* whdr = nullptr;         // MPH_PA_STAGED builds: per-wave column windows (kWinHdr each)
     VSrc vsrc;                    // slab mode: where the sort finds the kept entries of its input
-    // fewest particles for the work-balanced XCD map of the passes (k_xcd_split each step);
+    // fewest particles for the work-balanced XCD map of the passes (split in k_rank_scatter);
     // MPH_XCD_BAL_MIN overrides it at creation (tests force the map on small cases)
     int xcd_bal_min = 1 << 20;
     // pass A products (A order): pressure values, gravity centre (GC, PressureA), sums
@@ -123,8 +117,8 @@ struct Launch {
 };
 
 void launch_sort(const Launch& L, int mode);   // mode 0 init, 1 step, 2 step (motion done)
-void launch_neighbors(const Launch& L, int ck = 0);
-void launch_pass_a(const Launch& L, int ck = 0);
+void launch_neighbors(const Launch& L);
+void launch_pass_a(const Launch& L);
 // launch_neighbors + launch_pass_a
 void launch_search_pass_a(const Launch& L);
 void launch_pass_b(const Launch& L, int phase = 0);   // phase: 0 all, 1/2 slab inner/near-face

@@ -42,94 +42,21 @@
 #include "mph_kernels.h"
 #include "mph_params.h"
 
-// Tuning switches (A/B builds: tools/ab.sh): pass A gathers from the AoS records of A (1) or from
-// the SoA arrays (0); the search of interior waves stages each stencil column's candidates in LDS
-// (1) or gathers them per lane from global memory (0);
-// batch widths of the pass-A / pass-B neighbour loops (MPH_UA / MPH_UB below).  Defaults are the
-// D1M measurements of profiles/r01.
-#ifndef MPH_AOS_GATHER
-#define MPH_AOS_GATHER 1
-#endif
-#ifndef MPH_DIAG_SEARCH
-#define MPH_DIAG_SEARCH 0   // diagnostic builds only: 1 = stage but test nothing, 2 = no staging,
-                            // 4 = waves near a periodic face do nothing
-#endif
-#ifndef MPH_DIAG_CHUNK
-#define MPH_DIAG_CHUNK 0   // diagnostic builds only: the search buffers 4 stored entries per lane in LDS
-                           // and writes 16-byte chunks ([k / 4][lane][4] in the tile's unused upper
-                           // half; the passes read stale rows, as with MPH_DIAG_NOSTORE=1: timing only)
-#endif
-#ifndef MPH_DIAG_NOSTORE
-#define MPH_DIAG_NOSTORE 0   // diagnostic builds only: 1 = the search counts but stores no list,
-                             // 2 = every store goes to the lane's row 0 (same instructions, no list traffic)
-#endif
-#ifndef MPH_DIAG_GATHER
-#define MPH_DIAG_GATHER 0   // diagnostic builds only: 1 = list passes gather a dummy neighbour that does
-                            // not depend on the entry (j = lane id ^ 1; hipcc hoists those loads out of
-                            // the loop, so this times the passes without gathers), 2 = gathers only
-#endif
+// Tuning parameters (A/B builds: tools/ab.sh).  The rejected variants of rounds 1-5 (staged pass A,
+// row spreading, CU-affine tiles, paired / half-wave / compact 16-bit lists, chunked search, cache-
+// policy hints, record planes for pass A, block totals from k_prep, the diagnostic builds) were
+// removed in round 6; they are kept under the git tag r05-variants (profiles/r05/README.md).
 #ifndef MPH_SB
 // candidates per batch in the search: 2 (64 VGPRs) with the LDS capacity below gives 8 waves per
 // SIMD (round 3: D1M 0.355 -> 0.347 ms, D16M 4.11 -> 3.86, profiles/r03/search/sb2/); 3 took
 // 72 VGPRs and 7 waves (round 2: 0.395 ms against 0.433 at 4)
 #define MPH_SB 2
 #endif
-#ifndef MPH_SEARCH_LDS
-#define MPH_SEARCH_LDS 1
-#endif
-#ifndef MPH_PREP_RUNS
-#define MPH_PREP_RUNS 1   // k_prep: one cell-histogram atomic per run of equal keys in a wave
-#endif
 #ifndef MPH_LDS_CAP
-// candidates staged per wave and stencil column: 176 keeps a wave's staging at 5,072 B, so 32
-// waves (8 per SIMD) fit the 160 KB of LDS; wider windows take the global-gather loop
+// staging area per wave and stencil column, in FP64 candidates: 176 keeps a wave's staging at
+// 5,072 B, so 32 waves (8 per SIMD) fit the 160 KB of LDS; it holds 313 of the 16-byte FP32
+// records (kCap32), wider windows take the global-gather loop
 #define MPH_LDS_CAP 176
-#endif
-#ifndef MPH_BAND_MASK
-#define MPH_BAND_MASK 1   // scan_candidates_lds: the FP32 band's lanes selected by its wave mask
-#endif
-#ifndef MPH_COLR_LEAN
-#define MPH_COLR_LEAN 1   // scan_candidates_lds: the column ranges in fewer operations (same bounds)
-#endif
-#ifndef MPH_SPLIT32
-#define MPH_SPLIT32 1   // a wave across two cell rows stages its two runs of FP32 records (scan_candidates_lds)
-#endif
-#ifndef MPH_STAGE_CPOL
-#define MPH_STAGE_CPOL 0   // cache policy of the search's FP32 record staging loads (2: non-temporal)
-#endif
-#ifndef MPH_CHUNK_BUILD
-#define MPH_CHUNK_BUILD 0   // the chunked search + pass A (MPH_CHUNKS, measured and rejected)
-#endif
-#ifndef MPH_LIST_CPOL
-#define MPH_LIST_CPOL 0   // cache policy of the search's list stores (FP32 path)
-#endif
-#ifndef MPH_CAP32
-#define MPH_CAP32 1   // FP32-record windows up to the staging area's 16-byte capacity (313 at 176)
-#endif
-
-#if defined(MPH_LIST_SPREAD) && MPH_LIST_SPREAD && defined(MPH_PA_STAGED) && MPH_PA_STAGED
-#error "MPH_LIST_SPREAD lists hold sentinels the staged pass A does not skip"
-#endif
-#ifndef MPH_PA_STAGED
-// pass A of the interior waves in a kernel of its own (k_pass_a_st) that reads each stencil column's
-// window of 48-byte records from LDS, staged once per wave (the search writes the windows per wave:
-// kWinHdr), instead of per-lane gathers through L1; its lean register budget buys the occupancy that
-// hides the staging round trips (measured, opt-in)
-#define MPH_PA_STAGED 0
-#endif
-#ifndef MPH_SEARCH_F32
-// the search stages 16-byte FP32 candidate records {x, y, z, type} (Soa.f4, written by
-// k_rank_scatter) instead of 28 bytes of FP64 x, y, z and type, and decides in FP32 outside a band
-// around the cutoff wide enough for the records' rounding (DevParams.rc2f_lo/hi, set_uniforms);
-// inside it the FP64 test on the global positions decides, so the lists are identical (D1M search
-// -7.5 %, profiles/r04/search_f32/)
-#define MPH_SEARCH_F32 1
-#endif
-#ifndef MPH_DIAG_PA
-#define MPH_DIAG_PA 0   // diagnostic builds: the staged pass A checks it used every entry (DevState.overflow 32)
-#endif
-#ifndef MPH_PA_CAP
-#define MPH_PA_CAP 128   // records staged per column window (6 KB per wave; MPH_PAS_WPE waves per SIMD)
 #endif
 
 namespace mph {
@@ -149,31 +76,20 @@ __device__ __forceinline__ __attribute__((address_space(3))) void* lds_ptr(void*
 // A 4-byte load through a buffer descriptor that hipcc does not count (the search's start[]
 // loads, scan_candidates_lds): no s_waitcnt is emitted for it, so the caller waits for it with an
 // explicit vmcnt(0) on every path before start_landed() and the first use of the value.
-#ifndef MPH_START_ASM
-#define MPH_START_ASM 1   // 0: plain buffer loads hipcc counts (it then waits for them early)
-#endif
-#ifndef MPH_DIAG_BOUNDS
-#define MPH_DIAG_BOUNDS 0   // diagnostic builds: the search checks its column windows (DevState.overflow 8)
-#endif
 // Both bounds of a column range in one statement: the descriptor may come from SGPRs that a VALU
 // instruction (v_readlane of an SGPR spill) has just written, which a VMEM instruction may read only
 // 5 wait states later (hipcc pads only what it sees: s_nop 4 opens the string).
 __device__ __forceinline__ void start_load2(__amdgpu_buffer_rsrc_t r, unsigned ob, unsigned oe, int& b, int& e)
 {
-    if (MPH_START_ASM) {
-        asm volatile("s_nop 4\n\tbuffer_load_dword %0, %2, %4, 0 offen\n\tbuffer_load_dword %1, %3, %4, 0 offen"
-                     : "=&v"(b), "=&v"(e) : "v"(ob), "v"(oe), "s"(r) : "memory");
-    } else {
-        b = __builtin_amdgcn_raw_buffer_load_b32(r, ob, 0, 0);
-        e = __builtin_amdgcn_raw_buffer_load_b32(r, oe, 0, 0);
-    }
+    asm volatile("s_nop 4\n\tbuffer_load_dword %0, %2, %4, 0 offen\n\tbuffer_load_dword %1, %3, %4, 0 offen"
+                 : "=&v"(b), "=&v"(e) : "v"(ob), "v"(oe), "s"(r) : "memory");
 }
 // marks the start_load2 results as landed: no consumer is scheduled above this point
 __device__ __forceinline__ void start_landed(int& a, int& b) { asm volatile("" : "+v"(a), "+v"(b)); }
 
-// LDS staging of one wavefront in the search: x, y, z (stage_d doubles each, 16-byte aligned and
-// large enough for a 16-byte-aligned window of CAP candidates plus the SB-entry batch over-read),
-// then the types (stage_t ints, 4-aligned window).  Doubles per wave: stage_words.
+// LDS staging area of one wavefront in the search, in doubles: sized as the FP64 staging of CAP
+// candidates (x, y, z: stage_d doubles each, types: stage_t ints) of rounds 1-4, which it holds the
+// FP32 records of (16 bytes each, scan_candidates_lds kCap32).
 __host__ __device__ constexpr int stage_d(int cap, int sb) { return (cap + sb + 2 + 1) & ~1; }
 __host__ __device__ constexpr int stage_t(int cap, int sb) { return (cap + sb + 8 + 3) & ~3; }
 __host__ __device__ constexpr int stage_words(int cap, int sb) { return 3 * stage_d(cap, sb) + stage_t(cap, sb) / 2; }
@@ -334,42 +250,6 @@ __device__ __forceinline__ int xcd_block(int b, int nb)
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
 }
 
-#if MPH_DIAG_XCD
-// Diagnostic build: each wave of a list kernel records, from lane 0 at whichever return it takes,
-// its start and end (wall_clock64, 100 MHz) into DevState.xcd_diag[kernel][.][XCC_ID].
-struct XcdProbe {
-    unsigned long long* d;
-    unsigned long long t0;
-    unsigned long long* log;
-    int log_n;
-    __device__ XcdProbe(const DevState* st, int k)
-        : d(st ? &const_cast<DevState*>(st)->xcd_diag[k][0][0] : nullptr), t0(wall_clock64()),
-          log(st && k == 0 ? st->wave_log : nullptr), log_n(st ? st->wave_log_n : 0) {}
-    __device__ ~XcdProbe()
-    {
-        if (d && __lane_id() == 0) {
-            const unsigned long long t1 = wall_clock64();
-            const int x = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7;   // HW_REG_XCC_ID[3:0]
-            atomicMin(d + x, t0);
-            atomicMax(d + 8 + x, t1);
-            atomicAdd(d + 16 + x, t1 - t0);
-            atomicAdd(d + 24 + x, 1ull);
-            if (MPH_DIAG_XCD >= 2 && log) {   // the search's waves, one record each
-                const int slot = (int)blockIdx.x * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
-                if (slot < log_n) {
-                    log[3 * (size_t)slot] = t0;
-                    log[3 * (size_t)slot + 1] = t1;
-                    log[3 * (size_t)slot + 2] = (unsigned long long)x;
-                }
-            }
-        }
-    }
-};
-#define XCD_PROBE(st, k) XcdProbe xcd_probe_((st), (k))
-#else
-#define XCD_PROBE(st, k)
-#endif
-
 // Particles held by this context: exact on a single GPU; in slab mode the device-resident count
 // of the last redistribution (P.n is then only the capacity the grids are sized for).
 __device__ __forceinline__ int dev_n(const DevParams& P) { return P.n_dev ? *P.n_dev : P.n; }
@@ -397,23 +277,13 @@ __device__ __forceinline__ int list_blocks(int n) { return (n + MPH_LB - 1) / MP
 // The search itself keeps the equal ranges: its cost follows the candidates it scans, not the
 // lists it writes (balanced by list length it ran 8 % slower at D1M; by the previous step's wave
 // durations all three kernels oscillated, profiles/r03/xcd_balance/).
-#ifndef MPH_XCD_BAL
-#define MPH_XCD_BAL 1
-#endif
-#ifndef MPH_XCD_SAMPLE
-#define MPH_XCD_SAMPLE 1   // 1 of this many waves adds to the histogram (weighted)
-#endif
 constexpr int kWaveCost = 16;   // a wave's fixed cost, in list entries, for the work histogram
 
-#if MPH_CU_AFFINE
-__device__ int cu_affine_tile(DevState* st, int kern, int lo, int len);
-#endif
-// kern (MPH_CU_AFFINE builds): 1 pass A, 2 pass B -- the CU-affine claim inside the XCD range
-__device__ __forceinline__ int list_block(const DevState* st, int n, int kern = -1)
+__device__ __forceinline__ int list_block(const DevState* st, int n)
 {
     const int nb = list_blocks(n);
     const int b = blockIdx.x;
-    if (MPH_XCD_BAL && st) {
+    if (st) {
         const int* fr = st->xcd_frac;
         const int cap = gridDim.x >> 3;
         const int j = b & 7;
@@ -427,9 +297,6 @@ __device__ __forceinline__ int list_block(const DevState* st, int n, int kern = 
             lo = hi;
         }
         if (ok) {
-#if MPH_CU_AFFINE
-            if (kern >= 0) return cu_affine_tile(const_cast<DevState*>(st), kern, mine_lo, mine_c);
-#endif
             const int q = b >> 3;
             return q < mine_c ? mine_lo + q : -1;
         }
@@ -437,76 +304,17 @@ __device__ __forceinline__ int list_block(const DevState* st, int n, int kern = 
     return b < nb ? xcd_block(b, nb) : -1;
 }
 
-// Chunked search + pass A (Launch.chunks > 1, launch_search_pass_a; builds with MPH_CHUNK_BUILD=1
-// only, measured and rejected: profiles/r05/chunks_rejected/): launch c of C takes piece c
-// of every XCD's contiguous range of the equal map (xcd_block), so pass A of piece c, on a second
-// stream, runs beside the search of piece c + 1 and the XCDs keep their own ranges.
-// ck = c << 8 | C; returns the block's tile of MPH_LB particles or -1.
-__device__ __forceinline__ int chunk_block(int b, int nb, int ck)
-{
-    const int C = ck & 0xff, c = ck >> 8;
-    const int xcd = b & 7;
-    const int q = nb >> 3, r = nb & 7;
-    const int len = xcd < r ? q + 1 : q;
-    const int lo = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-    const int p0 = (int)(((long long)len * c) / C), p1 = (int)(((long long)len * (c + 1)) / C);
-    const int k = b >> 3;
-    return k < p1 - p0 ? lo + p0 + k : -1;
-}
-
-#if MPH_CU_AFFINE
-// CU-affine tile claim (MPH_CU_AFFINE): the logical XCD j = blockIdx & 7 keeps its contiguous range
-// [lo, lo + len) of tiles, split into kCuQueues contiguous queues; a block takes the next tile of
-// the queue of the CU it runs on (hardware HW_ID: CU, SH, SE), else steals from the other queues of
-// its XCD, so the four blocks resident on a CU work on neighbouring tiles (shared L1 lines) instead
-// of tiles 32 blocks apart.  Every block first takes a ticket; a launch's blocks all take one, so
-// ticket / gridDim is the launch's generation, which tags the queue counters (a stale counter is
-// reset by compare-and-swap): no reset pass, and each tile is claimed exactly once.  Returns the
-// block's tile or -1 (block-uniform, through LDS).
-__device__ int cu_affine_tile(DevState* st, int kern, int lo, int len)
-{
-    __shared__ int s_tile;
-    if (threadIdx.x == 0) {
-        const unsigned long long t = atomicAdd(&st->cu_tick[kern], 1ull);
-        const unsigned gen = (unsigned)(t / gridDim.x);
-        const int j = blockIdx.x & 7;
-        const unsigned hw = __builtin_amdgcn_s_getreg((7 << 11) | (8 << 6) | 4);   // HW_ID[15:8]: CU, SH, SE
-        const int q0 = (int)(hw % kCuQueues);
-        int tile = -1;
-        for (int r = 0; r < kCuQueues && tile < 0; ++r) {
-            const int q = (q0 + r) % kCuQueues;
-            const int a = lo + (int)(((long long)len * q) / kCuQueues);
-            const int b = lo + (int)(((long long)len * (q + 1)) / kCuQueues);
-            if (b <= a) continue;
-            unsigned long long* Q = &st->cu_q[kern][j][q];
-            unsigned long long v = __hip_atomic_load(Q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            while ((unsigned)(v >> 32) != gen) {
-                const unsigned long long w = atomicCAS(Q, v, (unsigned long long)gen << 32);
-                v = w == v ? (unsigned long long)gen << 32 : w;
-            }
-            if ((int)(unsigned)v >= b - a) continue;   // exhausted (no increment past it)
-            const unsigned long long old = atomicAdd(Q, 1ull);
-            const int k = (int)(unsigned)old;
-            if ((unsigned)(old >> 32) == gen && k < b - a) tile = a + k;
-        }
-        s_tile = tile;
-    }
-    __syncthreads();
-    return s_tile;
-}
-#endif
-
 // The search's contribution to the work histogram: its wave's longest list (all lanes converged;
 // one atomic per wave, spread over the 4096 runs).
 __device__ __forceinline__ void add_wave_work(DevState* st, int cnt, int i, int n)
 {
-    if (!MPH_XCD_BAL || !st) return;
+    if (!st) return;
     int m = cnt;
     for (int o = 32; o; o >>= 1) m = max(m, __shfl_xor(m, o));
     const int tile = __builtin_amdgcn_readfirstlane(i >> 6);
     const int ntile = (n + 63) >> 6;
-    if ((threadIdx.x & 63) == 0 && tile < ntile && tile % MPH_XCD_SAMPLE == 0)
-        atomicAdd(&st->seg_work[(int)(((long long)tile * kXcdSegs) / ntile)], (m + kWaveCost) * MPH_XCD_SAMPLE);
+    if ((threadIdx.x & 63) == 0 && tile < ntile)
+        atomicAdd(&st->seg_work[(int)(((long long)tile * kXcdSegs) / ntile)], m + kWaveCost);
 }
 
 __device__ __forceinline__ int nbr_entry(int j, int type) { return j | (type << kTypeShift); }
@@ -519,63 +327,19 @@ constexpr int kListKeep = 256 + (1 << 18), kListTotal = 1 << 18, kSoffMask = 0x1
 __device__ __forceinline__ int soff_total(int soff) { return (int)((unsigned)soff >> 18); }
 __device__ __forceinline__ int soff_stored(int soff) { return (soff >> 8) & 0x3FF; }
 
-// MPH_PA_STAGED: a wave's column windows {mn, mx} for pass A (kWinCols of them) and its format flag
-// (entry kWinCols: 1 = written by the staged search), kWinHdr int2 per wave (Launch.whdr)
-constexpr int kWinCols = kGroups * kGroups;   // 3-D stencil columns (2-D uses the first kGroups)
+// Pass B's gather record {x, y, z, PressureP} (Launch.rec) lives in two 16-byte planes: {x, y} of
+// particle j at [j], {z, P} at [ps + j], ps = the array capacity (DevParams.n).  A 16-byte gather
+// instruction of a wavefront then reads one plane: 64 lanes whose neighbours are consecutive
+// particles touch 1 KB (8 lines of 128 B) instead of 2 KB of whole records (same box: D1M pass B
+// 0.271 -> 0.251 ms, D16M 2.89 -> 2.66 ms, profiles/r05/planes/).  Pass A's 48-byte records
+// {x, y, z, vx, vy, vz} (Soa.p6) stay whole: in three planes pass A lost (0.376 -> 0.446 ms).
 
-// The gather records of the list passes -- pass A's {x, y, z, vx, vy, vz} (Soa.p6) and pass B's
-// {x, y, z, PressureP} (Launch.rec) -- can be split into 16-byte planes: piece k of particle j at
-// [k * ps + j], ps = the array capacity (DevParams.n).  A 16-byte gather instruction of a wavefront
-// then reads one plane: 64 lanes whose neighbours are consecutive particles touch 1 KB (8 lines of
-// 128 B) instead of 2-3 KB of whole records, the same instruction count, but a record's pieces now
-// come from 2-3 lines instead of 1-2.  Measured same box (profiles/r05/planes/): pass B's 32-byte
-// records gain (D1M 0.271 -> 0.251 ms, D16M 2.89 -> 2.66 ms: MPH_PLANES, default on), pass A's
-// 48-byte ones lose (0.376 -> 0.446 ms at rest, 0.510 -> 0.543 developed, D16M 3.81 -> 4.37 ms:
-// MPH_P6_PLANES, default off).
-#ifndef MPH_PLANES
-#define MPH_PLANES 1
-#endif
-#ifndef MPH_P6_PLANES
-#define MPH_P6_PLANES 0
-#endif
-// MPH_P6_PLANES=2: {x, y, z, vx} as 32-byte records, {vy, vz} in a 16-byte plane behind them
-__device__ __forceinline__ size_t p6_at(int ps, int j, int k)
+// Velocity of sorted particle i for the list passes, from its gather record {x, y, z, vx, vy, vz}
+// (k_rank_scatter then skips the SoA velocity stores).
+__device__ __forceinline__ void own_velocity(const Soa& A, int i, double& vx, double& vy, double& vz)
 {
-    if (MPH_P6_PLANES == 2) return k < 2 ? 2 * (size_t)j + k : 2 * (size_t)ps + j;
-    return MPH_P6_PLANES ? (size_t)k * ps + j : 3 * (size_t)j + k;
-}
-static_assert(!(MPH_PA_STAGED && MPH_P6_PLANES == 2), "the staged pass A stages whole records or three planes");
-
-// Velocity of sorted particle i for the list passes: from its gather record {x, y, z, vx, vy, vz}
-// (k_rank_scatter then skips the SoA velocity stores), or the SoA arrays.  ps: DevParams.n.
-__device__ __forceinline__ void own_velocity(const Soa& A, int i, double& vx, double& vy, double& vz, int ps)
-{
-    if (MPH_AOS_GATHER && A.p6) {
-        const double2 b = A.p6[p6_at(ps, i, 1)], c = A.p6[p6_at(ps, i, 2)];
-        vx = b.y; vy = c.x; vz = c.y;
-    } else {
-        vx = A.vx[i]; vy = A.vy[i]; vz = A.vz[i];
-    }
-}
-
-// The ELL list is written once per step and read once per pass.  MPH_LIST_NT=1 makes the pass
-// reads non-temporal (D1M: pass A -1 %, within noise); non-temporal list *stores* in the search
-// lose the write combining of the scattered 4-byte entries (search 0.41 -> 0.77 ms), so the
-// stores stay plain.
-#ifndef MPH_LIST_NT
-#define MPH_LIST_NT 0
-#endif
-__device__ __forceinline__ int list_load(const int* p)
-{
-    return MPH_LIST_NT ? __builtin_nontemporal_load(p) : *p;
-}
-#ifndef MPH_LIST_NT_STORE
-#define MPH_LIST_NT_STORE 0
-#endif
-__device__ __forceinline__ void list_store(int* p, int v)
-{
-    if (MPH_LIST_NT_STORE) __builtin_nontemporal_store(v, p);
-    else *p = v;
+    const double2 b = A.p6[3 * (size_t)i + 1], c = A.p6[3 * (size_t)i + 2];
+    vx = b.y; vy = c.x; vz = c.y;
 }
 
 __device__ __forceinline__ const int* ell_row(const int* nbr, int i)
@@ -583,118 +347,35 @@ __device__ __forceinline__ const int* ell_row(const int* nbr, int i)
     return nbr + (size_t)(i >> 6) * kTileStride + (i & 63);
 }
 
-// entry k of a lane from the lane's ell_row pointer (ell_slot: rows or pairs)
-template <typename T>
-__device__ __forceinline__ T* ell_at(T* row, int lane, int k)
+// entry k of a lane from the lane's ell_row pointer: row k of the wave's tile
+__device__ __forceinline__ const int* ell_at(const int* row, int lane, int k)
 {
     return row - lane + ell_slot(k, lane);
 }
 
-// the byte offset of a store slot in the wave's tile from the search's soff = k << 8 | lane << 2
-__device__ __forceinline__ unsigned ell_byte(unsigned soff)
-{
-    constexpr unsigned kLow = (unsigned)((1 << kListLg) - 1);
-    static_assert(kMaxNeighbor == 512, "half-wave rows: the upper half starts at 512 * 128 bytes");
-    if (kListHalf) return ((soff & 0x1FF00u) >> 1) | (soff & 0x7Cu) | ((soff & 0x80u) << 9);
-    return kListPairs ? ((soff & 0x1FF00u & ~(kLow << 8)) | ((soff & 0xFCu) << kListLg) | ((soff >> 6) & (kLow << 2)))
-                      : soff;
-}
-
-// Compact neighbour list (MPH_LIST16, the default for interior waves).  The stencil's columns
-// fall into kGroups groups (3-D: the 2 kReach + 1 columns of one slowest-axis offset, which are
-// consecutive in cell order; 2-D: each column), so every neighbour of a group lies in a short
-// index range from the group's wave-wide first candidate.  Entry k of a lane is 16 bits -- the
-// offset from its group's base (13 bits) and the neighbour's type (3 bits) -- two entries per
-// 32-bit word at word[k / 2][lane] of the wave's tile (same order as the ELL row, so sums are
-// bit-identical).  Per wave the header (kLhdr ints) holds the group bases, the format flag
-// (kHdrFlag; 1 = compact, 0 = the 32-bit ELL row: waves near a periodic face or whose group
-// ranges are too long) and, per lane, the count at the end of every group but the last (bytes; a
-// wave with more than 255 neighbours on a
-// lane, which the reference allows up to 511, is searched again into ELL rows: k_neighbors REDO).  Half the list bytes of the ELL rows.
-#ifndef MPH_LIST16
-#define MPH_LIST16 1
-#endif
-constexpr int kOff16 = 13;                  // offset bits of a compact entry (type above)
-constexpr int kSpan16 = (1 << kOff16) - 1;  // longest group range a compact wave may have
-
-#ifndef MPH_GB_LDS
-#define MPH_GB_LDS 1   // group base of an entry read from LDS (else a select tree)
-#endif
-static_assert(kTile == 64, "list rows are addressed as (k << 8) | (lane << 2) bytes");
-
+// The wave's ELL tile and the lane: entry k of the lane at row k, by a 32-bit byte offset from the
+// tile's (SGPR) base -- one shift-or per entry instead of 64-bit address arithmetic.
 struct NbrList {
-    const int* tile;                // the wave's list tile (wave-uniform)
+    const int* tile;   // the wave's list tile (wave-uniform)
     int lane;
-    const int* gb;                  // the wave's group bases, staged in LDS (kGroups ints)
-    int b[kGroups];                 // the same, wave-uniform (MPH_GB_LDS=0: selected by compares)
-    // the lane's counts at the ends of groups 0-3 and 4-5, one byte each (<= 127; unused bytes 127)
-    unsigned ends, ends2;
-    bool c16;                       // wave-uniform format flag
 };
 
-// sb: kGroups ints of LDS for this wave.  Every active lane stores the (wave-uniform) bases, so
-// the lanes that have already left do not matter.
-__device__ __forceinline__ NbrList nbr_list(const int* nbr, const int* lhdr, int i, int* sb)
+__device__ __forceinline__ NbrList nbr_list(const int* nbr, int i)
 {
     NbrList L;
-    const int tile = __builtin_amdgcn_readfirstlane(i >> 6);
-    L.tile = nbr + (size_t)tile * kTileStride;
+    L.tile = nbr + (size_t)__builtin_amdgcn_readfirstlane(i >> 6) * kTileStride;
     L.lane = i & 63;
-    L.gb = sb;
-    const int* h = lhdr ? lhdr + (size_t)tile * kLhdr : nullptr;
-    L.c16 = MPH_LIST16 && h && h[kHdrFlag] == 1;
-    L.ends = L.ends2 = 0x7F7F7F7Fu;
-#pragma unroll
-    for (int g = 0; g < kGroups; ++g) L.b[g] = 0;
-    if (L.c16) {
-#pragma unroll
-        for (int g = 0; g < kGroups; ++g) {
-            L.b[g] = h[g];
-            if (MPH_GB_LDS) sb[g] = h[g];
-        }
-        if (MPH_GB_LDS) __builtin_amdgcn_wave_barrier();
-        L.ends = (unsigned)h[8 + (i & 63)];
-        if (kGroups > 5) L.ends2 = (unsigned)h[8 + 64 + (i & 63)];
-    }
     return L;
 }
 
-// entry k of the lane: neighbour index j and type t.  The group of entry k is the number of
-// group ends <= k: with k and the ends below 128, (k | 0x80) - end per byte keeps its top bit
-// exactly when k >= end, so two subtractions and popcounts count them for all 6 ends at once.
-template <bool C16>
+// entry k of the lane: neighbour index j and type t
 __device__ __forceinline__ void nbr_at(const NbrList& L, int k, int& j, int& t)
 {
-    if (C16) {
-        const unsigned w = reinterpret_cast<const unsigned*>(L.tile)[(k >> 1) * kTile + L.lane];
-        const unsigned e = (k & 1) ? (w >> 16) : (w & 0xFFFFu);
-        const unsigned kk = ((unsigned)k * 0x01010101u) | 0x80808080u;
-        int g = __popc((kk - L.ends) & 0x80808080u);
-        if (kGroups > 5) g += __popc((kk - L.ends2) & 0x80808080u);
-        int b;
-        if (MPH_GB_LDS) {
-            b = L.gb[g];
-        } else {   // binary select tree over the uniform bases
-            const int s0 = (g & 1) ? L.b[1] : L.b[0];
-            const int s1 = (g & 1) ? L.b[3] : L.b[2];
-            const int s2 = (g & 1) ? L.b[kGroups > 5 ? 5 : 4] : L.b[4];
-            const int s3 = L.b[kGroups - 1];
-            const int t0 = (g & 2) ? s1 : s0;
-            const int t1 = (g & 2) ? s3 : s2;
-            b = (g & 4) ? t1 : t0;
-        }
-        j = b + (int)(e & kSpan16);
-        t = (int)(e >> kOff16);
-    } else {
-        // row k of the wave's tile by a 32-bit byte offset from its (SGPR) base: one shift-or per
-        // entry instead of 64-bit address arithmetic
-        using gcchar = const __attribute__((address_space(1))) char;
-        using gcint = const __attribute__((address_space(1))) int;
-        gcint* p = (gcint*)((gcchar*)L.tile + ((unsigned)ell_slot(k, L.lane) << 2));
-        const int e = MPH_LIST_NT ? __builtin_nontemporal_load(p) : *p;
-        j = e & kIndexMask;
-        t = e >> kTypeShift;
-    }
+    using gcchar = const __attribute__((address_space(1))) char;
+    using gcint = const __attribute__((address_space(1))) int;
+    const int e = *(gcint*)((gcchar*)L.tile + ((unsigned)ell_slot(k, L.lane) << 2));
+    j = e & kIndexMask;
+    t = e >> kTypeShift;
 }
 
 // ------------------------------------------------------------------------- sort phase -------
@@ -792,23 +473,15 @@ constexpr int kScanThreads = 256;
 #define MPH_SCAN_ITEMS 16
 #endif
 constexpr int kScanItems = MPH_SCAN_ITEMS;   // cells per thread (a multiple of 4)
-constexpr int kScanBlock = kScanThreads * kScanItems;   // 4096 cells per block (bsum arrays: ncell / 4096 + 2)
-// Block totals of the cell histogram from k_prep (MPH_PREP_BSUM, default): one atomic per run of equal
-// 4096-cell blocks among a wavefront's lanes adds the run's particles to the step's totals, so the
-// scan needs no k_scan_reduce pass over the whole histogram.  The totals live in two buffers of
-// bsum_stride(ncell) ints selected by the step's parity (DevState.seam_step, advanced by k_place):
-// k_prep adds into this step's buffer, k_scan_down reads it and clears the other one (all of its
-// blocks, so every entry a later k_prep can reach is zero), and mph_create zeroes both.
-#ifndef MPH_PREP_BSUM
-#define MPH_PREP_BSUM 0   // opt-in: same-box A/B D16M -0.3 %, D1M +0.3 % (profiles/r05/prep_bsum/)
-#endif
+constexpr int kScanBlock = kScanThreads * kScanItems;   // 4096 cells per block
+// ints of the scan's block totals (mph_ctx.hip allocates them)
 __host__ __device__ inline int bsum_stride(int ncell) { return ncell / kScanBlock + 2; }
-static_assert(kScanBlock == 4096, "mph_ctx.hip sizes the bsum buffers for 4096-cell blocks");
+static_assert(kScanBlock == 4096, "mph_ctx.hip sizes the bsum buffer for 4096-cell blocks");
 
 // The XCD split of the list passes (see list_block) from the search's work histogram: an inclusive
 // scan of the runs' work (kXcdSegs / blockDim.x consecutive runs per thread), the 7 inner cut
 // points at equal shares of the total (interpolated inside their run), then the histogram cleared.
-// One whole block calls it (k_xcd_split, or block 0 of k_prep with MPH_SPLIT_IN_PREP).
+// Block 0 of the next step's k_rank_scatter calls it (see there).
 template <int T>
 __device__ __forceinline__ void xcd_split_block(DevState* st)
 {
@@ -853,27 +526,16 @@ __device__ __forceinline__ void xcd_split_block(DevState* st)
     for (int r = 0; r < R; ++r) st->seg_work[t * R + r] = 0;
 }
 
-// MPH_SPLIT_IN_PREP: the split runs in block 0 of one of the next step's sort kernels (1: k_prep,
-// 2: k_rank_scatter, the longest, where it hides best), from the previous step's search (a wave's
-// work changes little from one step to the next, and the map only decides which block handles
-// which wave), so no launch of its own sits between the search and pass A; 0: k_xcd_split after
-// the search
-#ifndef MPH_SPLIT_IN_PREP
-#define MPH_SPLIT_IN_PREP 2
-#endif
-
 __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __restrict__ st, Soa C,
                                               int* __restrict__ key, int* __restrict__ slot,
-                                              int* __restrict__ cnt, int mode, VSrc vs,
-                                              int* __restrict__ bsum2, int split)
+                                              int* __restrict__ cnt, int mode, VSrc vs)
 {
-    if (MPH_SPLIT_IN_PREP == 1 && split && blockIdx.x == 0) xcd_split_block<256>(const_cast<DevState*>(st));
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     const int n = dev_n(P);
     Soa B = C;
     bool mig = false;
     const int b = p < n ? vsrc_entry(vs, C, p, B, mig) : p;
-    if (MPH_PREP_RUNS) {
+    {
         // The particles arrive in the previous cell order, so consecutive lanes often share a
         // cell: one histogram atomic per run of equal keys (slot = run base + rank in the run).
         // Every lane of the wave takes part in the shuffles; lanes past n form runs of their own.
@@ -900,17 +562,6 @@ __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __res
         if (live && head) base = atomicAdd(&cnt[k], next - lane);
         base = __shfl(base, hl, 64);
         if (live) slot[p] = base + (lane - hl);
-        if (bsum2) {
-            // this step's block totals: one atomic per run of equal 4096-cell blocks (dead lanes
-            // past n carry distinct negative blocks, so they never join a live run nor add)
-            int* bsum = bsum2 + (st->seam_step & 1) * bsum_stride(P.ncell);
-            const int blk = live ? k / kScanBlock : k;
-            const int bprev = __shfl_up(blk, 1, 64);
-            const bool bhead = lane == 0 || bprev != blk;
-            const unsigned long long babove = __ballot(bhead) & ~upto;
-            const int bnext = babove ? __ffsll((long long)babove) - 1 : 64;
-            if (live && bhead) atomicAdd(&bsum[blk], bnext - lane);
-        }
         // the block's face bits: OR-ed in LDS, then one device atomic per block, only for bits the
         // step's word does not hold yet (few blocks: the particles near a periodic face)
         __shared__ int s_occ;
@@ -927,25 +578,11 @@ __global__ __launch_bounds__(256) void k_prep(DevParams P, const DevState* __res
             const int cur = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (s_occ & ~cur) atomicOr(w, s_occ);
         }
-        return;
-    }
-    if (p >= n) return;
-    double x = B.x[b], y = B.y[b], z = B.z[b];
-    if (mode == 1) move_and_wrap(P, st, B, b, x, y, z);
-    if (!isfinite(x + y + z)) atomicOr(const_cast<int*>(&st->overflow), 4);   // MPH_ERR_NONFINITE
-    const int k = cell_id(P, x, y, z);
-    key[p] = k;
-    slot[p] = atomicAdd(&cnt[k], 1);
-    if (bsum2) atomicAdd(&bsum2[(st->seam_step & 1) * bsum_stride(P.ncell) + k / kScanBlock], 1);
-    const int occ = seam_bits(P, x, y, z);
-    if (occ) {
-        int* w = const_cast<int*>(&st->seam_occ[st->seam_step & 1]);
-        if (occ & ~__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicOr(w, occ);
     }
 }
 
-// Exclusive scan of the cell histogram (constants above k_prep): block totals (k_prep's atomics, or
-// a k_scan_reduce launch), the top-level scan (inside k_scan_down up to kScanFusedTop blocks, else a
+// Exclusive scan of the cell histogram (constants above k_prep): block totals (k_scan_reduce), the
+// top-level scan (inside k_scan_down up to kScanFusedTop blocks, else a
 // k_scan_top launch) and the down-sweep.
 
 __device__ __forceinline__ int block_exclusive_scan(int v, int* lds, int& total)
@@ -1004,11 +641,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const int* __restr
     if (threadIdx.x == 0) bsum[blockIdx.x] = total;
 }
 
-// st non-null: bsum is the pair of parity buffers of MPH_PREP_BSUM (this step's is scanned)
-__global__ __launch_bounds__(1024) void k_scan_top(int* __restrict__ bsum, int nb, const DevState* __restrict__ st,
-                                                   int stride)
+__global__ __launch_bounds__(1024) void k_scan_top(int* __restrict__ bsum, int nb)
 {
-    if (st) bsum += (st->seam_step & 1) * stride;
     // each thread a run of R consecutive totals: its sum, one block scan of the sums, then the
     // run's exclusive prefixes (one round trip to memory instead of nb / blockDim.x of them)
     __shared__ int lds[16];
@@ -1037,17 +671,9 @@ constexpr int kScanFusedTop = MPH_SCAN_FUSED_TOP;
 __global__ __launch_bounds__(kScanThreads) void k_scan_down(int* __restrict__ cnt, int ncell,
                                                             const int* __restrict__ bsum,
                                                             int* __restrict__ start, int n,
-                                                            const int* __restrict__ n_dev, int top,
-                                                            const DevState* __restrict__ st, int stride)
+                                                            const int* __restrict__ n_dev, int top)
 {
     __shared__ int lds[kScanThreads / 64];
-    if (st) {
-        // MPH_PREP_BSUM: this step's totals (from k_prep's atomics); the other parity's entry of this
-        // block is cleared for the next step's k_prep (nothing reads it during this step)
-        const int par = st->seam_step & 1;
-        if (threadIdx.x == 0) const_cast<int*>(bsum)[(par ^ 1) * stride + blockIdx.x] = 0;
-        bsum += par * stride;
-    }
     const int base = blockIdx.x * kScanBlock + threadIdx.x * kScanItems;
     int v[kScanItems];
     load16(cnt, base, ncell, v);
@@ -1131,7 +757,12 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
                                                       int* __restrict__ rank_of, int* __restrict__ dst_of,
                                                       int mode, VSrc vs, DevState* __restrict__ st, int split)
 {
-    if (MPH_SPLIT_IN_PREP == 2 && split && blockIdx.x == 0) xcd_split_block<256>(st);
+    // The passes' XCD split (list_block) runs here, in block 0 of the longest sort kernel, from
+    // the previous step's search: a wave's work changes little from one step to the next and the
+    // map only decides which block runs which wave, so no launch of its own sits between the
+    // search and pass A (its own launch after the search cost 0.45 % at rest, 0.24 % developed,
+    // profiles/r05/split_in_sort/)
+    if (split && blockIdx.x == 0) xcd_split_block<256>(st);
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= dev_n(P)) return;
     const int k = key[p];
@@ -1145,10 +776,9 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
     A.x[dst] = B.x[b];
     A.y[dst] = B.y[b];
     A.z[dst] = B.z[b];
-    // the sorted velocities are read only through the 48-byte records (own_velocity below), unless
-    // the passes gather SoA (MPH_AOS_GATHER=0), or at a slab context's initialisation sort (mode 0:
-    // dist_init copies the sorted set into B)
-    if (!MPH_AOS_GATHER || !A.p6 || (dst_of && mode == 0)) {
+    // the sorted velocities are read only through the 48-byte records (own_velocity), except at a
+    // slab context's initialisation sort (mode 0: dist_init copies the sorted set into B)
+    if (dst_of && mode == 0) {
         A.vx[dst] = B.vx[b];
         A.vy[dst] = B.vy[b];
         A.vz[dst] = B.vz[b];
@@ -1156,15 +786,11 @@ __global__ __launch_bounds__(256) void k_rank_scatter(DevParams P, const int* __
     A.type[dst] = B.type[b];
     const int id = mig ? -1 - B.id[b] : B.id[b];
     A.id[dst] = id;
-    if (A.p6) {
-        A.p6[p6_at(P.n, dst, 0)] = make_double2(B.x[b], B.y[b]);
-        A.p6[p6_at(P.n, dst, 1)] = make_double2(B.z[b], B.vx[b]);
-        A.p6[p6_at(P.n, dst, 2)] = make_double2(B.vy[b], B.vz[b]);
-    }
-    if (MPH_SEARCH_F32 && A.f4)
-        A.f4[dst] = make_float4((float)(B.x[b] - P.cref[0]), (float)(B.y[b] - P.cref[1]),
-                                (float)(B.z[b] - P.cref[2]), __int_as_float(B.type[b]));
-    if (kListSpread && P.pred) P.pred[dst] = P.pred_src[p];   // the row spread's prediction
+    A.p6[3 * (size_t)dst] = make_double2(B.x[b], B.y[b]);
+    A.p6[3 * (size_t)dst + 1] = make_double2(B.z[b], B.vx[b]);
+    A.p6[3 * (size_t)dst + 2] = make_double2(B.vy[b], B.vz[b]);
+    A.f4[dst] = make_float4((float)(B.x[b] - P.cref[0]), (float)(B.y[b] - P.cref[1]),
+                            (float)(B.z[b] - P.cref[2]), __int_as_float(B.type[b]));
     if (dst_of) dst_of[p] = dst;   // slab mode: ids are global (ghosts negative)
     else if (rank_of) rank_of[id] = dst;
 }
@@ -1273,32 +899,22 @@ struct PassAOut {
 };
 
 // pass B's gather record {x, y, z, PressureP} of sorted particle i (planes {x, y} and {z, P}, see
-// p6_at; ps = DevParams.n), and its PressureP alone (the halo)
+// above; ps = DevParams.n), and its PressureP alone (the halo)
 __device__ __forceinline__ void rec_store(double4* rec, int ps, int i, double x, double y, double z, double p)
 {
-    if (MPH_PLANES) {
-        double2* r = reinterpret_cast<double2*>(rec);
-        r[i] = make_double2(x, y);
-        r[(size_t)ps + i] = make_double2(z, p);
-    } else {
-        rec[i] = make_double4(x, y, z, p);
-    }
+    double2* r = reinterpret_cast<double2*>(rec);
+    r[i] = make_double2(x, y);
+    r[(size_t)ps + i] = make_double2(z, p);
 }
 __device__ __forceinline__ void rec_store_p(double4* rec, int ps, int i, double p)
 {
-    if (MPH_PLANES) reinterpret_cast<double2*>(rec)[(size_t)ps + i].y = p;
-    else rec[i].w = p;
+    reinterpret_cast<double2*>(rec)[(size_t)ps + i].y = p;
 }
 __device__ __forceinline__ void rec_load(const double4* rec, int ps, int j, double& x, double& y, double& z, double& p)
 {
-    if (MPH_PLANES) {
-        const double2* r = reinterpret_cast<const double2*>(rec);
-        const double2 a = r[j], b = r[(size_t)ps + j];
-        x = a.x; y = a.y; z = b.x; p = b.y;
-    } else {
-        const double4 r4 = rec[j];
-        x = r4.x; y = r4.y; z = r4.z; p = r4.w;
-    }
+    const double2* r = reinterpret_cast<const double2*>(rec);
+    const double2 a = r[j], b = r[(size_t)ps + j];
+    x = a.x; y = a.y; z = b.x; p = b.y;
 }
 
 __device__ __forceinline__ void pass_a_finish(const DevParams& P, const DevTables* T, int ti, int i,
@@ -1457,8 +1073,7 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
                         a = r2_exact(q0, q1, q2) <= P.rc2;
                     }
                     if (a && j < je && j != i) {
-                        if (!MPH_DIAG_NOSTORE && cnt < kMaxNeighbor)
-                            list_store(ell_at(out, (int)(threadIdx.x & 63), cnt), nbr_entry(j, A.type[j]));
+                        if (cnt < kMaxNeighbor) out[ell_slot(cnt, 0)] = nbr_entry(j, A.type[j]);
                         ++cnt;
                     }
                 }
@@ -1467,10 +1082,6 @@ __device__ __forceinline__ int scan_candidates(const DevParams& P, const Soa& A,
     }
     return cnt;
 }
-
-#ifndef MPH_DPP_REDUCE
-#define MPH_DPP_REDUCE 1   // wave min/max by DPP row shifts + row broadcasts (else ds_bpermute)
-#endif
 
 // Wave-wide min / max (result in every lane).  DPP form: shifts within 16-lane rows, then
 // row_bcast:15 / :31 carry the partial results across rows (gfx9 family), lane 63 holds the
@@ -1490,31 +1101,17 @@ __device__ __forceinline__ int wave_reduce_dpp(int v)
     return __builtin_amdgcn_readlane(v, 63);
 }
 
-__device__ __forceinline__ int wave_min(int v)
-{
-    if (MPH_DPP_REDUCE) return wave_reduce_dpp<false>(v);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-    return v;
-}
-
-__device__ __forceinline__ int wave_max(int v)
-{
-    if (MPH_DPP_REDUCE) return wave_reduce_dpp<true>(v);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-    return v;
-}
+__device__ __forceinline__ int wave_min(int v) { return wave_reduce_dpp<false>(v); }
+__device__ __forceinline__ int wave_max(int v) { return wave_reduce_dpp<true>(v); }
 
 // The search of a wave whose particles are all interior (FAST): per stencil column the union of
 // the 64 lanes' candidate ranges is one short index range (the lanes are consecutive in cell
 // order, mostly inside one or two cell columns), so the wave stages it in LDS with coalesced
 // loads and every lane then tests its own candidates from LDS.  The global gathers of the
 // per-lane loop cost ~19 L1 tag lookups per load instruction (PMC, profiles/r01) and the
-// texture-address unit was the bound; a staged column costs 4.  Same candidates, same order,
-// same FP64 test as scan_candidates, so the list is identical.  Every lane of the wave must call
-// this (act = live particle); the column loop and the staging are wave-uniform.  C16: the compact
-// 16-bit list format (opt-in, lh / o16 non-null).
+// texture-address unit was the bound; a staged column costs 4.  Same candidates, same order and,
+// where it decides, the same FP64 test as scan_candidates, so the list is identical.  Every lane of
+// the wave must call this (act = live particle); the column loop and the staging are wave-uniform.
 //
 // Per column the wave waits for memory once: the start[] loads of column col + 1 are issued before
 // column col's staging loads, so the one wait for the staging also covers them and the next
@@ -1523,25 +1120,14 @@ __device__ __forceinline__ int wave_max(int v)
 // the same counter -- each made it emit vmcnt(0) right after issuing them: two round trips per
 // column), so they are issued in asm (start_load), which hipcc does not count, and every path of a
 // column ends in an explicit vmcnt(0) before the next column reads them (start_landed).
-template <int DIM, int PERM, bool C16, int SB = MPH_SB, int CAP = MPH_LDS_CAP>
+template <int DIM, int PERM, int SB = MPH_SB, int CAP = MPH_LDS_CAP>
 __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa& A, const int* start,
                                                    int i, bool act, double xi, double yi, double zi,
-                                                   int cx, int cy, int cz, int* out, double* sx,
-                                                   int* lh, unsigned short* o16, DevState* dst, int2* whdr,
-                                                   int* stored)
+                                                   int cx, int cy, int cz, int* out, double* sx, int* stored)
 {
-    constexpr int SD = stage_d(CAP, SB);
-    // FP32 records fill the whole FP64 staging area: 16 bytes each, SB past the window's end
-    // MPH_DIAG_CHUNK: the last 1 KB of the wave's staging area holds the lanes' 4-entry chunks
-    constexpr int kChunkWords = MPH_DIAG_CHUNK == 2 ? 256 : MPH_DIAG_CHUNK ? 128 : 0;   // 8 / 4 entries per lane
-    constexpr int kCap32 = MPH_CAP32 ? (stage_words(CAP, SB) - kChunkWords) / 2 - SB - 1 : CAP;
-
-    double* sy = sx + SD;
-    double* sz = sx + 2 * SD;
-    int* st = reinterpret_cast<int*>(sx + 3 * SD);
+    // the staging area holds the window's 16-byte FP32 records, SB past the window's end
+    constexpr int kCap32 = stage_words(CAP, SB) / 2 - SB - 1;
     const int lane = threadIdx.x & 63;
-    [[maybe_unused]] int* const cbuf = reinterpret_cast<int*>(sx + stage_words(CAP, SB) - kChunkWords) +
-                                       (MPH_DIAG_CHUNK == 2 ? 8 : 4) * lane;
     // buffer descriptor of the wave's ELL tile (out - lane, wave-uniform): list stores take a 32-bit
     // lane offset instead of a 64-bit address; a store past the tile is dropped by the hardware
     const unsigned long long tb = (unsigned long long)(out - lane);
@@ -1552,7 +1138,6 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
         0x00020000);
     const double lo2 = P.rc2_lo, hi2 = P.rc2_hi;
     using X = CellAxes<DIM, PERM>;
-    int cnt = 0;
     constexpr int NCOL = DIM == 3 ? kGroups * kGroups : kGroups;
     const int cc[3] = {cx, cy, cz};
     const int cca = cc[X::A2];
@@ -1570,46 +1155,29 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     // The contiguous-axis offset is taken relative to the own cell in FP64 before the conversion
     // (ua ginv - c lies in [0, 1) for an interior lane), so the margin holds on any grid size.
     // The gap along the slowest axis changes once per group of columns (visited in order).
+    // An inactive lane gets a negative cutoff (no column opens); the gap margin mu is folded into
+    // the subtracted offsets; the range ends carry a bias of kBias cells, so truncation is floor
+    // (the ends lie within a few cells of the own cell) and the bias comes off in the row base.
+    // Each added rounding is below 1e-5 cells or 2^-24 of a cell width, far inside the margins.
     constexpr float kDn = 1.0f - 1.0f / (1 << 20), kUp = 1.0f + 1.0f / (1 << 19);
-#if MPH_COLR_LEAN
-    // The lean form (same bounds, fewer operations per column): an inactive lane gets a negative
-    // cutoff (no column opens); the gap margin mu is folded into the subtracted offsets; the range
-    // ends carry a bias of kBias cells, so truncation is floor (the ends lie within a few cells of
-    // the own cell) and the bias comes off in the row base.  Each added rounding is below 1e-5 cells
-    // or 2^-24 of a cell width, far inside the margins.
     constexpr float kBias = 32.0f;
     const float rcm2f = act ? (float)P.rc2_trim * kUp : -1.0f;
-#else
-    const float rcm2f = (float)P.rc2_trim * kUp;
-#endif
     float gx2f = 0.0f;
     const int c0l = cc[X::A0], c1l = DIM == 3 ? cc[X::A1] : 0;
     const float cw0f = (float)cw0, cw1f = (float)cw1;
     const float f0 = (float)(uu[X::A0] - c0l * cw0), f1 = DIM == 3 ? (float)(uu[X::A1] - c1l * cw1) : 0.0f;
     const float mu0 = cw0f * (1.0f / (1 << 20)), mu1 = cw1f * (1.0f / (1 << 20));
-#if MPH_COLR_LEAN
     const float g0p = f0 + mu0, g0m = (cw0f - f0) + mu0, g1p = f1 + mu1, g1m = (cw1f - f1) + mu1;
-#else
-    const float g0p = f0, g0m = cw0f - f0, g1p = f1, g1m = cw1f - f1;   // subtracted for d > 0 / d < 0
-#endif
     const float ginvaf = (float)ginva;
     const float caf = (float)(ua * ginva - (double)cca);   // offset inside the own cell, cells
-#if MPH_COLR_LEAN
     const float cal = (caf - 1e-3f) + kBias, cah = (caf + 1e-3f) + kBias;
     const float rgf = kUp * ginvaf;
     const int rowbase = (DIM == 3 ? (c0l * P.gc[X::A1] + c1l) * P.gc[X::A2] : c0l * P.gc[1]) + cca - (int)kBias;
-#else
-    const int rowbase = (DIM == 3 ? (c0l * P.gc[X::A1] + c1l) * P.gc[X::A2] : c0l * P.gc[1]) + cca;
-#endif
     const int sa = P.sa;
     const __amdgpu_buffer_rsrc_t srs = arr_rsrc(start);
-    auto gap32 = [](int d, float cwf, float gp, float gm, float mu) {
+    auto gap32 = [](int d, float cwf, float gp, float gm) {
         if (d == 0) return 0.0f;
-#if MPH_COLR_LEAN
         const float v = (float)(d > 0 ? d : -d) * cwf - (d > 0 ? gp : gm);
-#else
-        const float v = (float)(d > 0 ? d : -d) * cwf - (d > 0 ? gp : gm) - mu;
-#endif
         return v > 0.0f ? v : 0.0f;
     };
     auto col_range = [&](int col, int& jb, int& je) {
@@ -1618,141 +1186,36 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
         if (DIM == 3) {
             const int dxc = col / kGroups - kReach, dyc = col % kGroups - kReach;
             if (dyc == -kReach) {
-                const float gx = gap32(dxc, cw0f, g0p, g0m, mu0);
+                const float gx = gap32(dxc, cw0f, g0p, g0m);
                 gx2f = gx * gx * kDn;
             }
-            const float gy = gap32(dyc, cw1f, g1p, g1m, mu1);
+            const float gy = gap32(dyc, cw1f, g1p, g1m);
             d2f = (gx2f + gy * gy * kDn) * kDn;
             cofs = (dxc * P.gc[X::A1] + dyc) * P.gc[X::A2];
         } else {
             const int dxc = col - kReach;
-            const float gx = gap32(dxc, cw0f, g0p, g0m, mu0);
+            const float gx = gap32(dxc, cw0f, g0p, g0m);
             d2f = gx * gx * kDn;
             cofs = dxc * P.gc[1];
         }
-#if MPH_COLR_LEAN
         const bool ok = d2f <= rcm2f;
         const float rc = __builtin_amdgcn_sqrtf(fmaxf(rcm2f - d2f, 0.0f)) * rgf;   // half range, cells
         const int lo = max((int)(cal - rc), (int)kBias - sa);
         const int hi = min((int)(cah + rc), (int)kBias + sa);
-#else
-        const bool ok = act && d2f <= rcm2f;
-        const float rc = __builtin_amdgcn_sqrtf(fmaxf(rcm2f - d2f, 0.0f)) * kUp * ginvaf;   // half range, cells
-        const int lo = max((int)floorf(caf - rc - 1e-3f), -sa);
-        const int hi = min((int)floorf(caf + rc + 1e-3f), sa);
-#endif
         const int b = rowbase + cofs;
         // a lane without candidates reads start[0] twice (empty range)
         start_load2(srs, ok ? (unsigned)(b + lo) * 4u : 0u, ok ? (unsigned)(b + hi + 1) * 4u : 0u, jb, je);
     };
-    // compact list (nbr_list): the wave-wide index range of every column group, from the cell
-    // ranges of its first and last column (no column wraps: the wave is interior)
-    int gb[kGroups], gbase = 0;   // wave-uniform group bases
-    bool c16 = false;
-    if (C16) {
-        bool okg = true;
-#pragma unroll
-        for (int g = 0; g < kGroups; ++g) {
-            int lo = 0x7fffffff, hi = -1;
-            if (act) {
-                if (DIM == 3) {
-                    const int a0 = cc[X::A0] + g - kReach, c1 = cc[X::A1];
-                    lo = start[((a0 * P.gc[X::A1] + c1 - kReach) * P.gc[X::A2]) + cca - sa];
-                    hi = start[((a0 * P.gc[X::A1] + c1 + kReach) * P.gc[X::A2]) + cca + sa + 1];
-                } else {
-                    lo = start[(cx + g - kReach) * P.gc[1] + cca - sa];
-                    hi = start[(cx + g - kReach) * P.gc[1] + cca + sa + 1];
-                }
-            }
-            const int mn = wave_min(lo), mx = wave_max(hi);
-            okg = okg && (mx <= mn || mx - mn <= kSpan16 + 1);
-            gb[g] = mx > mn ? mn : 0;
-        }
-        c16 = okg;
-    }
-    // the lane's group ends go straight to the header (byte g - 1: the count at the end of group
-    // g - 1; unused bytes 127, nbr_at), so they hold no registers during the column loop
-    unsigned char* ends8 = c16 ? reinterpret_cast<unsigned char*>(lh + 8 + lane) : nullptr;
-    if (c16) {
-        lh[8 + lane] = 0x7F7F7F7F;
-        if (kGroups > 5) lh[8 + 64 + lane] = 0x7F7F7F7F;
-    }
-    // the lane's next list slot: C16 counts entries (cnt); the ELL rows keep the slot's byte offset
-    // in the wave's tile, soff = stored * 256 + lane * 4 (one add per entry, no address arithmetic);
-    // bits 18 and up count every accepted neighbour (NeighborCount), bits 8-17 the stored ones (the
-    // FP32 path keeps only r^2 <= P.rlf: kListTotal, kListKeep), so the store offset is soff & kSoffMask
+    // the lane's next list slot: soff = stored * 256 + lane * 4 (one add per entry, no address
+    // arithmetic); bits 18 and up count every accepted neighbour (NeighborCount), bits 8-17 the
+    // stored ones (the FP32 path keeps only r^2 <= P.rlf: kListTotal, kListKeep), so the store
+    // offset is soff & kSoffMask
     int soff = lane << 2;
-#if MPH_DIAG_PATHS
-    // diagnostic: this lane's rank in the wave by the previous step's NeighborCount
-    int seg_sorted = 0;
-    {
-        const int pv = act && dst->diag_prev ? dst->diag_prev[i] : 0x7fffffff;
-        int rk = 0;
-        for (int m = 0; m < 64; ++m) {
-            const int o = __builtin_amdgcn_readlane(pv, m);
-            rk += (o < pv || (o == pv && m < lane)) ? 1 : 0;
-        }
-        seg_sorted = rk >> 4;
-    }
-    auto seg_count = [&](bool st_on) {
-        const unsigned long long am = __ballot(st_on);
-        if (!am) return;
-        const int row = (soff >> 8) & 0x1FF;
-        const int kd = row * 4 + (lane >> 4), ks = row * 4 + seg_sorted;
-        bool dd = false, ds = false;
-        for (int m = 0; m < 64; ++m) {
-            if (!((am >> m) & 1ull)) continue;
-            const int od = __builtin_amdgcn_readlane(kd, m), os = __builtin_amdgcn_readlane(ks, m);
-            if (m < lane) { dd = dd || od == kd; ds = ds || os == ks; }
-        }
-        const int nd = __popcll(__ballot(st_on && !dd)), ns = __popcll(__ballot(st_on && !ds));
-        if (lane == 0) {
-            atomicAdd(&dst->path_diag[44], (unsigned long long)nd);
-            atomicAdd(&dst->path_diag[45], (unsigned long long)ns);
-            atomicAdd(&dst->path_diag[46], 1ull);
-            atomicAdd(&dst->path_diag[47], (unsigned long long)__popcll(am));
-        }
-    };
-#endif
-#if MPH_LIST_SPREAD
-    // proportional rows (kListSpread): stored entry k at row k * M / np below the prediction np,
-    // M + k - np past it; `cur` is the next row the lane has not written (rows skipped get the
-    // sentinel).  Identity (M = np = 0) without a prediction or above kSpreadMax.
-    int np = !C16 && P.pred && act ? min(P.pred[i], kMaxNeighbor - 1) : 0;
-    int Mw = __builtin_amdgcn_readfirstlane(wave_max(np));
-    if (Mw > kSpreadMax) Mw = 0;
-    if (Mw == 0) np = 0;
-    const unsigned rfx = np > 0 ? ((unsigned)Mw << 14) / (unsigned)np : (1u << 14);
-    int cur = 0;
-    const int sentinel = i | (int)0xF0000000;
-    auto put = [&](int e) {
-        const int k = (soff >> 8) & 0x1FF;
-        const int row = k < np ? (int)(((unsigned)k * rfx) >> 14) : Mw + k - np;
-        for (; cur < row && cur < kMaxNeighbor; ++cur)
-            __builtin_amdgcn_raw_buffer_store_b32(sentinel, tile_rsrc, ((unsigned)cur << 8) | (soff & 0xFC), 0, 0);
-        if (row < kMaxNeighbor)
-            __builtin_amdgcn_raw_buffer_store_b32(e, tile_rsrc, ((unsigned)row << 8) | (soff & 0xFC), 0, 0);
-        else
-            atomicOr(&dst->overflow, 1);   // past the tile (MPH_ERR_NEIGHBOR_OVERFLOW)
-        cur = row + 1;
-    };
-#endif
     constexpr int kSelfCol = DIM == 3 ? kReach * kGroups + kReach : kReach;   // the lane's own column
     // one stencil column: its range [jb, je) was loaded one column ahead; (nb_jb, nb_je) receive
     // column col + 1's.  The loop below is unrolled by two with the roles of the two register pairs
     // swapped, so no copy at the loop latch waits for the loads in flight.
     auto column = [&](int col, int jb, int je, int& nb_jb, int& nb_je) {
-        if (C16 && c16) {
-            // entering group g: the count so far ends group g - 1
-            const bool first = DIM == 3 ? col % kGroups == 0 : true;
-            const int g = DIM == 3 ? col / kGroups : col;
-            if (first && g > 0) ends8[g <= 4 ? g - 1 : 4 * 64 + g - 5] = (unsigned char)min(cnt, 127);
-            if (first) {
-#pragma unroll
-                for (int q = 0; q < kGroups; ++q)
-                    if (q == g) gbase = gb[q];
-            }
-        }
         start_landed(jb, je);   // loaded one column ahead; every path below ended in vmcnt(0)
         if (col + 1 < NCOL) col_range(col + 1, nb_jb, nb_je);
         const bool any = je > jb;
@@ -1760,7 +1223,6 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
         // normally has the lowest jb and the last the highest je -- read those two lanes, and take
         // the DPP reductions only when a lane says otherwise (wave-uniform check)
         const unsigned long long am = __ballot(any);
-        if (MPH_PA_STAGED && whdr && !am && lane == 0) whdr[col] = make_int2(0, 0);
         if (!am) {   // wave-uniform: no lane has candidates in this column
             // wait here for column col + 1's start[] loads, so that every path into the next column
             // has them landed and its first use needs no wait (which would also wait for this
@@ -1774,24 +1236,13 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             mn = wave_min(any ? jb : 0x7fffffff);
             mx = wave_max(any ? je : -1);
         }
-        if (MPH_DIAG_BOUNDS && (mn < 0 || mx > dev_n(P) || mx < mn)) {   // diagnostic builds only
-            if (lane == 0) atomicOr(&dst->overflow, 8);
-            __builtin_amdgcn_s_waitcnt(0x0F70);
-            return;
-        }
-        if (MPH_PA_STAGED && whdr && lane == 0) whdr[col] = make_int2(mn, mx);   // pass A's column windows
         const int span = mx - mn;
-        if (MPH_DIAG_SEARCH & 2) {   // never true: empty lists
-            __builtin_amdgcn_s_waitcnt(0x0F70);
-            soff += span == 0x7fffffff ? kListKeep : 0;
-            return;
-        }
         // A window wider than the staging area is mostly a wave across two cell rows: its lanes' ranges
         // form two runs far apart.  Split the lanes at the widest gap (a lane whose range starts past
         // every earlier lane's end) and stage each run's window, one after the other, when both fit.
         int lbase = mn, n1 = span, m2 = 0, n2 = 0;   // lane's record index j - lbase; the two windows
         bool two = false;
-        if (MPH_SEARCH_F32 && MPH_SPLIT32 != 0 && !C16 && span > (MPH_SPLIT32 > 1 ? MPH_SPLIT32 : kCap32)) {   // wave-uniform, rare
+        if (span > kCap32) {   // wave-uniform, rare
             int pm = any ? je : -1;   // running max of the ends over the lanes below and at this one
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
@@ -1817,30 +1268,14 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                 }
             }
         }
-#if MPH_DIAG_PATHS
-        {
-            const int path = MPH_SEARCH_F32 && !C16 && (span <= kCap32 || two) ? (two ? 1 : 0) : span <= CAP ? 2 : 3;
-            int cand = any ? je - jb : 0;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) cand += __shfl_xor(cand, o, 64);
-            if (lane == 0) {
-                atomicAdd(&dst->path_diag[path], 1ull);
-                atomicAdd(&dst->path_diag[4 + path], (unsigned long long)cand);
-                atomicAdd(&dst->path_diag[8 + path], (unsigned long long)(two ? n1 + n2 : span));
-                if (span > kCap32) atomicAdd(&dst->path_diag[two ? 14 : (n2 > 0 ? 13 : 12)], 1ull);
-                if (col == 0) atomicAdd(&dst->path_diag[15], 1ull);
-                if (span > 64) atomicAdd(&dst->path_diag[span > 256 ? 39 : span > 192 ? 38 : span > 160 ? 37 : span > 128 ? 36 : span > 96 ? 35 : 34], 1ull);
-            }
-        }
-#endif
-        if (MPH_SEARCH_F32 && !C16 && (span <= kCap32 || two)) {
+        if (span <= kCap32 || two) {
             // FP32 records: candidate j at record j - lbase, 64 records (1 KB) per instruction
             float4* s4 = reinterpret_cast<float4*>(sx);
             for (int p = 0; p * 64 < n1; ++p)   // wave-uniform
-                if (p * 64 + lane < n1) __builtin_amdgcn_global_load_lds(A.f4 + mn + p * 64 + lane, s4 + p * 64, 16, 0, MPH_STAGE_CPOL);
+                if (p * 64 + lane < n1) __builtin_amdgcn_global_load_lds(A.f4 + mn + p * 64 + lane, s4 + p * 64, 16, 0, 0);
             for (int p = 0; p * 64 < n2; ++p)   // the second run (two), after the first
                 if (p * 64 + lane < n2)
-                    __builtin_amdgcn_global_load_lds(A.f4 + m2 + p * 64 + lane, s4 + n1 + p * 64, 16, 0, MPH_STAGE_CPOL);
+                    __builtin_amdgcn_global_load_lds(A.f4 + m2 + p * 64 + lane, s4 + n1 + p * 64, 16, 0, 0);
             __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the records (and column col + 1's start[]) landed
             __builtin_amdgcn_wave_barrier();
             const float xf = (float)(xi - P.cref[0]), yf = (float)(yi - P.cref[1]), zf = (float)(zi - P.cref[2]);
@@ -1868,7 +1303,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                                                          __builtin_amdgcn_ballot_w64(live);
                         if (mband) {   // rare (wave-uniform): the FP64 test on the global positions
                             // the band lanes straight from the mask (no per-lane compare)
-                            if (MPH_BAND_MASK ? __builtin_amdgcn_inverse_ballot_w64(mband) : (le_hi & !le_lo & live)) {
+                            if (__builtin_amdgcn_inverse_ballot_w64(mband)) {
                                 // the index hidden from the loop's induction analysis, so the addresses
                                 // are formed here and not carried through the loop
                                 int jj = j;
@@ -1880,48 +1315,13 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                                 if ((r2a <= hi2) != in) a = accept_band(P, ddx, ddy, ddz);
                             }
                         }
-#if MPH_DIAG_PATHS
-                        seg_count(a && r2f <= P.rlf);
-#endif
                         if (a) {
                             // stored when within the passes' largest radius (FP32, an upper bound:
                             // the passes' own exact tests decide); counted always
                             const bool keep = r2f <= P.rlf;
-                            // diagnostic builds: MPH_DIAG_NOSTORE 1 no store, 2 the same stores to
-                            // the lane's row 0 (the instructions without the list traffic)
-#if MPH_LIST_SPREAD
-                            if (keep) put(nbr_entry(j, __float_as_int(r[u].w)));
-#elif MPH_DIAG_CHUNK
-                            if (keep && MPH_DIAG_CHUNK == 2) {
-                                // 8 entries (one 32-byte sector) per lane and chunk
-                                const int k = (soff >> 8) & 7;
-                                cbuf[k] = nbr_entry(j, __float_as_int(r[u].w));
-                                if (k == 7) {
-                                    typedef unsigned u4v __attribute__((ext_vector_type(4)));
-                                    const u4v v0 = *reinterpret_cast<const u4v*>(cbuf);
-                                    const u4v v1 = *reinterpret_cast<const u4v*>(cbuf + 4);
-                                    const int o = 65536 + (((soff >> 11) & 0x1F) * 64 + lane) * 32;
-                                    __builtin_amdgcn_raw_buffer_store_b128(v0, tile_rsrc, o, 0, 0);
-                                    __builtin_amdgcn_raw_buffer_store_b128(v1, tile_rsrc, o + 16, 0, 0);
-                                }
-                            } else if (keep) {
-                                const int k = (soff >> 8) & 3;
-                                cbuf[k] = nbr_entry(j, __float_as_int(r[u].w));
-                                if (k == 3) {
-                                    typedef unsigned u4v __attribute__((ext_vector_type(4)));
-                                    const u4v v = *reinterpret_cast<const u4v*>(cbuf);
-                                    // into the tile's upper half (rows 256 and up, unused), so the
-                                    // passes keep reading the stale rows, as with MPH_DIAG_NOSTORE=1
-                                    __builtin_amdgcn_raw_buffer_store_b128(
-                                        v, tile_rsrc, 65536 + (((soff >> 10) & 0x3F) * 64 + lane) * 16, 0, 0);
-                                }
-                            }
-#else
-                            if (keep && MPH_DIAG_NOSTORE != 1)
+                            if (keep)
                                 __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, __float_as_int(r[u].w)), tile_rsrc,
-                                                                      MPH_DIAG_NOSTORE == 2 ? (soff & 0xFF) : ell_byte(soff & kSoffMask),
-                                                                      0, MPH_LIST_CPOL);
-#endif
+                                                                      soff & kSoffMask, 0, 0);
                             soff += keep ? kListKeep : kListTotal;
                         }
                     }
@@ -1930,92 +1330,8 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
             if (col == kSelfCol) test32(std::true_type{});
             else test32(std::false_type{});
             __builtin_amdgcn_wave_barrier();   // every lane done reading before the next staging
-        } else if (span <= CAP) {
-            // the window from a 16-byte-aligned start: candidate j sits at j - mn + da in x, y, z
-            // and at j - mn + ta in the types; pieces of 128 doubles / 256 ints per instruction,
-            // lanes past the window masked (the arrays hold kPad elements beyond any window)
-            const int da = mn & 1, ta = mn & 3;
-            const int n2 = span + da, n4 = span + ta;
-            for (int p = 0; p * 128 < n2; ++p) {   // wave-uniform
-                const int e = p * 128 + 2 * lane;
-                if (e < n2) {
-                    __builtin_amdgcn_global_load_lds(A.x + (mn - da) + e, sx + p * 128, 16, 0, 0);
-                    __builtin_amdgcn_global_load_lds(A.y + (mn - da) + e, sy + p * 128, 16, 0, 0);
-                    __builtin_amdgcn_global_load_lds(A.z + (mn - da) + e, sz + p * 128, 16, 0, 0);
-                }
-            }
-            static_assert(CAP + 3 <= 256, "one 256-int piece holds the types of a window");
-            if (4 * lane < n4) __builtin_amdgcn_global_load_lds(A.type + (mn - ta) + 4 * lane, st, 16, 0, 0);
-            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the pieces (and column col + 1's start[]) landed
-            const int kofs = da, tofs = ta - da;
-            __builtin_amdgcn_wave_barrier();
-            if (MPH_DIAG_SEARCH & 1) { soff += sx[lane] == -1.25e300 ? kListKeep : 0; return; }   // (never true)
-            // this lane's candidates [jb, je) sit at staged position k = j - jd (types at k + tofs);
-            // the staging arrays are padded by SB entries, so a batch may read past je (masked).
-            // Per candidate: the FP64 distance (6), two compares -- the decision r2 <= rc2 (1 -
-            // 1e-10) and, XOR-ed with it, r2 <= rc2 (1 + 1e-10), which flags the rare band where the
-            // reference's own expression decides -- and, when accepted, the entry and one add.  The
-            // self test runs only in the lane's own column (SELF), the range test only past the
-            // batch's first candidate (the loop condition covers it).
-            const int jd = mn - kofs;
-            auto test = [&](auto self_tag) {
-                constexpr bool SELF = decltype(self_tag)::value;
-                for (int j0 = jb; j0 < je; j0 += SB) {
-                    double xs[SB], ys[SB], zs[SB];
-                    int ts[SB];
-                    const int k0 = j0 - jd;
-#pragma unroll
-                    for (int u = 0; u < SB; ++u) {
-                        xs[u] = sx[k0 + u];
-                        ys[u] = sy[k0 + u];
-                        zs[u] = sz[k0 + u];
-                        ts[u] = st[k0 + u + tofs];   // the types with the batch (no LDS wait per accepted entry)
-                    }
-#pragma unroll
-                    for (int u = 0; u < SB; ++u) {
-                        const int j = j0 + u;
-                        const double dx = xs[u] - xi, dy = ys[u] - yi, dz = zs[u] - zi;
-                        const double r2a = fma(dx, dx, fma(dy, dy, dz * dz));
-                        const bool in = r2a <= lo2;
-                        bool a = in;
-                        if ((r2a <= hi2) != in) a = accept_band(P, dx, dy, dz);
-                        if (u > 0) a = a & (j < je);
-                        if (SELF) a = a & (j != i);
-                        if (a) {
-                            if (C16 && c16) {
-                                const int k = min(cnt, kMaxNeighbor - 1);
-                                o16[(((k >> 1) * kTile + lane) << 1) + (k & 1)] =
-                                    (unsigned short)((j - gbase) | (ts[u] << kOff16));
-                                ++cnt;
-                            } else if (MPH_DIAG_NOSTORE == 2) {   // diagnostic: same stores, one row
-                                list_store(out, nbr_entry(j, ts[u]));
-                                soff += kListKeep;
-                            } else if (MPH_DIAG_NOSTORE) {
-                                soff += kListKeep;
-                            } else if (!C16) {
-                                // byte offset into the wave's tile (SGPR descriptor); an overflowing
-                                // lane (>= 512 neighbours) ends the run (MPH_ERR_NEIGHBOR_OVERFLOW)
-#if MPH_LIST_SPREAD
-                                put(nbr_entry(j, ts[u]));
-#else
-                                __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, ts[u]), tile_rsrc,
-                                                                      ell_byte(soff & kSoffMask), 0, 0);
-#endif
-                                soff += kListKeep;
-                            } else {
-                                __builtin_amdgcn_raw_buffer_store_b32(nbr_entry(j, ts[u]), tile_rsrc,
-                                                                      ell_slot(min(cnt, kMaxNeighbor - 1), lane) << 2,
-                                                                      0, 0);
-                                ++cnt;
-                            }
-                        }
-                    }
-                }
-            };
-            if (col == kSelfCol) test(std::true_type{});
-            else test(std::false_type{});
-            __builtin_amdgcn_wave_barrier();   // every lane done reading before the next staging
         } else {
+            // a window wider than the staging area: per-lane gathers, every accepted pair stored
             for (int j0 = jb; j0 < je; j0 += SB) {
                 double xs[SB], ys[SB], zs[SB];
 #pragma unroll
@@ -2029,120 +1345,24 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                 for (int u = 0; u < SB; ++u) {
                     const int j = j0 + u;
                     if (accept_interior(P, xs[u] - xi, ys[u] - yi, zs[u] - zi, lo2, hi2) && j < je && j != i) {
-                        if (C16) {
-                            if (cnt < kMaxNeighbor) {
-                                if (c16)
-                                    o16[(((cnt >> 1) * kTile + lane) << 1) + (cnt & 1)] =
-                                        (unsigned short)((j - gbase) | (A.type[j] << kOff16));
-                                else
-                                    list_store(ell_at(out, lane, cnt), nbr_entry(j, A.type[j]));
-                            }
-                            ++cnt;
-                        } else {
-#if MPH_LIST_SPREAD
-                            put(nbr_entry(j, A.type[j]));
-#else
-                            if (!MPH_DIAG_NOSTORE && soff_total(soff) < kMaxNeighbor)
-                                list_store(ell_at(out, lane, (soff & kSoffMask) >> 8), nbr_entry(j, A.type[j]));
-#endif
-                            soff += kListKeep;
-                        }
+                        if (soff_total(soff) < kMaxNeighbor)
+                            out[(size_t)((soff & kSoffMask) >> 8) * kTile] = nbr_entry(j, A.type[j]);
+                        soff += kListKeep;
                     }
                 }
             }
             __builtin_amdgcn_s_waitcnt(0x0F70);   // column col + 1's start[] loads (wide windows are rare)
         }
     };
-#if MPH_DIAG_PATHS
-    // diagnostic: the LDS row ring a wave would keep for its list (DevState.path_diag[16..33])
-    int sim_fl[2][4] = {};
-    int sim_prev = 0, sim_col = 0, sim_g0 = 0;
-    unsigned long long rows_col = 0, rows_grp = 0;
-    auto wsum = [](int v) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        return v;
-    };
-    auto ring_sim = [&]() {
-        const int c = (soff >> 8) & 0x1FF;
-        rows_col += wave_max(act ? c - sim_prev : 0);
-        if (sim_col % kGroups == kGroups - 1) {
-            rows_grp += wave_max(act ? c - sim_g0 : 0);
-            sim_g0 = c;
-        }
-        ++sim_col;
-        const int minc = wave_min(act ? c : 0x7fffffff), maxc = wave_max(act ? c : 0);
-        if (minc == 0x7fffffff) { sim_prev = c; return; }
-#pragma unroll
-        for (int rule = 0; rule < 2; ++rule)
-#pragma unroll
-            for (int ri = 0; ri < 4; ++ri) {
-                const int R = 4 << ri, fl = sim_fl[rule][ri];
-                const int ahead = wsum(max(0, c - max(sim_prev, fl + R)));
-                const int lag = wsum(max(0, min(c, fl) - sim_prev));
-                if (lane == 0) {
-                    atomicAdd(&dst->path_diag[16 + (rule * 4 + ri) * 2], (unsigned long long)ahead);
-                    atomicAdd(&dst->path_diag[17 + (rule * 4 + ri) * 2], (unsigned long long)lag);
-                }
-                const int nf = max(fl, rule == 0 ? minc : max(minc, maxc - R / 2));
-                if (lane == 0 && rule == 1 && ri == 2) atomicAdd(&dst->path_diag[33], (unsigned long long)(nf - fl));
-                sim_fl[rule][ri] = nf;
-            }
-        sim_prev = c;
-    };
-#endif
     int ra_b, ra_e, rb_b = 0, rb_e = 0;   // the two register pairs of the column ranges
     col_range(0, ra_b, ra_e);
     __builtin_amdgcn_s_waitcnt(0x0F70);
     for (int col = 0; col < NCOL; col += 2) {
         column(col, ra_b, ra_e, rb_b, rb_e);
-#if MPH_DIAG_PATHS
-        ring_sim();
-#endif
-        if (col + 1 < NCOL) {
-            column(col + 1, rb_b, rb_e, ra_b, ra_e);
-#if MPH_DIAG_PATHS
-            ring_sim();
-#endif
-        }
+        if (col + 1 < NCOL) column(col + 1, rb_b, rb_e, ra_b, ra_e);
     }
-#if MPH_DIAG_PATHS
-    if (!C16) {
-        const int tot = wsum(act ? (soff >> 8) & 0x1FF : 0);
-        const int longest = wave_max(act ? (soff >> 8) & 0x1FF : 0);
-        if (lane == 0) {
-            atomicAdd(&dst->path_diag[32], (unsigned long long)tot);
-            atomicAdd(&dst->path_diag[40], rows_col);
-            atomicAdd(&dst->path_diag[41], rows_grp);
-            atomicAdd(&dst->path_diag[42], (unsigned long long)longest);
-        }
-    }
-#endif
-    if (!C16) {
-        cnt = soff_total(soff);       // every neighbour (NeighborCount)
-        *stored = soff_stored(soff);  // the list's length (r^2 <= P.rlf)
-#if MPH_LIST_SPREAD
-        *stored = min(cur, kMaxNeighbor);   // rows the passes walk, sentinels included
-#endif
-    } else {
-        *stored = cnt;
-    }
-    if (C16 && c16) {
-        // the group ends are bytes below 128 (nbr_at): a wave with a lane past 127 neighbours (the
-        // reference allows 511) is marked for the ELL search of launch_neighbors' second launch
-        // (k_neighbors REDO)
-        if (wave_max(cnt) > P.l16max) {
-            if (lane == 0) lh[kHdrFlag] = 2;   // counted in DevState.list_redo by neighbors_body
-            return cnt;
-        }
-        // the bases and the format flag of the wave
-        if (lane == 0) {
-#pragma unroll
-            for (int g = 0; g < kGroups; ++g) lh[g] = gb[g];
-            lh[kHdrFlag] = 1;
-        }
-    }
-    return cnt;
+    *stored = soff_stored(soff);  // the list's length (r^2 <= P.rlf)
+    return soff_total(soff);      // every neighbour (NeighborCount)
 }
 
 // Slab mode: true when no lane of the wave holds an owned particle (ghost ids are negative).
@@ -2174,21 +1394,17 @@ __device__ __forceinline__ void slab_wave_flag(const DevParams& P, const Soa& A,
 
 // ncount: the length of each particle's stored list (what the passes walk); nbcount: NeighborCount,
 // every neighbour within the search radius (the two differ where the lists keep only r^2 <= P.rlf)
-template <int DIM, int PERM, bool C16, int REDO>
+template <int DIM, int PERM>
 __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, const int* start, int* nbr,
-                                               int* ncount, int* nbcount, int* lhdr, DevState* st, double* stage,
-                                               int i, int2* whdr_all = nullptr)
+                                               int* ncount, int* nbcount, DevState* st, double* stage, int i)
 {
     const int n = dev_n(P);
     const bool live = i < n;
     const int ii = live ? i : n - 1;
-    // list format of the wave: the 32-bit ELL row unless the interior search below goes compact
     const int tile = __builtin_amdgcn_readfirstlane(i >> 6);
     // a wave past the last particle (the launch has whole blocks of 4 waves): nothing to do, and its
-    // tile lies past the list and header arrays (sized for the particles' tiles)
+    // tile lies past the list array (sized for the particles' tiles)
     if (tile * kTile >= n) return 0;
-    int* lh = C16 && !REDO ? lhdr + (size_t)tile * kLhdr : nullptr;   // REDO: a marked wave, now into ELL rows
-    if (C16 && (threadIdx.x & 63) == 0) lhdr[(size_t)tile * kLhdr + kHdrFlag] = 0;
     if (wave_all_ghosts(P, A, live, ii)) {
         if (live) ncount[i] = 0;
         if (live) nbcount[i] = 0;
@@ -2203,30 +1419,15 @@ __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, 
     const int cy = cell_axis(yi, P.corg[1], P.dw[1], P.ginv[1], P.gc[1]);
     const int cz = DIM == 3 ? cell_axis(zi, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
     int* out = nbr + (size_t)(i >> 6) * kTileStride + (i & 63);
-    // MPH_PA_STAGED: the wave's column windows for pass A, flag kWinCols: 1 = written
-    int2* whdr = MPH_PA_STAGED && !C16 && !REDO && whdr_all ? whdr_all + (size_t)tile * kWinHdr : nullptr;
-    if (whdr && (threadIdx.x & 63) == 0) whdr[kWinCols] = make_int2(fast ? 1 : 0, 0);
-    if (MPH_SEARCH_LDS && fast) {
-        if (C16 && !REDO) {
-            cnt = scan_candidates_lds<DIM, PERM, true>(P, A, start, i, own, xi, yi, zi, cx, cy, cz, out, stage, lh,
-                                                       reinterpret_cast<unsigned short*>(
-                                                           nbr + (size_t)tile * kTileStride), st, nullptr,
-                                                       &stored);
-            if ((threadIdx.x & 63) == 0 && lh[kHdrFlag] == 2) atomicAdd(&st->list_redo, 1);
-        } else {
-            cnt = scan_candidates_lds<DIM, PERM, false>(P, A, start, i, own, xi, yi, zi, cx, cy, cz, out, stage,
-                                                        nullptr, nullptr, st, whdr, &stored);
-        }
-        if (live) ncount[i] = stored;
-        if (live) nbcount[i] = cnt;
+    if (fast) {
+        cnt = scan_candidates_lds<DIM, PERM>(P, A, start, i, own, xi, yi, zi, cx, cy, cz, out, stage, &stored);
     } else {
-        if (own && !(MPH_DIAG_SEARCH & 4))
-            cnt = fast ? scan_candidates<DIM, true, PERM>(P, A, start, i, xi, yi, zi, cx, cy, cz, out)
-                       : scan_candidates<DIM, false, PERM>(P, A, start, i, xi, yi, zi, cx, cy, cz, out);
+        if (own)
+            cnt = scan_candidates<DIM, false, PERM>(P, A, start, i, xi, yi, zi, cx, cy, cz, out);
         stored = cnt;
-        if (live && !(MPH_DIAG_SEARCH & 4)) ncount[i] = cnt;
-        if (live && !(MPH_DIAG_SEARCH & 4)) nbcount[i] = cnt;
     }
+    if (live) ncount[i] = stored;
+    if (live) nbcount[i] = cnt;
     // overflow flag (main.cpp:1766-1768 is the reference's limit).  No per-step statistics here:
     // one same-address device atomic per wave serialises at ~11 ns each (21.8k waves at D1M took
     // 0.5 ms); mph_neighbor_stats reduces ncount on demand.
@@ -2234,86 +1435,26 @@ __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, 
     return stored;
 }
 
-// one kernel per cell order (DevParams.perm) and list format, so each keeps its own register
-// budget; held to 64 VGPRs (8 waves per SIMD: the search waits on its start[] and staging loads).
-// bal: the passes' XCD split runs this step (launch_neighbors), so the waves feed its histogram.
+// one kernel per cell order (DevParams.perm), so each keeps its own register budget; held to 64
+// VGPRs (8 waves per SIMD: the search waits on its start[] and staging loads).  bal: the passes'
+// XCD split runs (launch_sort), so the waves feed its histogram.
 #ifndef MPH_NB_WPE
 #define MPH_NB_WPE 8
 #endif
-#ifndef MPH_NB_SHM_PAD
-#define MPH_NB_SHM_PAD 0   // diagnostic builds: unused dynamic LDS per block, to cap the search's occupancy
-#endif
-template <int DIM, int PERM, bool C16>
+template <int DIM, int PERM>
 __global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_WPE))) void k_neighbors(
     DevParams P, Soa A, const int* __restrict__ start, int* __restrict__ nbr, int* __restrict__ ncount,
-    int* __restrict__ nbcount, int* __restrict__ lhdr, DevState* __restrict__ st, int* __restrict__ wface, int bal,
-    int2* __restrict__ whdr, int ck)
+    int* __restrict__ nbcount, DevState* __restrict__ st, int* __restrict__ wface, int bal)
 {
     const int n = dev_n(P);
-#if MPH_CHUNK_BUILD
-    const int tb = ck ? chunk_block(blockIdx.x, list_blocks(n), ck)
-                      : ((int)blockIdx.x < list_blocks(n) ? xcd_block(blockIdx.x, list_blocks(n)) : -1);
-    if (tb < 0) return;
-#else
-    (void)ck;
-#if MPH_CU_AFFINE
-    int tb;
-    if (bal && st) {   // the equal XCD ranges of xcd_block, CU-affine inside them
-        const int nb = list_blocks(n), xq = nb >> 3, xr = nb & 7, j = blockIdx.x & 7;
-        tb = cu_affine_tile(st, 0, j < xr ? j * (xq + 1) : xr * (xq + 1) + (j - xr) * xq, j < xr ? xq + 1 : xq);
-    } else {
-        tb = (int)blockIdx.x < list_blocks(n) ? xcd_block(blockIdx.x, list_blocks(n)) : -1;
-    }
-    if (tb < 0) return;
-#else
     if ((int)blockIdx.x >= list_blocks(n)) return;
     const int tb = xcd_block(blockIdx.x, list_blocks(n));
-#endif
-#endif
-    XCD_PROBE(st, 0);
     __shared__ __attribute__((aligned(16))) double stage[kWB][stage_words(MPH_LDS_CAP, MPH_SB)];
     const int i = tb * blockDim.x + threadIdx.x;
     slab_wave_flag(P, A, i, n, wface);
-    const int cnt = neighbors_body<DIM, PERM, C16, 0>(P, A, start, nbr, ncount, nbcount, lhdr, st,
-                                                      stage[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], i, whdr);
+    const int cnt = neighbors_body<DIM, PERM>(P, A, start, nbr, ncount, nbcount, st,
+                                              stage[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], i);
     if (bal) add_wave_work(st, cnt, i, n);
-}
-
-// The XCD ranges of the list passes from the search's work histogram (see list_block): one block,
-// an inclusive scan of the runs' work (4 consecutive runs per thread), the 7 inner cut points at
-// equal shares of the total (interpolated inside their run), then the histogram cleared.
-__global__ __launch_bounds__(kXcdSplitThreads) void k_xcd_split(DevState* __restrict__ st)
-{
-    xcd_split_block<kXcdSplitThreads>(st);
-}
-
-// The second launch, over the waves whose compact list did not fit (scan_candidates_lds marks
-// them and counts them in DevState.list_redo): one block; it exits at once when the count is zero
-// (the rule: a lane past 255 neighbours, physically far off), else its 4 waves walk every wave
-// header and search the marked ones into ELL rows, then clear the count for the next step.
-template <int DIM, int PERM>
-__global__ __launch_bounds__(256) void k_neighbors_redo(DevParams P, Soa A, const int* __restrict__ start,
-                                                        int* __restrict__ nbr, int* __restrict__ ncount,
-                                                        int* __restrict__ nbcount, int* __restrict__ lhdr,
-                                                        DevState* __restrict__ st)
-{
-    if (st->list_redo == 0) return;
-    const int n = dev_n(P);
-    const int ntile = (n + kTile - 1) / kTile;
-    __shared__ __attribute__((aligned(16))) double stage[4][stage_words(MPH_LDS_CAP, MPH_SB)];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int t0 = wave * 64; t0 < ntile; t0 += 4 * 64) {
-        const int t = t0 + lane;   // the wave header this lane checks
-        unsigned long long m = __ballot(t < ntile && lhdr[(size_t)t * kLhdr + kHdrFlag] == 2);
-        while (m) {
-            const int b = __ffsll((long long)m) - 1;
-            m &= m - 1;
-            neighbors_body<DIM, PERM, true, 1>(P, A, start, nbr, ncount, nbcount, lhdr, st, stage[wave],
-                                               (t0 + b) * kTile + lane);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) st->list_redo = 0;
 }
 
 // ---------------------------------------------------------------------------- pass A -------
@@ -2326,7 +1467,7 @@ __global__ __launch_bounds__(256) void k_neighbors_redo(DevParams P, Soa A, cons
 #ifndef MPH_UB
 #define MPH_UB 8
 #endif
-template <bool FAST, bool C16, int DIM, bool EQR, int U = MPH_UA>
+template <bool FAST, int DIM, bool EQR, int U = MPH_UA>
 __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_ratio, const double* s_mu,
                                             const Soa& A,
                                             NbrList NL, int cnt, int ti, bool solid, double xi,
@@ -2338,27 +1479,17 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
         double X[U], Y[U], Z[U], VX[U], VY[U], VZ[U];
         int TT[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            nbr_at<C16>(NL, k0 + u < cnt ? k0 + u : cnt - 1, jj[u], TT[u]);
-            if (MPH_DIAG_GATHER == 1) jj[u] = min((int)(blockIdx.x * blockDim.x + threadIdx.x) ^ 1, dev_n(P) - 1);
-        }
+        for (int u = 0; u < U; ++u) nbr_at(NL, k0 + u < cnt ? k0 + u : cnt - 1, jj[u], TT[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (MPH_AOS_GATHER) {
-                const double2 a = A.p6[p6_at(P.n, jj[u], 0)], b = A.p6[p6_at(P.n, jj[u], 1)],
-                              c = A.p6[p6_at(P.n, jj[u], 2)];
-                X[u] = a.x; Y[u] = a.y; Z[u] = b.x;
-                VX[u] = b.y; VY[u] = c.x; VZ[u] = c.y;
-            } else {
-                X[u] = A.x[jj[u]]; Y[u] = A.y[jj[u]]; Z[u] = A.z[jj[u]];
-                VX[u] = A.vx[jj[u]]; VY[u] = A.vy[jj[u]]; VZ[u] = A.vz[jj[u]];
-            }
+            const double2* r = A.p6 + 3 * (size_t)jj[u];
+            const double2 a = r[0], b = r[1], c = r[2];
+            X[u] = a.x; Y[u] = a.y; Z[u] = b.x;
+            VX[u] = b.y; VY[u] = c.x; VZ[u] = c.y;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (k0 + u >= cnt) break;
-            if (kListSpread && TT[u] < 0) continue;   // a row the lane skipped (sentinel)
-            if (MPH_DIAG_GATHER == 2) { o.da += X[u] + Y[u] + Z[u] + VX[u] + VY[u] + VZ[u] + TT[u]; continue; }
             const double q0 = image_exact<FAST>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
             const double q1 = image_exact<FAST>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
             const double q2 = image_exact<FAST || DIM == 2>(Z[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
@@ -2366,121 +1497,6 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
                                    VX[u] - vxi, VY[u] - vyi, VZ[u] - vzi, o);
         }
     }
-}
-
-// The waves k_pass_a_st takes (MPH_PA_STAGED): interior waves of a single context whose search wrote
-// their column windows, at equal radii.  k_pass_a evaluates the same predicate and leaves them.
-__device__ __forceinline__ bool pa_staged_wave(const DevParams& P, const int2* whdr, int i, bool fast)
-{
-    if (!MPH_PA_STAGED || !whdr || !fast || P.slab_axis >= 0 || !pass_a_equal_radii(P)) return false;
-    return whdr[(size_t)__builtin_amdgcn_readfirstlane(i >> 6) * kWinHdr + kWinCols].x == 1;
-}
-
-// Pass A of an interior wave from LDS-staged column windows (MPH_PA_STAGED): the search recorded the
-// wave's window [mn, mx) of every stencil column (whdr); per column the wave stages the window's
-// 48-byte records {x, y, z, vx, vy, vz} with coalesced buffer loads into LDS (1 KB per instruction,
-// 8 L1 lines, instead of per-lane 16-byte gathers touching ~24-35 lines each), then every lane takes
-// its next list entries below the window's end mx (a lane's entries ascend through the columns)
-// and reads their records from LDS -- an entry below mn (a later column of a lane with no candidates
-// in this one, when the wave spans two cell rows) or in a window wider than CAP from global memory.
-// Same entries in the same order, same pass_a_term: every sum is bit-identical to pass_a_loop.  The
-// lane's entries come four at a time, the next four loaded while the current ones are used.
-template <int DIM, int CAP = MPH_PA_CAP>
-__device__ __forceinline__ void pass_a_staged(const DevParams& P, const double* s_ratio, const double* s_mu,
-                                              const Soa& A, const int* row, const int2* whdr, int cnt, int ti,
-                                              bool solid, double xi, double yi, double zi, double vxi, double vyi,
-                                              double vzi, PassA& o, double2* stage, const DevState* st)
-{
-    constexpr int NCOL = DIM == 3 ? kGroups * kGroups : kGroups;
-    const int lane = threadIdx.x & 63;
-    const __amdgpu_buffer_rsrc_t rp = arr_rsrc(A.p6);
-    const unsigned lane16 = (unsigned)lane * 16u;
-    // entry k of the lane's ELL row, or a sentinel past every window (index 2^28 - 1)
-    auto ld = [&](int k) { return k < cnt ? *ell_at(row, lane, k) : 0x7fffffff; };
-    int c0 = ld(0), c1 = ld(1), c2 = ld(2), c3 = ld(3);
-    int x0 = ld(4), x1 = ld(5), x2 = ld(6), x3 = ld(7);
-    int p = 0, kn = 8, used = 0;
-    for (int col = 0; col < NCOL; ++col) {
-        const int2 w = whdr[col];   // wave-uniform
-        if (w.y <= w.x) continue;
-        const int mn = w.x, mx = w.y;
-        const bool staged = mx - mn <= CAP;
-        if (staged) {
-            // the window's bytes [48 mn, 48 mx) in 16-byte pieces, 64 per instruction
-            const int pieces = 3 * (mx - mn);
-            const unsigned so = (unsigned)mn * 48u;
-            for (int q = 0; q * 64 < pieces; ++q)   // wave-uniform
-                if (lane < pieces - q * 64)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rp, lds_ptr(stage + q * 64), 16, lane16, so + q * 1024u, 0, 0);
-            __builtin_amdgcn_s_waitcnt(0x0F70);
-            __builtin_amdgcn_wave_barrier();
-        }
-        for (;;) {
-            const int e = p == 0 ? c0 : (p == 1 ? c1 : (p == 2 ? c2 : c3));
-            const int j = e & kIndexMask;
-            const bool a = j < mx;
-            if (!__ballot(a)) break;
-            if (a) {
-                double2 r0, r1, r2;
-                if (staged && j >= mn) {
-                    const double2* q = stage + 3 * (j - mn);
-                    r0 = q[0]; r1 = q[1]; r2 = q[2];
-                } else {
-                    r0 = A.p6[p6_at(P.n, j, 0)]; r1 = A.p6[p6_at(P.n, j, 1)]; r2 = A.p6[p6_at(P.n, j, 2)];
-                }
-                const double q0 = image_exact<true>(r0.x - xi, P.dw[0], P.hw[0], P.w075[0]);
-                const double q1 = image_exact<true>(r0.y - yi, P.dw[1], P.hw[1], P.w075[1]);
-                const double q2 = image_exact<true>(r1.x - zi, P.dw[2], P.hw[2], P.w075[2]);
-                pass_a_term<true, true>(P, s_ratio, s_mu, ti, e >> kTypeShift, solid, q0, q1, q2,
-                                        r2_exact(q0, q1, q2), r1.y - vxi, r2.x - vyi, r2.y - vzi, o);
-                ++used;
-                if (++p == 4) {   // the next four entries (loaded four entries ago), and four more
-                    c0 = x0; c1 = x1; c2 = x2; c3 = x3;
-                    x0 = ld(kn); x1 = ld(kn + 1); x2 = ld(kn + 2); x3 = ld(kn + 3);
-                    kn += 4;
-                    p = 0;
-                }
-            }
-        }
-        if (staged) __builtin_amdgcn_wave_barrier();   // every lane done reading before the next staging
-    }
-    if (MPH_DIAG_PA && used != cnt) atomicOr(&const_cast<DevState*>(st)->overflow, 32);   // entries left over
-}
-
-#ifndef MPH_PAS_WPE
-#define MPH_PAS_WPE 6   // k_pass_a_st: <= 84 VGPRs, 24 waves per CU with 6 KB of LDS each
-#endif
-template <int DIM>
-__global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_PAS_WPE))) void k_pass_a_st(
-    DevParams P, const DevTables* __restrict__ T, Soa A, const int* __restrict__ nbr, const int* __restrict__ ncount,
-    PassAOut pout, const DevState* __restrict__ st, const int2* __restrict__ whdr)
-{
-    const int n = dev_n(P);
-    const int lb = list_block(st, n);
-    if (lb < 0) return;
-    __shared__ double s_ratio[kTypes * kTypes];
-    __shared__ double s_mu[kTypes * kTypes];
-    __shared__ __attribute__((aligned(16))) double2 pstage[kWB][3 * MPH_PA_CAP];
-    if (threadIdx.x < kTypes * kTypes) {
-        s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
-        s_mu[threadIdx.x] = T->mu_ij[threadIdx.x] * (-P.cvis * P.cdv * P.vol);   // pass_a_term's viscous factor
-    }
-    __syncthreads();
-    const int i = lb * blockDim.x + threadIdx.x;
-    const bool live = i < n;
-    const int ii = live ? i : n - 1;
-    const double xi = A.x[ii], yi = A.y[ii], zi = A.z[ii];
-    const bool fast = wave_search_interior(P, st, live, xi, yi, zi);
-    if (!pa_staged_wave(P, whdr, i, fast)) return;
-    double vxi = 0.0, vyi = 0.0, vzi = 0.0;
-    own_velocity(A, ii, vxi, vyi, vzi, P.n);
-    const int ti = A.type[ii];
-    const int cnt = live ? min(ncount[i], kMaxNeighbor) : 0;
-    PassA o;
-    pass_a_staged<DIM>(P, s_ratio, s_mu, A, nbr + (size_t)(i >> 6) * kTileStride + (i & 63),
-                       whdr + (size_t)__builtin_amdgcn_readfirstlane(i >> 6) * kWinHdr, cnt, ti, dev_is_struct(ti),
-                       xi, yi, zi, vxi, vyi, vzi, o, pstage[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], st);
-    if (live) pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
 }
 
 #ifndef MPH_PA_WPE
@@ -2494,20 +1510,12 @@ __global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_PAS_
 template <int DIM>
 __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, const DevTables* __restrict__ T, Soa A,
                                                 const int* __restrict__ nbr,
-                                                const int* __restrict__ ncount,
-                                                const int* __restrict__ lhdr, PassAOut pout,
-                                                const DevState* __restrict__ st, const int2* __restrict__ whdr,
-                                                int ck)
+                                                const int* __restrict__ ncount, PassAOut pout,
+                                                const DevState* __restrict__ st)
 {
     const int n = dev_n(P);
-#if MPH_CHUNK_BUILD
-    const int lb = ck ? chunk_block(blockIdx.x, list_blocks(n), ck) : list_block(st, n);
-#else
-    (void)ck;
-    const int lb = list_block(st, n, 1);
-#endif
+    const int lb = list_block(st, n);
     if (lb < 0) return;
-    XCD_PROBE(st, 1);
     __shared__ double s_ratio[kTypes * kTypes];
     __shared__ double s_mu[kTypes * kTypes];
     if (threadIdx.x < kTypes * kTypes) {
@@ -2531,29 +1539,23 @@ __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, cons
     const bool own = live && !ghost;
     // the search's rule (its list order and the fast minimum image go together)
     const bool fast = wave_search_interior(P, st, own, xi, yi, zi);
-    if (pa_staged_wave(P, whdr, i, fast)) return;   // k_pass_a_st's wave
     if (!own) return;
     double vxi, vyi, vzi;
-    own_velocity(A, i, vxi, vyi, vzi, P.n);
+    own_velocity(A, i, vxi, vyi, vzi);
     const int ti = A.type[i];
     const bool solid = dev_is_struct(ti);
     const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
-    __shared__ int s_gb[kWB][8];
-    const NbrList NL = nbr_list(nbr, lhdr, i, s_gb[threadIdx.x >> 6]);
+    const NbrList NL = nbr_list(nbr, i);
     PassA o;
-    // wave-uniform: equal radii (every BASELINE config) take the single-cutoff form of the sums
+    // wave-uniform: equal radii (every BASELINE config) take the single-cutoff form of the sums in
+    // the interior waves; waves at a periodic face keep the general form
     const bool eqr = pass_a_equal_radii(P);
-    // (compact lists are only built at equal radii, launch_neighbors, so both list formats of an
-    // interior wave take the same form and stay bit-identical; waves at a periodic face, ELL rows
-    // in both formats, keep the general form)
-    if (NL.c16)   // compact lists come from interior searches only
-        pass_a_loop<true, true, DIM, true>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
-    else if (fast && eqr)
-        pass_a_loop<true, false, DIM, true>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+    if (fast && eqr)
+        pass_a_loop<true, DIM, true>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
     else if (fast)
-        pass_a_loop<true, false, DIM, false>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+        pass_a_loop<true, DIM, false>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
     else
-        pass_a_loop<false, false, DIM, false>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+        pass_a_loop<false, DIM, false>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
     pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
 }
 
@@ -2570,12 +1572,9 @@ __device__ __forceinline__ double4 struct_disp(const DevParams& P, double4 x, do
 
 // Pass B needs, per neighbour, only what pass A could not know: P_j (and, with surface tension,
 // GC_j and PA_j).  The P_i half of the pressure force and the viscous force were summed in pass A
-// (fpart), so the default gather per neighbour is one 32-byte record {x, y, z, P} (MPH_PB_REC=1)
-// or four SoA doubles (MPH_PB_REC=0); the type of j only for structure i (InterfaceForce) or
-// surface tension.
-#ifndef MPH_PB_REC
-#define MPH_PB_REC 1
-#endif
+// (fpart), so the gather per neighbour is one 32-byte record {x, y, z, P} (two 16-byte planes,
+// rec_load); the type of j (in the list entry) only for structure i (InterfaceForce) or surface
+// tension.
 // One neighbour's pair forces for pass B (see k_pass_b): PressureP's P_j half, and with surface
 // tension PressureA and DiffuseInterface; structure i takes non-structure j only.
 template <bool FAST, bool SURF, int DIM>
@@ -2634,9 +1633,9 @@ __device__ __forceinline__ void pass_b_term(const DevParams& P, const double* s_
     f2 += c * q2;
 }
 
-template <bool FAST, bool C16, bool SURF, int DIM, int U = MPH_UB>
-__device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_ratio, const Soa& A,
-                                            const double4* rec, const double* pres, const double* gx,
+template <bool FAST, bool SURF, int DIM, int U = MPH_UB>
+__device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_ratio,
+                                            const double4* rec, const double* gx,
                                             const double* gy, const double* gz, const double* pa,
                                             NbrList NL, int cnt, int ti, bool solid, double xi,
                                             double yi, double zi, double gxi, double gyi, double gzi,
@@ -2649,24 +1648,12 @@ __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_
         double X[U], Y[U], Z[U], PJ[U];
         int TT[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            nbr_at<C16>(NL, k0 + u < cnt ? k0 + u : cnt - 1, jj[u], TT[u]);
-            if (MPH_DIAG_GATHER == 1) jj[u] = min((int)(blockIdx.x * blockDim.x + threadIdx.x) ^ 1, dev_n(P) - 1);
-        }
+        for (int u = 0; u < U; ++u) nbr_at(NL, k0 + u < cnt ? k0 + u : cnt - 1, jj[u], TT[u]);
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (MPH_PB_REC) {
-                rec_load(rec, P.n, jj[u], X[u], Y[u], Z[u], PJ[u]);
-            } else {
-                X[u] = A.x[jj[u]]; Y[u] = A.y[jj[u]]; Z[u] = A.z[jj[u]];
-                PJ[u] = pres[jj[u]];
-            }
-        }
+        for (int u = 0; u < U; ++u) rec_load(rec, P.n, jj[u], X[u], Y[u], Z[u], PJ[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (k0 + u >= cnt) break;
-            if (kListSpread && TT[u] < 0) continue;   // a row the lane skipped (sentinel)
-            if (MPH_DIAG_GATHER == 2) { f0 += X[u] + Y[u] + Z[u] + PJ[u] + TT[u]; continue; }
             pass_b_term<FAST, SURF, DIM>(P, s_ratio, gx, gy, gz, pa, jj[u], TT[u], X[u], Y[u], Z[u], PJ[u], ti,
                                          solid, xi, yi, zi, gxi, gyi, gzi, pai, ai, dscale, cpv, f0, f1, f2);
         }
@@ -2689,22 +1676,19 @@ template <bool SURF, int DIM>
 __global__ __launch_bounds__(MPH_LB) MPH_PB_ATTR void k_pass_b(DevParams P, const DevTables* __restrict__ T, Soa A,
                                                 const double4* __restrict__ rec,
                                                 const double4* __restrict__ fpart,
-                                                const double* __restrict__ pres,
                                                 const double* __restrict__ gx,
                                                 const double* __restrict__ gy,
                                                 const double* __restrict__ gz,
                                                 const double* __restrict__ pa,
                                                 const int* __restrict__ nbr,
                                                 const int* __restrict__ ncount,
-                                                const int* __restrict__ lhdr,
                                                 double4* __restrict__ force, double4* __restrict__ acc,
                                                 Soa B, int phase, int* __restrict__ wface, StructHook H,
                                                 const DevState* __restrict__ st)
 {
     const int n = dev_n(P);
-    const int lb = list_block(st, n, 2);
+    const int lb = list_block(st, n);
     if (lb < 0) return;
-    XCD_PROBE(st, 2);
     __shared__ double s_ratio[kTypes * kTypes];
     if (SURF) {
         if (threadIdx.x < kTypes * kTypes) s_ratio[threadIdx.x] = T->ratio[threadIdx.x];
@@ -2742,19 +1726,15 @@ __global__ __launch_bounds__(MPH_LB) MPH_PB_ATTR void k_pass_b(DevParams P, cons
         ai = T->cofa[ti] * P.cofk * P.cofk;
     }
     const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
-    __shared__ int s_gb[kWB][8];
-    const NbrList NL = nbr_list(nbr, lhdr, i, s_gb[threadIdx.x >> 6]);
-    if (NL.c16)   // compact lists come from interior searches only
-        pass_b_loop<true, true, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, NL, cnt, ti, solid, xi, yi,
-                                           zi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
-    else if (fast)
-        pass_b_loop<true, false, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, NL, cnt, ti, solid, xi, yi,
-                                            zi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
+    const NbrList NL = nbr_list(nbr, i);
+    if (fast)
+        pass_b_loop<true, SURF, DIM>(P, s_ratio, rec, gx, gy, gz, pa, NL, cnt, ti, solid, xi, yi, zi, gxi, gyi,
+                                     gzi, pai, ai, f0, f1, f2);
     else
-        pass_b_loop<false, false, SURF, DIM>(P, s_ratio, A, rec, pres, gx, gy, gz, pa, NL, cnt, ti, solid, xi, yi,
-                                             zi, gxi, gyi, gzi, pai, ai, f0, f1, f2);
+        pass_b_loop<false, SURF, DIM>(P, s_ratio, rec, gx, gy, gz, pa, NL, cnt, ti, solid, xi, yi, zi, gxi, gyi,
+                                      gzi, pai, ai, f0, f1, f2);
     double vxi, vyi, vzi;
-    own_velocity(A, i, vxi, vyi, vzi, P.n);
+    own_velocity(A, i, vxi, vyi, vzi);
     double vo0 = vxi, vo1 = vyi, vo2 = vzi;
     double xo0 = xi, xo1 = yi, xo2 = zi;
     double4 ao = make_double4(0.0, 0.0, 0.0, 0.0);
@@ -2813,7 +1793,6 @@ __global__ __launch_bounds__(256) void k_virial(DevParams P, const DevTables* __
                                                 const double* __restrict__ gx, const double* __restrict__ gy,
                                                 const double* __restrict__ gz, const int* __restrict__ nbr,
                                                 const int* __restrict__ ncount,
-                                                const int* __restrict__ lhdr,
                                                 double* __restrict__ vir, double* __restrict__ vpres)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2830,19 +1809,9 @@ __global__ __launch_bounds__(256) void k_virial(DevParams P, const DevTables* __
     double S[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
     const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
     const int* row = ell_row(nbr, i);
-    // either list format (the neighbours come in the same order): ELL row or compact entries
-    __shared__ int s_gb[4][8];
-    const NbrList NL = nbr_list(nbr, lhdr, i, s_gb[threadIdx.x >> 6]);
     for (int k = 0; k < cnt; ++k) {
-        int j, tj;
-        if (NL.c16) {
-            nbr_at<true>(NL, k, j, tj);
-        } else {
-            const int e = *ell_at(row, (int)(i & 63), k);
-            if (kListSpread && e < 0) continue;   // a row the lane skipped (sentinel)
-            j = e & kIndexMask;
-            tj = e >> kTypeShift;
-        }
+        const int e = *ell_at(row, (int)(i & 63), k);
+        const int j = e & kIndexMask, tj = e >> kTypeShift;
         double q[3];
         q[0] = image_exact<false>(B.x[j] - xi, P.dw[0], P.hw[0], P.w075[0]);
         q[1] = image_exact<false>(B.y[j] - yi, P.dw[1], P.hw[1], P.w075[1]);
@@ -3725,7 +2694,7 @@ static inline int blocks(int n, int t) { return (n + t - 1) / t; }
 static inline int list_grid(int n)
 {
     const int nb = blocks(n, MPH_LB);
-    return MPH_XCD_BAL ? (nb + nb / 4 + 15) / 8 * 8 : nb;
+    return (nb + nb / 4 + 15) / 8 * 8;
 }
 
 // A profiled launch (mph_profile_steps): its start/stop events come from the kernel's dispatch
@@ -3757,29 +2726,14 @@ void launch_sort(const Launch& L, int mode)
     if (n == 0) return;
     const int nb = blocks(P.ncell, kScanBlock);
     const int top = nb <= kScanFusedTop;
-    const int bs = bsum_stride(P.ncell);
-    const int split = MPH_SPLIT_IN_PREP && MPH_XCD_BAL && n >= L.xcd_bal_min;   // the passes' XCD split (above)
-    if (MPH_PREP_BSUM) {
-        // block totals from k_prep into this step's parity buffer of L.bsum (no k_scan_reduce)
-        MPH_LAUNCH("prep", L.stream, k_prep, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.B,
-                   L.key, L.slot, L.cnt, mode, L.vsrc, L.bsum, split);
-        if (!top)
-            MPH_LAUNCH("scan_top", L.stream, k_scan_top, dim3(1), dim3(1024), 0, L.stream, L.bsum, nb,
-                       (const DevState*)L.st, bs);
-        MPH_LAUNCH("scan_down", L.stream, k_scan_down, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt,
-                   P.ncell, L.bsum, L.start, n, P.n_dev, top, (const DevState*)L.st, bs);
-    } else {
-        int* bsum = L.bsum + 2 * bs;   // the scratch third of L.bsum
-        MPH_LAUNCH("prep", L.stream, k_prep, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.B,
-                   L.key, L.slot, L.cnt, mode, L.vsrc, (int*)nullptr, split);
-        MPH_LAUNCH("scan_reduce", L.stream, k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt,
-                   P.ncell, bsum);
-        if (!top)
-            MPH_LAUNCH("scan_top", L.stream, k_scan_top, dim3(1), dim3(1024), 0, L.stream, bsum, nb,
-                       (const DevState*)nullptr, 0);
-        MPH_LAUNCH("scan_down", L.stream, k_scan_down, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt,
-                   P.ncell, bsum, L.start, n, P.n_dev, top, (const DevState*)nullptr, 0);
-    }
+    const int split = n >= L.xcd_bal_min;   // the passes' XCD split (list_grid, k_rank_scatter)
+    MPH_LAUNCH("prep", L.stream, k_prep, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.B, L.key,
+               L.slot, L.cnt, mode, L.vsrc);
+    MPH_LAUNCH("scan_reduce", L.stream, k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt, P.ncell,
+               L.bsum);
+    if (!top) MPH_LAUNCH("scan_top", L.stream, k_scan_top, dim3(1), dim3(1024), 0, L.stream, L.bsum, nb);
+    MPH_LAUNCH("scan_down", L.stream, k_scan_down, dim3(nb), dim3(kScanThreads), 0, L.stream, L.cnt, P.ncell,
+               L.bsum, L.start, n, P.n_dev, top);
     MPH_LAUNCH("place", L.stream, k_place, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P, L.st, L.key,
                L.slot, L.start, L.tmp, mode);
     MPH_LAUNCH("rank_scatter", L.stream, k_rank_scatter, dim3(blocks(n, 256)), dim3(256), 0, L.stream, P,
@@ -3791,39 +2745,15 @@ static PassAOut pass_a_out(const Launch& L)
     return PassAOut{L.pres, L.gx, L.gy, L.gz, L.pa, L.dens_a, L.vstrain, L.divp, L.fpart, L.rec};
 }
 
-static inline int chunk_grid(int n, int C)
-{
-    const int q = (blocks(n, MPH_LB) + 7) / 8;
-    return 8 * ((q + C - 1) / C + 1);
-}
-
-// ck: 0 the whole search (then the XCD split and the compact lists' REDO launch), else one piece
-// of a chunked search (launch_search_pass_a launches the split after the last piece)
-void launch_neighbors(const Launch& L, int ck)
+void launch_neighbors(const Launch& L)
 {
     Profiler* prof = L.prof;
     const DevParams& P = *L.P;
     if (P.n == 0) return;
-    // the second launch (REDO) only when compact lists are on; its waves exit at once unless the
-    // first marked them
-    const int bal = MPH_XCD_BAL && P.n >= L.xcd_bal_min;
-    const int nb_grid = ck ? chunk_grid(P.n, ck & 0xff) : blocks(P.n, MPH_LB);
-#define MPH_NEIGHBORS(D, PERM)                                                                               \
-    do {                                                                                                     \
-        if (L.lhdr)                                                                                          \
-            MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM, true>), dim3(nb_grid),                     \
-                       dim3(MPH_LB), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.nbcount, L.lhdr, L.st, L.wface, bal, \
-                       L.whdr, ck);                                                                          \
-        else                                                                                                 \
-            MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM, false>), dim3(nb_grid),                    \
-                       dim3(MPH_LB), MPH_NB_SHM_PAD, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.nbcount, L.lhdr, L.st, L.wface, bal, \
-                       L.whdr, ck);                                                                          \
-        if (bal && !ck && !MPH_SPLIT_IN_PREP)                                                                \
-            MPH_LAUNCH("xcd_split", L.stream, k_xcd_split, dim3(1), dim3(kXcdSplitThreads), 0, L.stream, L.st); \
-        if (L.lhdr)                                                                                          \
-            MPH_LAUNCH("neighbors_redo", L.stream, (k_neighbors_redo<D, PERM>), dim3(1),                     \
-                       dim3(256), 0, L.stream, P, L.A, L.start, L.nbr, L.ncount, L.nbcount, L.lhdr, L.st);    \
-    } while (0)
+    const int bal = P.n >= L.xcd_bal_min;
+#define MPH_NEIGHBORS(D, PERM)                                                                             \
+    MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM>), dim3(blocks(P.n, MPH_LB)), dim3(MPH_LB), 0, \
+               L.stream, P, L.A, L.start, L.nbr, L.ncount, L.nbcount, L.st, L.wface, bal)
     if (P.dim == 3) {
         switch (P.perm) {
         case 1: MPH_NEIGHBORS(3, 1); break;
@@ -3838,57 +2768,25 @@ void launch_neighbors(const Launch& L, int ck)
 #undef MPH_NEIGHBORS
 }
 
-void launch_pass_a(const Launch& L, int ck)
+void launch_pass_a(const Launch& L)
 {
     Profiler* prof = L.prof;
     const DevParams& P = *L.P;
     if (P.n == 0) return;
     const PassAOut po = pass_a_out(L);
-    const int2* wh = MPH_PA_STAGED && !L.lhdr ? L.whdr : nullptr;
-    if (wh && P.slab_axis < 0) {   // the interior waves first (k_pass_a leaves them)
-        if (P.dim == 3)
-            MPH_LAUNCH("pass_a_st", L.stream, k_pass_a_st<3>, dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P,
-                       L.T, L.A, L.nbr, L.ncount, po, L.st, wh);
-        else
-            MPH_LAUNCH("pass_a_st", L.stream, k_pass_a_st<2>, dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P,
-                       L.T, L.A, L.nbr, L.ncount, po, L.st, wh);
-    }
-    const int grid = ck ? chunk_grid(P.n, ck & 0xff) : list_grid(P.n);
     if (P.dim == 3)
-        MPH_LAUNCH("pass_a", L.stream, k_pass_a<3>, dim3(grid), dim3(MPH_LB), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, L.lhdr, po, L.st, wh, ck);
+        MPH_LAUNCH("pass_a", L.stream, k_pass_a<3>, dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P, L.T, L.A,
+                   L.nbr, L.ncount, po, L.st);
     else
-        MPH_LAUNCH("pass_a", L.stream, k_pass_a<2>, dim3(grid), dim3(MPH_LB), 0, L.stream, P, L.T,
-                   L.A, L.nbr, L.ncount, L.lhdr, po, L.st, wh, ck);
+        MPH_LAUNCH("pass_a", L.stream, k_pass_a<2>, dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P, L.T, L.A,
+                   L.nbr, L.ncount, po, L.st);
 }
 
-// calculateNeighbor + the pass-A sums (the search, the XCD split of the passes, pass A).  With
-// Launch.chunks = C > 1 (single context, full lists in ELL, no staged pass A) the search runs in C
-// pieces on L.stream and pass A of each piece on L.stream2 as soon as its piece is listed: pass A
-// (bound by L1 tag lookups) then shares the CUs with the next piece's search (bound by VALU issue
-// and address processing).  Pass A of a piece reads the lists of its own particles only.
+// calculateNeighbor + the pass-A sums
 void launch_search_pass_a(const Launch& L)
 {
-    const int C = MPH_CHUNK_BUILD ? L.chunks : 1;
-    if (C <= 1 || !L.stream2 || !L.ev_chunk || L.lhdr || MPH_PA_STAGED || L.P->slab_axis >= 0 || L.P->n == 0) {
-        launch_neighbors(L);
-        launch_pass_a(L);
-        return;
-    }
-    Profiler* prof = L.prof;
-    Launch La = L;
-    La.stream = L.stream2;
-    for (int c = 0; c < C; ++c) {
-        const int ck = c << 8 | C;
-        launch_neighbors(L, ck);
-        (void)hipEventRecord(L.ev_chunk[c], L.stream);
-        (void)hipStreamWaitEvent(L.stream2, L.ev_chunk[c], 0);
-        launch_pass_a(La, ck);
-    }
-    if (MPH_XCD_BAL && L.P->n >= L.xcd_bal_min && !MPH_SPLIT_IN_PREP)
-        MPH_LAUNCH("xcd_split", L.stream, k_xcd_split, dim3(1), dim3(kXcdSplitThreads), 0, L.stream, L.st);
-    (void)hipEventRecord(L.ev_chunk[C], L.stream2);
-    (void)hipStreamWaitEvent(L.stream, L.ev_chunk[C], 0);
+    launch_neighbors(L);
+    launch_pass_a(L);
 }
 
 static StructHook struct_hook(const Launch& L)
@@ -3918,7 +2816,7 @@ void launch_pass_b(const Launch& L, int phase)
     }
 #define MPH_PASS_B(S, D)                                                                            \
     MPH_LAUNCH(phase == 2 ? "pass_b_face" : "pass_b", L.stream, (k_pass_b<S, D>), dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P, \
-               L.T, L.A, L.rec, L.fpart, L.pres, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, L.lhdr, L.force, L.acc, L.B, \
+               L.T, L.A, L.rec, L.fpart, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, L.force, L.acc, L.B, \
                phase, L.wface, \
                struct_hook(L), L.st)
     if (P.surface) {
@@ -3936,10 +2834,10 @@ void launch_virial(const Launch& L, const Soa& X, double* vir, double* vpres)
     if (P.n == 0) return;
     if (P.dim == 3)
         MPH_LAUNCH("virial", L.stream, k_virial<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T, L.A, X,
-                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, L.lhdr, vir, vpres);
+                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, vir, vpres);
     else
         MPH_LAUNCH("virial", L.stream, k_virial<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T, L.A, X,
-                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, L.lhdr, vir, vpres);
+                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, vir, vpres);
 }
 
 // lanes per structure slot: one lane per slot while the launch has >= kStructLanesTarget lanes
@@ -3990,9 +2888,6 @@ void launch_struct_stress(const Launch& L, bool store, int s0, int s1)
     const StructDev& S = *L.S;
     if (s1 < 0) s1 = S.n_own;
     if (s1 <= s0) return;
-#ifdef MPH_STRUCT_STORE_ALL
-    store = true;   // A/B timing of the output stores
-#endif
     MPH_STRUCT_DISPATCH(k_struct_stress, "struct_stress", P, s0, s1, S.wo, S.ocnt, S.eo_nb, S.x0, S.u, S.L,
                         S.lame, S.P, S.F, S.E, S.S, S.fes, store ? 1 : 0);
 }
@@ -4030,7 +2925,7 @@ int launch_struct_init(const Launch& L, int ns, const double4* x0, int* key, int
     const dim3 g(blocks(ns, 256)), b(256);
     // bin the slots on the grid (L.cnt is zero between steps and the scan re-zeroes it)
     MPH_LAUNCH("sinit_bin", L.stream, k_sinit_bin, g, b, 0, L.stream, P, ns, x0, key, L.cnt, slot);
-    launch_scan(L.cnt, P.ncell, L.bsum + 2 * bsum_stride(P.ncell), L.start, ns, L.stream, prof);   // scratch third
+    launch_scan(L.cnt, P.ncell, L.bsum, L.start, ns, L.stream, prof);
     MPH_LAUNCH("sinit_place", L.stream, k_sinit_place, g, b, 0, L.stream, ns, key, slot, L.start, tmp, sorted, 0);
     MPH_LAUNCH("sinit_place", L.stream, k_sinit_place, g, b, 0, L.stream, ns, key, slot, L.start, tmp, sorted, 1);
     if (P.dim == 3)
@@ -4107,9 +3002,9 @@ void launch_scan(int* cnt, int ncell, int* bsum, int* start, int total, hipStrea
     const int top = nb <= kScanFusedTop;
     MPH_LAUNCH("scan_reduce", stream, k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, stream, cnt, ncell, bsum);
     if (!top)
-        MPH_LAUNCH("scan_top", stream, k_scan_top, dim3(1), dim3(1024), 0, stream, bsum, nb, (const DevState*)nullptr, 0);
+        MPH_LAUNCH("scan_top", stream, k_scan_top, dim3(1), dim3(1024), 0, stream, bsum, nb);
     MPH_LAUNCH("scan_down", stream, k_scan_down, dim3(nb), dim3(kScanThreads), 0, stream, cnt, ncell, bsum,
-               start, total, (const int*)nullptr, top, (const DevState*)nullptr, 0);
+               start, total, (const int*)nullptr, top);
 }
 
 int dist_blocks(int n) { return blocks(n > 0 ? n : 1, 256); }

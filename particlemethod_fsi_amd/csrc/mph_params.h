@@ -8,12 +8,6 @@
 
 #include "../../include/mph_gpu.h"
 
-#ifndef MPH_DIAG_XCD
-#define MPH_DIAG_XCD 0   // 1: per-XCD wave timing of the list kernels (diagnostic builds only)
-#endif
-#ifndef MPH_DIAG_PATHS
-#define MPH_DIAG_PATHS 0   // 1: the search's column paths counted (diagnostic builds only, mph_diag_paths)
-#endif
 
 namespace mph {
 
@@ -28,36 +22,15 @@ constexpr int kTile = 64;  // ELL neighbour-list tile = one wavefront of i-parti
 #define MPH_TILE_PAD 1
 #endif
 constexpr int kTileStride = kTile * (kMaxNeighbor + MPH_TILE_PAD);
-// Slot of entry k of lane `lane` in its wave's tile (ints).  Rows: entry k of the 64 lanes in one
-// 256-byte row, [k][lane].  MPH_LIST_PAIRS=1 / 2: entries of a lane in groups of 2 / 4 side by side,
-// [k / G][lane][G], so a 128-byte line holds the groups of 128 / (4 G) lanes.
-#ifndef MPH_LIST_PAIRS
-#define MPH_LIST_PAIRS 0
-#endif
-constexpr int kListLg = MPH_LIST_PAIRS;    // log2 of the group
-constexpr bool kListPairs = kListLg > 0;
-// MPH_LIST_HALF=1: each half-wave (32 lanes) has rows of its own, [lane / 32][k][lane % 32], so a
-// row is one 128-byte line written by 32 lanes instead of two lines written by 64
-#ifndef MPH_LIST_HALF
-#define MPH_LIST_HALF 0
-#endif
-constexpr bool kListHalf = MPH_LIST_HALF;
-// MPH_LIST_SPREAD=1: a lane's k-th stored neighbour goes to row k * M / n of its wave's tile (n:
-// the lane's NeighborCount of the last step, M: the wave's largest), the rows it skips hold a
-// sentinel (its own index with the type bits all set, which the list readers skip), so the lanes
-// fill their rows at the same pace and the wave's rows complete together (mph_kernels.hip search)
-#ifndef MPH_LIST_SPREAD
-#define MPH_LIST_SPREAD 0
-#endif
-constexpr bool kListSpread = MPH_LIST_SPREAD;
-constexpr int kSpreadMax = 192;   // waves predicted above this many neighbours keep rows = k
+// Slot of entry k of lane `lane` in its wave's tile (ints): entry k of the 64 lanes in one 256-byte
+// row, [k][lane].  (Entries in pairs or fours side by side, rows per half-wave and rows spread by the
+// last step's NeighborCount were measured in round 5 and rejected: DESIGN.md section 3.3.)
 #if defined(__HIPCC__)
 __host__ __device__
 #endif
 constexpr inline int ell_slot(int k, int lane)
 {
-    return kListHalf ? ((((lane >> 5) * kMaxNeighbor + k) << 5) | (lane & 31))
-                     : (((k >> kListLg) << (6 + kListLg)) | (lane << kListLg) | (k & ((1 << kListLg) - 1)));
+    return (k << 6) | lane;
 }
 // Stencil reach along the contiguous axis: cells there are >= rc / kContigReach wide, and a
 // column is the one index range of +-kContigReach cells (thin cells only sharpen the cutoff
@@ -75,33 +48,12 @@ constexpr int kContigReach = MPH_SA;
 #define MPH_R 3
 #endif
 constexpr int kReach = MPH_R;
-constexpr int kGroups = 2 * kReach + 1;   // compact-list groups: one per slowest-axis offset
+constexpr int kGroups = 2 * kReach + 1;   // stencil columns per axis across the column axes
 // ELL list entry = sorted index | (type << kTypeShift): pass A reads the neighbour's type with
 // its index instead of gathering it (requires fewer than 2^28 particles per context)
 constexpr int kTypeShift = 28;
 constexpr int kIndexMask = (1 << kTypeShift) - 1;
 constexpr int kPad = 8;         // extra elements behind every per-particle array (vector over-reads)
-// Compact neighbour list of a wavefront (mph_kernels.hip, MPH_LIST16): ints per wave header --
-// kGroups (<= 7) group bases, the format flag at kHdrFlag, then the 64 lanes' group ends: the
-// ends of groups 0-3 (4 bytes) at [8 + lane], of groups 4-5 at [8 + 64 + lane]
-constexpr int kHdrFlag = 7;
-// the default list format: compact pays at kReach = 2 (D1M -1 %, D16M -6 %); at kReach = 3 the
-// passes' gathers are coherent and the 16-bit decode (group of the entry, then its base) costs
-// more than the list bytes it saves (D1M pass A 0.381 -> 0.416 ms)
-#ifndef MPH_LIST_COMPACT
-#define MPH_LIST_COMPACT (MPH_R == 2)
-#endif
-constexpr bool kListCompact = MPH_LIST_COMPACT;
-constexpr int kLhdr = 8 + 2 * 64;
-// pieces of the chunked search + pass A (launch_search_pass_a; MPH_CHUNKS overrides at creation);
-// 1 = one search launch, then one pass-A launch
-#ifndef MPH_SEARCH_CHUNKS
-#define MPH_SEARCH_CHUNKS 1
-#endif
-constexpr int kSearchChunks = MPH_SEARCH_CHUNKS;
-// per-wave column windows of the staged pass A (MPH_PA_STAGED, mph_kernels.hip): int2 entries
-constexpr int kWinHdr = (2 * 3 + 1) * (2 * 3 + 1) + 1;
-static_assert(kGroups <= kHdrFlag, "group bases overlap the format flag");
 
 inline bool is_fluid(int t) { return t >= 0 && t < 2; }   // main.cpp:69-70
 inline bool is_struct(int t) { return t >= 2 && t < 4; }  // main.cpp:71-72
@@ -143,8 +95,6 @@ struct DevParams {
     // wavefronts the list kernels skip) while every XCD's contiguous share of the sorted arrays
     // stays a band of that slowest axis through the whole slab (L2 locality); 1, 2 put z slowest
     int perm;
-    int l16max;        // most neighbours a lane of a compact-list wave may have (127: byte group
-                       // ends; lower only to test the ELL redo, MPH_LIST16_MAX)
     int fast_ok;       // every active axis has > 12 GPU cells: interior waves may skip the
                        // periodic branch of the minimum image (see k_neighbors)
     double inner_lo[3], inner_hi[3];   // interior box: >= 3 GPU cells from every periodic face
@@ -188,18 +138,14 @@ struct DevParams {
     double rc2_trim;         // rc2 (1 + 4e-6): the column-trimming bound
     double cwid[3];          // 1 / ginv: GPU cell widths
     double rg_r2g;           // rg / r2g (GravityCenter, DiffuseInterface)
-    double cref[3];          // MPH_SEARCH_F32: the domain centre the FP32 records are taken from
-    float rc2f_lo, rc2f_hi;  // MPH_SEARCH_F32: below lo the FP32 r^2 accepts, above hi it rejects
+    double cref[3];          // the domain centre the search's FP32 records are taken from
+    float rc2f_lo, rc2f_hi;  // below lo the FP32 r^2 accepts, above hi it rejects (FP64 between)
     // The search stores a neighbour in the list only if its FP32 r^2 <= rlf: the largest radius of
     // the passes' sums (MaxRadius, main.cpp:1199) squared, widened by the FP32 records' error band,
     // so the list holds every pair any sum can take (the passes' exact tests decide) and not the
     // shell MaxRadius < r <= MaxRadius + MARGIN that the reference's list carries and NeighborCount
     // counts.  FLT_MAX (MPH_LIST_FULL=1): the reference's whole list.
     float rlf;
-    // MPH_LIST_SPREAD, single contexts: pred[i] the sorted particle i's NeighborCount of the last
-    // step, written by k_rank_scatter from pred_src (the last step's NeighborCount, its order)
-    int* pred = nullptr;
-    const int* pred_src = nullptr;
 };
 
 // Derived uniforms of DevParams (same expressions the kernels used, so the same bits).
@@ -210,7 +156,7 @@ inline void set_uniforms(DevParams& P)
     P.rc2_trim = P.rc2 * (1.0 + 4e-6);
     for (int d = 0; d < 3; ++d) P.cwid[d] = 1.0 / P.ginv[d];
     P.rg_r2g = P.rg / P.r2g;
-    // FP32 records (MPH_SEARCH_F32): coordinates within half a domain width of the centre, each
+    // FP32 records (the search's): coordinates within half a domain width of the centre, each
     // rounded once (<= 2^-24 x that); a difference is off by <= 2^-23 hw, r^2 near the cutoff by
     // <= 2 sqrt(3) 2^-23 hw / rc relative plus the FP32 sum's few ulp: the band is twice that
     double hwm = 0.0;
@@ -229,13 +175,6 @@ inline void set_uniforms(DevParams& P)
 // work histogram of the XCD map: waves in 4096 equal runs (D16M: ~60 waves per run, so the
 // search's per-wave atomics spread over ~100 addresses at a time; 512 runs cost its search 7 %)
 constexpr int kXcdSegs = 4096;
-// MPH_CU_AFFINE=1: each CU takes the list kernels' tiles from a contiguous range of its own, so
-// the blocks resident on a CU are neighbours in the cell order and share L1 lines
-#ifndef MPH_CU_AFFINE
-#define MPH_CU_AFFINE 0
-#endif
-constexpr int kCuQueues = 32;
-constexpr int kXcdSplitThreads = 1024;   // k_xcd_split: 4 runs per thread
 
 // Mutable per-step device scalars (so a captured hipGraph can replay many steps).
 struct DevState {
@@ -245,8 +184,9 @@ struct DevState {
     double wall_omega[kTypes][3];// WallOmega
     double wall_rot[kTypes][3][3];  // WallRotation (initializeWall)
     int overflow;                // error bits: 1 neighbour overflow (> MAX_NEIGHBOR_COUNT),
-                                 // 2 slab jump (mph_dist), 4 non-finite position
-    int list_redo;               // waves of this step's search left for k_neighbors_redo
+                                 // 2 slab jump (mph_dist), 4 non-finite position, 8 message
+                                 // capacity (mph_dist), 64 inconsistent cell histogram
+    int pad0;
     // particles within the face box margin of a periodic face, per axis (bit 2k: low face, 2k+1:
     // high face), gathered by k_prep into seam_occ[seam_step & 1]; k_place clears the other word
     // and advances seam_step, so the search reads seam_occ[(seam_step - 1) & 1]
@@ -255,45 +195,11 @@ struct DevState {
     int seam_pad;
     // work-balanced XCD map of the two list passes (mph_kernels.hip, list_block): the search adds
     // each wave's work (its longest list + a fixed cost) into seg_work[its 1/kXcdSegs of the waves];
-    // k_xcd_split turns that into the XCDs' contiguous block ranges (xcd_frac: fractions of 2^16,
-    // 0 ... 65536) for this step's passes and clears seg_work
+    // the next step's k_rank_scatter turns that into the XCDs' contiguous block ranges (xcd_frac:
+    // fractions of 2^16, 0 ... 65536) for the passes and clears seg_work
     int seg_work[kXcdSegs];
     int xcd_frac[9];
     int xcd_pad[3];
-#if MPH_CU_AFFINE
-    // CU-affine tiles of the list kernels (mph_kernels.hip, cu_affine_tile): per kernel a block
-    // ticket counter (its generation: ticket / blocks of the launch) and per logical XCD and queue
-    // the claimed count of the queue's tiles, tagged with the generation in the high 32 bits
-    unsigned long long cu_tick[3];
-    unsigned long long cu_pad;
-    unsigned long long cu_q[3][8][kCuQueues];
-#endif
-#if MPH_DIAG_PATHS
-    // diagnostic build only (tools/search_paths.py): per search path of a wave's stencil column
-    // (0 one FP32 window, 1 two FP32 runs, 2 FP64 staged, 3 per-lane global loads) the columns, the
-    // lanes' candidates (sum of je - jb) and the window's records (span, or n1 + n2); [12..15]
-    // the split's outcome when the window was too wide (no gap, runs too wide, ok) and the waves;
-    // [16..31] a simulated LDS row ring of R = 4, 8, 16, 32 rows (flushed at column ends: rule 0
-    // the rows every lane has passed, rule 1 also partial rows to keep R / 2 rows of headroom): the
-    // stored entries it could not take, {ahead of the ring, behind it} per (rule, R); [32] the
-    // stored entries; [33] the rows flushed by rule 1 with R = 16; [34..39] the columns whose window
-    // spans (64, 96], (96, 128], (128, 160], (160, 192], (192, 256], > 256 records; [40..42] the rows
-    // of column-aligned lists (per column, per group of kGroups columns) and of today's (the longest)
-    unsigned long long path_diag[48];
-    // [44..47] of path_diag: the list stores' 64-byte segments per store instruction with the lanes
-    // in order and with the lanes ranked by the previous step's NeighborCount (diag_prev), the
-    // store instructions and their entries
-    const int* diag_prev;
-#endif
-#if MPH_DIAG_XCD
-    // diagnostic build only (tools/xcd_diag.py): per list kernel (search, pass A, pass B) and XCD,
-    // the first wave's start, the last wave's end (wall_clock64), the summed wave time, the waves
-    unsigned long long xcd_diag[3][4][8];
-    // per-wave log of the search (MPH_DIAG_XCD >= 2): {start, end, XCC_ID} per wave slot of the launch
-    unsigned long long* wave_log;
-    int wave_log_n;
-    int wave_log_pad;
-#endif
 };
 // the part of DevState the host reads back after steps (the error bits and the step scalars)
 constexpr size_t kStateHead = offsetof(DevState, seg_work);
@@ -305,8 +211,7 @@ constexpr size_t kStateHead = offsetof(DevState, seg_work);
 #endif
 
 // Pass A's single-cutoff form (pass_a_term<.., true>) when RadiusA = RadiusP = RadiusV (RadiusG =
-// RadiusA, main.cpp:1195-1198), as in every BASELINE config; compact lists are built only then
-// (ctx_fill_launch), so both list formats of an interior wave take the same form.
+// RadiusA, main.cpp:1195-1198), as in every BASELINE config.
 #ifndef MPH_PA_EQR
 #define MPH_PA_EQR 1
 #endif

@@ -56,11 +56,11 @@ EXPORTED_SYMBOLS = [
     "mph_config_sizeof", "mph_write_vtk_async", "mph_output_wait", "mph_write_grid_binary",
     "mph_write_vtu_arrays", "mph_write_vtu", "mph_velocity_profile_arrays",
     "mph_set_initial_velocity_profile", "mph_dist_info", "mph_create_slab", "mph_slab_window",
-    "mph_list_formats", "mph_abi_version", "mph_phase_timing", "mph_phase_times",
+    "mph_list_stats", "mph_abi_version", "mph_phase_timing", "mph_phase_times",
     "mph_set_step_batching", "mph_neighbor_rows", "mph_dist_overlap",
 ]
 
-ABI_VERSION = 3   # MPH_ABI_VERSION of include/mph_gpu.h that these bindings follow
+ABI_VERSION = 4   # MPH_ABI_VERSION of include/mph_gpu.h that these bindings follow
 
 # mph_host_exchange_fn (include/mph_gpu.h): (user, send_l, n, send_r, n, recv_l, n, recv_r, n)
 HOST_EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
@@ -149,7 +149,7 @@ def load_library() -> ctypes.CDLL:
         "mph_velocity_profile_arrays": (ip, [cfgp, dp, ip, vp, vp, vp, vp]),
         "mph_set_initial_velocity_profile": (ip, [vp]),
         "mph_dist_info": (ip, [vp, vp]),
-        "mph_list_formats": (ip, [vp, vp]),
+        "mph_list_stats": (ip, [vp, vp, vp]),
         "mph_create_slab": (ip, [ctypes.POINTER(vp), cfgp, ip, vp, vp, vp, vp, ip, ctypes.POINTER(MphSlabOptions)]),
         "mph_slab_window": (ip, [cfgp, ip, ip, ip, vp, vp]),
         "mph_phase_timing": (ip, [vp, ip]),
@@ -160,14 +160,17 @@ def load_library() -> ctypes.CDLL:
     }
     # entry points an older library may lack (A/B runs against earlier builds)
     optional = {"mph_phase_timing", "mph_phase_times", "mph_set_step_batching", "mph_neighbor_rows",
-                "mph_dist_overlap", "mph_profile_graphs"}
+                "mph_dist_overlap", "mph_profile_graphs", "mph_list_stats"}
     for name, (res, args) in sig.items():
         if name in optional and not hasattr(L, name):
             continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    if L.mph_abi_version() != ABI_VERSION:
+    # MPH_ABI_ACCEPT=3: an A/B run against a round-5 build (ABI 3 differs only by mph_list_formats,
+    # replaced by mph_list_stats in 4; tools/lib_bitwise.py)
+    accept = {ABI_VERSION} | {int(v) for v in os.environ.get("MPH_ABI_ACCEPT", "").split(",") if v.strip()}
+    if L.mph_abi_version() not in accept:
         raise ImportError("%s has C ABI version %d, these bindings expect %d (rebuild the library)"
                           % (LIB_PATH, L.mph_abi_version(), ABI_VERSION))
     if L.mph_config_sizeof() != ctypes.sizeof(mphio.MphConfig):
@@ -460,11 +463,13 @@ class MphSolver:
         _check(self._L.mph_owned_ids(self._h, out.ctypes.data), self._h)
         return out[:k].copy()
 
-    def list_formats(self) -> tuple:
-        """(wavefronts with compact 16-bit neighbour lists, all wavefronts) of the last search."""
-        a = np.zeros(2, np.int32)
-        _check(self._L.mph_list_formats(self._h, a.ctypes.data), self._h)
-        return int(a[0]), int(a[1])
+    def list_stats(self):
+        """(mean, max) length of the stored neighbour lists of the last search (mph_list_stats: the
+        pairs the passes walk; every neighbour with MPH_LIST_FULL=1)."""
+        m = ctypes.c_double()
+        x = ctypes.c_int()
+        _check(self._L.mph_list_stats(self._h, ctypes.byref(m), ctypes.byref(x)), self._h)
+        return m.value, x.value
 
     def neighbor_rows(self, first: int = 0, count: int | None = None):
         """(counts, offsets, ids): the neighbour sets of the particles [first, first + count) from

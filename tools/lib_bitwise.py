@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Bitwise A/B of two builds (bit-identical variants such as MPH_PA_STAGED): run each case for a
+"""Bitwise A/B of two builds (e.g. the round-6 cleanup against e6081fe): run each case for a
 few steps with the library of MPH_GPU_LIB and save every per-particle field, or compare two saved
 runs.
 

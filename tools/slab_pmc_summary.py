@@ -1,4 +1,4 @@
-"""Per-dispatch pass-B counters of tools/r03_slabpmc.sh: with the overlap every step of a rank
+"""Per-dispatch pass-B counters of the round-3 slab PMC runs (tag r05-variants, tools/r03_slabpmc.sh): with the overlap every step of a rank
 launches pass B twice (interior waves, face waves) -- told apart by their VALU counts (the
 interior launch does most of the work); without it once.  Prints the mean per launch kind."""
 import collections

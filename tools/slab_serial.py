@@ -180,16 +180,7 @@ def run_ranks(args, R, axis, cuts, locals_, records=None, replay=None):
                     graph = s.profile_graphs(8)
                 except Exception:  # noqa: BLE001 -- older library
                     graph = None
-            xcd = None
-            if os.environ.get("MPH_XCD_DIAG") == "1":   # diagnostic build: tools/xcd_diag.py
-                from xcd_diag import xcd_read
-                with token.lock:
-                    xcd_read(s, reset=True)
-                # one more step (all ranks take it: it exchanges); each context's words are its own
-                with token.lock:
-                    s.step(1)
-                    s.synchronize()
-                    xcd = xcd_read(s, reset=True)
+            xcd = None   # (per-XCD wave timing: the diagnostic build of tag r05-variants)
             with token.lock:   # device copies: not beside another rank's timed work
                 info = s.dist_info()
                 owned = len(s.owned_ids())
