@@ -318,6 +318,7 @@ def main():
     solver.step(args.steps)
     barrier()
     elapsed = time.perf_counter() - t0
+    elapsed_local = elapsed
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -354,6 +355,19 @@ def main():
     checks = None
     if dist is not None:
         checks = slab_checks(solver, dist, n_total, case_name, args.warmup + args.steps + args.profile_steps)
+        # per rank, so that the first multi-GPU run is diagnosable: the rank's own wall time per
+        # timed step (before the max over ranks), its kernels' summed HIP-event time per step
+        # (compute, mph_profile_steps) and the rest (exchange + waiting for the slowest neighbour)
+        info = solver.dist_info()
+        kern_ms = sum(v["avg_ms"] * v["launches"] for k, v in prof.items() if k != "gpu_busy") / max(1, args.profile_steps)
+        mine = {"rank": rank, "owned": len(solver.owned_ids()), "held": info["held"],
+                "ms_per_step": elapsed_local * 1e3 / args.steps, "compute_ms": kern_ms,
+                "exchange_and_wait_ms": elapsed_local * 1e3 / args.steps - kern_ms,
+                "kernels_ms": {k: round(v["avg_ms"] * v["launches"] / max(1, args.profile_steps), 5)
+                               for k, v in prof.items() if k != "gpu_busy"}}
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
+        checks["per_rank"] = per_rank
     ns, mean_ns = 0, 0.0
     if any(k in prof for k in STRUCT_BYTES):
         isnc = solver.get("InitialStructureNeighborCount")

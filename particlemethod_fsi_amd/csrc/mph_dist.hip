@@ -502,21 +502,36 @@ int collective_max(MphCtx* c, double* v, int n)
 // MPH_SLAB_OVERLAP unset ("auto"): the ranks choose the pass-B mode together at creation, from
 // what this machine and transport do.  On the initial state (after the init sums) every rank times,
 // with events on its stream, best of three after a warm-up:
-//   th  the halo exchange of the pass-A values (the step's own, at its message capacities),
-//   tr  an exchange of the redistribution messages at their capacities (dry: nothing is unpacked),
+//   th  the halo exchange of the pass-A values,
+//   tr  an exchange of the redistribution messages,
 //   ts  pass B as the overlap splits it (interior, then face waves) minus pass B in one launch;
 // the maxima over ranks decide: overlap when th + tr > ts, i.e. when the exchanges it can hide
 // behind the interior pass B (and, with the early send, behind the next partition) cost more than
-// splitting pass B does.  The probe's pass B writes B, which is then restored from A (the state
-// dist_init left).  Contexts with elastic particles keep the overlap off (their substeps write
-// the slot arrays from pass B).
+// splitting pass B does.  The exchanges are timed at their message capacities, which is what the
+// steps send: the messages of a step have fixed, capacity-sized lengths (the live counts travel in
+// their headers), so that RCCL steps can be replayed from captured graphs.
+// The probe touches no live state: its halo packs from and unpacks into the redistribution
+// scratch set C (which every step rewrites before reading, dist_enqueue_step), its redistribution
+// exchange moves the message buffers only, and its trial pass B integrates into C with the output
+// stores (Force, Acceleration) off.  Every rank takes part or none: a rank holding elastic
+// particles (whose pass B also hands them to the substep slots) keeps the overlap off on all ranks,
+// agreed through a collective max, since the structure need not reach every slab.
 int overlap_probe(MphCtx* c)
 {
     MphDist& D = *c->dist;
     D.overlap = D.overlap_mode == 1;
-    if (D.overlap_mode >= 0 || c->P.n_struct > 0) return MPH_OK;
+    if (D.overlap_mode >= 0) return MPH_OK;
+    double any_struct = c->P.n_struct > 0 ? 1.0 : 0.0;
+    MPH_CK(collective_max(c, &any_struct, 1));
+    if (any_struct > 0.0) return MPH_OK;
     Launch L = c->L;
     L.wface = D.wface;
+    L.B = D.C;                   // the trial pass B's integrated state: scratch
+    L.force = L.acc = nullptr;   // no output stores
+    HaloFields F = halo_fields(c);
+    double* scratch[5] = {D.C.x, D.C.y, D.C.z, D.C.vx, D.C.vy};
+    for (int k = 0; k < F.nf; ++k) F.f[k] = scratch[k];
+    F.rec = nullptr;
     hipEvent_t e[5] = {};
     struct Ev {
         hipEvent_t* e;
@@ -526,7 +541,7 @@ int overlap_probe(MphCtx* c)
     double best[3] = {1e30, 1e30, 1e30};
     for (int rep = 0; rep < 4; ++rep) {
         MPH_HIP_OK(c, hipEventRecord(e[0], c->stream));
-        MPH_CK(halo_exchange(c, nullptr, c->stream));
+        MPH_CK(halo_exchange(c, nullptr, c->stream, &F));
         MPH_HIP_OK(c, hipEventRecord(e[1], c->stream));
         MPH_CK(exchange(c, c->stream, D.send_l, kMsgHead + kMsgBytes * D.cap_sl, D.send_r,
                         kMsgHead + kMsgBytes * D.cap_sr, D.recv_l, kMsgHead + kMsgBytes * D.cap_rl, D.recv_r,
@@ -546,11 +561,6 @@ int overlap_probe(MphCtx* c)
         best[1] = std::min(best[1], (double)ms[1]);
         best[2] = std::min(best[2], (double)ms[3] - (double)ms[2]);
     }
-    // undo the trial pass B: B as dist_init left it, Force / Acceleration zero as after creation
-    MPH_CK(copy_soa(c, c->B, c->A, c->n));
-    MPH_HIP_OK(c, hipMemsetAsync(c->force, 0, sizeof(double4) * std::max(c->P.n, 1), c->stream));
-    MPH_HIP_OK(c, hipMemsetAsync(c->acc, 0, sizeof(double4) * std::max(c->P.n, 1), c->stream));
-    MPH_HIP_OK(c, hipStreamSynchronize(c->stream));
     MPH_CK(collective_max(c, best, 3));
     for (int k = 0; k < 3; ++k) D.probe_ms[k] = best[k];
     D.overlap = best[0] + best[1] > best[2];

@@ -210,3 +210,31 @@ def gpu_capacity_worker(rank, world, port, case, batches, out_dir):
              code=np.array([code]), **res)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def gpu_state_worker(rank, world, port, case, state_path, axis, nsteps, fields, out_dir, cuts_mode=None):
+    """One slab rank of `case` on cuda:0 started from a saved state (state_path .npz: position,
+    velocity, time -- what the reference's .prof restart holds; property and InitialPosition from
+    the case), host-staged transport: record the owned ids at creation, run `nsteps`, then save the
+    owned ids and their `fields` to out_dir/rank<r>.npz."""
+    dist = _init(rank, world, port)
+    from particlemethod_fsi_amd import MphSolver, cases, mphio
+    from particlemethod_fsi_amd.dist import gloo_slab
+    c = cases.get(case)
+    cfg, parts = c.build()
+    z = np.load(state_path)
+    cfg.time = float(z["time"][0])
+    parts = mphio.Particles(parts.property, np.ascontiguousarray(z["position"]), parts.initial_position,
+                            np.ascontiguousarray(z["velocity"]))
+    cuts = make_cuts(c, world, axis, cuts_mode)
+    with MphSolver(cfg, parts, device=0, slab=gloo_slab(rank, world, axis, cuts=cuts)) as s:
+        del parts
+        ids0 = s.owned_ids()
+        s.step(nsteps)
+        ids = s.owned_ids()
+        res = {"ids0": ids0, "ids": ids, "time": np.array([s.time])}
+        for f in fields:
+            res[f] = s.get(f)[ids]
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), **res)
+    dist.barrier()
+    dist.destroy_process_group()

@@ -17,7 +17,9 @@ handed to the CPU oracle, bit-identical to the reference, as the reference's own
   * the state did leave the lattice: NeighborCount differs from the creation's for >= 1 % of the
     particles, and the fluid front moved by more than 10 dx.
 """
+import multiprocessing as mp
 import os
+import socket
 
 import numpy as np
 import pytest
@@ -79,3 +81,72 @@ def test_d1m_developed_matches_oracle(steps):
                 err = float(np.max(np.abs(a - b)))
                 assert err <= t, (k, f, err, t)
         assert s.time == o.time
+
+
+SLAB_FIELDS = ["Position", "Velocity", "PressureP", "NeighborCount", "VolStrainP", "DivergenceP"]
+
+
+def test_d1m_developed_slab8_matches_single_context(tmp_path):
+    """The multi-GPU path in the developed flow: the D1M state at t = 0.25 s
+    (2,500 steps on one context; off the lattice, NeighborCount changed for most particles) split
+    into the 8 z slabs of bench.py --gpus 8 (8 ranks sharing the test GPU, host-staged transport;
+    every rank created from the whole state, equal cuts) against one context started from the same
+    state, 10 steps: ownership a partition of all particles, NeighborCount exact, positions 1e-12 m,
+    velocities 1e-9 m/s, the sums 1e-8 relative + the floors above -- and particles did migrate
+    between slabs (owner at the end differs from the owner at creation)."""
+    import dist_worker
+    world, steps = 8, 10
+    cfg, parts = cases.get("d1m").build()
+    with MphSolver(cfg, parts) as s:
+        nc0 = s.get("NeighborCount")
+        s.step(DEVELOPED_STEPS)
+        pos, vel, t = s.get("Position"), s.get("Velocity"), s.time
+        assert float((s.get("NeighborCount") != nc0).mean()) >= 0.01
+    state = str(tmp_path / "state.npz")
+    np.savez(state, position=pos, velocity=vel, time=np.array([t]))
+    rcfg = cfg.copy()
+    rcfg.time = t
+    with MphSolver(rcfg, mphio.Particles(parts.property, pos, parts.initial_position, vel)) as s:
+        s.step(steps)
+        ref = {f: s.get(f) for f in SLAB_FIELDS}
+        ref_time = s.time
+    ctx = mp.get_context("spawn")
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ps = [ctx.Process(target=dist_worker.gpu_state_worker,
+                      args=(r, world, port, "d1m", state, 2, steps, SLAB_FIELDS, str(tmp_path)))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(600)
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    n = parts.n
+    seen = np.zeros(n, np.int32)
+    owner0 = np.full(n, -1, np.int32)
+    owner1 = np.full(n, -1, np.int32)
+    for r in range(world):
+        z = np.load(str(tmp_path / ("rank%d.npz" % r)))
+        ids = z["ids"]
+        owner0[z["ids0"]] = r
+        owner1[ids] = r
+        seen[ids] += 1
+        assert float(z["time"][0]) == ref_time
+        for f in SLAB_FIELDS:
+            a, b = z[f], ref[f][ids]
+            if f == "NeighborCount":
+                assert np.array_equal(a, b), (r, f, int((a != b).sum()))
+                continue
+            err = float(np.max(np.abs(a - b))) if len(ids) else 0.0
+            tol = {"Position": 1e-12, "Velocity": 1e-9}.get(
+                f, 1e-8 * float(np.max(np.abs(ref[f]))) + FLOOR.get(f, 1e-12))
+            assert err <= tol, (r, f, err, tol)
+    assert (seen == 1).all(), "ownership is not a partition: %d missing, %d duplicated" % (
+        int((seen == 0).sum()), int((seen > 1).sum()))
+    migrants = int((owner0 != owner1).sum())
+    print("developed slab8: %d particles changed slab in %d steps" % (migrants, steps))
+    assert (owner0 >= 0).all() and migrants > 0, migrants

@@ -160,7 +160,8 @@ def test_slab_early_send_bitwise(tmp_path, case, world, monkeypatch):
     the next step's messages leave from pass B's face wavefronts while the interior ones run;
     with elastic particles, after the substeps) sends exactly the bytes the late pack would, so
     every field is bit-identical to MPH_SLAB_EARLY=0 -- over batches of 1, 4 and 15 steps.  The early
-    send rides on the split pass B, so the overlap is switched on (MPH_SLAB_OVERLAP=1, default off)."""
+    send rides on the split pass B, so the overlap is forced on (MPH_SLAB_OVERLAP=1; unset, the
+    ranks choose the mode at creation, test_slab_overlap_probe)."""
     fields = STRUCT_FIELDS if case.startswith(("bar", "gate")) else FIELDS
     monkeypatch.setenv("MPH_SLAB_OVERLAP", "1")
     out = {}
@@ -192,7 +193,8 @@ def test_slab_overlap_probe(tmp_path, monkeypatch):
     measured halo / redistribution exchange times against the cost of splitting pass B (max over
     ranks, mph_dist_overlap).  With 25 ms injected into every host exchange (a slow link) the
     exchanges dominate and the overlap is chosen; the rule holds in every run; and the chosen mode
-    gives the bits of either forced mode (the probe's trial pass B is undone)."""
+    gives the bits of either forced mode: the probe writes no live buffer (its halo, messages and
+    trial pass B go to the redistribution scratch set, overlap_probe in mph_dist.hip)."""
     monkeypatch.delenv("MPH_SLAB_OVERLAP", raising=False)
     monkeypatch.setenv("MPH_HOST_EXCHANGE_DELAY_MS", "25")
     slow = run_slab("channel3d", 2, [1, 9], str(tmp_path / "slow.npz"))
