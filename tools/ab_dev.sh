@@ -15,10 +15,10 @@ for r in $(seq 1 ${ROUNDS:-2}); do
     if [[ "$v" == *=* ]]; then envset=("$v")   # VAR=VALUE: a run-time setting on the base library
     elif [ $v != base ]; then lib=$PWD/particlemethod_fsi_amd/lib_$v/libmph_gpu.so; fi
     tag=${v//=/-}
-    env "${envset[@]}" MPH_GPU_LIB=$lib timeout -k 10 300 python3 bench.py --developed-steps 0 --steps 20 --warmup 4 --no-cpu-baseline > $OUT/rest_${tag}_$r.json 2> $OUT/rest_$tag.err || exit 22
-    env "${envset[@]}" MPH_GPU_LIB=$lib timeout -k 10 300 python3 bench.py --state $OUT/d1m_dev.gridb --steps 20 --warmup 4 --no-cpu-baseline > $OUT/dev_${tag}_$r.json 2> $OUT/dev_$tag.err || exit 23
+    env "${envset[@]}" MPH_GPU_LIB=$lib timeout -k 10 300 python3 bench.py --developed-steps 0 --run-average-end 0 --steps 20 --warmup 4 --no-cpu-baseline > $OUT/rest_${tag}_$r.json 2> $OUT/rest_$tag.err || exit 22
+    env "${envset[@]}" MPH_GPU_LIB=$lib timeout -k 10 300 python3 bench.py --state $OUT/d1m_dev.gridb --run-average-end 0 --steps 20 --warmup 4 --no-cpu-baseline > $OUT/dev_${tag}_$r.json 2> $OUT/dev_$tag.err || exit 23
     if [ "${D16M:-0}" = 1 ]; then
-      env "${envset[@]}" MPH_GPU_LIB=$lib timeout -k 10 300 python3 bench.py --case d16m --steps 12 --warmup 4 --no-cpu-baseline > $OUT/d16m_${tag}_$r.json 2> $OUT/d16m_$tag.err || exit 24
+      env "${envset[@]}" MPH_GPU_LIB=$lib timeout -k 10 300 python3 bench.py --case d16m --run-average-end 0 --steps 12 --warmup 4 --no-cpu-baseline > $OUT/d16m_${tag}_$r.json 2> $OUT/d16m_$tag.err || exit 24
     fi
   done
 done
