@@ -173,7 +173,9 @@ _reg(Case("fsi3d", 3, "dam", 0.001, (-0.01, 0.0, -0.01), (0.31, 0.40, 0.11), [
     Cuboid(4, (-0.003, 0.0, 0.0), (0.0, 0.2, 0.1), 0.001),
     Cuboid(4, (-0.003, 0.0, -0.003), (0.303, 0.2, 0.0), 0.001),
     Cuboid(4, (-0.003, 0.0, 0.1), (0.303, 0.2, 0.103), 0.001),
-], note="3-D dam break onto an elastic gate, coupled FSI (SURVEY 8d FSI, BASELINE configs[3])"))
+], note="3-D dam break onto an elastic gate, coupled FSI (SURVEY 8d FSI, BASELINE configs[3]) at the survey's "
+        "ElasticDt = Dt, at which the reference's own gate goes unstable within ~50 steps; the FSI "
+        "workload that runs to completion is fsi3d_sub"))
 
 # SURVEY 8d Bar (parity size): 2-D cantilever, Bar_Module, 4,000 structure particles
 _reg(Case("bar2d", 2, "bar", 0.001, (-0.01, -0.1, 0.0), (0.25, 0.1, 0.001), [
