@@ -12,5 +12,5 @@ i=0
 for grp in "$@"; do
   i=$((i+1))
   timeout -k 10 600 rocprofv3 --pmc $grp --output-format csv -d $OUT/g$i -o g$i -- \
-      python3 bench.py --case $CASE --steps 8 --warmup 8 --no-cpu-baseline --developed-steps 0 $BENCH_EXTRA --profile-steps 8 > $OUT/g$i.log 2>&1 || exit 30
+      python3 bench.py --case $CASE --steps 8 --warmup 8 --no-cpu-baseline --developed-steps 0 --run-average-end 0 $BENCH_EXTRA --profile-steps 8 > $OUT/g$i.log 2>&1 || exit 30
 done

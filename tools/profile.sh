@@ -11,8 +11,8 @@ export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
 CASE=${CASE:-d1m}
-ARGS="--case $CASE --steps ${STEPS:-24} --warmup 8 --no-cpu-baseline --developed-steps 0 $BENCH_EXTRA"
-PMC_ARGS="--case $CASE --steps 8 --warmup 8 --profile-steps 8 --no-cpu-baseline --developed-steps 0 $BENCH_EXTRA"
+ARGS="--case $CASE --steps ${STEPS:-24} --warmup 8 --no-cpu-baseline --developed-steps 0 --run-average-end 0 $BENCH_EXTRA"
+PMC_ARGS="--case $CASE --steps 8 --warmup 8 --profile-steps 8 --no-cpu-baseline --developed-steps 0 --run-average-end 0 $BENCH_EXTRA"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- \
     python3 bench.py $ARGS > $OUT/bench_under_kt.log 2>&1 || exit 21
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- \
