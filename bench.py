@@ -410,7 +410,10 @@ def main():
     # passes; algorithmic 4 B per entry against the search's measured WRITE_SIZE
     list_info = None
     if world == 1:
-        mean_stored = solver.list_stats()[0]   # the stored lists (the passes' radius), not NeighborCount
+        try:
+            mean_stored = solver.list_stats()[0]   # the stored lists (the passes' radius), not NeighborCount
+        except AttributeError:   # an ABI-3 library in a same-box A/B (MPH_ABI_ACCEPT=3)
+            mean_stored = solver.neighbor_stats()[0]
         list_alg = 4.0 * mean_stored * n_local
         wr = load_pmc("pmc_traffic", case_name, "neighbors", "write_kib")
         list_info = {"entries_per_particle": mean_stored, "alg_bytes_written": list_alg,
