@@ -119,7 +119,8 @@ struct MphCtx {
     int* rank_of = nullptr;
     int *key = nullptr, *slot = nullptr, *tmp = nullptr, *cnt = nullptr, *start = nullptr, *bsum = nullptr;
     double *vir = nullptr, *vpres = nullptr;   // VirialStress [cap][9] / VirialPressure (A order), lazy
-    int *nbr = nullptr, *ncount = nullptr, *nbcount = nullptr;   // list lengths / NeighborCount
+    int *nbr = nullptr, *ncount = nullptr, *nbcount = nullptr;   // list rows / NeighborCount
+    unsigned long long *lhdr = nullptr, *lgap = nullptr;          // the lists' row jumps (RowMask)
     double *pres = nullptr, *gx = nullptr, *gy = nullptr, *gz = nullptr, *pa = nullptr;
     double4 *force = nullptr, *acc = nullptr, *fpart = nullptr, *rec = nullptr;
     double *dens_a = nullptr, *vstrain = nullptr, *divp = nullptr;

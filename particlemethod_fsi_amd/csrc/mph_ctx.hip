@@ -74,7 +74,7 @@ void ctx_fill_launch(MphCtx* c)
     // returned through A.id), so k_rank_scatter skips that scatter; slab mode uses dst_of.
     L.A = c->A; L.B = c->B; L.rank_of = nullptr; L.dst_of = nullptr;
     L.key = c->key; L.slot = c->slot; L.tmp = c->tmp; L.cnt = c->cnt; L.start = c->start; L.bsum = c->bsum;
-    L.nbr = c->nbr; L.ncount = c->ncount; L.nbcount = c->nbcount;
+    L.nbr = c->nbr; L.ncount = c->ncount; L.nbcount = c->nbcount; L.lhdr = c->lhdr; L.lgap = c->lgap;
     // work-balanced XCD map of the passes from this many particles (MPH_XCD_BAL_MIN: tests force it
     // on small cases, the default keeps it off below 2^20 where the split kernel costs more)
     const char* bm = std::getenv("MPH_XCD_BAL_MIN");
@@ -467,6 +467,8 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     CK(dalloc(c, &c->bsum, bs));
     CK(dalloc(c, &c->nbr, ntile * kTileStride)); CK(dalloc(c, &c->ncount, cap));
     CK(dalloc(c, &c->nbcount, cap));
+    // the lists' row jumps: a header word per wave, a word of gap starts per lane (whole tiles)
+    CK(dalloc(c, &c->lhdr, ntile)); CK(dalloc(c, &c->lgap, ntile * kTile));
     CK(dalloc(c, &c->pres, cap)); CK(dalloc(c, &c->gx, cap)); CK(dalloc(c, &c->gy, cap)); CK(dalloc(c, &c->gz, cap));
     CK(dalloc(c, &c->pa, cap)); CK(dalloc(c, &c->force, cap)); CK(dalloc(c, &c->acc, cap));
     CK(dalloc(c, &c->fpart, cap)); CK(dalloc(c, &c->rec, cap));
@@ -1233,13 +1235,56 @@ int mph_neighbor_stats(MphCtx* c, double* mean, int* mx)
     return MPH_OK;
 }
 
+// The lists' rows as the last search left them (mph_kernels.hip RowMask): per particle (sorted
+// order) its rows [0, ncount) and, per wave, the row jumps -- gap k of lane s is the rows
+// [byte k of lgap[s], byte k of lhdr[s >> 6]) for k below the jump count in byte 7 of the header.
+struct HostRows {
+    std::vector<int> rows;
+    std::vector<unsigned long long> hdr, gap;
+    // whether row r of particle s holds one of its entries
+    bool ok(int s, int r) const
+    {
+        const unsigned long long h = hdr[s >> 6];
+        const int J = (int)(h >> 56);
+        for (int k = 0; k < J; ++k) {
+            const int a = (int)((gap[s] >> (8 * k)) & 0xff), b = (int)((h >> (8 * k)) & 0xff);
+            if (r >= a && r < b) return false;
+        }
+        return r < rows[s];
+    }
+    int entries(int s) const
+    {
+        const unsigned long long h = hdr[s >> 6];
+        const int J = (int)(h >> 56);
+        int e = std::min(rows[s], kTileRows);
+        for (int k = 0; k < J; ++k) e -= (int)((h >> (8 * k)) & 0xff) - (int)((gap[s] >> (8 * k)) & 0xff);
+        return e;
+    }
+};
+
+static int host_rows(MphCtx* c, HostRows& R)
+{
+    const int n = c->n;
+    const size_t ntile = ((size_t)n + kTile - 1) / kTile;
+    R.rows.resize(n);
+    R.hdr.resize(ntile);
+    R.gap.resize(ntile * kTile);
+    if (!n) return MPH_OK;
+    HIP_OK(c, hipMemcpy(R.rows.data(), c->ncount, sizeof(int) * n, hipMemcpyDeviceToHost));
+    HIP_OK(c, hipMemcpy(R.hdr.data(), c->lhdr, sizeof(unsigned long long) * ntile, hipMemcpyDeviceToHost));
+    HIP_OK(c, hipMemcpy(R.gap.data(), c->lgap, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
+    return MPH_OK;
+}
+
 int mph_list_stats(MphCtx* c, double* mean, int* mx)
 {
     if (!c || !mean || !mx) return MPH_ERR_ARG;
     CK(ctx_flush(c));
     HIP_OK(c, hipSetDevice(c->device));
-    std::vector<int> h(c->n);   // stored list lengths (ncount), reduced on the host
-    if (c->n) HIP_OK(c, hipMemcpy(h.data(), c->ncount, sizeof(int) * c->n, hipMemcpyDeviceToHost));
+    HostRows R;   // stored list lengths (the rows outside the gaps), reduced on the host
+    CK(host_rows(c, R));
+    std::vector<int> h(c->n);
+    for (int s = 0; s < c->n; ++s) h[s] = R.entries(s);
     long long sum = 0;
     int m = 0;
     for (int v : h) { sum += v; m = v > m ? v : m; }
@@ -1262,10 +1307,12 @@ int mph_neighbor_rows(MphCtx* c, int first, int count, int* counts, int* ids, lo
                                             "radius (create the context with MPH_LIST_FULL=1 for the reference's lists)");
     // the last search's rows are in its sorted order A: A.id maps a row (and an entry) back to the
     // original index, ncount holds the list's length and nbcount NeighborCount in the same order
-    std::vector<int> id(n), nc(n), nv(n);
+    std::vector<int> id(n), nv(n);
     HIP_OK(c, hipMemcpy(id.data(), c->A.id, sizeof(int) * n, hipMemcpyDeviceToHost));
-    HIP_OK(c, hipMemcpy(nc.data(), c->ncount, sizeof(int) * n, hipMemcpyDeviceToHost));
     HIP_OK(c, hipMemcpy(nv.data(), c->nbcount, sizeof(int) * n, hipMemcpyDeviceToHost));
+    HostRows R;
+    CK(host_rows(c, R));
+    const std::vector<int>& nc = R.rows;
     std::vector<int> row_of(count, -1);
     for (int s = 0; s < n; ++s)
         if (id[s] >= first && id[s] < first + count) row_of[id[s] - first] = s;
@@ -1283,7 +1330,7 @@ int mph_neighbor_rows(MphCtx* c, int first, int count, int* counts, int* ids, lo
         const int t = row_of[k] >> 6;
         if (tiles.count(t)) continue;
         int m = 0;
-        for (int s = t * kTile; s < std::min(n, (t + 1) * kTile); ++s) m = std::max(m, std::min(nc[s], kMaxNeighbor));
+        for (int s = t * kTile; s < std::min(n, (t + 1) * kTile); ++s) m = std::max(m, std::min(nc[s], kTileRows));
         std::vector<int>& buf = tiles[t];
         buf.resize((size_t)m * kTile);
         if (m) HIP_OK(c, hipMemcpy(buf.data(), c->nbr + (size_t)t * kTileStride, sizeof(int) * buf.size(),
@@ -1291,10 +1338,11 @@ int mph_neighbor_rows(MphCtx* c, int first, int count, int* counts, int* ids, lo
     }
     long long w = 0;
     for (int k = 0; k < count; ++k) {
-        const int s = row_of[k], m = std::min(counts[k], kMaxNeighbor), rows = std::min(nc[s], kMaxNeighbor);
+        const int s = row_of[k], m = std::min(counts[k], kMaxNeighbor), rows = std::min(nc[s], kTileRows);
         const std::vector<int>& buf = tiles[s >> 6];
         int q = 0;
         for (int e = 0; e < rows; ++e) {
+            if (!R.ok(s, e)) continue;   // a gap of the row jumps
             const int v = buf[(size_t)ell_slot(e, s & 63)];
             const int j = v & kIndexMask;
             if (j >= n || q >= m) return fail(c, MPH_ERR_HIP, "mph_neighbor_rows: list entry past the particle count");

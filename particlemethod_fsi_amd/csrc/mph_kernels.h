@@ -99,9 +99,12 @@ struct Launch {
     int* rank_of = nullptr;
     int* dst_of = nullptr;        // slab mode: pre-sort index -> sorted index (else rank_of[id])
     int *key = nullptr, *slot = nullptr, *tmp = nullptr, *cnt = nullptr, *start = nullptr, *bsum = nullptr;
-    // ncount: each list's length (what the passes walk); nbcount: NeighborCount (every neighbour within
+    // ncount: each list's rows (what the passes walk); nbcount: NeighborCount (every neighbour within
     // the search radius; the lists keep only r^2 <= DevParams.rlf)
     int *nbr = nullptr, *ncount = nullptr, *nbcount = nullptr;
+    // the row jumps of the lists (mph_kernels.hip RowMask): one header word per wave, one word of gap
+    // starts per particle; ncount counts rows, gaps included
+    unsigned long long *lhdr = nullptr, *lgap = nullptr;
     int* wface = nullptr;         // slab mode: face-wavefront flags written by pass B (early send)
     VSrc vsrc;                    // slab mode: where the sort finds the kept entries of its input
     // fewest particles for the work-balanced XCD map of the passes (split in k_rank_scatter);

@@ -318,12 +318,13 @@ __device__ __forceinline__ void add_wave_work(DevState* st, int cnt, int i, int 
 }
 
 __device__ __forceinline__ int nbr_entry(int j, int type) { return j | (type << kTypeShift); }
-// The search's per-lane counter (scan_candidates_lds): lane x 4 in bits 0-7, the stored entries in
-// bits 8-17 (up to 1023, so a lane that keeps all 512 entries the reference allows does not carry
-// into the total) and every accepted neighbour from bit 18.  The next list slot's byte offset in the
-// wave's ELL tile is soff & kSoffMask (stored mod 512 rows): only an overflowing lane (> 512, the
-// step's MPH_ERR_NEIGHBOR_OVERFLOW) wraps, and it stays inside its own tile.
-constexpr int kListKeep = 256 + (1 << 18), kListTotal = 1 << 18, kSoffMask = 0x1FFFF;
+// The search's per-lane counter (scan_candidates_lds): lane x 4 in bits 0-7, the row of the next
+// stored entry in bits 8-17 (the stored entries so far plus the gaps of the row jumps; up to 1023,
+// so a lane that keeps all 512 entries the reference allows does not carry into the total) and
+// every accepted neighbour from bit 18.  The next list slot's byte offset in the wave's ELL tile is
+// soff & kSoffMask; a row past the tile's kTileRows (only an overflowing lane, > 512 entries, the
+// step's MPH_ERR_NEIGHBOR_OVERFLOW) is dropped by the tile's buffer descriptor.
+constexpr int kListKeep = 256 + (1 << 18), kListTotal = 1 << 18, kSoffMask = 0x3FFFF;
 __device__ __forceinline__ int soff_total(int soff) { return (int)((unsigned)soff >> 18); }
 __device__ __forceinline__ int soff_stored(int soff) { return (soff >> 8) & 0x3FF; }
 
@@ -377,6 +378,107 @@ __device__ __forceinline__ void nbr_at(const NbrList& L, int k, int& j, int& t)
     j = e & kIndexMask;
     t = e >> kTypeShift;
 }
+
+// Aligned rows (mph_params.h kAlignRows).  A wave's jumps are recorded in two places: the wave's
+// header word lhdr[tile] (byte k < kMaxJumps: the row the lanes moved on to at jump k; byte 7: the
+// number of jumps J), and per lane lgap[i] (byte k: the lane's own row when it jumped), so the
+// lane's gap k is the rows [lgap byte k, lhdr byte k).  Every row of [0, end) outside the gaps
+// holds an entry (end = the lane's ncount), in the lane's list order.  A wave that never jumps
+// (J = 0: on the lattice, and every wave of the per-lane search) has plain rows, entry k at row k.
+// RowMask: the rows below kAlignRows that hold an entry, one bit each; rows from kAlignRows on
+// hold one exactly when they are below end.
+struct RowMask {
+    unsigned long long lo, hi;
+};
+
+// bits [k, 64) of a 64-bit word, k clamped to [0, 64]
+__device__ __forceinline__ unsigned long long bits_from(int k)
+{
+    return k <= 0 ? ~0ull : (k >= 64 ? 0ull : (~0ull << k));
+}
+
+__device__ __forceinline__ RowMask row_mask(unsigned long long hdr, const unsigned long long* lgap, int i, int end)
+{
+    RowMask m;
+    m.lo = ~bits_from(end);
+    m.hi = ~bits_from(end - 64);
+    const int J = (int)(hdr >> 56);
+    if (J) {   // wave-uniform
+        const unsigned long long g = lgap[i];
+        for (int k = 0; k < J; ++k) {
+            const int a = (int)((g >> (8 * k)) & 0xff), b = (int)((hdr >> (8 * k)) & 0xff);
+            m.lo &= ~(bits_from(a) & ~bits_from(b));
+            m.hi &= ~(bits_from(a - 64) & ~bits_from(b - 64));
+        }
+    }
+    return m;
+}
+
+// whether row r holds one of the lane's entries
+__device__ __forceinline__ bool row_ok(const RowMask& m, int r, int end)
+{
+    if (r < 64) return (m.lo >> r) & 1;
+    if (r < kAlignRows) return (m.hi >> (r - 64)) & 1;
+    return r < end;
+}
+
+// rows [k0 + a, k0 + b) as bits 0..31, a, b clamped to [0, 32]
+__device__ __forceinline__ unsigned bit_range(int a, int b)
+{
+    auto low = [](int n) { return n <= 0 ? 0u : (n >= 32 ? ~0u : (1u << n) - 1u); };
+    return low(b) & ~low(a);
+}
+
+// the rows from kAlignRows on: bit u set when row k0 + u holds an entry there (k0 + u < end)
+__device__ __forceinline__ unsigned tail_bits(int k0, int end)
+{
+    return bit_range(kAlignRows - k0, end - k0);
+}
+
+// bit u: row k0 + u holds one of the lane's entries (k0 wave-uniform in the list loops; bits
+// 0..31), without branches
+__device__ __forceinline__ unsigned row_bits(const RowMask& m, int k0, int end)
+{
+    const int k = k0 < kAlignRows ? k0 : kAlignRows - 1;
+    const unsigned long long lo = k < 64 ? m.lo : m.hi, hi = k < 64 ? m.hi : 0ull;
+    const int sh = k & 63;
+    const unsigned b = (unsigned)((lo >> sh) | (sh ? hi << (64 - sh) : 0ull));
+    return (b & bit_range(0, kAlignRows - k0)) | tail_bits(k0, end);
+}
+
+// The 128 mask bits of the lanes of a wave in LDS, 6 dwords per lane (the last two zero; a 24-byte
+// stride keeps the 32 lanes of a read group on distinct banks): pass A, whose registers are full
+constexpr int kMaskWords = 6;
+__device__ __forceinline__ void mask_to_lds(unsigned* lm, const RowMask& m)
+{
+    lm[0] = (unsigned)m.lo;
+    lm[1] = (unsigned)(m.lo >> 32);
+    lm[2] = (unsigned)m.hi;
+    lm[3] = (unsigned)(m.hi >> 32);
+    lm[4] = 0u;
+    lm[5] = 0u;
+}
+__device__ __forceinline__ unsigned row_bits_lds(const unsigned* lm, int k0, int end)
+{
+    const int d = k0 < kAlignRows ? k0 >> 5 : 3;
+    const unsigned long long v = (unsigned long long)lm[d] | ((unsigned long long)lm[d + 1] << 32);
+    return ((unsigned)(v >> (k0 & 31)) & bit_range(0, kAlignRows - k0)) | tail_bits(k0, end);
+}
+
+
+// the wave's header word (scalar load)
+__device__ __forceinline__ unsigned long long wave_hdr(const unsigned long long* lhdr, int i)
+{
+    return lhdr[__builtin_amdgcn_readfirstlane(i >> 6)];
+}
+
+// The search's row jumps: a jump at a stencil group end only when the wave's rows have drifted at
+// least this far apart (highest - lowest row of the live lanes); 1 = at every group end where the
+// rows differ, a value > kAlignRows = never (plain rows)
+#ifndef MPH_ALIGN_DRIFT
+#define MPH_ALIGN_DRIFT 1
+#endif
+constexpr int kAlignDrift = MPH_ALIGN_DRIFT;
 
 // ------------------------------------------------------------------------- sort phase -------
 
@@ -1123,7 +1225,8 @@ __device__ __forceinline__ int wave_max(int v) { return wave_reduce_dpp<true>(v)
 template <int DIM, int PERM, int SB = MPH_SB, int CAP = MPH_LDS_CAP>
 __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa& A, const int* start,
                                                    int i, bool act, double xi, double yi, double zi,
-                                                   int cx, int cy, int cz, int* out, double* sx, int* stored)
+                                                   int cx, int cy, int cz, int* out, double* sx, int* stored,
+                                                   unsigned long long* lgap, unsigned long long* lhdr)
 {
     // the staging area holds the window's 16-byte FP32 records, SB past the window's end
     constexpr int kCap32 = stage_words(CAP, SB) / 2 - SB - 1;
@@ -1134,7 +1237,7 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     const unsigned tlo = __builtin_amdgcn_readfirstlane((unsigned)tb);
     const unsigned thi = __builtin_amdgcn_readfirstlane((unsigned)(tb >> 32));
     const __amdgpu_buffer_rsrc_t tile_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(((unsigned long long)thi << 32) | tlo), 0, kTile * kMaxNeighbor * (int)sizeof(int),
+        reinterpret_cast<void*>(((unsigned long long)thi << 32) | tlo), 0, kTile * kTileRows * (int)sizeof(int),
         0x00020000);
     const double lo2 = P.rc2_lo, hi2 = P.rc2_hi;
     using X = CellAxes<DIM, PERM>;
@@ -1211,12 +1314,54 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     // stored ones (the FP32 path keeps only r^2 <= P.rlf: kListTotal, kListKeep), so the store
     // offset is soff & kSoffMask
     int soff = lane << 2;
+    // Row jumps (aligned rows, see RowMask): at the end of a stencil group (3-D: the 7 columns of
+    // one slowest-axis offset; 2-D: a column) the lanes' next rows move on to the wave's highest
+    // row, so the next group's entries start on one row for all lanes however far their counts
+    // drifted (off the lattice a store instruction otherwise touches as many rows as it has lanes,
+    // and the list lines leave L2 partly written).  Only while the highest
+    // row is below kAlignRows and the rows differ by kAlignDrift or more; on the lattice the lanes'
+    // counts agree and the wave keeps plain rows.
+    // The jumps are recorded as they happen (byte stores: the wave's header byte k, the lane's gap
+    // byte k), so that no register holds them across the columns (the search is at its 64-VGPR
+    // budget); the jump count goes to header byte 7 at the end.
+    // jumps: the jumps so far; past kMaxJumps once the wave stops jumping (one SGPR)
+    constexpr int GSZ = DIM == 3 ? kGroups : 1;
+    int jumps = kAlignDrift <= kAlignRows ? 0 : kMaxJumps;
+    // the wave's header bytes, formed where they are stored (not held in SGPRs across the columns)
+    auto hdr_byte = [&](int k) {
+        int ii = i;
+        asm volatile("" : "+v"(ii));
+        return reinterpret_cast<unsigned char*>(lhdr + __builtin_amdgcn_readfirstlane(ii >> 6)) + k;
+    };
+    auto group_end = [&]() {
+        if (jumps >= kMaxJumps) return;
+        const int row = soff_stored(soff);
+        const int m = __builtin_amdgcn_readfirstlane(wave_max(row));
+        if (m >= kAlignRows) {
+            jumps += kMaxJumps + 1;   // no more jumps
+            return;
+        }
+        if (kAlignDrift <= 1) {
+            if (!__ballot(act && row != m)) return;   // the rows agree
+        } else {
+            const int mn = __builtin_amdgcn_readfirstlane(wave_min(act ? row : m));
+            if (m - mn < kAlignDrift) return;
+        }
+        // the address formed here, not hoisted out of the column loop as a register pair
+        int ii = i;
+        asm volatile("" : "+v"(ii));
+        reinterpret_cast<unsigned char*>(lgap + ii)[jumps] = (unsigned char)row;   // the lane's gap [row, m)
+        if (lane == 0) *hdr_byte(jumps) = (unsigned char)m;
+        soff += (m - row) << 8;
+        ++jumps;
+    };
     constexpr int kSelfCol = DIM == 3 ? kReach * kGroups + kReach : kReach;   // the lane's own column
     // one stencil column: its range [jb, je) was loaded one column ahead; (nb_jb, nb_je) receive
     // column col + 1's.  The loop below is unrolled by two with the roles of the two register pairs
     // swapped, so no copy at the loop latch waits for the loads in flight.
     auto column = [&](int col, int jb, int je, int& nb_jb, int& nb_je) {
         start_landed(jb, je);   // loaded one column ahead; every path below ended in vmcnt(0)
+        if (col > 0 && col % GSZ == 0) group_end();
         if (col + 1 < NCOL) col_range(col + 1, nb_jb, nb_je);
         const bool any = je > jb;
         // the wave's window [mn, mx): the lanes are in cell order, so the first lane with candidates
@@ -1345,8 +1490,9 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
                 for (int u = 0; u < SB; ++u) {
                     const int j = j0 + u;
                     if (accept_interior(P, xs[u] - xi, ys[u] - yi, zs[u] - zi, lo2, hi2) && j < je && j != i) {
-                        if (soff_total(soff) < kMaxNeighbor)
-                            out[(size_t)((soff & kSoffMask) >> 8) * kTile] = nbr_entry(j, A.type[j]);
+                        const int row = soff_stored(soff);
+                        if (soff_total(soff) < kMaxNeighbor && row < kTileRows)
+                            out[(size_t)row * kTile] = nbr_entry(j, A.type[j]);
                         soff += kListKeep;
                     }
                 }
@@ -1361,7 +1507,8 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
         column(col, ra_b, ra_e, rb_b, rb_e);
         if (col + 1 < NCOL) column(col + 1, rb_b, rb_e, ra_b, ra_e);
     }
-    *stored = soff_stored(soff);  // the list's length (r^2 <= P.rlf)
+    *stored = soff_stored(soff);  // the list's rows, gaps included (entries: r^2 <= P.rlf)
+    if (lane == 0) *hdr_byte(7) = (unsigned char)(jumps > kMaxJumps ? jumps - kMaxJumps - 1 : jumps);
     return soff_total(soff);      // every neighbour (NeighborCount)
 }
 
@@ -1392,11 +1539,13 @@ __device__ __forceinline__ void slab_wave_flag(const DevParams& P, const Soa& A,
     if ((threadIdx.x & 63) == 0) wface[i >> 6] = face ? 1 : 0;
 }
 
-// ncount: the length of each particle's stored list (what the passes walk); nbcount: NeighborCount,
-// every neighbour within the search radius (the two differ where the lists keep only r^2 <= P.rlf)
+// ncount: the rows of each particle's stored list, gaps included (what the passes walk; the
+// entries, r^2 <= P.rlf, are the rows outside the gaps, RowMask); nbcount: NeighborCount, every
+// neighbour within the search radius; lhdr / lgap: the row jumps (RowMask)
 template <int DIM, int PERM>
 __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, const int* start, int* nbr,
-                                               int* ncount, int* nbcount, DevState* st, double* stage, int i)
+                                               int* ncount, int* nbcount, unsigned long long* lhdr,
+                                               unsigned long long* lgap, DevState* st, double* stage, int i)
 {
     const int n = dev_n(P);
     const bool live = i < n;
@@ -1408,6 +1557,7 @@ __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, 
     if (wave_all_ghosts(P, A, live, ii)) {
         if (live) ncount[i] = 0;
         if (live) nbcount[i] = 0;
+        if ((threadIdx.x & 63) == 0) lhdr[tile] = 0;
         return 0;
     }
     // the ghost lanes of a mixed wave take no part either (empty list)
@@ -1420,11 +1570,13 @@ __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, 
     const int cz = DIM == 3 ? cell_axis(zi, P.corg[2], P.dw[2], P.ginv[2], P.gc[2]) : 0;
     int* out = nbr + (size_t)(i >> 6) * kTileStride + (i & 63);
     if (fast) {
-        cnt = scan_candidates_lds<DIM, PERM>(P, A, start, i, own, xi, yi, zi, cx, cy, cz, out, stage, &stored);
+        cnt = scan_candidates_lds<DIM, PERM>(P, A, start, i, own, xi, yi, zi, cx, cy, cz, out, stage, &stored,
+                                             lgap, lhdr);
     } else {
         if (own)
             cnt = scan_candidates<DIM, false, PERM>(P, A, start, i, xi, yi, zi, cx, cy, cz, out);
         stored = cnt;
+        if ((threadIdx.x & 63) == 0) lhdr[tile] = 0;   // plain rows
     }
     if (live) ncount[i] = stored;
     if (live) nbcount[i] = cnt;
@@ -1444,7 +1596,8 @@ __device__ __forceinline__ int neighbors_body(const DevParams& P, const Soa& A, 
 template <int DIM, int PERM>
 __global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_WPE))) void k_neighbors(
     DevParams P, Soa A, const int* __restrict__ start, int* __restrict__ nbr, int* __restrict__ ncount,
-    int* __restrict__ nbcount, DevState* __restrict__ st, int* __restrict__ wface, int bal)
+    int* __restrict__ nbcount, unsigned long long* __restrict__ lhdr, unsigned long long* __restrict__ lgap,
+    DevState* __restrict__ st, int* __restrict__ wface, int bal)
 {
     const int n = dev_n(P);
     if ((int)blockIdx.x >= list_blocks(n)) return;
@@ -1452,7 +1605,7 @@ __global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_W
     __shared__ __attribute__((aligned(16))) double stage[kWB][stage_words(MPH_LDS_CAP, MPH_SB)];
     const int i = tb * blockDim.x + threadIdx.x;
     slab_wave_flag(P, A, i, n, wface);
-    const int cnt = neighbors_body<DIM, PERM>(P, A, start, nbr, ncount, nbcount, st,
+    const int cnt = neighbors_body<DIM, PERM>(P, A, start, nbr, ncount, nbcount, lhdr, lgap, st,
                                               stage[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], i);
     if (bal) add_wave_work(st, cnt, i, n);
 }
@@ -1467,19 +1620,38 @@ __global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_W
 #ifndef MPH_UB
 #define MPH_UB 8
 #endif
+// The rows of a lane's list (RowMask): the lane walks rows [0, end); a row that is a gap of its
+// row jumps takes the lane's own record (in cache, never summed) instead of an entry.
+// The batch of U rows from k0: the entries' loads first, then which rows hold entries (bits_of(),
+// from the lane's mask in LDS or registers) -- so the loads are in flight while the bits are formed
+template <int U, typename Bits>
+__device__ __forceinline__ void list_batch(const NbrList& NL, Bits bits_of, int k0, int end, int self,
+                                           bool (&ok)[U], int (&jj)[U], int (&TT)[U])
+{
+    int e[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) nbr_at(NL, k0 + u < end ? k0 + u : end - 1, e[u], TT[u]);
+    const unsigned bits = bits_of();
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        ok[u] = (bits & (1u << u)) != 0;
+        jj[u] = ok[u] ? e[u] : self;
+    }
+}
+
 template <bool FAST, int DIM, bool EQR, int U = MPH_UA>
 __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_ratio, const double* s_mu,
                                             const Soa& A,
-                                            NbrList NL, int cnt, int ti, bool solid, double xi,
-                                            double yi, double zi, double vxi, double vyi, double vzi,
-                                            PassA& o)
+                                            NbrList NL, const unsigned* lm, int end, int self, int ti,
+                                            bool solid, double xi, double yi, double zi, double vxi, double vyi,
+                                            double vzi, PassA& o)
 {
-    for (int k0 = 0; k0 < cnt; k0 += U) {
+    for (int k0 = 0; k0 < end; k0 += U) {
         int jj[U];
         double X[U], Y[U], Z[U], VX[U], VY[U], VZ[U];
         int TT[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) nbr_at(NL, k0 + u < cnt ? k0 + u : cnt - 1, jj[u], TT[u]);
+        bool ok[U];
+        list_batch<U>(NL, [&] { return row_bits_lds(lm, k0, end); }, k0, end, self, ok, jj, TT);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const double2* r = A.p6 + 3 * (size_t)jj[u];
@@ -1489,7 +1661,10 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (k0 + u >= cnt) break;
+            // the gathered values used on every path, so that hipcc does not sink a row's loads into
+            // its `ok` branch (issued there, late, they would not overlap the batch's other loads)
+            asm volatile("" ::"v"(X[u]), "v"(Y[u]), "v"(Z[u]), "v"(VX[u]), "v"(VY[u]), "v"(VZ[u]));
+            if (!ok[u]) continue;
             const double q0 = image_exact<FAST>(X[u] - xi, P.dw[0], P.hw[0], P.w075[0]);
             const double q1 = image_exact<FAST>(Y[u] - yi, P.dw[1], P.hw[1], P.w075[1]);
             const double q2 = image_exact<FAST || DIM == 2>(Z[u] - zi, P.dw[2], P.hw[2], P.w075[2]);
@@ -1510,7 +1685,9 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
 template <int DIM>
 __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, const DevTables* __restrict__ T, Soa A,
                                                 const int* __restrict__ nbr,
-                                                const int* __restrict__ ncount, PassAOut pout,
+                                                const int* __restrict__ ncount,
+                                                const unsigned long long* __restrict__ lhdr,
+                                                const unsigned long long* __restrict__ lgap, PassAOut pout,
                                                 const DevState* __restrict__ st)
 {
     const int n = dev_n(P);
@@ -1544,18 +1721,21 @@ __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, cons
     own_velocity(A, i, vxi, vyi, vzi);
     const int ti = A.type[i];
     const bool solid = dev_is_struct(ti);
-    const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
+    const int end = ncount[i] < kTileRows ? ncount[i] : kTileRows;
+    __shared__ unsigned s_mask[kWB][kTile * kMaskWords];
+    unsigned* lm = &s_mask[threadIdx.x >> 6][(threadIdx.x & 63) * kMaskWords];
+    mask_to_lds(lm, row_mask(wave_hdr(lhdr, i), lgap, i, end));   // (each lane reads back only its own)
     const NbrList NL = nbr_list(nbr, i);
     PassA o;
     // wave-uniform: equal radii (every BASELINE config) take the single-cutoff form of the sums in
     // the interior waves; waves at a periodic face keep the general form
     const bool eqr = pass_a_equal_radii(P);
     if (fast && eqr)
-        pass_a_loop<true, DIM, true>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+        pass_a_loop<true, DIM, true>(P, s_ratio, s_mu, A, NL, lm, end, i, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
     else if (fast)
-        pass_a_loop<true, DIM, false>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+        pass_a_loop<true, DIM, false>(P, s_ratio, s_mu, A, NL, lm, end, i, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
     else
-        pass_a_loop<false, DIM, false>(P, s_ratio, s_mu, A, NL, cnt, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+        pass_a_loop<false, DIM, false>(P, s_ratio, s_mu, A, NL, lm, end, i, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
     pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
 }
 
@@ -1637,23 +1817,24 @@ template <bool FAST, bool SURF, int DIM, int U = MPH_UB>
 __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_ratio,
                                             const double4* rec, const double* gx,
                                             const double* gy, const double* gz, const double* pa,
-                                            NbrList NL, int cnt, int ti, bool solid, double xi,
-                                            double yi, double zi, double gxi, double gyi, double gzi,
+                                            NbrList NL, const RowMask& M, int end, int self, int ti, bool solid,
+                                            double xi, double yi, double zi, double gxi, double gyi, double gzi,
                                             double pai, double ai, double& f0, double& f1, double& f2)
 {
     const double dscale = P.rg_r2g * (P.vol / P.dx);
     const double cpv = P.cdp * P.vol;
-    for (int k0 = 0; k0 < cnt; k0 += U) {
+    for (int k0 = 0; k0 < end; k0 += U) {
         int jj[U];
         double X[U], Y[U], Z[U], PJ[U];
         int TT[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) nbr_at(NL, k0 + u < cnt ? k0 + u : cnt - 1, jj[u], TT[u]);
+        bool ok[U];
+        list_batch<U>(NL, [&] { return row_bits(M, k0, end); }, k0, end, self, ok, jj, TT);
 #pragma unroll
         for (int u = 0; u < U; ++u) rec_load(rec, P.n, jj[u], X[u], Y[u], Z[u], PJ[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (k0 + u >= cnt) break;
+            asm volatile("" ::"v"(X[u]), "v"(Y[u]), "v"(Z[u]), "v"(PJ[u]));   // (see pass_a_loop)
+            if (!ok[u]) continue;
             pass_b_term<FAST, SURF, DIM>(P, s_ratio, gx, gy, gz, pa, jj[u], TT[u], X[u], Y[u], Z[u], PJ[u], ti,
                                          solid, xi, yi, zi, gxi, gyi, gzi, pai, ai, dscale, cpv, f0, f1, f2);
         }
@@ -1682,6 +1863,8 @@ __global__ __launch_bounds__(MPH_LB) MPH_PB_ATTR void k_pass_b(DevParams P, cons
                                                 const double* __restrict__ pa,
                                                 const int* __restrict__ nbr,
                                                 const int* __restrict__ ncount,
+                                                const unsigned long long* __restrict__ lhdr,
+                                                const unsigned long long* __restrict__ lgap,
                                                 double4* __restrict__ force, double4* __restrict__ acc,
                                                 Soa B, int phase, int* __restrict__ wface, StructHook H,
                                                 const DevState* __restrict__ st)
@@ -1725,14 +1908,15 @@ __global__ __launch_bounds__(MPH_LB) MPH_PB_ATTR void k_pass_b(DevParams P, cons
         gxi = gx[ii]; gyi = gy[ii]; gzi = gz[ii]; pai = pa[ii];
         ai = T->cofa[ti] * P.cofk * P.cofk;
     }
-    const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
+    const int end = ncount[i] < kTileRows ? ncount[i] : kTileRows;
+    const RowMask M = row_mask(wave_hdr(lhdr, i), lgap, i, end);
     const NbrList NL = nbr_list(nbr, i);
     if (fast)
-        pass_b_loop<true, SURF, DIM>(P, s_ratio, rec, gx, gy, gz, pa, NL, cnt, ti, solid, xi, yi, zi, gxi, gyi,
-                                     gzi, pai, ai, f0, f1, f2);
+        pass_b_loop<true, SURF, DIM>(P, s_ratio, rec, gx, gy, gz, pa, NL, M, end, i, ti, solid, xi, yi, zi, gxi,
+                                     gyi, gzi, pai, ai, f0, f1, f2);
     else
-        pass_b_loop<false, SURF, DIM>(P, s_ratio, rec, gx, gy, gz, pa, NL, cnt, ti, solid, xi, yi, zi, gxi, gyi,
-                                      gzi, pai, ai, f0, f1, f2);
+        pass_b_loop<false, SURF, DIM>(P, s_ratio, rec, gx, gy, gz, pa, NL, M, end, i, ti, solid, xi, yi, zi, gxi,
+                                      gyi, gzi, pai, ai, f0, f1, f2);
     double vxi, vyi, vzi;
     own_velocity(A, i, vxi, vyi, vzi);
     double vo0 = vxi, vo1 = vyi, vo2 = vzi;
@@ -1793,6 +1977,8 @@ __global__ __launch_bounds__(256) void k_virial(DevParams P, const DevTables* __
                                                 const double* __restrict__ gx, const double* __restrict__ gy,
                                                 const double* __restrict__ gz, const int* __restrict__ nbr,
                                                 const int* __restrict__ ncount,
+                                                const unsigned long long* __restrict__ lhdr,
+                                                const unsigned long long* __restrict__ lgap,
                                                 double* __restrict__ vir, double* __restrict__ vpres)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1807,9 +1993,11 @@ __global__ __launch_bounds__(256) void k_virial(DevParams P, const DevTables* __
     const double dscale = P.rg_r2g * (P.vol / P.dx);
     const double cvis = DIM == 2 ? 8.0 : 10.0;
     double S[3][3] = {{0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}, {0.0, 0.0, 0.0}};
-    const int cnt = ncount[i] < kMaxNeighbor ? ncount[i] : kMaxNeighbor;
+    const int end = ncount[i] < kTileRows ? ncount[i] : kTileRows;
+    const RowMask M = row_mask(lhdr[i >> 6], lgap, i, end);
     const int* row = ell_row(nbr, i);
-    for (int k = 0; k < cnt; ++k) {
+    for (int k = 0; k < end; ++k) {
+        if (!row_ok(M, k, end)) continue;
         const int e = *ell_at(row, (int)(i & 63), k);
         const int j = e & kIndexMask, tj = e >> kTypeShift;
         double q[3];
@@ -2753,7 +2941,7 @@ void launch_neighbors(const Launch& L)
     const int bal = P.n >= L.xcd_bal_min;
 #define MPH_NEIGHBORS(D, PERM)                                                                             \
     MPH_LAUNCH("neighbors", L.stream, (k_neighbors<D, PERM>), dim3(blocks(P.n, MPH_LB)), dim3(MPH_LB), 0, \
-               L.stream, P, L.A, L.start, L.nbr, L.ncount, L.nbcount, L.st, L.wface, bal)
+               L.stream, P, L.A, L.start, L.nbr, L.ncount, L.nbcount, L.lhdr, L.lgap, L.st, L.wface, bal)
     if (P.dim == 3) {
         switch (P.perm) {
         case 1: MPH_NEIGHBORS(3, 1); break;
@@ -2776,10 +2964,10 @@ void launch_pass_a(const Launch& L)
     const PassAOut po = pass_a_out(L);
     if (P.dim == 3)
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<3>, dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P, L.T, L.A,
-                   L.nbr, L.ncount, po, L.st);
+                   L.nbr, L.ncount, L.lhdr, L.lgap, po, L.st);
     else
         MPH_LAUNCH("pass_a", L.stream, k_pass_a<2>, dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P, L.T, L.A,
-                   L.nbr, L.ncount, po, L.st);
+                   L.nbr, L.ncount, L.lhdr, L.lgap, po, L.st);
 }
 
 // calculateNeighbor + the pass-A sums
@@ -2816,7 +3004,7 @@ void launch_pass_b(const Launch& L, int phase)
     }
 #define MPH_PASS_B(S, D)                                                                            \
     MPH_LAUNCH(phase == 2 ? "pass_b_face" : "pass_b", L.stream, (k_pass_b<S, D>), dim3(list_grid(P.n)), dim3(MPH_LB), 0, L.stream, P, \
-               L.T, L.A, L.rec, L.fpart, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, L.force, L.acc, L.B, \
+               L.T, L.A, L.rec, L.fpart, L.gx, L.gy, L.gz, L.pa, L.nbr, L.ncount, L.lhdr, L.lgap, L.force, L.acc, L.B, \
                phase, L.wface, \
                struct_hook(L), L.st)
     if (P.surface) {
@@ -2834,10 +3022,10 @@ void launch_virial(const Launch& L, const Soa& X, double* vir, double* vpres)
     if (P.n == 0) return;
     if (P.dim == 3)
         MPH_LAUNCH("virial", L.stream, k_virial<3>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T, L.A, X,
-                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, vir, vpres);
+                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, L.lhdr, L.lgap, vir, vpres);
     else
         MPH_LAUNCH("virial", L.stream, k_virial<2>, dim3(blocks(P.n, 256)), dim3(256), 0, L.stream, P, L.T, L.A, X,
-                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, vir, vpres);
+                   L.pres, L.pa, L.gx, L.gy, L.gz, L.nbr, L.ncount, L.lhdr, L.lgap, vir, vpres);
 }
 
 // lanes per structure slot: one lane per slot while the launch has >= kStructLanesTarget lanes

@@ -14,14 +14,26 @@ namespace mph {
 constexpr int kTypes = MPH_TYPE_COUNT;
 constexpr int kMaxNeighbor = MPH_MAX_NEIGHBOR_COUNT;
 constexpr int kTile = 64;  // ELL neighbour-list tile = one wavefront of i-particles
-// Ints from one wave's list tile to the next: kMaxNeighbor rows of 64, plus MPH_TILE_PAD rows, so
+// Aligned rows (round 6): at the end of a stencil group the search may move
+// every lane of a wave on to the wave's highest row, so that the lanes write (and the passes read)
+// the rows of the next group together however far their per-column counts drifted apart.  The
+// rows a lane skips are gaps; they all lie below kAlignRows (a wave jumps only while its highest
+// row is below it), so a lane's list is its rows [0, end) minus at most kMaxJumps gaps, and from
+// kAlignRows on it is contiguous.  A tile therefore holds kMaxNeighbor + kAlignRows rows.
+constexpr int kAlignRows = 128;
+constexpr int kMaxJumps = 6;   // one per interior stencil group end (7 groups)
+#ifndef MPH_TILE_EXTRA
+#define MPH_TILE_EXTRA kAlignRows   // (A/B diagnostics only: the tile's rows past kMaxNeighbor)
+#endif
+constexpr int kTileRows = kMaxNeighbor + MPH_TILE_EXTRA;
+// Ints from one wave's list tile to the next: kTileRows rows of 64, plus MPH_TILE_PAD rows, so
 // that the tiles do not all start on the same power-of-two boundary.  One row: the search 3-4 %
 // faster at rest and in the developed flow (five same-box rounds; 4 and 9 rows no faster; the
 // list's write-backs unchanged), steps within noise (profiles/r05/tile_pad/)
 #ifndef MPH_TILE_PAD
 #define MPH_TILE_PAD 1
 #endif
-constexpr int kTileStride = kTile * (kMaxNeighbor + MPH_TILE_PAD);
+constexpr int kTileStride = kTile * (kTileRows + MPH_TILE_PAD);
 // Slot of entry k of lane `lane` in its wave's tile (ints): entry k of the 64 lanes in one 256-byte
 // row, [k][lane].  (Entries in pairs or fours side by side, rows per half-wave and rows spread by the
 // last step's NeighborCount were measured in round 5 and rejected: DESIGN.md section 3.3.)
