@@ -426,6 +426,9 @@ static int ctx_init(MphCtx* c, const MphConfig* cfg, int n, const int* property,
     if (cap > kIndexMask)
         return fail(c, MPH_ERR_UNSUPPORTED, "more than 2^28 particles in one context (neighbour-list entries "
                                             "carry the type in their top bits)");
+    if ((long long)cap * 48 >= (long long)kGatherOob)
+        return fail(c, MPH_ERR_UNSUPPORTED, "more than 89 million particles in one context (the list passes "
+                                            "gather with 32-bit byte offsets)");
     {
         // the search addresses the cell table with 32-bit byte offsets (buffer descriptors)
         const long long nc = (long long)c->P.gc[0] * c->P.gc[1] * c->P.gc[2];

@@ -68,6 +68,18 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t arr_rsrc(const void* p)
 {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, -1, 0x00020000);
 }
+// a buffer descriptor over `bytes` bytes: loads past them return zeros without a memory access
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sized_rsrc(const void* p, unsigned bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+// 16 bytes at byte offset off of a buffer, as two doubles
+__device__ __forceinline__ double2 buf_ld16(__amdgpu_buffer_rsrc_t r, unsigned off)
+{
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    return __builtin_bit_cast(double2, v);
+}
 __device__ __forceinline__ __attribute__((address_space(3))) void* lds_ptr(void* p)
 {
     return (__attribute__((address_space(3))) void*)p;
@@ -1620,12 +1632,12 @@ __global__ __launch_bounds__(MPH_LB) __attribute__((amdgpu_waves_per_eu(MPH_NB_W
 #ifndef MPH_UB
 #define MPH_UB 8
 #endif
-// The rows of a lane's list (RowMask): the lane walks rows [0, end); a row that is a gap of its
-// row jumps takes the lane's own record (in cache, never summed) instead of an entry.
+// The rows of a lane's list (RowMask): the lane walks rows [0, end); a row that holds no entry of
+// it (a gap of its row jumps, or past its end) gathers nothing and is not summed.
 // The batch of U rows from k0: the entries' loads first, then which rows hold entries (bits_of(),
 // from the lane's mask in LDS or registers) -- so the loads are in flight while the bits are formed
 template <int U, typename Bits>
-__device__ __forceinline__ void list_batch(const NbrList& NL, Bits bits_of, int k0, int end, int self,
+__device__ __forceinline__ void list_batch(const NbrList& NL, Bits bits_of, int k0, int end,
                                            bool (&ok)[U], int (&jj)[U], int (&TT)[U])
 {
     int e[U];
@@ -1635,27 +1647,30 @@ __device__ __forceinline__ void list_batch(const NbrList& NL, Bits bits_of, int 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         ok[u] = (bits & (1u << u)) != 0;
-        jj[u] = ok[u] ? e[u] : self;
+        jj[u] = e[u];
     }
 }
 
 template <bool FAST, int DIM, bool EQR, int U = MPH_UA>
 __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_ratio, const double* s_mu,
                                             const Soa& A,
-                                            NbrList NL, const unsigned* lm, int end, int self, int ti,
+                                            NbrList NL, const unsigned* lm, int end, int ti,
                                             bool solid, double xi, double yi, double zi, double vxi, double vyi,
                                             double vzi, PassA& o)
 {
+    const __amdgpu_buffer_rsrc_t p6r = sized_rsrc(A.p6, (unsigned)P.n * 48u);
     for (int k0 = 0; k0 < end; k0 += U) {
         int jj[U];
         double X[U], Y[U], Z[U], VX[U], VY[U], VZ[U];
         int TT[U];
         bool ok[U];
-        list_batch<U>(NL, [&] { return row_bits_lds(lm, k0, end); }, k0, end, self, ok, jj, TT);
+        list_batch<U>(NL, [&] { return row_bits_lds(lm, k0, end); }, k0, end, ok, jj, TT);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const double2* r = A.p6 + 3 * (size_t)jj[u];
-            const double2 a = r[0], b = r[1], c = r[2];
+            // a row without an entry of the lane (a gap, or past its end) reads past the buffer:
+            // zeros, no cache lookup
+            const unsigned off = ok[u] ? (unsigned)jj[u] * 48u : kGatherOob;
+            const double2 a = buf_ld16(p6r, off), b = buf_ld16(p6r, off + 16u), c = buf_ld16(p6r, off + 32u);
             X[u] = a.x; Y[u] = a.y; Z[u] = b.x;
             VX[u] = b.y; VY[u] = c.x; VZ[u] = c.y;
         }
@@ -1731,11 +1746,11 @@ __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, cons
     // the interior waves; waves at a periodic face keep the general form
     const bool eqr = pass_a_equal_radii(P);
     if (fast && eqr)
-        pass_a_loop<true, DIM, true>(P, s_ratio, s_mu, A, NL, lm, end, i, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+        pass_a_loop<true, DIM, true>(P, s_ratio, s_mu, A, NL, lm, end, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
     else if (fast)
-        pass_a_loop<true, DIM, false>(P, s_ratio, s_mu, A, NL, lm, end, i, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+        pass_a_loop<true, DIM, false>(P, s_ratio, s_mu, A, NL, lm, end, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
     else
-        pass_a_loop<false, DIM, false>(P, s_ratio, s_mu, A, NL, lm, end, i, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+        pass_a_loop<false, DIM, false>(P, s_ratio, s_mu, A, NL, lm, end, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
     pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
 }
 
@@ -1817,20 +1832,27 @@ template <bool FAST, bool SURF, int DIM, int U = MPH_UB>
 __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_ratio,
                                             const double4* rec, const double* gx,
                                             const double* gy, const double* gz, const double* pa,
-                                            NbrList NL, const RowMask& M, int end, int self, int ti, bool solid,
+                                            NbrList NL, const RowMask& M, int end, int ti, bool solid,
                                             double xi, double yi, double zi, double gxi, double gyi, double gzi,
                                             double pai, double ai, double& f0, double& f1, double& f2)
 {
     const double dscale = P.rg_r2g * (P.vol / P.dx);
     const double cpv = P.cdp * P.vol;
+    // the record's two planes {x, y} at [j], {z, P} at [ps + j] (rec_load), 16 bytes each
+    const unsigned ps16 = (unsigned)P.n * 16u;
+    const __amdgpu_buffer_rsrc_t recr = sized_rsrc(rec, 2u * ps16);
     for (int k0 = 0; k0 < end; k0 += U) {
         int jj[U];
         double X[U], Y[U], Z[U], PJ[U];
         int TT[U];
         bool ok[U];
-        list_batch<U>(NL, [&] { return row_bits(M, k0, end); }, k0, end, self, ok, jj, TT);
+        list_batch<U>(NL, [&] { return row_bits(M, k0, end); }, k0, end, ok, jj, TT);
 #pragma unroll
-        for (int u = 0; u < U; ++u) rec_load(rec, P.n, jj[u], X[u], Y[u], Z[u], PJ[u]);
+        for (int u = 0; u < U; ++u) {   // (rows without an entry: past the buffer, as in pass_a_loop)
+            const unsigned off = ok[u] ? (unsigned)jj[u] * 16u : kGatherOob;
+            const double2 a = buf_ld16(recr, off), b = buf_ld16(recr, off == kGatherOob ? off : off + ps16);
+            X[u] = a.x; Y[u] = a.y; Z[u] = b.x; PJ[u] = b.y;
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             asm volatile("" ::"v"(X[u]), "v"(Y[u]), "v"(Z[u]), "v"(PJ[u]));   // (see pass_a_loop)
@@ -1912,10 +1934,10 @@ __global__ __launch_bounds__(MPH_LB) MPH_PB_ATTR void k_pass_b(DevParams P, cons
     const RowMask M = row_mask(wave_hdr(lhdr, i), lgap, i, end);
     const NbrList NL = nbr_list(nbr, i);
     if (fast)
-        pass_b_loop<true, SURF, DIM>(P, s_ratio, rec, gx, gy, gz, pa, NL, M, end, i, ti, solid, xi, yi, zi, gxi,
+        pass_b_loop<true, SURF, DIM>(P, s_ratio, rec, gx, gy, gz, pa, NL, M, end, ti, solid, xi, yi, zi, gxi,
                                      gyi, gzi, pai, ai, f0, f1, f2);
     else
-        pass_b_loop<false, SURF, DIM>(P, s_ratio, rec, gx, gy, gz, pa, NL, M, end, i, ti, solid, xi, yi, zi, gxi,
+        pass_b_loop<false, SURF, DIM>(P, s_ratio, rec, gx, gy, gz, pa, NL, M, end, ti, solid, xi, yi, zi, gxi,
                                       gyi, gzi, pai, ai, f0, f1, f2);
     double vxi, vyi, vzi;
     own_velocity(A, i, vxi, vyi, vzi);

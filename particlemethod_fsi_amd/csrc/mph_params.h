@@ -64,6 +64,10 @@ constexpr int kGroups = 2 * kReach + 1;   // stencil columns per axis across the
 // ELL list entry = sorted index | (type << kTypeShift): pass A reads the neighbour's type with
 // its index instead of gathering it (requires fewer than 2^28 particles per context)
 constexpr int kTypeShift = 28;
+// The list passes gather through buffer descriptors with 32-bit byte offsets; a row without an
+// entry of the lane takes this offset, past every record, so the hardware returns zeros without a
+// memory access (no cache lookup)
+constexpr unsigned kGatherOob = 0xFFFFFFC0u;
 constexpr int kIndexMask = (1 << kTypeShift) - 1;
 constexpr int kPad = 8;         // extra elements behind every per-particle array (vector over-reads)
 
