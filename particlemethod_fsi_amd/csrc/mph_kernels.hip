@@ -381,7 +381,8 @@ __device__ __forceinline__ NbrList nbr_list(const int* nbr, int i)
     return L;
 }
 
-// entry k of the lane: neighbour index j and type t
+// entry k of the lane: neighbour index j and type t.  (A buffer descriptor here, to skip the loads
+// past a lane's end, costs pass A 4 more SGPRs than it has: spills inside its loop.)
 __device__ __forceinline__ void nbr_at(const NbrList& L, int k, int& j, int& t)
 {
     using gcchar = const __attribute__((address_space(1))) char;
@@ -1336,9 +1337,11 @@ __device__ __forceinline__ int scan_candidates_lds(const DevParams& P, const Soa
     // The jumps are recorded as they happen (byte stores: the wave's header byte k, the lane's gap
     // byte k), so that no register holds them across the columns (the search is at its 64-VGPR
     // budget); the jump count goes to header byte 7 at the end.
-    // jumps: the jumps so far; past kMaxJumps once the wave stops jumping (one SGPR)
+    // jumps: the jumps so far, plus kMaxJumps + 1 once the wave stops jumping (one SGPR)
     constexpr int GSZ = DIM == 3 ? kGroups : 1;
-    int jumps = kAlignDrift <= kAlignRows ? 0 : kMaxJumps;
+    // (3-D only: the 2-D lists, ~20 entries in 7 columns, drift little, and the checks cost the Bar
+    // search 9 %)
+    int jumps = DIM == 3 && kAlignDrift <= kAlignRows ? 0 : kMaxJumps + 1;   // (stopped, none made)
     // the wave's header bytes, formed where they are stored (not held in SGPRs across the columns)
     auto hdr_byte = [&](int k) {
         int ii = i;
@@ -1654,7 +1657,7 @@ __device__ __forceinline__ void list_batch(const NbrList& NL, Bits bits_of, int 
 template <bool FAST, int DIM, bool EQR, int U = MPH_UA>
 __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_ratio, const double* s_mu,
                                             const Soa& A,
-                                            NbrList NL, const unsigned* lm, int end, int ti,
+                                            NbrList NL, bool plain, const unsigned* lm, int end, int ti,
                                             bool solid, double xi, double yi, double zi, double vxi, double vyi,
                                             double vzi, PassA& o)
 {
@@ -1664,7 +1667,8 @@ __device__ __forceinline__ void pass_a_loop(const DevParams& P, const double* s_
         double X[U], Y[U], Z[U], VX[U], VY[U], VZ[U];
         int TT[U];
         bool ok[U];
-        list_batch<U>(NL, [&] { return row_bits_lds(lm, k0, end); }, k0, end, ok, jj, TT);
+        list_batch<U>(NL, [&] { return plain ? bit_range(0, end - k0) : row_bits_lds(lm, k0, end); }, k0, end,
+                      ok, jj, TT);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             // a row without an entry of the lane (a gap, or past its end) reads past the buffer:
@@ -1739,18 +1743,21 @@ __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, cons
     const int end = ncount[i] < kTileRows ? ncount[i] : kTileRows;
     __shared__ unsigned s_mask[kWB][kTile * kMaskWords];
     unsigned* lm = &s_mask[threadIdx.x >> 6][(threadIdx.x & 63) * kMaskWords];
-    mask_to_lds(lm, row_mask(wave_hdr(lhdr, i), lgap, i, end));   // (each lane reads back only its own)
+    // a wave without jumps (plain rows: on the lattice, in 2-D) needs no mask, only its lanes' ends
+    const unsigned long long hdr = wave_hdr(lhdr, i);
+    const bool plain = (hdr >> 56) == 0;
+    if (!plain) mask_to_lds(lm, row_mask(hdr, lgap, i, end));   // (each lane reads back only its own)
     const NbrList NL = nbr_list(nbr, i);
     PassA o;
     // wave-uniform: equal radii (every BASELINE config) take the single-cutoff form of the sums in
     // the interior waves; waves at a periodic face keep the general form
     const bool eqr = pass_a_equal_radii(P);
     if (fast && eqr)
-        pass_a_loop<true, DIM, true>(P, s_ratio, s_mu, A, NL, lm, end, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+        pass_a_loop<true, DIM, true>(P, s_ratio, s_mu, A, NL, plain, lm, end, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
     else if (fast)
-        pass_a_loop<true, DIM, false>(P, s_ratio, s_mu, A, NL, lm, end, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+        pass_a_loop<true, DIM, false>(P, s_ratio, s_mu, A, NL, plain, lm, end, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
     else
-        pass_a_loop<false, DIM, false>(P, s_ratio, s_mu, A, NL, lm, end, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
+        pass_a_loop<false, DIM, false>(P, s_ratio, s_mu, A, NL, plain, lm, end, ti, solid, xi, yi, zi, vxi, vyi, vzi, o);
     pass_a_finish(P, T, ti, i, o, pout, xi, yi, zi);
 }
 
@@ -1832,7 +1839,7 @@ template <bool FAST, bool SURF, int DIM, int U = MPH_UB>
 __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_ratio,
                                             const double4* rec, const double* gx,
                                             const double* gy, const double* gz, const double* pa,
-                                            NbrList NL, const RowMask& M, int end, int ti, bool solid,
+                                            NbrList NL, bool plain, const RowMask& M, int end, int ti, bool solid,
                                             double xi, double yi, double zi, double gxi, double gyi, double gzi,
                                             double pai, double ai, double& f0, double& f1, double& f2)
 {
@@ -1846,7 +1853,8 @@ __device__ __forceinline__ void pass_b_loop(const DevParams& P, const double* s_
         double X[U], Y[U], Z[U], PJ[U];
         int TT[U];
         bool ok[U];
-        list_batch<U>(NL, [&] { return row_bits(M, k0, end); }, k0, end, ok, jj, TT);
+        list_batch<U>(NL, [&] { return plain ? bit_range(0, end - k0) : row_bits(M, k0, end); }, k0, end, ok, jj,
+                      TT);
 #pragma unroll
         for (int u = 0; u < U; ++u) {   // (rows without an entry: past the buffer, as in pass_a_loop)
             const unsigned off = ok[u] ? (unsigned)jj[u] * 16u : kGatherOob;
@@ -1931,13 +1939,15 @@ __global__ __launch_bounds__(MPH_LB) MPH_PB_ATTR void k_pass_b(DevParams P, cons
         ai = T->cofa[ti] * P.cofk * P.cofk;
     }
     const int end = ncount[i] < kTileRows ? ncount[i] : kTileRows;
-    const RowMask M = row_mask(wave_hdr(lhdr, i), lgap, i, end);
+    const unsigned long long hdr = wave_hdr(lhdr, i);
+    const bool plain = (hdr >> 56) == 0;   // no jumps: rows [0, end) (see k_pass_a)
+    const RowMask M = row_mask(hdr, lgap, i, end);
     const NbrList NL = nbr_list(nbr, i);
     if (fast)
-        pass_b_loop<true, SURF, DIM>(P, s_ratio, rec, gx, gy, gz, pa, NL, M, end, ti, solid, xi, yi, zi, gxi,
+        pass_b_loop<true, SURF, DIM>(P, s_ratio, rec, gx, gy, gz, pa, NL, plain, M, end, ti, solid, xi, yi, zi, gxi,
                                      gyi, gzi, pai, ai, f0, f1, f2);
     else
-        pass_b_loop<false, SURF, DIM>(P, s_ratio, rec, gx, gy, gz, pa, NL, M, end, ti, solid, xi, yi, zi, gxi,
+        pass_b_loop<false, SURF, DIM>(P, s_ratio, rec, gx, gy, gz, pa, NL, plain, M, end, ti, solid, xi, yi, zi, gxi,
                                       gyi, gzi, pai, ai, f0, f1, f2);
     double vxi, vyi, vzi;
     own_velocity(A, i, vxi, vyi, vzi);
