@@ -291,7 +291,9 @@ __device__ __forceinline__ int list_blocks(int n) { return (n + MPH_LB - 1) / MP
 // durations all three kernels oscillated, profiles/r03/xcd_balance/).
 constexpr int kWaveCost = 16;   // a wave's fixed cost, in list entries, for the work histogram
 
-__device__ __forceinline__ int list_block(const DevState* st, int n)
+// rev: each XCD takes its range from the far end (pass A: it starts on the list tiles the search
+// wrote last, which the Infinity Cache still holds)
+__device__ __forceinline__ int list_block(const DevState* st, int n, bool rev = false)
 {
     const int nb = list_blocks(n);
     const int b = blockIdx.x;
@@ -310,10 +312,16 @@ __device__ __forceinline__ int list_block(const DevState* st, int n)
         }
         if (ok) {
             const int q = b >> 3;
-            return q < mine_c ? mine_lo + q : -1;
+            return q < mine_c ? mine_lo + (rev ? mine_c - 1 - q : q) : -1;
         }
     }
-    return b < nb ? xcd_block(b, nb) : -1;
+    if (b >= nb) return -1;
+    if (!rev) return xcd_block(b, nb);
+    // xcd_block's range of XCD b & 7 from its end
+    const int xcd = b & 7, q = nb >> 3, r = nb & 7;
+    const int lo = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    const int cnt = q + (xcd < r ? 1 : 0);
+    return lo + cnt - 1 - (b >> 3);
 }
 
 // The search's contribution to the work histogram: its wave's longest list (all lanes converged;
@@ -488,6 +496,9 @@ __device__ __forceinline__ unsigned long long wave_hdr(const unsigned long long*
 // The search's row jumps: a jump at a stencil group end only when the wave's rows have drifted at
 // least this far apart (highest - lowest row of the live lanes); 1 = at every group end where the
 // rows differ, a value > kAlignRows = never (plain rows)
+#ifndef MPH_PASS_A_REV
+#define MPH_PASS_A_REV 1
+#endif
 #ifndef MPH_ALIGN_DRIFT
 #define MPH_ALIGN_DRIFT 1
 #endif
@@ -1710,7 +1721,7 @@ __global__ __launch_bounds__(MPH_LB) MPH_PA_ATTR void k_pass_a(DevParams P, cons
                                                 const DevState* __restrict__ st)
 {
     const int n = dev_n(P);
-    const int lb = list_block(st, n);
+    const int lb = list_block(st, n, MPH_PASS_A_REV);
     if (lb < 0) return;
     __shared__ double s_ratio[kTypes * kTypes];
     __shared__ double s_mu[kTypes * kTypes];
