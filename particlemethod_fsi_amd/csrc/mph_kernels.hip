@@ -1949,7 +1949,9 @@ __global__ __launch_bounds__(MPH_LB) MPH_PB_ATTR void k_pass_b(DevParams P, cons
         gxi = gx[ii]; gyi = gy[ii]; gzi = gz[ii]; pai = pa[ii];
         ai = T->cofa[ti] * P.cofk * P.cofk;
     }
-    const int end = ncount[i] < kTileRows ? ncount[i] : kTileRows;
+    // a wall's pair forces only go to the Force output (walls are not kicked or drifted, K17/K18):
+    // on the steps that do not store it (force null, enqueue_step) its list loop is skipped
+    const int end = !force && dev_is_wall(ti) ? 0 : (ncount[i] < kTileRows ? ncount[i] : kTileRows);
     const unsigned long long hdr = wave_hdr(lhdr, i);
     const bool plain = (hdr >> 56) == 0;   // no jumps: rows [0, end) (see k_pass_a)
     const RowMask M = row_mask(hdr, lgap, i, end);
