@@ -265,6 +265,7 @@ def main():
 
     dist = None
     cuts = None
+    fallback = None
     case_name = args.case
     if world > 1:
         # one process per GPU; torch.distributed (gloo) is only the control plane (rendezvous,
@@ -285,9 +286,36 @@ def main():
         # slab boundaries at the particle-count quantiles (equal shares; MPH_SLAB_EQUAL=1: equal widths)
         cuts = None if os.environ.get("MPH_SLAB_EQUAL") == "1" else balanced_cuts(case, world, axis)
         cfg, parts, ids, n_total = build_local(case, rank, world, axis, cuts)
-        mk = gloo_slab if os.environ.get("MPH_SLAB_TRANSPORT") == "host" else rccl_slab
-        solver = MphSolver(cfg, parts, device=device,
-                           slab=mk(rank, world, axis, ids=ids, n_glob=n_total, cuts=cuts))
+        host = os.environ.get("MPH_SLAB_TRANSPORT") == "host"
+        mk = gloo_slab if host else rccl_slab
+
+        def agreed(ok):   # every rank's verdict (gloo all-reduce): False if any rank failed
+            import torch
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            return bool(t.item())
+
+        # RCCL over xGMI has not run on this code's 8-GPU path before the driver's first scaling
+        # run: a rank whose RCCL communicator or first (graph-captured) step fails makes every rank
+        # fall back to the host-staged transport, and the line says so (`slab.transport_fallback`)
+        # instead of the job dying.  (A hang cannot be caught this way.)
+        solver, err = None, None
+        try:
+            solver = MphSolver(cfg, parts, device=device,
+                               slab=mk(rank, world, axis, ids=ids, n_glob=n_total, cuts=cuts))
+            solver.step(1)
+            solver.synchronize()
+        except Exception as e:   # noqa: BLE001 -- reported in the JSON line
+            err = "%s: %s" % (type(e).__name__, e)
+        if not host and not agreed(err is None):
+            fallback = {"from": "rccl", "to": "host-staged", "rank": rank, "error": err}
+            if solver is not None:
+                solver.close()
+            solver = MphSolver(cfg, parts, device=device,
+                               slab=gloo_slab(rank, world, axis, ids=ids, n_glob=n_total, cuts=cuts))
+            solver.step(1)
+        elif err is not None:
+            raise RuntimeError(err)
         del parts, ids
         n_local = len(solver.owned_ids())
     else:
@@ -312,7 +340,7 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
-    solver.step(args.warmup)
+    solver.step(max(0, args.warmup - (1 if dist is not None else 0)))   # (slab mode: one step ran above)
     barrier()
     t0 = time.perf_counter()
     solver.step(args.steps)
@@ -354,7 +382,7 @@ def main():
     graph_timed = world == 1 and dist is None and graph_times(solver, prof)
     checks = None
     if dist is not None:
-        checks = slab_checks(solver, dist, n_total, case_name, args.warmup + args.steps + args.profile_steps)
+        checks = slab_checks(solver, dist, n_total, case_name, max(args.warmup, 1) + args.steps + args.profile_steps)
         # per rank, so that the first multi-GPU run is diagnosable: the rank's own wall time per
         # timed step (before the max over ranks), its kernels' summed HIP-event time per step
         # (compute, mph_profile_steps) and the rest (exchange + waiting for the slowest neighbour)
@@ -528,7 +556,7 @@ def main():
                    "particles": n_total, "dim": case.dim, "module": case.module, "dt": cfg.dt,
                    "parallelism": "single" if world == 1 else "slab%d-%s (%s halo exchange, %s)" % (
                        world, "xyz"[SLAB_AXIS[case.dim]],
-                       "host-staged" if os.environ.get("MPH_SLAB_TRANSPORT") == "host" else "RCCL",
+                       "host-staged" if os.environ.get("MPH_SLAB_TRANSPORT") == "host" or fallback else "RCCL",
                        "equal widths" if cuts is None else "cuts at particle-count quantiles"),
                 "slab_cuts": None if cuts is None else [round(float(x), 9) for x in cuts]},
         "achieved_hbm_gbps_alg": B_ALG_STEP * value / 1e9,
@@ -574,6 +602,8 @@ def main():
         "run_average": run_average,
     }
     if checks is not None:
+        if fallback is not None:
+            checks["transport_fallback"] = fallback
         out["slab"] = checks
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if case_name == "d16m":
