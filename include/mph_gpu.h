@@ -392,8 +392,9 @@ int mph_dist_info(const MphCtx* ctx, int* out8);
 int mph_dist_overlap(const MphCtx* ctx, double* out5);
 /* Mean/max length of the stored neighbour lists of the last search (what the passes walk: the
  * pairs within the passes' largest radius; with MPH_LIST_FULL=1 at creation every
- * neighbour, = mph_neighbor_stats).  ABI 4 (round 6): replaces mph_list_formats, which reported
- * the compact 16-bit list format removed from the product.                                   */
+ * neighbour, = mph_neighbor_stats): entries, not rows (the gap rows of the aligned lists do not
+ * count).  ABI 4 (round 6): replaces mph_list_formats, which reported the compact 16-bit list
+ * format removed from the product.                                                            */
 int mph_list_stats(MphCtx* ctx, double* mean, int* max);
 /* The neighbour lists of calculateNeighbor themselves (main.cpp:1764-1772: Neighbor[i][k] = j for
  * k < 512), for verification: the sets of the `count` particles [first, first + count) (original
@@ -403,9 +404,9 @@ int mph_list_stats(MphCtx* ctx, double* mean, int* max);
  * it), ids_cap its capacity in ints.  Returns the number of ids written, or a negative MphStatus
  * (MPH_ERR_ARG when ids_cap is too small).  Single contexts with the reference's whole lists only
  * (created with MPH_LIST_FULL=1 in the environment: by default the lists keep only the pairs
- * within the largest radius of the passes' sums, NeighborCount still counts every neighbour) and
- * 32-bit ELL rows (MPH_ERR_UNSUPPORTED in slab mode, without MPH_LIST_FULL=1, or while a wave
- * holds a compact 16-bit list).                                                                */
+ * within the largest radius of the passes' sums, NeighborCount still counts every neighbour;
+ * MPH_ERR_UNSUPPORTED in slab mode or without MPH_LIST_FULL=1).  The gap rows of the aligned
+ * lists are skipped.                                                          */
 int mph_neighbor_rows(MphCtx* ctx, int first, int count, int* counts, int* ids, long long ids_cap);
 /* Particles currently owned by this rank (after the last migration); their original indices.  */
 int mph_owned_count(const MphCtx* ctx);
