@@ -1,0 +1,18 @@
+#!/bin/bash
+# The search's occupancy and staging re-tuned on the aligned-rows build (8 waves per SIMD at 64 VGPRs,
+# 176-candidate staging): 7 waves (72 VGPRs), 7 waves with 200-candidate staging, and 3 candidates per
+# batch at 7 waves; bitwise against the build on the small cases, then D1M rest / t = 0.25 s, 2 rounds.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+O=gpurun_out/${OUT:-ab_search_occ}
+mkdir -p $O
+V="w7 cap200w7 sb3w7"
+L=particlemethod_fsi_amd
+MPH_GPU_LIB=$PWD/$L/lib/libmph_gpu.so timeout -k 10 300 python3 tools/lib_bitwise.py run $O/bw_base.npz > $O/bw.log 2>&1 || exit 11
+for v in $V; do
+  MPH_GPU_LIB=$PWD/$L/lib_$v/libmph_gpu.so timeout -k 10 300 python3 tools/lib_bitwise.py run $O/bw_$v.npz >> $O/bw.log 2>&1 || exit 12
+  python3 tools/lib_bitwise.py compare $O/bw_base.npz $O/bw_$v.npz > $O/bw_cmp_$v.txt 2>&1; echo "$v $?" >> $O/bw.log
+done
+rm -f $O/bw_*.npz
+OUT=$O VARIANTS="$V" ROUNDS=2 bash tools/ab_dev.sh || exit 17
+python3 tools/ab_dev_summary.py $O > $O/summary.txt 2>&1
